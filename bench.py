@@ -1,0 +1,282 @@
+"""bench.py -- LangSplat train step on MI355X: rasterizer fwd+bwd blends/s and train-step ms.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C3|C2|C4|C5] [--no-cpu-baseline]
+
+BASELINE.json metric: "train-step ms & Gaussian-pixel blends/sec (fwd+bwd) @1M Gaussians 1080p,
+1/2/4/8 GPU".  One step mirrors train.py:76-138 in LangSplat's language-feature mode
+(include_feature=True, the default of arguments/__init__.py:84): render() of one view (activations
++ the rasterizer forward, gaussian_renderer/__init__.py:19-115), masked L1 on the language image
+(train.py:96-99), loss.backward() (the full rasterizer backward into means/cov/opacity/SH/language),
+[N>1: one RCCL all-reduce of the trainable gradient bucket], Adam step, zero_grad.
+
+N = 1 runs BASELINE configs[2] (C3: 1M Gaussians, one 1920x1080 camera); N > 1 runs configs[3]
+(C4: the same scene, camera `rank % 8` of 8 on a circle, one per GPU: weak scaling).  Data is
+synthetic (seeded).  `value` = Gaussian-pixel blends (sum of n_contrib, the
+forward's contributor counts = the pairs the backward replays) of all ranks per step x steps /
+max-over-ranks wall time of the timed steps.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from langsplat_amd import _native  # noqa: E402
+from langsplat_amd.distributed import GradBucket, init_from_env  # noqa: E402
+from langsplat_amd.render import render  # noqa: E402
+from langsplat_amd.synthetic import CONFIGS, activated_inputs, make_cameras, make_gaussians  # noqa: E402
+
+METRIC = "train-step ms & Gaussian-pixel blends/sec (fwd+bwd) @1M Gaussians 1080p, 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip parameters (8.0 TB/s spec)
+
+
+class Model:
+    """GaussianModel's getters over synthetic raw parameters (scene/gaussian_model.py:134-164)."""
+
+    def __init__(self, params, include_feature=True):
+        self.max_sh_degree = params.max_sh_degree
+        self.active_sh_degree = params.max_sh_degree
+        self._xyz = torch.nn.Parameter(params.xyz, requires_grad=not include_feature)
+        self._features_dc = torch.nn.Parameter(params.features_dc, requires_grad=not include_feature)
+        self._features_rest = torch.nn.Parameter(params.features_rest, requires_grad=not include_feature)
+        self._scaling = torch.nn.Parameter(params.scaling, requires_grad=not include_feature)
+        self._rotation = torch.nn.Parameter(params.rotation, requires_grad=not include_feature)
+        self._opacity = torch.nn.Parameter(params.opacity, requires_grad=not include_feature)
+        self._language_feature = torch.nn.Parameter(params.language_feature, requires_grad=include_feature)
+
+    def trainable(self):
+        return [p for p in (self._xyz, self._features_dc, self._features_rest, self._opacity, self._scaling,
+                            self._rotation, self._language_feature) if p.requires_grad]
+
+    @property
+    def get_xyz(self):
+        return self._xyz
+
+    @property
+    def get_scaling(self):
+        return torch.exp(self._scaling)
+
+    @property
+    def get_rotation(self):
+        return torch.nn.functional.normalize(self._rotation)
+
+    @property
+    def get_opacity(self):
+        return torch.sigmoid(self._opacity)
+
+    @property
+    def get_features(self):
+        return torch.cat((self._features_dc, self._features_rest), dim=1)
+
+    @property
+    def get_language_feature(self):
+        return self._language_feature
+
+    def get_covariance(self, scaling_modifier=1.0):
+        raise NotImplementedError("compute_cov3D_python is off in the benchmark (PipelineParams default)")
+
+
+class Pipe:
+    convert_SHs_python = False
+    compute_cov3D_python = False
+    debug = False
+
+
+class Opt:
+    include_feature = True
+
+
+def algorithmic_bytes(stage, P, V, R, HW, M):
+    """Compulsory HBM bytes per launch of each stage (SURVEY.md §8d per-unit model)."""
+    sh = 12 * M
+    return {
+        # reads means 12, scale 12, rot 16, opacity 4, SH, lang 12; writes radii 4 + key 4 + tiles 4
+        # + rect 8 + clamp 4 (all P) and the 48 B record for visible Gaussians
+        "preprocess": P * (12 + 12 + 16 + 4 + sh + 12 + 24) + V * 48,
+        # per instance: list id 4 + gathered record 48; per pixel: colour 12 + language 12 + T 4 + count 4
+        "render forward": R * 52 + HW * 32,
+        # per instance: id 4 + record 48; per pixel: dL/dcolour 12 + dL/dlanguage 12 + T 4 + count 4;
+        # per visible Gaussian: the 12-float gradient record (48 B) accumulated once
+        "render backward": R * 52 + HW * 32 + V * 48,
+        # reads means/scale/rot/SH/radii/clamp + 48 B grad record; writes every gradient output
+        "preprocess backward": P * (12 + 12 + 16 + sh + 4 + 4) + V * 48 + P * (12 + 12 + 12 + 4 + 12 + sh + 12 + 16),
+    }.get(stage)
+
+
+def cpu_baseline(cfg, seconds_budget=25.0):
+    """Oracle (oracle/lsr_oracle.c, 1 thread) fwd+bwd on a bounded sample of the same workload:
+    the first P/4 Gaussians of the C3 scene, same camera and resolution."""
+    from oracle import oracle
+    from tests.scenes import settings_for
+    c = CONFIGS[cfg]
+    frac = 4
+    Ps = c["P"] // frac
+    g = make_gaussians(c["P"], seed=0)
+    cam = make_cameras(1, c["width"], c["height"])[0]
+    st = settings_for(cam, sh_degree=3)
+    with torch.no_grad():
+        inp = {k: (v[:Ps].contiguous() if v.dim() and v.shape[0] == c["P"] else v)
+               for k, v in activated_inputs(g).items()}
+    H, W = c["height"], c["width"]
+    gen = torch.Generator().manual_seed(1)
+    gcol = torch.randn((3, H, W), generator=gen) / (3 * H * W)
+    glang = torch.randn((3, H, W), generator=gen) / (3 * H * W)
+    t0 = time.perf_counter()
+    run = oracle.forward(st, **inp)
+    run.backward(gcol, glang)
+    dt = time.perf_counter() - t0
+    blends = run.blends
+    return {"value": blends / dt, "unit": "blends/s", "cores": 1, "kind": "port",
+            "sample": f"{cfg} scene, first {Ps} of {c['P']} Gaussians, {W}x{H}, one fwd+bwd "
+                      f"({blends} blends, {dt:.1f} s, single-threaded C oracle)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default=None)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--json-out", default=None)
+    args = ap.parse_args()
+
+    rank, world = init_from_env()
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    cfg = args.config or ("C3" if world == 1 else "C4")
+    c = CONFIGS[cfg]
+    P, W, H = c["P"], c["width"], c["height"]
+    view = rank % c["views"] if c["views"] > 1 else 0
+
+    params = make_gaussians(P, seed=0, sh_degree=c["sh_degree"]).to(dev)
+    model = Model(params, include_feature=True)
+    cam = make_cameras(c["views"], W, H, device=dev)[view]
+    bg = torch.zeros(3, device=dev)
+    gen = torch.Generator().manual_seed(100 + view)
+    gt = torch.nn.functional.normalize(torch.randn((3, H, W), generator=gen), dim=0).to(dev)
+    mask = (torch.rand((1, H, W), generator=gen) < 0.9).float().to(dev)
+    optim = torch.optim.Adam([{"params": [model._language_feature], "lr": 0.0025, "name": "language_feature"}],
+                             lr=0.0, eps=1e-15)
+    bucket = GradBucket(model.trainable())
+
+    def step():
+        pkg = render(cam, model, Pipe, bg, Opt)
+        lang = pkg["language_feature_image"]
+        loss = (lang * mask - gt * mask).abs().mean()
+        loss.backward()
+        if world > 1:
+            bucket.all_reduce(average=True)
+        optim.step()
+        optim.zero_grad(set_to_none=False)
+        return loss
+
+    # blends and instance counts of this view (constant over steps: geometry is frozen)
+    with torch.no_grad():
+        inp = activated_inputs(params)
+        from langsplat_amd.render import GaussianRasterizationSettings
+        st = GaussianRasterizationSettings(H, W, math.tan(cam.FoVx * 0.5), math.tan(cam.FoVy * 0.5), bg, 1.0,
+                                           cam.world_view_transform, cam.full_proj_transform, 3,
+                                           cam.camera_center, False, False, True)
+        nr, _, _, radii, geom, binning, image = _native.rasterize_gaussians(
+            st, inp["means3D"], inp["shs"], None, inp["language_feature_precomp"], inp["opacities"],
+            inp["scales"], inp["rotations"], None)
+        lay = _native.state_layout(P, W, H, nr)
+        ncon = image[lay["n_contrib"]:lay["n_contrib"] + 4 * W * H].view(torch.int32)
+        blends = int(ncon.to(torch.int64).sum().item())
+        visible = int((radii > 0).sum().item())
+        del geom, binning, image, inp
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    _native.profile_enable(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    _native.profile_enable(False)
+    prof = _native.profile_report()
+
+    t = torch.tensor([elapsed, float(blends)], dtype=torch.float64, device=dev)
+    if world > 1:
+        tmax = t[:1].clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        tsum = t[1:].clone()
+        dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
+        elapsed_max, blends_all = float(tmax.item()), float(tsum.item())
+    else:
+        elapsed_max, blends_all = elapsed, float(blends)
+
+    if rank != 0:
+        dist.barrier()
+        dist.destroy_process_group()
+        return
+
+    ms_per_step = 1000.0 * elapsed_max / args.steps
+    value = blends_all * args.steps / elapsed_max
+    raster_ms = sum(v["total_ms"] for k, v in prof.items()) / args.steps
+    dom_name, dom = max(prof.items(), key=lambda kv: kv[1]["total_ms"])
+    M = (c["sh_degree"] + 1) ** 2
+    bytes_dom = algorithmic_bytes(dom_name, P, visible, nr, W * H, M)
+    roofline = None
+    if bytes_dom is not None:
+        achieved = bytes_dom / (dom["avg_ms"] * 1e-3) / 1e9
+        roofline = {"bound": "hbm", "kernel": dom_name, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                    "avg_ms": round(dom["avg_ms"], 4), "bytes_per_launch": int(bytes_dom)}
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(cfg)
+    out = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "blends/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic (seeded random Gaussians / cameras, SURVEY.md §8d)",
+        "config": {"workload": f"{cfg}: {P} Gaussians, {W}x{H}, SH deg 3 + 3-ch language feature, "
+                               f"include_feature train step, 1 view per GPU",
+                   "gaussians": P, "width": W, "height": H, "views": world, "parallelism": f"dp{world} (views)",
+                   "blends_per_step": blends_all, "num_rendered_rank0": nr, "visible_rank0": visible},
+        "raster_ms_per_step": round(raster_ms, 4),
+        "stages_ms_per_step": {k: round(v["total_ms"] / args.steps, 4) for k, v in sorted(prof.items())},
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+    }
+    line = json.dumps(out)
+    print(line, flush=True)
+    if args.json_out:
+        with open(args.json_out, "w") as f:
+            f.write(line + "\n")
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

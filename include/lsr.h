@@ -1,0 +1,195 @@
+/*
+ * lsr.h -- C ABI of the MI355X-native LangSplat Gaussian rasterizer (liblsr.so).
+ *
+ * This is the drop-in boundary for the hot path named in BASELINE.json "north_star": the
+ * forward and backward of RasterizeGaussians.  Each entry point replaces one native entry of
+ * the reference's (absent) submodules/langsplat-rasterization extension, whose Python face
+ * is used at:
+ *
+ *   reference interface (call site)                              replaced by
+ *   ------------------------------------------------------------ ---------------------------
+ *   _C.rasterize_gaussians            (called via GaussianRasterizer.forward,
+ *                                      gaussian_renderer/__init__.py:96-105)        lsr_forward
+ *   _C.rasterize_gaussians_backward   (autograd backward of the same call;
+ *                                      train.py:104 loss.backward())                lsr_backward
+ *   _C.mark_visible                   (GaussianRasterizer.markVisible; upstream API,
+ *                                      unused by the reference scripts)             lsr_mark_visible
+ *   C++ exception text -> RuntimeError (upstream error path)        lsr_last_error
+ *
+ * Conventions:
+ *   - All array pointers are DEVICE pointers to contiguous fp32/int32 data, borrowed for the
+ *     duration of the call.  Outputs are written in full; callers never need to pre-zero.
+ *   - Matrices are the reference's row-vector matrices stored row-major, exactly the memory of
+ *     Camera.world_view_transform / full_proj_transform (scene/cameras.py:54-56).
+ *   - Work is enqueued on `stream` (a hipStream_t; NULL = legacy default stream).  lsr_forward
+ *     performs ONE stream synchronisation to learn num_rendered (as upstream does).
+ *   - Scratch is owned by the caller and requested through `alloc` (upstream's resizable
+ *     geometry/binning/image buffers).  The three forward buffers must be kept alive, unchanged,
+ *     and passed back to lsr_backward.
+ *   - Return value: LSR_OK or an error code; lsr_last_error() describes the last failure on the
+ *     calling thread.  The only process-wide state is the opt-in kernel profiler below (off by
+ *     default, mutex-protected); rasterization itself is re-entrant.
+ */
+#ifndef LSR_H
+#define LSR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LSR_ABI_VERSION 1
+
+enum lsr_status {
+    LSR_OK = 0,
+    LSR_ERR_INVALID = 1,     /* bad argument (null pointer, negative size, ...) */
+    LSR_ERR_HIP = 2,         /* a HIP runtime call or kernel launch failed */
+    LSR_ERR_ALLOC = 3,       /* the alloc callback returned NULL */
+    LSR_ERR_PREFILTERED = 4  /* prefiltered=1 but a Gaussian failed the frustum test */
+};
+
+/* Scratch buffers requested through the allocator (upstream geomBuffer/binningBuffer/imgBuffer) */
+enum lsr_buffer {
+    LSR_BUF_GEOM = 0,     /* per Gaussian; forward -> backward */
+    LSR_BUF_BINNING = 1,  /* per tile instance; forward -> backward */
+    LSR_BUF_IMAGE = 2,    /* per pixel / per tile; forward -> backward */
+    LSR_BUF_BACKWARD = 3  /* per Gaussian gradient scratch, backward only */
+};
+
+/* Returns device memory of at least `bytes` bytes, 256-byte aligned, valid until the caller
+ * releases it; NULL on failure.  Called synchronously from the calling thread. */
+typedef void* (*lsr_alloc_fn)(void* user, int32_t which, size_t bytes);
+
+/* GaussianRasterizationSettings (gaussian_renderer/__init__.py:37-51), device-pointer form. */
+typedef struct lsr_settings {
+    int32_t image_height;
+    int32_t image_width;
+    float tanfovx;
+    float tanfovy;
+    float scale_modifier;
+    int32_t sh_degree;        /* active SH degree D (0..3) */
+    int32_t prefiltered;
+    int32_t debug;            /* sync + check after every kernel */
+    int32_t include_feature;  /* composite the 3-channel language feature */
+    int32_t reserved;
+    const float* bg;          /* [3] */
+    const float* viewmatrix;  /* [16] world_view_transform */
+    const float* projmatrix;  /* [16] full_proj_transform */
+    const float* campos;      /* [3] camera_center */
+} lsr_settings;
+
+/* Inputs/outputs of _C.rasterize_gaussians.  Exactly one of {shs, colors_precomp} and one of
+ * {scales+rotations, cov3D_precomp} is non-NULL (GaussianRasterizer.forward validates). */
+typedef struct lsr_forward_args {
+    int32_t P;                       /* number of Gaussians */
+    int32_t M;                       /* SH coefficients stored per Gaussian (shs: P x M x 3) */
+    const float* means3D;            /* P x 3 */
+    const float* shs;                /* P x M x 3 or NULL */
+    const float* colors_precomp;     /* P x 3 or NULL */
+    const float* language_feature;   /* P x 3, or NULL when include_feature == 0 */
+    const float* opacities;          /* P */
+    const float* scales;             /* P x 3 or NULL */
+    const float* rotations;          /* P x 4 (already normalised) or NULL */
+    const float* cov3D_precomp;      /* P x 6 or NULL */
+    float* out_color;                /* 3 x H x W */
+    float* out_language_feature;     /* 3 x H x W */
+    int32_t* radii;                  /* P */
+} lsr_forward_args;
+
+/* Inputs/outputs of _C.rasterize_gaussians_backward.  Every non-NULL output is fully written
+ * (zeros for culled Gaussians).  dL_dsh may be NULL when shs is NULL; dL_dscales/dL_drotations
+ * may be NULL when cov3D_precomp is given; dL_dcov3D may be NULL when scales are given. */
+typedef struct lsr_backward_args {
+    int32_t P;
+    int32_t M;
+    int64_t num_rendered;            /* value returned by lsr_forward */
+    const float* means3D;
+    const float* shs;
+    const float* colors_precomp;
+    const float* language_feature;
+    const float* opacities;
+    const float* scales;
+    const float* rotations;
+    const float* cov3D_precomp;
+    const int32_t* radii;
+    const float* dL_dout_color;             /* 3 x H x W */
+    const float* dL_dout_language_feature;  /* 3 x H x W or NULL (treated as zeros) */
+    void* geom_buffer;
+    void* binning_buffer;
+    void* image_buffer;
+    float* dL_dmeans2D;              /* P x 3 (z = 0) */
+    float* dL_dcolors;               /* P x 3 */
+    float* dL_dlanguage_feature;     /* P x 3 */
+    float* dL_dopacity;              /* P */
+    float* dL_dmeans3D;              /* P x 3 */
+    float* dL_dcov3D;                /* P x 6 or NULL */
+    float* dL_dsh;                   /* P x M x 3 or NULL */
+    float* dL_dscales;               /* P x 3 or NULL */
+    float* dL_drotations;            /* P x 4 or NULL */
+} lsr_backward_args;
+
+/* Byte offsets of the internal state inside the forward buffers, for inspection by tests and
+ * for debug dumps.  All arrays are tightly packed at the given offsets. */
+typedef struct lsr_state_layout {
+    /* geometry buffer */
+    size_t depth_key;      /* uint32[P]  float bits of view depth, 0xFFFFFFFF if culled */
+    size_t tiles_touched;  /* uint32[P] */
+    size_t rect;           /* uint32[2P] (minx | miny << 16, maxx | maxy << 16) */
+    size_t record;         /* float4[3P] {x, y, conic.x, conic.y}{conic.z, opacity, r, g}{b, f0, f1, f2} */
+    size_t clamped;        /* uint32[P]  bit c = SH colour channel c clamped */
+    size_t sorted_ids;     /* uint32[P]  Gaussians by (depth, id); visible ones first */
+    size_t depth_rank;     /* uint32[P]  inverse of sorted_ids for visible Gaussians */
+    /* image buffer */
+    size_t counters;       /* uint32[16] {visible, num_rendered, error, n_oversize, ...} */
+    size_t tile_start;     /* uint32[T+1] exclusive scan of per-tile counts */
+    size_t final_T;        /* float[H*W] */
+    size_t n_contrib;      /* uint32[H*W] */
+    /* binning buffer */
+    size_t point_list;     /* uint32[num_rendered] Gaussian ids, tile-major, depth order */
+    size_t list_rank;      /* uint32[num_rendered] unsorted depth ranks (emit order) */
+} lsr_state_layout;
+
+int32_t lsr_abi_version(void);
+const char* lsr_last_error(void);
+
+/* Sizes (bytes) of the forward scratch buffers. */
+size_t lsr_geom_bytes(int32_t P);
+size_t lsr_image_bytes(int32_t width, int32_t height);
+size_t lsr_binning_bytes(int64_t num_rendered);
+size_t lsr_backward_bytes(int32_t P);
+int32_t lsr_state_layout_of(int32_t P, int32_t width, int32_t height, int64_t num_rendered,
+                            lsr_state_layout* out);
+
+/* _C.rasterize_gaussians: preprocess, depth sort, tile binning, per-tile sort, front-to-back
+ * compositing.  Writes out_color, out_language_feature, radii and *num_rendered. */
+int32_t lsr_forward(const lsr_settings* settings, const lsr_forward_args* args,
+                    lsr_alloc_fn alloc, void* alloc_user, void* stream, int64_t* num_rendered);
+
+/* _C.rasterize_gaussians_backward: back-to-front replay and per-Gaussian chain rule. */
+int32_t lsr_backward(const lsr_settings* settings, const lsr_backward_args* args,
+                     lsr_alloc_fn alloc, void* alloc_user, void* stream);
+
+/* Per-stage device time, measured with HIP events recorded on the caller's stream around each
+ * launch group while profiling is enabled (measurement support for bench.py; no reference
+ * counterpart).  lsr_profile_enable(1) clears and starts, (0) stops; lsr_profile_report
+ * synchronises the recorded events and returns the number of stages written to `out`. */
+typedef struct lsr_kernel_stat {
+    char name[32];
+    int64_t launches;
+    double total_ms;
+} lsr_kernel_stat;
+
+int32_t lsr_profile_enable(int32_t on);
+int32_t lsr_profile_report(lsr_kernel_stat* out, int32_t capacity);
+
+/* _C.mark_visible: visible[i] = 1 iff Gaussian i passes the near-plane frustum test. */
+int32_t lsr_mark_visible(int32_t P, const float* means3D, const float* viewmatrix,
+                         const float* projmatrix, uint8_t* visible, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* LSR_H */

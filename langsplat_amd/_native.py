@@ -1,0 +1,303 @@
+"""ctypes binding of liblsr.so (the C ABI in include/lsr.h).
+
+This is the reference-side binding a maintainer would add in place of the CUDA extension's
+pybind module `diff_gaussian_rasterization._C`.  Tensors are passed as raw
+device pointers; scratch buffers are torch uint8 tensors handed out through the allocator
+callback (so the caching allocator owns them and autograd keeps them alive for backward).
+
+There is no CPU fallback: if liblsr.so cannot be loaded the import of this module fails.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Dict, Optional
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "liblsr.so")
+
+LSR_BUF_GEOM, LSR_BUF_BINNING, LSR_BUF_IMAGE, LSR_BUF_BACKWARD = 0, 1, 2, 3
+_vp = ctypes.c_void_p
+
+
+class LsrSettings(ctypes.Structure):
+    _fields_ = [
+        ("image_height", ctypes.c_int32),
+        ("image_width", ctypes.c_int32),
+        ("tanfovx", ctypes.c_float),
+        ("tanfovy", ctypes.c_float),
+        ("scale_modifier", ctypes.c_float),
+        ("sh_degree", ctypes.c_int32),
+        ("prefiltered", ctypes.c_int32),
+        ("debug", ctypes.c_int32),
+        ("include_feature", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+        ("bg", _vp),
+        ("viewmatrix", _vp),
+        ("projmatrix", _vp),
+        ("campos", _vp),
+    ]
+
+
+class LsrForwardArgs(ctypes.Structure):
+    _fields_ = [("P", ctypes.c_int32), ("M", ctypes.c_int32)] + [
+        (n, _vp) for n in ("means3D", "shs", "colors_precomp", "language_feature", "opacities", "scales",
+                           "rotations", "cov3D_precomp", "out_color", "out_language_feature", "radii")
+    ]
+
+
+class LsrBackwardArgs(ctypes.Structure):
+    _fields_ = [("P", ctypes.c_int32), ("M", ctypes.c_int32), ("num_rendered", ctypes.c_int64)] + [
+        (n, _vp) for n in ("means3D", "shs", "colors_precomp", "language_feature", "opacities", "scales",
+                           "rotations", "cov3D_precomp", "radii", "dL_dout_color", "dL_dout_language_feature",
+                           "geom_buffer", "binning_buffer", "image_buffer", "dL_dmeans2D", "dL_dcolors",
+                           "dL_dlanguage_feature", "dL_dopacity", "dL_dmeans3D", "dL_dcov3D", "dL_dsh",
+                           "dL_dscales", "dL_drotations")
+    ]
+
+
+class LsrStateLayout(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_size_t) for n in (
+        "depth_key", "tiles_touched", "rect", "record", "clamped", "sorted_ids", "depth_rank",
+        "counters", "tile_start", "final_T", "n_contrib", "point_list", "list_rank")]
+
+
+class LsrKernelStat(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char * 32), ("launches", ctypes.c_int64), ("total_ms", ctypes.c_double)]
+
+
+ALLOC_FN = ctypes.CFUNCTYPE(_vp, _vp, ctypes.c_int32, ctypes.c_size_t)
+
+# symbol -> (restype, argtypes); must cover every function declared in include/lsr.h
+SIGNATURES = {
+    "lsr_abi_version": (ctypes.c_int32, []),
+    "lsr_last_error": (ctypes.c_char_p, []),
+    "lsr_geom_bytes": (ctypes.c_size_t, [ctypes.c_int32]),
+    "lsr_image_bytes": (ctypes.c_size_t, [ctypes.c_int32, ctypes.c_int32]),
+    "lsr_binning_bytes": (ctypes.c_size_t, [ctypes.c_int64]),
+    "lsr_backward_bytes": (ctypes.c_size_t, [ctypes.c_int32]),
+    "lsr_state_layout_of": (ctypes.c_int32, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int64,
+                                             ctypes.POINTER(LsrStateLayout)]),
+    "lsr_forward": (ctypes.c_int32, [ctypes.POINTER(LsrSettings), ctypes.POINTER(LsrForwardArgs), ALLOC_FN, _vp,
+                                     _vp, ctypes.POINTER(ctypes.c_int64)]),
+    "lsr_backward": (ctypes.c_int32, [ctypes.POINTER(LsrSettings), ctypes.POINTER(LsrBackwardArgs), ALLOC_FN, _vp,
+                                      _vp]),
+    "lsr_mark_visible": (ctypes.c_int32, [ctypes.c_int32, _vp, _vp, _vp, _vp, _vp]),
+    "lsr_profile_enable": (ctypes.c_int32, [ctypes.c_int32]),
+    "lsr_profile_report": (ctypes.c_int32, [ctypes.POINTER(LsrKernelStat), ctypes.c_int32]),
+}
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+def load(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load liblsr.so (building it first if it is absent and hipcc is available)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        from . import build as _build  # compiles the HIP sources; not a fallback path
+        _build.build()
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.lsr_abi_version() != 1:
+        raise RuntimeError("liblsr.so ABI version mismatch")
+    _lib = lib
+    return lib
+
+
+def last_error() -> str:
+    return load().lsr_last_error().decode(errors="replace")
+
+
+def _check(status: int, what: str):
+    if status != 0:
+        raise RuntimeError(f"{what} failed (status {status}): {last_error()}")
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    if t is None or t.numel() == 0:
+        return None
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _stream(device: torch.device) -> ctypes.c_void_p:
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+class _Allocator:
+    """Hands out torch uint8 device tensors for the ABI's scratch requests."""
+
+    def __init__(self, device: torch.device):
+        self.device = device
+        self.buffers: Dict[int, torch.Tensor] = {}
+
+        def _cb(user, which, nbytes):
+            try:
+                t = torch.empty((max(int(nbytes), 1),), dtype=torch.uint8, device=self.device)
+            except Exception:  # noqa: BLE001 -- reported to C as NULL -> LSR_ERR_ALLOC
+                return None
+            self.buffers[int(which)] = t
+            return t.data_ptr()
+
+        self.fn = ALLOC_FN(_cb)
+
+    def get(self, which: int) -> torch.Tensor:
+        t = self.buffers.get(which)
+        return t if t is not None else torch.empty((0,), dtype=torch.uint8, device=self.device)
+
+
+def make_settings(rs, keep: list) -> LsrSettings:
+    """lsr_settings from a GaussianRasterizationSettings (gaussian_renderer/__init__.py:37-51)."""
+    s = LsrSettings()
+    s.image_height = int(rs.image_height)
+    s.image_width = int(rs.image_width)
+    s.tanfovx = float(rs.tanfovx)
+    s.tanfovy = float(rs.tanfovy)
+    s.scale_modifier = float(rs.scale_modifier)
+    s.sh_degree = int(rs.sh_degree)
+    s.prefiltered = int(bool(rs.prefiltered))
+    s.debug = int(bool(rs.debug))
+    s.include_feature = int(bool(getattr(rs, "include_feature", False)))
+    for name in ("bg", "viewmatrix", "projmatrix", "campos"):
+        t = getattr(rs, name).detach().to(torch.float32).contiguous()
+        keep.append(t)
+        setattr(s, name, t.data_ptr())
+    return s
+
+
+def rasterize_gaussians(rs, means3D, shs, colors_precomp, language_feature, opacities, scales, rotations,
+                        cov3D_precomp):
+    """Native forward: returns (num_rendered, color, language_feature_image, radii, geom, binning, image)."""
+    lib = load()
+    device = means3D.device
+    P = int(means3D.shape[0])
+    H, W = int(rs.image_height), int(rs.image_width)
+    keep: list = []
+    s = make_settings(rs, keep)
+    color = torch.empty((3, H, W), dtype=torch.float32, device=device)
+    lang = torch.empty((3, H, W), dtype=torch.float32, device=device)
+    radii = torch.zeros((P,), dtype=torch.int32, device=device)
+    a = LsrForwardArgs()
+    a.P = P
+    a.M = int(shs.shape[1]) if shs is not None and shs.numel() > 0 else 0
+    a.means3D = _ptr(means3D)
+    a.shs = _ptr(shs)
+    a.colors_precomp = _ptr(colors_precomp)
+    a.language_feature = _ptr(language_feature)
+    a.opacities = _ptr(opacities)
+    a.scales = _ptr(scales)
+    a.rotations = _ptr(rotations)
+    a.cov3D_precomp = _ptr(cov3D_precomp)
+    a.out_color = _ptr(color)
+    a.out_language_feature = _ptr(lang)
+    a.radii = _ptr(radii)
+    alloc = _Allocator(device)
+    nr = ctypes.c_int64(0)
+    with torch.cuda.device(device):
+        _check(lib.lsr_forward(ctypes.byref(s), ctypes.byref(a), alloc.fn, None, _stream(device), ctypes.byref(nr)),
+               "lsr_forward")
+    return (int(nr.value), color, lang, radii, alloc.get(LSR_BUF_GEOM), alloc.get(LSR_BUF_BINNING),
+            alloc.get(LSR_BUF_IMAGE))
+
+
+def rasterize_gaussians_backward(rs, means3D, shs, colors_precomp, language_feature, scales, rotations,
+                                 cov3D_precomp, radii, grad_color, grad_language, num_rendered, geom, binning,
+                                 image):
+    """Native backward: returns the gradient tensors keyed like the reference's inputs."""
+    lib = load()
+    device = means3D.device
+    P = int(means3D.shape[0])
+    M = int(shs.shape[1]) if shs is not None and shs.numel() > 0 else 0
+    keep: list = []
+    s = make_settings(rs, keep)
+    f32 = dict(dtype=torch.float32, device=device)
+    g = {
+        "means2D": torch.empty((P, 3), **f32),
+        "colors_precomp": torch.empty((P, 3), **f32),
+        "language_feature_precomp": torch.empty((P, 3), **f32),
+        "opacities": torch.empty((P, 1), **f32),
+        "means3D": torch.empty((P, 3), **f32),
+        "cov3D_precomp": torch.empty((P, 6), **f32) if _ptr(cov3D_precomp) is not None else None,
+        "shs": torch.empty((P, M, 3), **f32) if M > 0 else None,
+        "scales": torch.empty((P, 3), **f32) if _ptr(scales) is not None else None,
+        "rotations": torch.empty((P, 4), **f32) if _ptr(rotations) is not None else None,
+    }
+    if P == 0:
+        return {k: (v.zero_() if v is not None else None) for k, v in g.items()}
+    a = LsrBackwardArgs()
+    a.P = P
+    a.M = M
+    a.num_rendered = int(num_rendered)
+    a.means3D = _ptr(means3D)
+    a.shs = _ptr(shs)
+    a.colors_precomp = _ptr(colors_precomp)
+    a.language_feature = _ptr(language_feature)
+    a.scales = _ptr(scales)
+    a.rotations = _ptr(rotations)
+    a.cov3D_precomp = _ptr(cov3D_precomp)
+    a.radii = _ptr(radii)
+    gc = grad_color.detach().to(torch.float32).contiguous()
+    a.dL_dout_color = _ptr(gc)
+    gl = None
+    if grad_language is not None:
+        gl = grad_language.detach().to(torch.float32).contiguous()
+        a.dL_dout_language_feature = _ptr(gl)
+    a.geom_buffer = _ptr(geom)
+    a.binning_buffer = _ptr(binning)
+    a.image_buffer = _ptr(image)
+    a.dL_dmeans2D = _ptr(g["means2D"])
+    a.dL_dcolors = _ptr(g["colors_precomp"])
+    a.dL_dlanguage_feature = _ptr(g["language_feature_precomp"])
+    a.dL_dopacity = _ptr(g["opacities"])
+    a.dL_dmeans3D = _ptr(g["means3D"])
+    a.dL_dcov3D = _ptr(g["cov3D_precomp"])
+    a.dL_dsh = _ptr(g["shs"])
+    a.dL_dscales = _ptr(g["scales"])
+    a.dL_drotations = _ptr(g["rotations"])
+    alloc = _Allocator(device)
+    with torch.cuda.device(device):
+        _check(lib.lsr_backward(ctypes.byref(s), ctypes.byref(a), alloc.fn, None, _stream(device)), "lsr_backward")
+    return g
+
+
+def mark_visible(means3D, viewmatrix, projmatrix):
+    lib = load()
+    device = means3D.device
+    P = int(means3D.shape[0])
+    vis = torch.zeros((P,), dtype=torch.uint8, device=device)
+    m = means3D.detach().to(torch.float32).contiguous()
+    v = viewmatrix.detach().to(torch.float32).contiguous()
+    p = projmatrix.detach().to(torch.float32).contiguous()
+    with torch.cuda.device(device):
+        _check(lib.lsr_mark_visible(P, _ptr(m), _ptr(v), _ptr(p), _ptr(vis), _stream(device)), "lsr_mark_visible")
+    return vis.bool()
+
+
+def state_layout(P: int, W: int, H: int, num_rendered: int) -> Dict[str, int]:
+    lay = LsrStateLayout()
+    _check(load().lsr_state_layout_of(P, W, H, num_rendered, ctypes.byref(lay)), "lsr_state_layout_of")
+    return {name: int(getattr(lay, name)) for name, _ in LsrStateLayout._fields_}
+
+
+def profile_enable(on: bool = True):
+    load().lsr_profile_enable(1 if on else 0)
+
+
+def profile_report() -> Dict[str, Dict[str, float]]:
+    """{stage: {"launches": n, "total_ms": t, "avg_ms": t / n}} (synchronises recorded events)."""
+    lib = load()
+    n = lib.lsr_profile_report(None, 0)
+    arr = (LsrKernelStat * max(n, 1))()
+    n = lib.lsr_profile_report(arr, n)
+    out = {}
+    for i in range(n):
+        k = arr[i].name.decode()
+        out[k] = {"launches": int(arr[i].launches), "total_ms": float(arr[i].total_ms),
+                  "avg_ms": float(arr[i].total_ms) / max(int(arr[i].launches), 1)}
+    return out

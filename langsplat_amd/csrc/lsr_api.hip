@@ -1,0 +1,365 @@
+// lsr_api.hip -- the extern "C" boundary of liblsr.so (declared in include/lsr.h).
+//
+// Orchestration mirrors the reference's two native entry points (see include/lsr.h for the
+// call sites they replace): forward = preprocess -> depth sort -> tile counts/scan ->
+// [one D2H read of num_rendered] -> emit -> per-tile order -> render; backward = render
+// replay -> per-Gaussian chain rule.
+#include <stdio.h>
+#include <string.h>
+
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "lsr_internal.h"
+
+using namespace lsr;
+
+static thread_local std::string g_last_error;
+
+// ------------------------------------------------------------------ opt-in event profiler
+namespace {
+struct Pending {
+    const char* name;
+    hipEvent_t a, b;
+};
+struct Profiler {
+    std::mutex mu;
+    bool on = false;
+    std::vector<Pending> pending;
+    std::vector<hipEvent_t> pool;
+    std::map<std::string, std::pair<int64_t, double>> stats;
+
+    hipEvent_t get()
+    {
+        if (!pool.empty()) {
+            hipEvent_t e = pool.back();
+            pool.pop_back();
+            return e;
+        }
+        hipEvent_t e = nullptr;
+        if (hipEventCreate(&e) != hipSuccess) return nullptr;
+        return e;
+    }
+    void drain()
+    {
+        for (auto& p : pending) {
+            float ms = 0.f;
+            if (hipEventSynchronize(p.b) == hipSuccess && hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+                auto& st = stats[p.name];
+                st.first += 1;
+                st.second += ms;
+            }
+            pool.push_back(p.a);
+            pool.push_back(p.b);
+        }
+        pending.clear();
+    }
+};
+Profiler g_prof;
+
+// Records an event pair around one launch group when profiling is on.
+struct Scope {
+    hipEvent_t a = nullptr, b = nullptr;
+    const char* name;
+    hipStream_t s;
+    Scope(const char* n, hipStream_t st) : name(n), s(st)
+    {
+        std::lock_guard<std::mutex> g(g_prof.mu);
+        if (!g_prof.on) return;
+        a = g_prof.get();
+        b = g_prof.get();
+        if (a && b) (void)hipEventRecord(a, s);
+    }
+    ~Scope()
+    {
+        if (!a || !b) return;
+        (void)hipEventRecord(b, s);
+        std::lock_guard<std::mutex> g(g_prof.mu);
+        g_prof.pending.push_back({name, a, b});
+    }
+};
+}  // namespace
+
+static int32_t fail(int32_t code, const char* what, hipError_t e = hipSuccess)
+{
+    char buf[512];
+    if (e != hipSuccess)
+        snprintf(buf, sizeof(buf), "%s: %s (%s)", what, hipGetErrorString(e), hipGetErrorName(e));
+    else
+        snprintf(buf, sizeof(buf), "%s", what);
+    g_last_error = buf;
+    return code;
+}
+
+#define LSR_TRY(expr, what)                                                  \
+    do {                                                                     \
+        hipError_t _e;                                                       \
+        {                                                                    \
+            Scope _scope(what, stream);                                      \
+            _e = (expr);                                                     \
+        }                                                                    \
+        if (_e == hipSuccess && debug) _e = hipStreamSynchronize(stream);    \
+        if (_e == hipSuccess && debug) _e = hipGetLastError();               \
+        if (_e != hipSuccess) return fail(LSR_ERR_HIP, what, _e);            \
+    } while (0)
+
+extern "C" {
+
+int32_t lsr_abi_version(void) { return LSR_ABI_VERSION; }
+
+const char* lsr_last_error(void) { return g_last_error.c_str(); }
+
+size_t lsr_geom_bytes(int32_t P) { return make_layout(P, 0, 0, 0).geom_bytes; }
+
+size_t lsr_image_bytes(int32_t width, int32_t height) { return make_layout(0, width, height, 0).image_bytes; }
+
+size_t lsr_binning_bytes(int64_t num_rendered) { return make_layout(0, 0, 0, num_rendered).binning_bytes; }
+
+size_t lsr_backward_bytes(int32_t P) { return 4 * (size_t)kGradStride * (size_t)(P > 0 ? P : 1); }
+
+int32_t lsr_state_layout_of(int32_t P, int32_t width, int32_t height, int64_t num_rendered, lsr_state_layout* out)
+{
+    if (!out || P < 0 || width < 0 || height < 0 || num_rendered < 0)
+        return fail(LSR_ERR_INVALID, "lsr_state_layout_of: invalid argument");
+    const Layout L = make_layout(P, width, height, num_rendered);
+    out->depth_key = L.depth_key;
+    out->tiles_touched = L.tiles_touched;
+    out->rect = L.rect;
+    out->record = L.record;
+    out->clamped = L.clamped;
+    out->sorted_ids = L.sorted_ids;
+    out->depth_rank = L.depth_rank;
+    out->counters = L.counters;
+    out->tile_start = L.tile_start;
+    out->final_T = L.final_T;
+    out->n_contrib = L.n_contrib;
+    out->point_list = L.point_list;
+    out->list_rank = L.list_rank;
+    return LSR_OK;
+}
+
+int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_fn alloc, void* user,
+                    void* stream_ptr, int64_t* num_rendered)
+{
+    if (!s || !a || !alloc || !num_rendered) return fail(LSR_ERR_INVALID, "lsr_forward: null argument");
+    const int P = a->P, W = s->image_width, H = s->image_height;
+    if (P < 0 || W <= 0 || H <= 0 || W > 65535 * kTile || H > 65535 * kTile)
+        return fail(LSR_ERR_INVALID, "lsr_forward: invalid P or image size");
+    if (s->sh_degree < 0 || s->sh_degree > 3) return fail(LSR_ERR_INVALID, "lsr_forward: sh_degree must be 0..3");
+    if (!a->out_color || !a->out_language_feature || (P > 0 && (!a->radii || !a->means3D || !a->opacities)))
+        return fail(LSR_ERR_INVALID, "lsr_forward: missing input/output pointer");
+    if (P > 0 && (!a->shs) == (!a->colors_precomp))
+        return fail(LSR_ERR_INVALID, "lsr_forward: provide exactly one of shs / colors_precomp");
+    if (P > 0 && ((a->scales && a->rotations) ? 1 : 0) == (a->cov3D_precomp ? 1 : 0))
+        return fail(LSR_ERR_INVALID, "lsr_forward: provide exactly one of scales+rotations / cov3D_precomp");
+    if (a->shs && (a->M < (s->sh_degree + 1) * (s->sh_degree + 1)))
+        return fail(LSR_ERR_INVALID, "lsr_forward: M smaller than (sh_degree+1)^2");
+    if (!s->bg || !s->viewmatrix || !s->projmatrix || !s->campos)
+        return fail(LSR_ERR_INVALID, "lsr_forward: settings tensors missing");
+    hipStream_t stream = reinterpret_cast<hipStream_t>(stream_ptr);
+    const bool debug = s->debug != 0;
+    *num_rendered = 0;
+    const size_t HW = (size_t)W * H;
+    if (P == 0) {
+        // upstream leaves the images at their zero initialisation when there is nothing to draw
+        LSR_TRY(hipMemsetAsync(a->out_color, 0, 3 * HW * 4, stream), "memset color");
+        LSR_TRY(hipMemsetAsync(a->out_language_feature, 0, 3 * HW * 4, stream), "memset language");
+        return LSR_OK;
+    }
+
+    Layout L = make_layout(P, W, H, 0);
+    char* geom = static_cast<char*>(alloc(user, LSR_BUF_GEOM, L.geom_bytes));
+    char* image = static_cast<char*>(alloc(user, LSR_BUF_IMAGE, L.image_bytes));
+    if (!geom || !image) return fail(LSR_ERR_ALLOC, "lsr_forward: geometry/image buffer allocation failed");
+    uint32_t* counters = reinterpret_cast<uint32_t*>(image + L.counters);
+    LSR_TRY(hipMemsetAsync(counters, 0, 4 * kCntSlots, stream), "memset counters");
+
+    PreprocessParams pp{};
+    pp.P = P;
+    pp.M = a->M;
+    pp.D = s->sh_degree;
+    pp.W = W;
+    pp.H = H;
+    pp.gx = L.gx;
+    pp.gy = L.gy;
+    pp.tanfovx = s->tanfovx;
+    pp.tanfovy = s->tanfovy;
+    pp.focal_y = (float)H / (2.0f * s->tanfovy);
+    pp.focal_x = (float)W / (2.0f * s->tanfovx);
+    pp.scale_modifier = s->scale_modifier;
+    pp.include_feature = s->include_feature;
+    pp.prefiltered = s->prefiltered;
+    pp.means = a->means3D;
+    pp.shs = a->shs;
+    pp.colors = a->colors_precomp;
+    pp.lang = a->language_feature;
+    pp.opac = a->opacities;
+    pp.scales = a->scales;
+    pp.rots = a->rotations;
+    pp.cov_pre = a->cov3D_precomp;
+    pp.view = s->viewmatrix;
+    pp.proj = s->projmatrix;
+    pp.campos = s->campos;
+    pp.radii = a->radii;
+    pp.depth_key = reinterpret_cast<uint32_t*>(geom + L.depth_key);
+    pp.tiles = reinterpret_cast<uint32_t*>(geom + L.tiles_touched);
+    pp.rect = reinterpret_cast<uint32_t*>(geom + L.rect);
+    pp.clamped = reinterpret_cast<uint32_t*>(geom + L.clamped);
+    pp.record = reinterpret_cast<float4*>(geom + L.record);
+    pp.counters = counters;
+    LSR_TRY(launch_preprocess(pp, stream), "preprocess");
+    LSR_TRY(launch_depth_sort(P, L, geom, counters, stream, debug), "depth sort");
+    LSR_TRY(launch_tile_count(P, L, geom, image, stream), "tile count");
+    LSR_TRY(launch_tile_scan(L, image, stream), "tile scan");
+
+    // the one host synchronisation: visible count, num_rendered, error flag
+    uint32_t host_cnt[4] = {0, 0, 0, 0};
+    LSR_TRY(hipMemcpyAsync(host_cnt, counters, sizeof(host_cnt), hipMemcpyDeviceToHost, stream), "read counters");
+    LSR_TRY(hipStreamSynchronize(stream), "synchronize");
+    if (host_cnt[kCntError] && s->prefiltered)
+        return fail(LSR_ERR_PREFILTERED, "lsr_forward: prefiltered=True but a Gaussian is outside the frustum");
+    const int64_t R = host_cnt[kCntRendered];
+    *num_rendered = R;
+
+    L = make_layout(P, W, H, R);
+    char* binning = static_cast<char*>(alloc(user, LSR_BUF_BINNING, L.binning_bytes));
+    if (!binning) return fail(LSR_ERR_ALLOC, "lsr_forward: binning buffer allocation failed");
+    if (R > 0) {
+        LSR_TRY(launch_emit(P, L, geom, image, binning, stream), "emit");
+        LSR_TRY(launch_tile_sort(L, geom, image, binning, stream, debug), "tile sort");
+    }
+    RenderParams rp{};
+    rp.W = W;
+    rp.H = H;
+    rp.gx = L.gx;
+    rp.gy = L.gy;
+    rp.include_feature = (s->include_feature && a->language_feature) ? 1 : 0;
+    rp.tile_start = reinterpret_cast<const uint32_t*>(image + L.tile_start);
+    rp.point_list = reinterpret_cast<const uint32_t*>(binning + L.point_list);
+    rp.record = reinterpret_cast<const float4*>(geom + L.record);
+    rp.bg = s->bg;
+    rp.final_T = reinterpret_cast<float*>(image + L.final_T);
+    rp.n_contrib = reinterpret_cast<uint32_t*>(image + L.n_contrib);
+    rp.out_color = a->out_color;
+    rp.out_lang = a->out_language_feature;
+    LSR_TRY(launch_render_forward(rp, L.tiles, stream), "render forward");
+    return LSR_OK;
+}
+
+int32_t lsr_backward(const lsr_settings* s, const lsr_backward_args* a, lsr_alloc_fn alloc, void* user,
+                     void* stream_ptr)
+{
+    if (!s || !a || !alloc) return fail(LSR_ERR_INVALID, "lsr_backward: null argument");
+    const int P = a->P, W = s->image_width, H = s->image_height;
+    if (P < 0 || W <= 0 || H <= 0) return fail(LSR_ERR_INVALID, "lsr_backward: invalid P or image size");
+    if (!a->dL_dmeans2D || !a->dL_dcolors || !a->dL_dlanguage_feature || !a->dL_dopacity || !a->dL_dmeans3D)
+        return fail(LSR_ERR_INVALID, "lsr_backward: missing output pointer");
+    if ((a->shs && !a->dL_dsh) || (a->cov3D_precomp && !a->dL_dcov3D))
+        return fail(LSR_ERR_INVALID, "lsr_backward: missing dL_dsh / dL_dcov3D output");
+    hipStream_t stream = reinterpret_cast<hipStream_t>(stream_ptr);
+    const bool debug = s->debug != 0;
+    if (P == 0) return LSR_OK;
+    if (!a->dL_dout_color || !a->geom_buffer || !a->image_buffer || !a->binning_buffer || !a->radii)
+        return fail(LSR_ERR_INVALID, "lsr_backward: missing forward state");
+    const Layout L = make_layout(P, W, H, a->num_rendered);
+    char* geom = static_cast<char*>(a->geom_buffer);
+    char* image = static_cast<char*>(a->image_buffer);
+    char* binning = static_cast<char*>(a->binning_buffer);
+    float* grad = static_cast<float*>(alloc(user, LSR_BUF_BACKWARD, lsr_backward_bytes(P)));
+    if (!grad) return fail(LSR_ERR_ALLOC, "lsr_backward: gradient scratch allocation failed");
+    LSR_TRY(hipMemsetAsync(grad, 0, lsr_backward_bytes(P), stream), "memset grad");
+
+    RenderParams rp{};
+    rp.W = W;
+    rp.H = H;
+    rp.gx = L.gx;
+    rp.gy = L.gy;
+    rp.include_feature = (s->include_feature && a->language_feature) ? 1 : 0;
+    rp.tile_start = reinterpret_cast<const uint32_t*>(image + L.tile_start);
+    rp.point_list = reinterpret_cast<const uint32_t*>(binning + L.point_list);
+    rp.record = reinterpret_cast<const float4*>(geom + L.record);
+    rp.bg = s->bg;
+    rp.final_T = reinterpret_cast<float*>(image + L.final_T);
+    rp.n_contrib = reinterpret_cast<uint32_t*>(image + L.n_contrib);
+    rp.dL_dcolor = a->dL_dout_color;
+    rp.dL_dlang = a->dL_dout_language_feature;
+    rp.grad = grad;
+    if (a->num_rendered > 0) LSR_TRY(launch_render_backward(rp, L.tiles, stream), "render backward");
+
+    PreprocessBwdParams bp{};
+    bp.P = P;
+    bp.M = a->M;
+    bp.D = s->sh_degree;
+    bp.W = W;
+    bp.H = H;
+    bp.tanfovx = s->tanfovx;
+    bp.tanfovy = s->tanfovy;
+    bp.focal_y = (float)H / (2.0f * s->tanfovy);
+    bp.focal_x = (float)W / (2.0f * s->tanfovx);
+    bp.scale_modifier = s->scale_modifier;
+    bp.means = a->means3D;
+    bp.shs = a->shs;
+    bp.scales = a->scales;
+    bp.rots = a->rotations;
+    bp.cov_pre = a->cov3D_precomp;
+    bp.view = s->viewmatrix;
+    bp.proj = s->projmatrix;
+    bp.campos = s->campos;
+    bp.radii = a->radii;
+    bp.clamped = reinterpret_cast<const uint32_t*>(geom + L.clamped);
+    bp.grad = grad;
+    bp.dmeans2D = a->dL_dmeans2D;
+    bp.dcolors = a->dL_dcolors;
+    bp.dlang = a->dL_dlanguage_feature;
+    bp.dopac = a->dL_dopacity;
+    bp.dmeans3D = a->dL_dmeans3D;
+    bp.dcov = a->dL_dcov3D;
+    bp.dsh = a->shs ? a->dL_dsh : nullptr;
+    bp.dscales = a->dL_dscales;
+    bp.drots = a->dL_drotations;
+    if (!a->shs && a->dL_dsh && a->M > 0)
+        LSR_TRY(hipMemsetAsync(a->dL_dsh, 0, (size_t)P * a->M * 3 * 4, stream), "memset dsh");
+    LSR_TRY(launch_preprocess_backward(bp, stream), "preprocess backward");
+    return LSR_OK;
+}
+
+int32_t lsr_profile_enable(int32_t on)
+{
+    std::lock_guard<std::mutex> g(g_prof.mu);
+    g_prof.drain();
+    if (on) g_prof.stats.clear();
+    g_prof.on = on != 0;
+    return LSR_OK;
+}
+
+int32_t lsr_profile_report(lsr_kernel_stat* out, int32_t capacity)
+{
+    std::lock_guard<std::mutex> g(g_prof.mu);
+    g_prof.drain();
+    int32_t n = 0;
+    for (auto& kv : g_prof.stats) {
+        if (out && n < capacity) {
+            memset(out[n].name, 0, sizeof(out[n].name));
+            strncpy(out[n].name, kv.first.c_str(), sizeof(out[n].name) - 1);
+            out[n].launches = kv.second.first;
+            out[n].total_ms = kv.second.second;
+        }
+        n++;
+    }
+    return n;
+}
+
+int32_t lsr_mark_visible(int32_t P, const float* means3D, const float* viewmatrix, const float* projmatrix,
+                         uint8_t* visible, void* stream_ptr)
+{
+    if (P < 0 || (P > 0 && (!means3D || !viewmatrix || !projmatrix || !visible)))
+        return fail(LSR_ERR_INVALID, "lsr_mark_visible: invalid argument");
+    hipStream_t stream = reinterpret_cast<hipStream_t>(stream_ptr);
+    const bool debug = false;
+    LSR_TRY(launch_mark_visible(P, means3D, viewmatrix, projmatrix, visible, stream), "mark visible");
+    return LSR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,207 @@
+// lsr_device.h -- device math shared by the rasterizer kernels (gfx950).
+//
+// Every expression here has the same explicit evaluation order as the CPU oracle
+// (oracle/lsr_oracle.c); the kernels are compiled with -ffp-contract=off, so preprocessing and
+// compositing produce bit-identical values on both sides.  Algorithm: the published 3DGS
+// rasterizer forked by submodules/langsplat-rasterization (absent from the reference snapshot,
+// SURVEY.md §0); call-site contract gaussian_renderer/__init__.py:37-105.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace lsr {
+
+constexpr int kTile = 16;              // BLOCK_X = BLOCK_Y = 16
+constexpr int kTilePixels = kTile * kTile;
+
+// SH constants, utils/sh_utils.py:26-45
+constexpr float SH_C0 = 0.28209479177387814f;
+constexpr float SH_C1 = 0.4886025119029199f;
+constexpr float SH_C2_0 = 1.0925484305920792f, SH_C2_1 = -1.0925484305920792f,
+                SH_C2_2 = 0.31539156525252005f, SH_C2_3 = -1.0925484305920792f,
+                SH_C2_4 = 0.5462742152960396f;
+constexpr float SH_C3_0 = -0.5900435899266435f, SH_C3_1 = 2.890611442640554f,
+                SH_C3_2 = -0.4570457994644658f, SH_C3_3 = 0.3731763325901154f,
+                SH_C3_4 = -0.4570457994644658f, SH_C3_5 = 1.445305721320277f,
+                SH_C3_6 = -0.5900435899266435f;
+
+// exp restatement (Cody-Waite by ln2 + degree-7 Taylor); identical op sequence to lso_expf.
+__device__ __forceinline__ float expf_exact(float x)
+{
+    if (x < -87.0f) return 0.0f;
+    float n = __builtin_rintf(x * 1.44269504088896341f);
+    float r = __builtin_fmaf(n, -0.693145751953125f, x);
+    r = __builtin_fmaf(n, -1.42860682030941723212e-6f, r);
+    float p = 1.98412698e-4f;
+    p = __builtin_fmaf(p, r, 1.38888889e-3f);
+    p = __builtin_fmaf(p, r, 8.33333333e-3f);
+    p = __builtin_fmaf(p, r, 4.16666667e-2f);
+    p = __builtin_fmaf(p, r, 1.66666667e-1f);
+    p = __builtin_fmaf(p, r, 0.5f);
+    p = __builtin_fmaf(p, r, 1.0f);
+    p = __builtin_fmaf(p, r, 1.0f);
+    int e = (int)n;
+    return p * __uint_as_float((uint32_t)(e + 127) << 23);
+}
+
+__device__ __forceinline__ float fma_(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+
+// 3-term dot in the oracle's order: fma(a2,b2, fma(a1,b1, a0*b0))
+__device__ __forceinline__ float dot3(float a0, float a1, float a2, float b0, float b1, float b2)
+{
+    return fma_(a2, b2, fma_(a1, b1, a0 * b0));
+}
+
+// Row-vector point transforms over a row-major 4x4 (scene/cameras.py:54-56 memory layout).
+__device__ __forceinline__ float3 xform4x3(const float* m, float px, float py, float pz)
+{
+    return make_float3(fma_(m[8], pz, fma_(m[4], py, m[0] * px)) + m[12],
+                       fma_(m[9], pz, fma_(m[5], py, m[1] * px)) + m[13],
+                       fma_(m[10], pz, fma_(m[6], py, m[2] * px)) + m[14]);
+}
+
+__device__ __forceinline__ float xform4w(const float* m, float px, float py, float pz)
+{
+    return fma_(m[11], pz, fma_(m[7], py, m[3] * px)) + m[15];
+}
+
+__device__ __forceinline__ float ndc2pix(float v, int S)
+{
+    return (float)((((double)v + 1.0) * (double)S - 1.0) * 0.5);
+}
+
+struct Mat3 { float m[3][3]; };
+
+__device__ __forceinline__ Mat3 quat_to_rot(float r, float x, float y, float z)
+{
+    Mat3 R;
+    R.m[0][0] = 1.f - 2.f * (y * y + z * z);
+    R.m[0][1] = 2.f * (x * y - r * z);
+    R.m[0][2] = 2.f * (x * z + r * y);
+    R.m[1][0] = 2.f * (x * y + r * z);
+    R.m[1][1] = 1.f - 2.f * (x * x + z * z);
+    R.m[1][2] = 2.f * (y * z - r * x);
+    R.m[2][0] = 2.f * (x * z - r * y);
+    R.m[2][1] = 2.f * (y * z + r * x);
+    R.m[2][2] = 1.f - 2.f * (x * x + y * y);
+    return R;
+}
+
+// Sigma = (R S)(R S)^T, packed (xx, xy, xz, yy, yz, zz): scene/gaussian_model.py:27-31
+__device__ __forceinline__ void cov3d(float sx, float sy, float sz, float mod, float4 q, float* cov)
+{
+    Mat3 R = quat_to_rot(q.x, q.y, q.z, q.w);
+    float s[3] = {mod * sx, mod * sy, mod * sz};
+    float M[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+        for (int k = 0; k < 3; k++) M[i][k] = R.m[i][k] * s[k];
+    cov[0] = dot3(M[0][0], M[0][1], M[0][2], M[0][0], M[0][1], M[0][2]);
+    cov[1] = dot3(M[0][0], M[0][1], M[0][2], M[1][0], M[1][1], M[1][2]);
+    cov[2] = dot3(M[0][0], M[0][1], M[0][2], M[2][0], M[2][1], M[2][2]);
+    cov[3] = dot3(M[1][0], M[1][1], M[1][2], M[1][0], M[1][1], M[1][2]);
+    cov[4] = dot3(M[1][0], M[1][1], M[1][2], M[2][0], M[2][1], M[2][2]);
+    cov[5] = dot3(M[2][0], M[2][1], M[2][2], M[2][0], M[2][1], M[2][2]);
+}
+
+struct Cov2D {
+    float t[3];      // clamped camera-space mean
+    float A[2][3];   // J W
+    float a, b, c;   // 2D covariance (+0.3 low-pass on a, c)
+    float txtz, tytz;
+};
+
+// EWA projection A = J W; cov2D = A Sigma A^T + 0.3 I.
+__device__ __forceinline__ Cov2D cov2d(float px, float py, float pz, float fx, float fy,
+                                       float tanfovx, float tanfovy, const float* cov,
+                                       const float* view)
+{
+    Cov2D o;
+    float3 t = xform4x3(view, px, py, pz);
+    float limx = 1.3f * tanfovx, limy = 1.3f * tanfovy;
+    float txtz = t.x / t.z, tytz = t.y / t.z;
+    t.x = fminf(limx, fmaxf(-limx, txtz)) * t.z;
+    t.y = fminf(limy, fmaxf(-limy, tytz)) * t.z;
+    float tz2 = t.z * t.z;
+    float j00 = fx / t.z;
+    float j02 = -(fx * t.x) / tz2;
+    float j11 = fy / t.z;
+    float j12 = -(fy * t.y) / tz2;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        float w0 = view[4 * k + 0], w1 = view[4 * k + 1], w2 = view[4 * k + 2];
+        o.A[0][k] = fma_(j02, w2, j00 * w0);
+        o.A[1][k] = fma_(j12, w2, j11 * w1);
+    }
+    const float S[3][3] = {{cov[0], cov[1], cov[2]}, {cov[1], cov[3], cov[4]}, {cov[2], cov[4], cov[5]}};
+    float u0[3], u1[3];
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+        u0[r] = dot3(S[r][0], S[r][1], S[r][2], o.A[0][0], o.A[0][1], o.A[0][2]);
+        u1[r] = dot3(S[r][0], S[r][1], S[r][2], o.A[1][0], o.A[1][1], o.A[1][2]);
+    }
+    o.a = dot3(o.A[0][0], o.A[0][1], o.A[0][2], u0[0], u0[1], u0[2]) + 0.3f;
+    o.b = dot3(o.A[1][0], o.A[1][1], o.A[1][2], u0[0], u0[1], u0[2]);
+    o.c = dot3(o.A[1][0], o.A[1][1], o.A[1][2], u1[0], u1[1], u1[2]) + 0.3f;
+    o.t[0] = t.x;
+    o.t[1] = t.y;
+    o.t[2] = t.z;
+    o.txtz = txtz;
+    o.tytz = tytz;
+    return o;
+}
+
+// SH -> RGB for one channel (utils/sh_utils.py:57-112).  sh points at coefficient 0 of the
+// channel, coefficients strided by 3 (P x M x 3 layout of GaussianModel.get_features).
+__device__ __forceinline__ float sh_eval_channel(int deg, const float* sh, float x, float y, float z)
+{
+    float res = SH_C0 * sh[0];
+    if (deg > 0) {
+        res = res - (SH_C1 * y) * sh[1 * 3];
+        res = res + (SH_C1 * z) * sh[2 * 3];
+        res = res - (SH_C1 * x) * sh[3 * 3];
+        if (deg > 1) {
+            float xx = x * x, yy = y * y, zz = z * z;
+            float xy = x * y, yz = y * z, xz = x * z;
+            res = res + (SH_C2_0 * xy) * sh[4 * 3];
+            res = res + (SH_C2_1 * yz) * sh[5 * 3];
+            res = res + (SH_C2_2 * (2.0f * zz - xx - yy)) * sh[6 * 3];
+            res = res + (SH_C2_3 * xz) * sh[7 * 3];
+            res = res + (SH_C2_4 * (xx - yy)) * sh[8 * 3];
+            if (deg > 2) {
+                res = res + (SH_C3_0 * y * (3.0f * xx - yy)) * sh[9 * 3];
+                res = res + (SH_C3_1 * xy * z) * sh[10 * 3];
+                res = res + (SH_C3_2 * y * (4.0f * zz - xx - yy)) * sh[11 * 3];
+                res = res + (SH_C3_3 * z * (2.0f * zz - 3.0f * xx - 3.0f * yy)) * sh[12 * 3];
+                res = res + (SH_C3_4 * x * (4.0f * zz - xx - yy)) * sh[13 * 3];
+                res = res + (SH_C3_5 * z * (xx - yy)) * sh[14 * 3];
+                res = res + (SH_C3_6 * x * (xx - 3.0f * yy)) * sh[15 * 3];
+            }
+        }
+    }
+    return res;
+}
+
+// Tile rectangle of a projected Gaussian (upstream getRect; clamped to the tile grid).
+__device__ __forceinline__ void tile_rect(float ix, float iy, int r, int gx, int gy, int* r4)
+{
+    int v0 = (int)((ix - (float)r) / (float)kTile);
+    int v1 = (int)((iy - (float)r) / (float)kTile);
+    int v2 = (int)((ix + (float)r + (float)kTile - 1.0f) / (float)kTile);
+    int v3 = (int)((iy + (float)r + (float)kTile - 1.0f) / (float)kTile);
+    r4[0] = min(gx, max(0, v0));
+    r4[1] = min(gy, max(0, v1));
+    r4[2] = min(gx, max(0, v2));
+    r4[3] = min(gy, max(0, v3));
+}
+
+// Per-Gaussian record gathered by the render kernels (48 B = 3 x dwordx4).
+struct Record {
+    float4 a;  // x, y, conic.x, conic.y
+    float4 b;  // conic.z, opacity, r, g
+    float4 c;  // b, f0, f1, f2
+};
+
+}  // namespace lsr

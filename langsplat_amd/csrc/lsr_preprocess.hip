@@ -1,0 +1,409 @@
+// lsr_preprocess.hip -- per-Gaussian kernels: projection/culling/SH (forward) and the chain rule
+// back to means, SH, scales and rotations (backward).  One thread per Gaussian; HBM-streaming.
+//
+// Forward restates upstream FORWARD::preprocessCUDA; backward
+// restates computeCov2DCUDA + BACKWARD::preprocessCUDA (a12, a13, App. A.6).  Operation order
+// mirrors oracle/lsr_oracle.c (preprocess_one / preprocess_backward_one).
+#include "lsr_internal.h"
+
+namespace lsr {
+
+__global__ __launch_bounds__(256) void k_preprocess(PreprocessParams p)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= p.P) return;
+    p.radii[i] = 0;
+    p.tiles[i] = 0;
+    p.depth_key[i] = 0xFFFFFFFFu;
+    const float px = p.means[3 * i], py = p.means[3 * i + 1], pz = p.means[3 * i + 2];
+    const float3 pv = xform4x3(p.view, px, py, pz);
+    if (pv.z <= 0.2f) {
+        if (p.prefiltered) atomicOr(&p.counters[kCntError], 1u);
+        return;
+    }
+    const float3 hom = xform4x3(p.proj, px, py, pz);
+    const float hw = xform4w(p.proj, px, py, pz);
+    const float p_w = 1.0f / (hw + 0.0000001f);
+    const float proj_x = hom.x * p_w, proj_y = hom.y * p_w;
+
+    float cov_local[6];
+    const float* cov;
+    if (p.cov_pre) {
+        cov = p.cov_pre + 6 * (size_t)i;
+    } else {
+        const float4 q = *reinterpret_cast<const float4*>(p.rots + 4 * (size_t)i);
+        cov3d(p.scales[3 * i], p.scales[3 * i + 1], p.scales[3 * i + 2], p.scale_modifier, q, cov_local);
+        cov = cov_local;
+    }
+    const Cov2D cv = cov2d(px, py, pz, p.focal_x, p.focal_y, p.tanfovx, p.tanfovy, cov, p.view);
+    const float a = cv.a, b = cv.b, c = cv.c;
+    const float det = a * c - b * b;
+    if (det == 0.0f) return;
+    const float det_inv = 1.f / det;
+    const float cx = c * det_inv, cy = -b * det_inv, cz = a * det_inv;
+    const float mid = 0.5f * (a + c);
+    const float disc = fmaxf(0.1f, mid * mid - det);
+    const float sq = sqrtf(disc);
+    const float l1 = mid + sq, l2 = mid - sq;
+    const float my_radius = ceilf(3.f * sqrtf(fmaxf(l1, l2)));
+    const float ix = ndc2pix(proj_x, p.W), iy = ndc2pix(proj_y, p.H);
+    const int r = (int)my_radius;
+    int r4[4];
+    tile_rect(ix, iy, r, p.gx, p.gy, r4);
+    const uint32_t area = (uint32_t)((r4[2] - r4[0]) * (r4[3] - r4[1]));
+    if (area == 0) return;
+
+    float rgb[3];
+    uint32_t clamp_bits = 0;
+    if (p.shs) {
+        const float dox = px - p.campos[0], doy = py - p.campos[1], doz = pz - p.campos[2];
+        const float len = sqrtf(dot3(dox, doy, doz, dox, doy, doz));
+        const float x = dox / len, y = doy / len, z = doz / len;
+        const float* sh = p.shs + (size_t)i * p.M * 3;
+#pragma unroll
+        for (int ch = 0; ch < 3; ch++) {
+            const float v = sh_eval_channel(p.D, sh + ch, x, y, z) + 0.5f;
+            clamp_bits |= (v < 0.0f ? 1u : 0u) << ch;
+            rgb[ch] = fmaxf(v, 0.0f);
+        }
+    } else {
+        rgb[0] = p.colors[3 * i];
+        rgb[1] = p.colors[3 * i + 1];
+        rgb[2] = p.colors[3 * i + 2];
+    }
+    float f0 = 0.f, f1 = 0.f, f2 = 0.f;
+    if (p.include_feature && p.lang) {
+        f0 = p.lang[3 * i];
+        f1 = p.lang[3 * i + 1];
+        f2 = p.lang[3 * i + 2];
+    }
+    p.depth_key[i] = __float_as_uint(pv.z);
+    p.radii[i] = r;
+    p.tiles[i] = area;
+    p.rect[2 * i] = (uint32_t)r4[0] | ((uint32_t)r4[1] << 16);
+    p.rect[2 * i + 1] = (uint32_t)r4[2] | ((uint32_t)r4[3] << 16);
+    p.clamped[i] = clamp_bits;
+    float4* rec = p.record + 3 * (size_t)i;
+    rec[0] = make_float4(ix, iy, cx, cy);
+    rec[1] = make_float4(cz, p.opac[i], rgb[0], rgb[1]);
+    rec[2] = make_float4(rgb[2], f0, f1, f2);
+    atomicAdd(&p.counters[kCntVisible], 1u);
+}
+
+hipError_t launch_preprocess(const PreprocessParams& p, hipStream_t s)
+{
+    if (p.P == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_preprocess, dim3((p.P + 255) / 256), dim3(256), 0, s, p);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+// backward
+// ------------------------------------------------------------------------------------------
+
+__device__ __forceinline__ void dnormvdv(float vx, float vy, float vz, float dx, float dy, float dz,
+                                         float* out)
+{
+    const float sum2 = dot3(vx, vy, vz, vx, vy, vz);
+    const float invsum32 = 1.0f / sqrtf(sum2 * sum2 * sum2);
+    out[0] = ((sum2 - vx * vx) * dx - vy * vx * dy - vz * vx * dz) * invsum32;
+    out[1] = (-vx * vy * dx + (sum2 - vy * vy) * dy - vz * vy * dz) * invsum32;
+    out[2] = (-vx * vz * dx - vy * vz * dy + (sum2 - vz * vz) * dz) * invsum32;
+}
+
+// SH backward (lso_sh_backward): writes all M coefficients of dsh, returns dL/dmean via the
+// view direction.  drgb already masked by the clamp flags.
+__device__ void sh_backward(int deg, int M, const float* sh, float dox, float doy, float doz,
+                            const float* drgb, float* dsh, float* dmean)
+{
+    const float len = sqrtf(dot3(dox, doy, doz, dox, doy, doz));
+    const float x = dox / len, y = doy / len, z = doz / len;
+    float basis[16];
+    float dx[3] = {0.f, 0.f, 0.f}, dy[3] = {0.f, 0.f, 0.f}, dz[3] = {0.f, 0.f, 0.f};
+    const int K = (deg + 1) * (deg + 1);
+    basis[0] = SH_C0;
+    if (deg > 0) {
+        basis[1] = -SH_C1 * y;
+        basis[2] = SH_C1 * z;
+        basis[3] = -SH_C1 * x;
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            dx[c] = -SH_C1 * sh[3 * 3 + c];
+            dy[c] = -SH_C1 * sh[1 * 3 + c];
+            dz[c] = SH_C1 * sh[2 * 3 + c];
+        }
+        if (deg > 1) {
+            const float xx = x * x, yy = y * y, zz = z * z;
+            const float xy = x * y, yz = y * z, xz = x * z;
+            basis[4] = SH_C2_0 * xy;
+            basis[5] = SH_C2_1 * yz;
+            basis[6] = SH_C2_2 * (2.f * zz - xx - yy);
+            basis[7] = SH_C2_3 * xz;
+            basis[8] = SH_C2_4 * (xx - yy);
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+                const float* s = sh + c;
+                dx[c] = dx[c] + (SH_C2_0 * y * s[4 * 3] + SH_C2_2 * 2.f * -x * s[6 * 3] +
+                                 SH_C2_3 * z * s[7 * 3] + SH_C2_4 * 2.f * x * s[8 * 3]);
+                dy[c] = dy[c] + (SH_C2_0 * x * s[4 * 3] + SH_C2_1 * z * s[5 * 3] +
+                                 SH_C2_2 * 2.f * -y * s[6 * 3] + SH_C2_4 * 2.f * -y * s[8 * 3]);
+                dz[c] = dz[c] + (SH_C2_1 * y * s[5 * 3] + SH_C2_2 * 2.f * 2.f * z * s[6 * 3] +
+                                 SH_C2_3 * x * s[7 * 3]);
+            }
+            if (deg > 2) {
+                basis[9] = SH_C3_0 * y * (3.f * xx - yy);
+                basis[10] = SH_C3_1 * xy * z;
+                basis[11] = SH_C3_2 * y * (4.f * zz - xx - yy);
+                basis[12] = SH_C3_3 * z * (2.f * zz - 3.f * xx - 3.f * yy);
+                basis[13] = SH_C3_4 * x * (4.f * zz - xx - yy);
+                basis[14] = SH_C3_5 * z * (xx - yy);
+                basis[15] = SH_C3_6 * x * (xx - 3.f * yy);
+#pragma unroll
+                for (int c = 0; c < 3; c++) {
+                    const float* s = sh + c;
+                    dx[c] = dx[c] + (SH_C3_0 * s[9 * 3] * 3.f * 2.f * xy + SH_C3_1 * s[10 * 3] * yz +
+                                     SH_C3_2 * s[11 * 3] * -2.f * xy +
+                                     SH_C3_3 * s[12 * 3] * -3.f * 2.f * xz +
+                                     SH_C3_4 * s[13 * 3] * (-3.f * xx + 4.f * zz - yy) +
+                                     SH_C3_5 * s[14 * 3] * 2.f * xz +
+                                     SH_C3_6 * s[15 * 3] * 3.f * (xx - yy));
+                    dy[c] = dy[c] + (SH_C3_0 * s[9 * 3] * 3.f * (xx - yy) + SH_C3_1 * s[10 * 3] * xz +
+                                     SH_C3_2 * s[11 * 3] * (-3.f * yy + 4.f * zz - xx) +
+                                     SH_C3_3 * s[12 * 3] * -3.f * 2.f * yz +
+                                     SH_C3_4 * s[13 * 3] * -2.f * xy +
+                                     SH_C3_5 * s[14 * 3] * -2.f * yz +
+                                     SH_C3_6 * s[15 * 3] * -3.f * 2.f * xy);
+                    dz[c] = dz[c] + (SH_C3_1 * s[10 * 3] * xy + SH_C3_2 * s[11 * 3] * 4.f * 2.f * yz +
+                                     SH_C3_3 * s[12 * 3] * 3.f * (2.f * zz - xx - yy) +
+                                     SH_C3_4 * s[13 * 3] * 4.f * 2.f * xz +
+                                     SH_C3_5 * s[14 * 3] * (xx - yy));
+                }
+            }
+        }
+    }
+    for (int k = 0; k < M; k++) {
+        const float bk = k < K ? basis[k] : 0.0f;
+        const bool live = k < K;
+#pragma unroll
+        for (int c = 0; c < 3; c++) dsh[3 * k + c] = live ? bk * drgb[c] : 0.0f;
+    }
+    const float ddx = dot3(dx[0], dx[1], dx[2], drgb[0], drgb[1], drgb[2]);
+    const float ddy = dot3(dy[0], dy[1], dy[2], drgb[0], drgb[1], drgb[2]);
+    const float ddz = dot3(dz[0], dz[1], dz[2], drgb[0], drgb[1], drgb[2]);
+    dnormvdv(dox, doy, doz, ddx, ddy, ddz, dmean);
+}
+
+__device__ void cov3d_backward(float sx, float sy, float sz, float mod, float4 q, const float* dcov,
+                               float* dscale, float* drot)
+{
+    const Mat3 R = quat_to_rot(q.x, q.y, q.z, q.w);
+    const float s[3] = {mod * sx, mod * sy, mod * sz};
+    float M[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+        for (int k = 0; k < 3; k++) M[i][k] = R.m[i][k] * s[k];
+    const float D[3][3] = {{dcov[0], 0.5f * dcov[1], 0.5f * dcov[2]},
+                           {0.5f * dcov[1], dcov[3], 0.5f * dcov[4]},
+                           {0.5f * dcov[2], 0.5f * dcov[4], dcov[5]}};
+    float G[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+        for (int k = 0; k < 3; k++)
+            G[i][k] = 2.0f * fma_(D[i][2], M[2][k], fma_(D[i][1], M[1][k], D[i][0] * M[0][k]));
+#pragma unroll
+    for (int k = 0; k < 3; k++)
+        dscale[k] = fma_(G[2][k], R.m[2][k], fma_(G[1][k], R.m[1][k], G[0][k] * R.m[0][k]));
+    float dR[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+        for (int k = 0; k < 3; k++) dR[i][k] = G[i][k] * s[k];
+    const float r = q.x, x = q.y, y = q.z, z = q.w;
+    drot[0] = 2.f * z * (dR[1][0] - dR[0][1]) + 2.f * y * (dR[0][2] - dR[2][0]) +
+              2.f * x * (dR[2][1] - dR[1][2]);
+    drot[1] = 2.f * y * (dR[0][1] + dR[1][0]) + 2.f * z * (dR[0][2] + dR[2][0]) +
+              2.f * r * (dR[2][1] - dR[1][2]) - 4.f * x * (dR[2][2] + dR[1][1]);
+    drot[2] = 2.f * x * (dR[0][1] + dR[1][0]) + 2.f * r * (dR[0][2] - dR[2][0]) +
+              2.f * z * (dR[2][1] + dR[1][2]) - 4.f * y * (dR[2][2] + dR[0][0]);
+    drot[3] = 2.f * r * (dR[1][0] - dR[0][1]) + 2.f * x * (dR[0][2] + dR[2][0]) +
+              2.f * y * (dR[2][1] + dR[1][2]) - 4.f * z * (dR[1][1] + dR[0][0]);
+}
+
+__global__ __launch_bounds__(256) void k_preprocess_backward(PreprocessBwdParams p)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= p.P) return;
+    const size_t i3 = 3 * (size_t)i;
+    if (!(p.radii[i] > 0)) {
+        // culled: every output row is zero (upstream torch::zeros + skipped threads)
+        for (int k = 0; k < 3; k++) {
+            p.dmeans2D[i3 + k] = 0.f;
+            p.dcolors[i3 + k] = 0.f;
+            p.dlang[i3 + k] = 0.f;
+            p.dmeans3D[i3 + k] = 0.f;
+            if (p.dscales) p.dscales[i3 + k] = 0.f;
+        }
+        p.dopac[i] = 0.f;
+        if (p.drots) *reinterpret_cast<float4*>(p.drots + 4 * (size_t)i) = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (p.dcov)
+            for (int k = 0; k < 6; k++) p.dcov[6 * (size_t)i + k] = 0.f;
+        if (p.dsh)
+            for (int k = 0; k < 3 * p.M; k++) p.dsh[(size_t)i * 3 * p.M + k] = 0.f;
+        return;
+    }
+    const float4* g4 = reinterpret_cast<const float4*>(p.grad + (size_t)i * kGradStride);
+    const float4 ga = g4[0], gb = g4[1], gc = g4[2];
+    // record: [0] dx [1] dy [2] dconic.x [3] dconic.y [4] dconic.w [5] dopacity [6..8] drgb [9..11] dlang
+    const float dxy0 = ga.x, dxy1 = ga.y;
+    const float dcx = ga.z, dcy = ga.w, dcz = gb.x;
+    const float drgb_in[3] = {gb.z, gb.w, gc.x};
+    p.dmeans2D[i3] = dxy0;
+    p.dmeans2D[i3 + 1] = dxy1;
+    p.dmeans2D[i3 + 2] = 0.f;
+    p.dcolors[i3] = drgb_in[0];
+    p.dcolors[i3 + 1] = drgb_in[1];
+    p.dcolors[i3 + 2] = drgb_in[2];
+    p.dlang[i3] = gc.y;
+    p.dlang[i3 + 1] = gc.z;
+    p.dlang[i3 + 2] = gc.w;
+    p.dopac[i] = gb.y;
+
+    const float px = p.means[i3], py = p.means[i3 + 1], pz = p.means[i3 + 2];
+    float cov_local[6];
+    const float* cov;
+    float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (p.cov_pre) {
+        cov = p.cov_pre + 6 * (size_t)i;
+    } else {
+        q = *reinterpret_cast<const float4*>(p.rots + 4 * (size_t)i);
+        cov3d(p.scales[i3], p.scales[i3 + 1], p.scales[i3 + 2], p.scale_modifier, q, cov_local);
+        cov = cov_local;
+    }
+    const Cov2D cv = cov2d(px, py, pz, p.focal_x, p.focal_y, p.tanfovx, p.tanfovy, cov, p.view);
+    const float limx = 1.3f * p.tanfovx, limy = 1.3f * p.tanfovy;
+    const float x_grad_mul = (cv.txtz < -limx || cv.txtz > limx) ? 0.0f : 1.0f;
+    const float y_grad_mul = (cv.tytz < -limy || cv.tytz > limy) ? 0.0f : 1.0f;
+    const float a = cv.a, b = cv.b, c = cv.c;
+    const float denom = a * c - b * b;
+    float dL_da = 0.f, dL_db = 0.f, dL_dc = 0.f;
+    const float denom2inv = 1.0f / (denom * denom + 0.0000001f);
+    float dcov[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const float(&A)[2][3] = cv.A;
+    if (denom2inv != 0.0f) {
+        dL_da = denom2inv * (-c * c * dcx + 2.f * b * c * dcy + (denom - a * c) * dcz);
+        dL_dc = denom2inv * (-a * a * dcz + 2.f * a * b * dcy + (denom - a * c) * dcx);
+        dL_db = denom2inv * 2.f * (b * c * dcx - (denom + 2.f * b * b) * dcy + a * b * dcz);
+        dcov[0] = A[0][0] * A[0][0] * dL_da + A[0][0] * A[1][0] * dL_db + A[1][0] * A[1][0] * dL_dc;
+        dcov[3] = A[0][1] * A[0][1] * dL_da + A[0][1] * A[1][1] * dL_db + A[1][1] * A[1][1] * dL_dc;
+        dcov[5] = A[0][2] * A[0][2] * dL_da + A[0][2] * A[1][2] * dL_db + A[1][2] * A[1][2] * dL_dc;
+        dcov[1] = 2.f * A[0][0] * A[0][1] * dL_da + (A[0][0] * A[1][1] + A[0][1] * A[1][0]) * dL_db +
+                  2.f * A[1][0] * A[1][1] * dL_dc;
+        dcov[2] = 2.f * A[0][0] * A[0][2] * dL_da + (A[0][0] * A[1][2] + A[0][2] * A[1][0]) * dL_db +
+                  2.f * A[1][0] * A[1][2] * dL_dc;
+        dcov[4] = 2.f * A[0][2] * A[0][1] * dL_da + (A[0][1] * A[1][2] + A[0][2] * A[1][1]) * dL_db +
+                  2.f * A[1][1] * A[1][2] * dL_dc;
+    }
+    const float S[3][3] = {{cov[0], cov[1], cov[2]}, {cov[1], cov[3], cov[4]}, {cov[2], cov[4], cov[5]}};
+    float SA0[3], SA1[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        SA0[k] = dot3(A[0][0], A[0][1], A[0][2], S[k][0], S[k][1], S[k][2]);
+        SA1[k] = dot3(A[1][0], A[1][1], A[1][2], S[k][0], S[k][1], S[k][2]);
+    }
+    float dA0[3], dA1[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        dA0[k] = 2.f * SA0[k] * dL_da + SA1[k] * dL_db;
+        dA1[k] = 2.f * SA1[k] * dL_dc + SA0[k] * dL_db;
+    }
+    const float* v = p.view;
+    const float dJ00 = fma_(v[8], dA0[2], fma_(v[4], dA0[1], v[0] * dA0[0]));
+    const float dJ02 = fma_(v[10], dA0[2], fma_(v[6], dA0[1], v[2] * dA0[0]));
+    const float dJ11 = fma_(v[9], dA1[2], fma_(v[5], dA1[1], v[1] * dA1[0]));
+    const float dJ12 = fma_(v[10], dA1[2], fma_(v[6], dA1[1], v[2] * dA1[0]));
+    const float tz = 1.f / cv.t[2];
+    const float tz2 = tz * tz;
+    const float tz3 = tz2 * tz;
+    const float fx = p.focal_x, fy = p.focal_y;
+    const float dtx = x_grad_mul * -fx * tz2 * dJ02;
+    const float dty = y_grad_mul * -fy * tz2 * dJ12;
+    const float dtz = -fx * tz2 * dJ00 - fy * tz2 * dJ11 + (2.f * fx * cv.t[0]) * tz3 * dJ02 +
+                      (2.f * fy * cv.t[1]) * tz3 * dJ12;
+    float dmean[3];
+    dmean[0] = fma_(v[2], dtz, fma_(v[1], dty, v[0] * dtx));
+    dmean[1] = fma_(v[6], dtz, fma_(v[5], dty, v[4] * dtx));
+    dmean[2] = fma_(v[10], dtz, fma_(v[9], dty, v[8] * dtx));
+
+    const float* m = p.proj;
+    const float3 hom = xform4x3(m, px, py, pz);
+    const float hw = xform4w(m, px, py, pz);
+    const float m_w = 1.0f / (hw + 0.0000001f);
+    const float mul1 = hom.x * m_w * m_w;
+    const float mul2 = hom.y * m_w * m_w;
+    dmean[0] += (m[0] * m_w - m[3] * mul1) * dxy0 + (m[1] * m_w - m[3] * mul2) * dxy1;
+    dmean[1] += (m[4] * m_w - m[7] * mul1) * dxy0 + (m[5] * m_w - m[7] * mul2) * dxy1;
+    dmean[2] += (m[8] * m_w - m[11] * mul1) * dxy0 + (m[9] * m_w - m[11] * mul2) * dxy1;
+
+    if (p.shs) {
+        const uint32_t cb = p.clamped[i];
+        float drgb[3];
+#pragma unroll
+        for (int ch = 0; ch < 3; ch++) drgb[ch] = ((cb >> ch) & 1u) ? 0.0f : drgb_in[ch];
+        float dm_sh[3];
+        sh_backward(p.D, p.M, p.shs + (size_t)i * p.M * 3, px - p.campos[0], py - p.campos[1],
+                    pz - p.campos[2], drgb, p.dsh + (size_t)i * p.M * 3, dm_sh);
+        dmean[0] += dm_sh[0];
+        dmean[1] += dm_sh[1];
+        dmean[2] += dm_sh[2];
+    } else if (p.dsh) {
+        for (int k = 0; k < 3 * p.M; k++) p.dsh[(size_t)i * 3 * p.M + k] = 0.f;
+    }
+    p.dmeans3D[i3] = dmean[0];
+    p.dmeans3D[i3 + 1] = dmean[1];
+    p.dmeans3D[i3 + 2] = dmean[2];
+    if (p.dcov)
+        for (int k = 0; k < 6; k++) p.dcov[6 * (size_t)i + k] = dcov[k];
+    if (!p.cov_pre) {
+        float ds[3], dr[4];
+        cov3d_backward(p.scales[i3], p.scales[i3 + 1], p.scales[i3 + 2], p.scale_modifier, q, dcov, ds, dr);
+        if (p.dscales) {
+            p.dscales[i3] = ds[0];
+            p.dscales[i3 + 1] = ds[1];
+            p.dscales[i3 + 2] = ds[2];
+        }
+        if (p.drots) *reinterpret_cast<float4*>(p.drots + 4 * (size_t)i) = make_float4(dr[0], dr[1], dr[2], dr[3]);
+    } else {
+        if (p.dscales)
+            for (int k = 0; k < 3; k++) p.dscales[i3 + k] = 0.f;
+        if (p.drots) *reinterpret_cast<float4*>(p.drots + 4 * (size_t)i) = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+}
+
+hipError_t launch_preprocess_backward(const PreprocessBwdParams& p, hipStream_t s)
+{
+    if (p.P == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_preprocess_backward, dim3((p.P + 255) / 256), dim3(256), 0, s, p);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void k_mark_visible(int P, const float* means, const float* view,
+                                                      const float* proj, uint8_t* visible)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    const float3 pv = xform4x3(view, means[3 * i], means[3 * i + 1], means[3 * i + 2]);
+    (void)proj;
+    visible[i] = pv.z > 0.2f ? 1 : 0;
+}
+
+hipError_t launch_mark_visible(int P, const float* means, const float* view, const float* proj,
+                               uint8_t* visible, hipStream_t s)
+{
+    if (P == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_mark_visible, dim3((P + 255) / 256), dim3(256), 0, s, P, means, view, proj, visible);
+    return hipGetLastError();
+}
+
+}  // namespace lsr

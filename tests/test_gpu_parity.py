@@ -1,0 +1,282 @@
+"""HIP path (liblsr.so through the C ABI) vs the CPU oracle -- the parity gate.
+
+Forward: bit-exact (images, radii, per-tile ranges and Gaussian order, final T, contributor
+counts), because kernels and oracle evaluate the same IEEE operation sequence.
+Backward: the GPU sums per-Gaussian partials with float atomics in arbitrary order, the oracle in
+double; tolerance (north_star: 1e-4 relative) is |gpu - oracle| <= 1e-4 * (|oracle| + floor) with
+floor = 1e-2 * max|oracle| per tensor, i.e. relative error 1e-4 except near-zero entries.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from langsplat_amd import _native
+from langsplat_amd.rasterizer import GaussianRasterizer
+from oracle import oracle
+from tests.scenes import grad_seed, scene, settings_for, to_device
+from langsplat_amd.camera import look_at_origin, make_camera
+from langsplat_amd.synthetic import CONFIGS, activated_inputs, make_cameras, make_gaussians
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+GRAD_RTOL = 1e-4
+GRAD_FLOOR = 1e-2
+
+
+def native_forward(st, inp):
+    std, ind = to_device(st, inp, DEV)
+    out = _native.rasterize_gaussians(std, ind["means3D"], ind.get("shs"), ind.get("colors_precomp"),
+                                      ind.get("language_feature_precomp") if st.include_feature else None,
+                                      ind["opacities"], ind.get("scales"), ind.get("rotations"),
+                                      ind.get("cov3D_precomp"))
+    torch.cuda.synchronize()
+    return std, ind, out
+
+
+def state(out, P, W, H):
+    nr, color, lang, radii, geom, binning, image = out
+    lay = _native.state_layout(P, W, H, nr)
+    T = ((W + 15) // 16) * ((H + 15) // 16)
+
+    def u32(buf, off, n):
+        return buf[off:off + 4 * n].view(torch.int32).cpu().numpy().view(np.uint32)
+
+    return dict(
+        tile_start=u32(image, lay["tile_start"], T + 1),
+        point_list=u32(binning, lay["point_list"], nr),
+        final_T=image[lay["final_T"]:lay["final_T"] + 4 * W * H].view(torch.float32).cpu().numpy().reshape(H, W),
+        n_contrib=u32(image, lay["n_contrib"], W * H).reshape(H, W),
+        depth_key=u32(geom, lay["depth_key"], P),
+        counters=u32(image, lay["counters"], 16),
+    )
+
+
+def check_forward_exact(st, inp, run=None):
+    P = inp["means3D"].shape[0]
+    W, H = st.image_width, st.image_height
+    if run is None:
+        run = oracle.forward(st, **inp)
+    std, ind, out = native_forward(st, inp)
+    nr, color, lang, radii, geom, binning, image = out
+    assert nr == run.num_rendered
+    np.testing.assert_array_equal(radii.cpu().numpy(), run.radii)
+    np.testing.assert_array_equal(color.cpu().numpy(), run.color)
+    np.testing.assert_array_equal(lang.cpu().numpy(), run.language)
+    if P > 0:
+        s = state(out, P, W, H)
+        rg = run.get("ranges")
+        ts = s["tile_start"]
+        nonempty = rg[:, 1] > rg[:, 0]
+        np.testing.assert_array_equal(ts[:-1][nonempty], rg[nonempty, 0])
+        np.testing.assert_array_equal(ts[1:][nonempty], rg[nonempty, 1])
+        np.testing.assert_array_equal(s["point_list"], run.get("point_list"))
+        np.testing.assert_array_equal(s["final_T"], run.get("final_T"))
+        np.testing.assert_array_equal(s["n_contrib"], run.get("n_contrib"))
+    return run, std, ind, out
+
+
+def assert_grad_close(name, gpu, ref):
+    gpu = np.asarray(gpu, dtype=np.float64)
+    ref = np.asarray(ref, dtype=np.float64)
+    assert gpu.shape == ref.shape, name
+    floor = GRAD_FLOOR * (np.max(np.abs(ref)) if ref.size else 0.0) + 1e-30
+    bad = np.abs(gpu - ref) > GRAD_RTOL * (np.abs(ref) + floor)
+    if bad.any():
+        i = np.argmax(np.abs(gpu - ref) / (np.abs(ref) + floor))
+        raise AssertionError(f"{name}: {bad.sum()} / {bad.size} entries off; worst gpu={gpu.flat[i]} "
+                             f"ref={ref.flat[i]} floor={floor}")
+
+
+def check_backward(st, inp, run, out, seed=7):
+    W, H = st.image_width, st.image_height
+    gc, gl = grad_seed(H, W, seed=seed)
+    ref = run.backward(gc, gl if st.include_feature else None)
+    nr, color, lang, radii, geom, binning, image = out
+    std, ind = to_device(st, inp, DEV)
+    g = _native.rasterize_gaussians_backward(
+        std, ind["means3D"], ind.get("shs"), ind.get("colors_precomp"),
+        ind.get("language_feature_precomp") if st.include_feature else None, ind.get("scales"),
+        ind.get("rotations"), ind.get("cov3D_precomp"), radii, gc.to(DEV), gl.to(DEV) if st.include_feature else None,
+        nr, geom, binning, image)
+    torch.cuda.synchronize()
+    names = ["means2D", "colors_precomp", "opacities", "means3D"]
+    if st.include_feature:
+        names.append("language_feature_precomp")
+    if "shs" in inp:
+        names.append("shs")
+    if "cov3D_precomp" in inp:
+        names.append("cov3D_precomp")
+    else:
+        names += ["scales", "rotations"]
+    for n in names:
+        assert_grad_close(n, g[n].cpu().numpy(), ref[n])
+    return g, ref
+
+
+CASES = [
+    dict(P=300, W=64, H=48, seed=0, sh_degree=3),
+    dict(P=500, W=67, H=45, seed=1, sh_degree=2, bg=(0.2, 0.5, 0.9)),
+    dict(P=400, W=48, H=40, seed=2, sh_degree=1, include_feature=False),
+    dict(P=400, W=80, H=64, seed=3, sh_degree=0, scale_modifier=1.3),
+    dict(P=2000, W=128, H=96, seed=4, sh_degree=3, bg=(1.0, 1.0, 1.0)),
+]
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_forward_bit_exact_and_backward(case):
+    st, inp = scene(scale_range=(0.03, 0.2), **case)
+    run, std, ind, out = check_forward_exact(st, inp)
+    if case.get("scale_modifier", 1.0) == 1.0:
+        check_backward(st, inp, run, out)
+
+
+def test_colors_precomp_and_cov3d_precomp_paths():
+    st, inp = scene(P=400, W=64, H=48, seed=11, sh_degree=3, scale_range=(0.03, 0.2))
+    run0 = oracle.forward(st, **inp)
+    rgb = torch.tensor(run0.get("rgb"))
+    inp2 = dict(inp)
+    del inp2["shs"]
+    inp2["colors_precomp"] = rgb.clone()
+    cov = torch.tensor(oracle.cov3d(inp["scales"].numpy(), 1.0, inp["rotations"].numpy()))
+    del inp2["scales"], inp2["rotations"]
+    inp2["cov3D_precomp"] = cov
+    run, std, ind, out = check_forward_exact(st, inp2)
+    check_backward(st, inp2, run, out)
+
+
+def test_empty_and_fully_culled():
+    st, inp = scene(P=50, W=32, H=32, seed=0)
+    empty = {k: v[:0] for k, v in inp.items()}
+    st_bg = st._replace(bg=torch.tensor([0.3, 0.3, 0.3]))
+    check_forward_exact(st_bg, empty)
+    culled = dict(inp)
+    culled["means3D"] = inp["means3D"] * 0.01 + torch.tensor([0.0, 0.0, -3.9])  # behind the near plane
+    run, std, ind, out = check_forward_exact(st_bg, culled)
+    assert out[0] == 0
+    np.testing.assert_array_equal(out[1].cpu().numpy(), np.broadcast_to(np.float32(0.3), (3, 32, 32)))
+
+
+def test_oversized_tile_uses_bitmap_path():
+    """> 8192 instances in one tile exercises the LDS-bitmap ordering path."""
+    P = 12000
+    g = torch.Generator().manual_seed(9)
+    W = H = 32
+    cam = make_cameras(1, W, H)[0]
+    st = settings_for(cam, sh_degree=0)
+    inp = dict(means3D=(torch.rand((P, 3), generator=g) - 0.5) * 0.05,
+               opacities=torch.rand((P, 1), generator=g) * 0.05 + 0.004,
+               colors_precomp=torch.rand((P, 3), generator=g),
+               language_feature_precomp=torch.nn.functional.normalize(torch.randn((P, 3), generator=g)),
+               scales=torch.full((P, 3), 0.01), rotations=torch.tensor([[1.0, 0.0, 0.0, 0.0]]).repeat(P, 1))
+    run, std, ind, out = check_forward_exact(st, inp)
+    s = state(out, P, W, H)
+    assert s["counters"][3] >= 1  # oversize tiles were present
+    check_backward(st, inp, run, out)
+
+
+def test_large_gaussian_covering_all_tiles():
+    W, H = 100, 70
+    cam = make_cameras(1, W, H)[0]
+    st = settings_for(cam, sh_degree=0, bg=(0.1, 0.2, 0.3))
+    inp = dict(means3D=torch.tensor([[0.0, 0.0, 0.0], [0.1, 0.1, 0.5]]), opacities=torch.tensor([[0.7], [0.5]]),
+               colors_precomp=torch.tensor([[1.0, 0.0, 0.0], [0.0, 1.0, 0.0]]),
+               language_feature_precomp=torch.tensor([[0.0, 1.0, 0.0], [1.0, 0.0, 0.0]]),
+               scales=torch.tensor([[3.0, 3.0, 3.0], [0.1, 0.2, 0.3]]),
+               rotations=torch.nn.functional.normalize(torch.tensor([[1.0, 0.0, 0.0, 0.0], [0.3, 0.2, 0.1, 0.9]])))
+    run, std, ind, out = check_forward_exact(st, inp)
+    check_backward(st, inp, run, out)
+
+
+def test_c1_config_parity():
+    """BASELINE.json configs[0]: 10k Gaussians, 400x300, 3-ch language feature."""
+    c = CONFIGS["C1"]
+    g = make_gaussians(c["P"], seed=0)
+    cam = make_cameras(1, c["width"], c["height"])[0]
+    st = settings_for(cam, sh_degree=3)
+    with torch.no_grad():
+        inp = {k: v.contiguous() for k, v in activated_inputs(g).items()}
+    run, std, ind, out = check_forward_exact(st, inp)
+    check_backward(st, inp, run, out)
+
+
+def test_autograd_api_end_to_end():
+    """GaussianRasterizer + torch.autograd (the render() path) reproduce the oracle gradients,
+    including the means2D sink and needs_input_grad handling."""
+    st, inp = scene(P=600, W=64, H=48, seed=21, scale_range=(0.03, 0.2))
+    run = oracle.forward(st, **inp)
+    gc, gl = grad_seed(48, 64, seed=3)
+    ref = run.backward(gc, gl)
+    std, ind = to_device(st, inp, DEV)
+    leaves = {k: v.clone().requires_grad_(True) for k, v in ind.items()}
+    means2D = torch.zeros_like(leaves["means3D"], requires_grad=True)
+    rast = GaussianRasterizer(std)
+    color, lang, radii = rast(means3D=leaves["means3D"], means2D=means2D, opacities=leaves["opacities"],
+                              shs=leaves["shs"], language_feature_precomp=leaves["language_feature_precomp"],
+                              scales=leaves["scales"], rotations=leaves["rotations"])
+    np.testing.assert_array_equal(color.detach().cpu().numpy(), run.color)
+    np.testing.assert_array_equal(lang.detach().cpu().numpy(), run.language)
+    ((color * gc.to(DEV)).sum() + (lang * gl.to(DEV)).sum()).backward()
+    assert_grad_close("means2D", means2D.grad.cpu().numpy(), ref["means2D"])
+    for k in ("means3D", "opacities", "shs", "scales", "rotations", "language_feature_precomp"):
+        assert_grad_close(k, leaves[k].grad.cpu().numpy(), ref[k])
+    vis = rast.markVisible(ind["means3D"]).cpu().numpy()
+    assert vis.dtype == bool and vis.shape == (600,)
+
+
+def test_forward_is_deterministic():
+    st, inp = scene(P=3000, W=160, H=120, seed=5, scale_range=(0.03, 0.2))
+    _, _, out1 = native_forward(st, inp)
+    _, _, out2 = native_forward(st, inp)
+    for a, b in zip(out1[1:4], out2[1:4]):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("cfg", ["C2", "C3"])
+def test_full_size_properties(cfg):
+    """BASELINE.json full sizes: per-tile lists sorted by (depth, id), instance accounting, and the
+    backward is linear in the upstream gradient (size-independent properties)."""
+    c = CONFIGS[cfg]
+    g = make_gaussians(c["P"], seed=0)
+    cam = make_cameras(1, c["width"], c["height"])[0]
+    st = settings_for(cam, sh_degree=3)
+    with torch.no_grad():
+        inp = {k: v.contiguous() for k, v in activated_inputs(g).items()}
+    std, ind, out = native_forward(st, inp)
+    nr, color, lang, radii, geom, binning, image = out
+    P, W, H = c["P"], c["width"], c["height"]
+    s = state(out, P, W, H)
+    assert s["counters"][1] == nr and s["tile_start"][-1] == nr
+    # sortedness within every tile: (depth key, id) ascending
+    pl = s["point_list"].astype(np.int64)
+    dk = s["depth_key"].astype(np.int64)
+    key = dk[pl] * (1 << 32) + pl
+    ts = s["tile_start"].astype(np.int64)
+    tile_of = np.repeat(np.arange(len(ts) - 1), np.diff(ts))
+    same = tile_of[1:] == tile_of[:-1]
+    assert np.all(key[1:][same] > key[:-1][same])
+    # every visible Gaussian appears exactly tiles_touched times
+    counts = np.bincount(pl, minlength=P)
+    rad = radii.cpu().numpy()
+    assert np.all((counts > 0) == (rad > 0))
+    # determinism of the full-size forward
+    _, _, out2 = native_forward(st, inp)
+    assert torch.equal(out2[1], color) and torch.equal(out2[2], lang)
+    # linearity of the backward in (dL/dcolor, dL/dlang)
+    g1 = grad_seed(H, W, seed=1, scale=1.0 / (3 * H * W))
+    g2 = grad_seed(H, W, seed=2, scale=1.0 / (3 * H * W))
+    args = (ind["means3D"], ind["shs"], None, ind["language_feature_precomp"], ind["scales"], ind["rotations"],
+            None, radii)
+
+    def bwd(gcol, glang):
+        return _native.rasterize_gaussians_backward(std, *args, gcol.to(DEV), glang.to(DEV), nr, geom, binning,
+                                                    image)
+    ga, gb = bwd(*g1), bwd(*g2)
+    gab = bwd(g1[0] + g2[0], g1[1] + g2[1])
+    for k in ("means2D", "opacities", "language_feature_precomp", "colors_precomp"):
+        lhs = gab[k].double()
+        rhs = ga[k].double() + gb[k].double()
+        scale = rhs.abs().max().item() + 1e-30
+        assert (lhs - rhs).abs().max().item() <= 1e-3 * scale, k

@@ -1,0 +1,98 @@
+"""C-ABI library: loads without a GPU, exports every entry point include/lsr.h declares, and its
+Python front-end enforces the reference's API contract (gaussian_renderer/__init__.py:37-105)."""
+import os
+import re
+
+import pytest
+import torch
+
+from langsplat_amd import _native
+from langsplat_amd.rasterizer import GaussianRasterizationSettings, GaussianRasterizer
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared_functions():
+    src = open(os.path.join(ROOT, "include", "lsr.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(lsr_\w+)\s*\(", src, flags=re.M)
+    return sorted(set(names))
+
+
+def test_header_declares_expected_entry_points():
+    names = _declared_functions()
+    for n in ("lsr_forward", "lsr_backward", "lsr_mark_visible", "lsr_last_error", "lsr_abi_version"):
+        assert n in names
+
+
+def test_library_loads_and_exports_every_declared_symbol():
+    lib = _native.load()
+    for name in _declared_functions():
+        assert hasattr(lib, name), name
+        assert name in _native.SIGNATURES, f"ctypes binding misses {name}"
+    assert lib.lsr_abi_version() == 1
+
+
+def test_sizes_and_layout_are_consistent():
+    lib = _native.load()
+    P, W, H, R = 1000, 100, 70, 12345
+    lay = _native.state_layout(P, W, H, R)
+    assert lay["record"] % 16 == 0 and lay["record"] + 48 * P <= lib.lsr_geom_bytes(P)
+    assert lay["n_contrib"] + 4 * W * H <= lib.lsr_image_bytes(W, H)
+    assert lay["point_list"] + 4 * R <= lib.lsr_binning_bytes(R)
+    assert lib.lsr_backward_bytes(P) == 64 * P
+    assert lib.lsr_geom_bytes(2 * P) > lib.lsr_geom_bytes(P)
+
+
+def test_invalid_arguments_report_errors_without_gpu():
+    lib = _native.load()
+    assert lib.lsr_state_layout_of(-1, 10, 10, 0, None) != 0
+    assert "invalid" in _native.last_error()
+    assert lib.lsr_mark_visible(-5, None, None, None, None, None) != 0
+
+
+def _settings(device="cpu", include_feature=True):
+    return GaussianRasterizationSettings(
+        image_height=8, image_width=8, tanfovx=0.5, tanfovy=0.5, bg=torch.zeros(3, device=device),
+        scale_modifier=1.0, viewmatrix=torch.eye(4, device=device), projmatrix=torch.eye(4, device=device),
+        sh_degree=0, campos=torch.zeros(3, device=device), prefiltered=False, debug=False,
+        include_feature=include_feature)
+
+
+def test_settings_namedtuple_has_the_13_reference_fields():
+    s = _settings()
+    assert GaussianRasterizationSettings._fields == (
+        "image_height", "image_width", "tanfovx", "tanfovy", "bg", "scale_modifier", "viewmatrix", "projmatrix",
+        "sh_degree", "campos", "prefiltered", "debug", "include_feature")
+    assert s.include_feature is True
+
+
+def test_exactly_one_of_validation():
+    r = GaussianRasterizer(_settings())
+    m = torch.zeros((4, 3))
+    o = torch.ones((4, 1))
+    with pytest.raises(Exception, match="exactly one of either SHs|excatly one of either SHs"):
+        r(means3D=m, means2D=m, opacities=o, scales=m, rotations=torch.zeros((4, 4)))
+    with pytest.raises(Exception, match="SHs or precomputed colors"):
+        r(means3D=m, means2D=m, opacities=o, shs=torch.zeros((4, 1, 3)), colors_precomp=m, scales=m,
+          rotations=torch.zeros((4, 4)))
+    with pytest.raises(Exception, match="scale/rotation pair or precomputed 3D covariance"):
+        r(means3D=m, means2D=m, opacities=o, colors_precomp=m)
+    with pytest.raises(Exception, match="scale/rotation pair or precomputed 3D covariance"):
+        r(means3D=m, means2D=m, opacities=o, colors_precomp=m, scales=m, rotations=torch.zeros((4, 4)),
+          cov3D_precomp=torch.zeros((4, 6)))
+
+
+def test_cpu_tensors_are_rejected_loudly():
+    """No silent CPU fallback in the product path."""
+    r = GaussianRasterizer(_settings())
+    m = torch.zeros((4, 3))
+    with pytest.raises(RuntimeError, match="ROCm GPU"):
+        r(means3D=m, means2D=m, opacities=torch.ones((4, 1)), colors_precomp=m, scales=m,
+          rotations=torch.zeros((4, 4)))
+
+
+def test_drop_in_module_name():
+    import diff_gaussian_rasterization as dgr
+    assert dgr.GaussianRasterizer is GaussianRasterizer
+    assert dgr.GaussianRasterizationSettings is GaussianRasterizationSettings
