@@ -140,15 +140,15 @@ typedef struct lsr_state_layout {
     size_t record;         /* float4[3P] {x, y, conic.x, conic.y}{conic.z, opacity, r, g}{b, f0, f1, f2} */
     size_t clamped;        /* uint32[P]  bit c = SH colour channel c clamped */
     size_t sorted_ids;     /* uint32[P]  Gaussians by (depth, id); visible ones first */
-    size_t depth_rank;     /* uint32[P]  inverse of sorted_ids for visible Gaussians */
+    size_t inst_offset;    /* uint32[P]  first tile instance of the Gaussian of depth rank r */
     /* image buffer */
-    size_t counters;       /* uint32[16] {visible, num_rendered, error, n_oversize, ...} */
-    size_t tile_start;     /* uint32[T+1] exclusive scan of per-tile counts */
+    size_t counters;       /* uint32[16] {visible, num_rendered, error, ...} */
+    size_t ranges;         /* uint32[2T] [start, end) of each tile in point_list */
     size_t final_T;        /* float[H*W] */
     size_t n_contrib;      /* uint32[H*W] */
     /* binning buffer */
-    size_t point_list;     /* uint32[num_rendered] Gaussian ids, tile-major, depth order */
-    size_t list_rank;      /* uint32[num_rendered] unsorted depth ranks (emit order) */
+    size_t point_list;     /* uint32[num_rendered] Gaussian ids, tile-major, (depth, id) order */
+    size_t list_keys;      /* uint32[num_rendered] tile id of each point_list entry */
 } lsr_state_layout;
 
 int32_t lsr_abi_version(void);

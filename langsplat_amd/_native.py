@@ -60,8 +60,8 @@ class LsrBackwardArgs(ctypes.Structure):
 
 class LsrStateLayout(ctypes.Structure):
     _fields_ = [(n, ctypes.c_size_t) for n in (
-        "depth_key", "tiles_touched", "rect", "record", "clamped", "sorted_ids", "depth_rank",
-        "counters", "tile_start", "final_T", "n_contrib", "point_list", "list_rank")]
+        "depth_key", "tiles_touched", "rect", "record", "clamped", "sorted_ids", "inst_offset",
+        "counters", "ranges", "final_T", "n_contrib", "point_list", "list_keys")]
 
 
 class LsrKernelStat(ctypes.Structure):

@@ -130,13 +130,13 @@ int32_t lsr_state_layout_of(int32_t P, int32_t width, int32_t height, int64_t nu
     out->record = L.record;
     out->clamped = L.clamped;
     out->sorted_ids = L.sorted_ids;
-    out->depth_rank = L.depth_rank;
+    out->inst_offset = L.inst_offset;
     out->counters = L.counters;
-    out->tile_start = L.tile_start;
+    out->ranges = L.ranges;
     out->final_T = L.final_T;
     out->n_contrib = L.n_contrib;
     out->point_list = L.point_list;
-    out->list_rank = L.list_rank;
+    out->list_keys = L.list_keys;
     return LSR_OK;
 }
 
@@ -210,9 +210,7 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
     pp.record = reinterpret_cast<float4*>(geom + L.record);
     pp.counters = counters;
     LSR_TRY(launch_preprocess(pp, stream), "preprocess");
-    LSR_TRY(launch_depth_sort(P, L, geom, counters, stream, debug), "depth sort");
-    LSR_TRY(launch_tile_count(P, L, geom, image, stream), "tile count");
-    LSR_TRY(launch_tile_scan(L, image, stream), "tile scan");
+    LSR_TRY(launch_depth_order(P, L, geom, counters, stream, debug), "depth order");
 
     // the one host synchronisation: visible count, num_rendered, error flag
     uint32_t host_cnt[4] = {0, 0, 0, 0};
@@ -226,17 +224,14 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
     L = make_layout(P, W, H, R);
     char* binning = static_cast<char*>(alloc(user, LSR_BUF_BINNING, L.binning_bytes));
     if (!binning) return fail(LSR_ERR_ALLOC, "lsr_forward: binning buffer allocation failed");
-    if (R > 0) {
-        LSR_TRY(launch_emit(P, L, geom, image, binning, stream), "emit");
-        LSR_TRY(launch_tile_sort(L, geom, image, binning, stream, debug), "tile sort");
-    }
+    LSR_TRY(launch_binning(P, R, L, geom, image, binning, stream, debug), "binning");
     RenderParams rp{};
     rp.W = W;
     rp.H = H;
     rp.gx = L.gx;
     rp.gy = L.gy;
     rp.include_feature = (s->include_feature && a->language_feature) ? 1 : 0;
-    rp.tile_start = reinterpret_cast<const uint32_t*>(image + L.tile_start);
+    rp.ranges = reinterpret_cast<const uint2*>(image + L.ranges);
     rp.point_list = reinterpret_cast<const uint32_t*>(binning + L.point_list);
     rp.record = reinterpret_cast<const float4*>(geom + L.record);
     rp.bg = s->bg;
@@ -277,7 +272,7 @@ int32_t lsr_backward(const lsr_settings* s, const lsr_backward_args* a, lsr_allo
     rp.gx = L.gx;
     rp.gy = L.gy;
     rp.include_feature = (s->include_feature && a->language_feature) ? 1 : 0;
-    rp.tile_start = reinterpret_cast<const uint32_t*>(image + L.tile_start);
+    rp.ranges = reinterpret_cast<const uint2*>(image + L.ranges);
     rp.point_list = reinterpret_cast<const uint32_t*>(binning + L.point_list);
     rp.record = reinterpret_cast<const float4*>(geom + L.record);
     rp.bg = s->bg;

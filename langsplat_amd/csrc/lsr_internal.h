@@ -15,30 +15,28 @@ enum Counter : int {
     kCntVisible = 0,
     kCntRendered = 1,
     kCntError = 2,
-    kCntOversize = 3,
     kCntSlots = 16
 };
 
 constexpr int kRadixThreads = 256;
 constexpr int kRadixItems = 16;
 constexpr int kRadixTile = kRadixThreads * kRadixItems;  // keys per block per pass
-constexpr int kTileSortCap = 8192;                       // LDS bitonic capacity (32 KB)
-constexpr int kBigSortThreads = 1024;
-constexpr int kBitmapWords = 32768;                      // 1 Mi ranks per LDS window (128 KB)
 constexpr int kGradStride = 16;                          // floats per Gaussian grad record
 
+size_t radix_hist_words(int64_t n);   // per-block digit histograms for n keys
+size_t scan_scratch_words(int64_t n); // block sums of a multi-block scan of n words
+
 struct Layout {
-    // geometry
-    size_t depth_key, tiles_touched, rect, record, clamped, sorted_ids, depth_rank;
-    size_t keys_a, keys_b, vals_b, radix_hist;
+    // geometry (per Gaussian)
+    size_t depth_key, tiles_touched, rect, record, clamped, sorted_ids, inst_offset;
+    size_t keys_a, keys_b, vals_b, radix_hist, scan_scratch;
     size_t geom_bytes;
-    // image
-    size_t counters, tile_start, tile_cursor, oversize, final_T, n_contrib;
+    // image (per pixel / tile)
+    size_t counters, ranges, final_T, n_contrib;
     size_t image_bytes;
-    // binning
-    size_t point_list, list_rank;
+    // binning (per tile instance)
+    size_t list_keys, point_list, alt_keys, alt_vals, bin_radix_hist, bin_scan_scratch;
     size_t binning_bytes;
-    int radix_blocks;
     int gx, gy, tiles;
 };
 
@@ -50,18 +48,20 @@ inline Layout make_layout(int P, int W, int H, int64_t R)
     size_t o = 0;
     auto take = [&](size_t bytes) { size_t r = o; o = align_up(o + bytes); return r; };
     const size_t p = (size_t)(P > 0 ? P : 1);
-    L.radix_blocks = (int)((p + kRadixTile - 1) / kRadixTile);
     L.depth_key = take(4 * p);
     L.tiles_touched = take(4 * p);
     L.rect = take(8 * p);
     L.record = take(48 * p);
     L.clamped = take(4 * p);
     L.sorted_ids = take(4 * p);
-    L.depth_rank = take(4 * p);
+    L.inst_offset = take(4 * (p + 1));
     L.keys_a = take(4 * p);
     L.keys_b = take(4 * p);
     L.vals_b = take(4 * p);
-    L.radix_hist = take(4 * 256 * (size_t)L.radix_blocks);
+    const size_t hw_p = radix_hist_words((int64_t)p);
+    L.radix_hist = take(4 * hw_p);
+    const size_t sw_p = scan_scratch_words((int64_t)(hw_p > p ? hw_p : p));
+    L.scan_scratch = take(4 * sw_p);
     L.geom_bytes = o;
 
     L.gx = (W + kTile - 1) / kTile;
@@ -71,17 +71,20 @@ inline Layout make_layout(int P, int W, int H, int64_t R)
     const size_t HW = (size_t)W * (size_t)H;
     o = 0;
     L.counters = take(4 * kCntSlots);
-    L.tile_start = take(4 * (T + 1));
-    L.tile_cursor = take(4 * T);
-    L.oversize = take(4 * T);
+    L.ranges = take(8 * T);
     L.final_T = take(4 * (HW > 0 ? HW : 1));
     L.n_contrib = take(4 * (HW > 0 ? HW : 1));
     L.image_bytes = o;
 
     o = 0;
     const size_t r = (size_t)(R > 0 ? R : 1);
+    L.list_keys = take(4 * r);
     L.point_list = take(4 * r);
-    L.list_rank = take(4 * r);
+    L.alt_keys = take(4 * r);
+    L.alt_vals = take(4 * r);
+    const size_t hw_r = radix_hist_words((int64_t)r);
+    L.bin_radix_hist = take(4 * hw_r);
+    L.bin_scan_scratch = take(4 * scan_scratch_words((int64_t)hw_r));
     L.binning_bytes = o;
     return L;
 }
@@ -109,7 +112,7 @@ struct PreprocessBwdParams {
 
 struct RenderParams {
     int W, H, gx, gy, include_feature;
-    const uint32_t* tile_start;
+    const uint2* ranges;
     const uint32_t* point_list;
     const float4* record;
     const float* bg;
@@ -126,14 +129,13 @@ hipError_t launch_preprocess_backward(const PreprocessBwdParams& p, hipStream_t 
 hipError_t launch_mark_visible(int P, const float* means, const float* view, const float* proj,
                                uint8_t* visible, hipStream_t s);
 
-// depth sort of all P Gaussians by (depth key, id) -> sorted_ids; and depth_rank inverse
-hipError_t launch_depth_sort(int P, const Layout& L, char* geom, uint32_t* counters, hipStream_t s,
-                             bool debug);
-hipError_t launch_tile_count(int P, const Layout& L, char* geom, char* image, hipStream_t s);
-hipError_t launch_tile_scan(const Layout& L, char* image, hipStream_t s);
-hipError_t launch_emit(int P, const Layout& L, char* geom, char* image, char* binning, hipStream_t s);
-hipError_t launch_tile_sort(const Layout& L, char* geom, char* image, char* binning, hipStream_t s,
-                            bool debug);
+// depth sort of all P Gaussians by (depth key, id) -> sorted_ids; per-Gaussian instance offsets in
+// that order; counters[kCntRendered] = number of tile instances
+hipError_t launch_depth_order(int P, const Layout& L, char* geom, uint32_t* counters, hipStream_t s,
+                              bool debug);
+// emit instances in depth order, stable sort on tile bits -> point_list; tile ranges
+hipError_t launch_binning(int P, int64_t R, const Layout& L, char* geom, char* image, char* binning,
+                          hipStream_t s, bool debug);
 
 hipError_t launch_render_forward(const RenderParams& p, int tiles, hipStream_t s);
 hipError_t launch_render_backward(const RenderParams& p, int tiles, hipStream_t s);

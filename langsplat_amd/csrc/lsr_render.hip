@@ -9,10 +9,10 @@
 //
 // Backward gradient scatter: every lane of a wave visits the same list entry at the same
 // iteration, so the 12 per-Gaussian partials of a wave are reduced in registers by a
-// reduce-scatter (16 values over 64 lanes in 6 shuffle steps) and written with ONE
-// 12-lane atomic instruction into a 64-byte-aligned per-Gaussian record -- instead of the
-// upstream 12 scattered atomics per pixel per blend.  Entries no lane contributes to are
-// skipped by a ballot.
+// reduce-scatter (permlane32/16 swaps + DPP mirrors, ~35 VALU ops), the 4 waves' results are summed
+// in LDS (ds_add_f32), and after each batch ONE 12-lane atomic instruction per (tile, Gaussian)
+// adds the tile's total into a 64-byte-aligned per-Gaussian record -- instead of the upstream 12
+// scattered atomics per pixel per blend.  Entries no lane contributes to are skipped by a ballot.
 #include "lsr_internal.h"
 
 namespace lsr {
@@ -30,7 +30,8 @@ __global__ __launch_bounds__(kTilePixels) void k_render_forward(RenderParams p)
     const int px = tx * kTile + (t & (kTile - 1)), py = ty * kTile + (t >> 4);
     const bool inside = px < p.W && py < p.H;
     const float pfx = (float)px, pfy = (float)py;
-    const uint32_t start = p.tile_start[tile], end = p.tile_start[tile + 1];
+    const uint2 range = p.ranges[tile];
+    const uint32_t start = range.x, end = range.y;
     const bool feat = p.include_feature != 0;
 
     float T = 1.0f;
@@ -107,27 +108,54 @@ hipError_t launch_render_forward(const RenderParams& p, int tiles, hipStream_t s
 // backward
 // ------------------------------------------------------------------------------------------
 
-// Reduce-scatter of 16 per-lane values over the wave: afterwards lane l holds the wave total of
-// value index vidx(l) = bitrev4(l >> 2) (every 4 consecutive lanes hold the same value).
-__device__ __forceinline__ float wave_reduce_scatter16(float (&v)[16])
+// Cross-lane helpers for the wave64 reduce-scatter (gfx950).
+//   swap32/16: v_permlane{32,16}_swap exchanges half-waves / odd-even rows, so for a value pair
+//   (lo, hi) the sum of the two results is lo+lo' on the lanes that keep `lo` and hi+hi' on the
+//   lanes that keep `hi` -- one exchange and one add per pair, no selects;
+//   mirror: DPP row_mirror / row_half_mirror pair the lower and upper 8 / 4 lanes of a row.
+__device__ __forceinline__ float swap32_add(float lo, float hi)
 {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int step = 0; step < 4; step++) {
-        const int d = 32 >> step;   // 32, 16, 8, 4
-        const int half = 8 >> step; // values kept after this step
-        const bool upper = (lane & d) != 0;
-#pragma unroll
-        for (int k = 0; k < half; k++) {
-            const float send = upper ? v[k] : v[k + half];
-            const float keep = upper ? v[k + half] : v[k];
-            v[k] = keep + __shfl_xor(send, d, 64);
-        }
-    }
-    float x = v[0];
-    x += __shfl_xor(x, 2, 64);
-    x += __shfl_xor(x, 1, 64);
-    return x;
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(lo), __float_as_uint(hi), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+__device__ __forceinline__ float swap16_add(float lo, float hi)
+{
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(lo), __float_as_uint(hi), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+template <int kCtrl>
+__device__ __forceinline__ float dpp(float x)
+{
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), kCtrl, 0xF, 0xF, true));
+}
+
+template <int kCtrl>
+__device__ __forceinline__ float mirror_add(float lo, float hi, bool upper)
+{
+    const float send = upper ? lo : hi;
+    const float keep = upper ? hi : lo;
+    return keep + dpp<kCtrl>(send);
+}
+
+// Reduce-scatter of 12 per-lane values (slots 12..15 implicit zeros) over the wave: afterwards
+// lane l holds the wave total of value index bitrev(l>>2) (4 consecutive lanes hold the same one).
+__device__ __forceinline__ float wave_reduce_scatter12(const float (&v)[12], int lane)
+{
+    const float r0 = swap32_add(v[0], v[8]), r1 = swap32_add(v[1], v[9]);
+    const float r2 = swap32_add(v[2], v[10]), r3 = swap32_add(v[3], v[11]);
+    const float r4 = swap32_add(v[4], 0.0f), r5 = swap32_add(v[5], 0.0f);
+    const float r6 = swap32_add(v[6], 0.0f), r7 = swap32_add(v[7], 0.0f);
+    const float s0 = swap16_add(r0, r4), s1 = swap16_add(r1, r5);
+    const float s2 = swap16_add(r2, r6), s3 = swap16_add(r3, r7);
+    const bool u8 = (lane & 8) != 0, u4 = (lane & 4) != 0;
+    const float t0 = mirror_add<0x140>(s0, s2, u8);  // row_mirror
+    const float t1 = mirror_add<0x140>(s1, s3, u8);
+    float w = mirror_add<0x141>(t0, t1, u4);         // row_half_mirror
+    w += dpp<0x4E>(w);                               // quad_perm [2,3,0,1]
+    w += dpp<0xB1>(w);                               // quad_perm [1,0,3,2]
+    return w;
 }
 
 __device__ __forceinline__ int scatter_index(int lane)
@@ -143,6 +171,7 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
     __shared__ float4 sC[kTilePixels];  // r, g, b, f0
     __shared__ float2 sD[kTilePixels];  // f1, f2
     __shared__ uint32_t sId[kTilePixels];
+    __shared__ float sG[kTilePixels * 12];  // per-entry gradient sums of the tile (12 floats)
     __shared__ uint32_t s_max;
 
     const int tile = blockIdx.x;
@@ -153,7 +182,7 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
     const float pfx = (float)px, pfy = (float)py;
     const size_t HW = (size_t)p.W * p.H;
     const size_t pix = (size_t)py * p.W + px;
-    const uint32_t start = p.tile_start[tile];
+    const uint32_t start = p.ranges[tile].x;
     const bool feat = p.include_feature != 0;
 
     const float T_final = inside ? p.final_T[pix] : 0.0f;
@@ -202,13 +231,15 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
             sD[t] = make_float2(c.z, c.w);
             sId[t] = g;
         }
+#pragma unroll
+        for (int q = 0; q < 12; q++) sG[q * kTilePixels + t] = 0.f;
         __syncthreads();
         const int cnt = min(kTilePixels, maxl - done_cnt);
         for (int j = 0; j < cnt; j++) {
             const int kk = maxl - 1 - (done_cnt + j);  // list index of this entry
-            float v[16];
+            float v[12];
 #pragma unroll
-            for (int q = 0; q < 16; q++) v[q] = 0.f;
+            for (int q = 0; q < 12; q++) v[q] = 0.f;
             bool hit = false;
             if (kk < (int)last) {
                 const float4 A = sA[j];
@@ -271,9 +302,17 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
                 }
             }
             if (__ballot(hit) == 0ull) continue;  // wave-uniform skip
-            const float tot = wave_reduce_scatter16(v);
-            if ((lane & 3) == 0 && vidx < 12)
-                atomicAdd(&p.grad[(size_t)sId[j] * kGradStride + vidx], tot);
+            const float tot = wave_reduce_scatter12(v, lane);
+            if ((lane & 3) == 0 && vidx < 12) atomicAdd(&sG[j * 12 + vidx], tot);
+        }
+        __syncthreads();
+        // flush: 16 lanes per entry (12 active) -> one 48-byte atomic row per (tile, Gaussian)
+        for (int slot = t; slot < cnt * 16; slot += kTilePixels) {
+            const int e = slot >> 4, q = slot & 15;
+            if (q < 12) {
+                const float val = sG[e * 12 + q];
+                if (val != 0.0f) atomicAdd(&p.grad[(size_t)sId[e] * kGradStride + q], val);
+            }
         }
     }
 }

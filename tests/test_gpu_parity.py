@@ -45,7 +45,7 @@ def state(out, P, W, H):
         return buf[off:off + 4 * n].view(torch.int32).cpu().numpy().view(np.uint32)
 
     return dict(
-        tile_start=u32(image, lay["tile_start"], T + 1),
+        ranges=u32(image, lay["ranges"], 2 * T).reshape(T, 2),
         point_list=u32(binning, lay["point_list"], nr),
         final_T=image[lay["final_T"]:lay["final_T"] + 4 * W * H].view(torch.float32).cpu().numpy().reshape(H, W),
         n_contrib=u32(image, lay["n_contrib"], W * H).reshape(H, W),
@@ -68,10 +68,10 @@ def check_forward_exact(st, inp, run=None):
     if P > 0:
         s = state(out, P, W, H)
         rg = run.get("ranges")
-        ts = s["tile_start"]
+        gr = s["ranges"]
         nonempty = rg[:, 1] > rg[:, 0]
-        np.testing.assert_array_equal(ts[:-1][nonempty], rg[nonempty, 0])
-        np.testing.assert_array_equal(ts[1:][nonempty], rg[nonempty, 1])
+        np.testing.assert_array_equal(gr[nonempty], rg[nonempty])
+        assert np.all(gr[~nonempty, 1] == gr[~nonempty, 0])
         np.testing.assert_array_equal(s["point_list"], run.get("point_list"))
         np.testing.assert_array_equal(s["final_T"], run.get("final_T"))
         np.testing.assert_array_equal(s["n_contrib"], run.get("n_contrib"))
@@ -159,8 +159,8 @@ def test_empty_and_fully_culled():
     np.testing.assert_array_equal(out[1].cpu().numpy(), np.broadcast_to(np.float32(0.3), (3, 32, 32)))
 
 
-def test_oversized_tile_uses_bitmap_path():
-    """> 8192 instances in one tile exercises the LDS-bitmap ordering path."""
+def test_very_long_tile_lists():
+    """> 8192 instances in one tile (dense cluster): long per-tile lists, many LDS batches."""
     P = 12000
     g = torch.Generator().manual_seed(9)
     W = H = 32
@@ -172,8 +172,7 @@ def test_oversized_tile_uses_bitmap_path():
                language_feature_precomp=torch.nn.functional.normalize(torch.randn((P, 3), generator=g)),
                scales=torch.full((P, 3), 0.01), rotations=torch.tensor([[1.0, 0.0, 0.0, 0.0]]).repeat(P, 1))
     run, std, ind, out = check_forward_exact(st, inp)
-    s = state(out, P, W, H)
-    assert s["counters"][3] >= 1  # oversize tiles were present
+    assert np.diff(run.get("ranges").astype(np.int64), axis=1).max() > 8192
     check_backward(st, inp, run, out)
 
 
@@ -248,13 +247,16 @@ def test_full_size_properties(cfg):
     nr, color, lang, radii, geom, binning, image = out
     P, W, H = c["P"], c["width"], c["height"]
     s = state(out, P, W, H)
-    assert s["counters"][1] == nr and s["tile_start"][-1] == nr
-    # sortedness within every tile: (depth key, id) ascending
+    assert s["counters"][1] == nr
+    rg = s["ranges"].astype(np.int64)
+    assert np.diff(rg, axis=1).sum() == nr
+    # sortedness within every tile: (depth key, id) ascending; tiles laid out in tile order
     pl = s["point_list"].astype(np.int64)
     dk = s["depth_key"].astype(np.int64)
     key = dk[pl] * (1 << 32) + pl
-    ts = s["tile_start"].astype(np.int64)
-    tile_of = np.repeat(np.arange(len(ts) - 1), np.diff(ts))
+    nonempty = np.nonzero(rg[:, 1] > rg[:, 0])[0]
+    assert np.all(rg[nonempty[1:], 0] == rg[nonempty[:-1], 1]) and rg[nonempty[0], 0] == 0
+    tile_of = np.repeat(nonempty, (rg[nonempty, 1] - rg[nonempty, 0]))
     same = tile_of[1:] == tile_of[:-1]
     assert np.all(key[1:][same] > key[:-1][same])
     # every visible Gaussian appears exactly tiles_touched times
