@@ -30,6 +30,13 @@
  * oracle and the GPU.  Gradients are accumulated here in double (the GPU uses float atomics in
  * arbitrary order) so backward parity is a tolerance, not bit-exactness.
  *
+ * Pinning: the SH basis and its backward, the camera matrices and the
+ * covariance are pinned to the reference's own Python (tests/golden, generated from
+ * /root/reference/utils); the compositing core is PARITY UNPINNED against the reference
+ * implementation (its source is the absent submodule) and is pinned instead to the published
+ * algorithm by analytic known-answer tests and by the independent autograd formulation in
+ * oracle/torch_ref.py.
+ *
  * Upstream-vs-fork decisions (SURVEY.md marks them <U?>) taken here and in the kernels:
  *   - language channel composited with the same weights as RGB, with NO background term;
  *   - language channel contributes to dL/dalpha (the mathematically exact gradient);
