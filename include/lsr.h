@@ -142,7 +142,7 @@ typedef struct lsr_state_layout {
     size_t sorted_ids;     /* uint32[P]  Gaussians by (depth, id); visible ones first */
     size_t inst_offset;    /* uint32[P]  first tile instance of the Gaussian of depth rank r */
     /* image buffer */
-    size_t counters;       /* uint32[16] {visible, num_rendered, error, ...} */
+    size_t counters;       /* uint32[16] {reserved, num_rendered, error, ...} */
     size_t ranges;         /* uint32[2T] [start, end) of each tile in point_list */
     size_t final_T;        /* float[H*W] */
     size_t n_contrib;      /* uint32[H*W] */

@@ -168,41 +168,88 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_hist(const uint32_t* __
     if (t <= (int)mask) hist[t * nblk + blockIdx.x] = h[t];
 }
 
+// Stable scatter of one block's kRadixTile keys.  Ranks are computed round by round in input order
+// (wave64 ballot match + per-wave digit counts), the block is reordered by digit in LDS, and the
+// output is written from LDS in digit-contiguous runs, so global stores coalesce (a direct scatter
+// would send the 64 lanes of a store to up to 64 different buckets).
 __global__ __launch_bounds__(kRadixThreads) void k_radix_scatter(
     const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in, int n, int shift, int nbits,
     const uint32_t* __restrict__ hist, int nblk, uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out)
 {
-    __shared__ uint32_t base_s[256];
+    __shared__ uint32_t sk[kRadixTile];
+    __shared__ uint32_t sv[kRadixTile];
+    __shared__ uint32_t gbase[256];     // global output position of this block's first key per digit
+    __shared__ uint32_t dstart[256];    // block-local start of each digit in the reordered tile
+    __shared__ uint32_t run[256];       // per-digit count so far in this block
     __shared__ uint32_t wcount[kRadixThreads / 64][256];
-    const int t = threadIdx.x, wave = t >> 6;
+    __shared__ uint32_t wsum[kRadixThreads / 64];
+    const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
     const uint32_t mask = (1u << nbits) - 1u;
-    base_s[t] = t <= (int)mask ? hist[t * nblk + blockIdx.x] : 0u;
+    gbase[t] = t <= (int)mask ? hist[t * nblk + blockIdx.x] : 0u;
+    run[t] = 0;
     const int base = blockIdx.x * kRadixTile;
+    uint32_t key[kRadixItems], val[kRadixItems], rank[kRadixItems];
+#pragma unroll
+    for (int it = 0; it < kRadixItems; it++) {
+        const int idx = base + it * kRadixThreads + t;
+        const bool valid = idx < n;
+        key[it] = valid ? keys_in[idx] : 0u;
+        val[it] = valid ? (vals_in ? vals_in[idx] : (uint32_t)idx) : 0u;
+    }
+#pragma unroll
     for (int it = 0; it < kRadixItems; it++) {
 #pragma unroll
         for (int w = 0; w < kRadixThreads / 64; w++) wcount[w][t] = 0;
         __syncthreads();
-        const int idx = base + it * kRadixThreads + t;
-        const bool valid = idx < n;
-        const uint32_t key = valid ? keys_in[idx] : 0u;
-        const uint32_t val = valid ? (vals_in ? vals_in[idx] : (uint32_t)idx) : 0u;
-        const uint32_t d = (key >> shift) & mask;
+        const bool valid = base + it * kRadixThreads + t < n;
+        const uint32_t d = (key[it] >> shift) & mask;
         const uint64_t peers = match_digit(d, valid, nbits);
-        const uint32_t rank = (uint32_t)__popcll(peers & lanemask_lt());
-        if (valid && rank == 0) wcount[wave][d] = (uint32_t)__popcll(peers);
+        const uint32_t r = (uint32_t)__popcll(peers & lanemask_lt());
+        if (valid && r == 0) wcount[wave][d] = (uint32_t)__popcll(peers);
         __syncthreads();
-        if (valid) {
-            uint32_t off = base_s[d] + rank;
-            for (int w = 0; w < wave; w++) off += wcount[w][d];
-            keys_out[off] = key;
-            vals_out[off] = val;
-        }
+        uint32_t off = run[d] + r;
+        for (int w = 0; w < wave; w++) off += wcount[w][d];
+        rank[it] = off;
         __syncthreads();
         uint32_t add = 0;
 #pragma unroll
         for (int w = 0; w < kRadixThreads / 64; w++) add += wcount[w][t];
-        base_s[t] += add;
+        run[t] += add;
+    }
+    __syncthreads();
+    // block-local exclusive scan of the digit counts
+    {
+        const uint32_t c = run[t];
+        uint32_t x = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) wsum[wave] = x;
         __syncthreads();
+        uint32_t before = 0;
+        for (int w = 0; w < wave; w++) before += wsum[w];
+        dstart[t] = before + x - c;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < kRadixItems; it++) {
+        if (base + it * kRadixThreads + t < n) {
+            const uint32_t d = (key[it] >> shift) & mask;
+            const uint32_t pos = dstart[d] + rank[it];
+            sk[pos] = key[it];
+            sv[pos] = val[it];
+        }
+    }
+    __syncthreads();
+    const int cnt = min(kRadixTile, n - base);
+    for (int i = t; i < cnt; i += kRadixThreads) {
+        const uint32_t k = sk[i];
+        const uint32_t d = (k >> shift) & mask;
+        const uint32_t o = gbase[d] + (uint32_t)i - dstart[d];
+        keys_out[o] = k;
+        vals_out[o] = sv[i];
     }
 }
 

@@ -12,7 +12,6 @@ namespace lsr {
 
 // counters[] slots in the image buffer
 enum Counter : int {
-    kCntVisible = 0,
     kCntRendered = 1,
     kCntError = 2,
     kCntSlots = 16

@@ -8,9 +8,43 @@
 
 namespace lsr {
 
+// SH coefficients of the block's 256 Gaussians are moved between HBM and LDS with coalesced
+// accesses (the AoS P x M x 3 layout gives each lane 12M contiguous bytes, i.e. 48 separate cache
+// lines per wave load otherwise); LDS rows are padded to 3M+1 floats, which keeps the per-lane
+// row reads bank-conflict free.
+__device__ __forceinline__ void stage_sh_in(const float* __restrict__ shs, int P, int M, float* lds)
+{
+    const int w = 3 * M, ws = w + 1;
+    const int g0 = blockIdx.x * blockDim.x;
+    const int n = min((int)blockDim.x, P - g0) * w;
+    const float* src = shs + (size_t)g0 * w;
+    for (int k = threadIdx.x; k < n; k += blockDim.x) {
+        const int gi = k / w;
+        lds[gi * ws + (k - gi * w)] = src[k];
+    }
+}
+
+__device__ __forceinline__ void stage_sh_out(float* __restrict__ dst_all, int P, int M, const float* lds)
+{
+    const int w = 3 * M, ws = w + 1;
+    const int g0 = blockIdx.x * blockDim.x;
+    const int n = min((int)blockDim.x, P - g0) * w;
+    float* dst = dst_all + (size_t)g0 * w;
+    for (int k = threadIdx.x; k < n; k += blockDim.x) {
+        const int gi = k / w;
+        dst[k] = lds[gi * ws + (k - gi * w)];
+    }
+}
+
 __global__ __launch_bounds__(256) void k_preprocess(PreprocessParams p)
 {
+    extern __shared__ float s_sh[];
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p.shs) {
+        if (blockIdx.x * blockDim.x >= p.P) return;  // block-uniform
+        stage_sh_in(p.shs, p.P, p.M, s_sh);
+        __syncthreads();
+    }
     if (i >= p.P) return;
     p.radii[i] = 0;
     p.tiles[i] = 0;
@@ -26,14 +60,13 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessParams p)
     const float p_w = 1.0f / (hw + 0.0000001f);
     const float proj_x = hom.x * p_w, proj_y = hom.y * p_w;
 
-    float cov_local[6];
-    const float* cov;
+    float cov[6];
     if (p.cov_pre) {
-        cov = p.cov_pre + 6 * (size_t)i;
+#pragma unroll
+        for (int k = 0; k < 6; k++) cov[k] = p.cov_pre[6 * (size_t)i + k];
     } else {
         const float4 q = *reinterpret_cast<const float4*>(p.rots + 4 * (size_t)i);
-        cov3d(p.scales[3 * i], p.scales[3 * i + 1], p.scales[3 * i + 2], p.scale_modifier, q, cov_local);
-        cov = cov_local;
+        cov3d(p.scales[3 * i], p.scales[3 * i + 1], p.scales[3 * i + 2], p.scale_modifier, q, cov);
     }
     const Cov2D cv = cov2d(px, py, pz, p.focal_x, p.focal_y, p.tanfovx, p.tanfovy, cov, p.view);
     const float a = cv.a, b = cv.b, c = cv.c;
@@ -59,7 +92,7 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessParams p)
         const float dox = px - p.campos[0], doy = py - p.campos[1], doz = pz - p.campos[2];
         const float len = sqrtf(dot3(dox, doy, doz, dox, doy, doz));
         const float x = dox / len, y = doy / len, z = doz / len;
-        const float* sh = p.shs + (size_t)i * p.M * 3;
+        const float* sh = s_sh + threadIdx.x * (3 * p.M + 1);
 #pragma unroll
         for (int ch = 0; ch < 3; ch++) {
             const float v = sh_eval_channel(p.D, sh + ch, x, y, z) + 0.5f;
@@ -87,13 +120,24 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessParams p)
     rec[0] = make_float4(ix, iy, cx, cy);
     rec[1] = make_float4(cz, p.opac[i], rgb[0], rgb[1]);
     rec[2] = make_float4(rgb[2], f0, f1, f2);
-    atomicAdd(&p.counters[kCntVisible], 1u);
+}
+
+static size_t sh_lds_bytes(const float* shs, int M) { return shs ? 256 * (size_t)(3 * M + 1) * 4 : 0; }
+
+// dynamic LDS beyond the 64 KiB default (M > 20 stored SH coefficients) must be opted into
+static hipError_t allow_lds(const void* fn, size_t bytes)
+{
+    if (bytes <= 65536) return hipSuccess;
+    if (bytes > 160 * 1024) return hipErrorInvalidValue;
+    return hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
 
 hipError_t launch_preprocess(const PreprocessParams& p, hipStream_t s)
 {
     if (p.P == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_preprocess, dim3((p.P + 255) / 256), dim3(256), 0, s, p);
+    hipError_t e = allow_lds((const void*)k_preprocess, sh_lds_bytes(p.shs, p.M));
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_preprocess, dim3((p.P + 255) / 256), dim3(256), sh_lds_bytes(p.shs, p.M), s, p);
     return hipGetLastError();
 }
 
@@ -231,10 +275,27 @@ __device__ void cov3d_backward(float sx, float sy, float sz, float mod, float4 q
               2.f * y * (dR[2][1] + dR[1][2]) - 4.f * z * (dR[1][1] + dR[0][0]);
 }
 
+__device__ __forceinline__ void preprocess_backward_one(const PreprocessBwdParams& p, int i, float* sh_row);
+
 __global__ __launch_bounds__(256) void k_preprocess_backward(PreprocessBwdParams p)
 {
+    extern __shared__ float s_sh[];
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= p.P) return;
+    if (blockIdx.x * blockDim.x >= p.P) return;  // block-uniform
+    if (p.shs) {
+        stage_sh_in(p.shs, p.P, p.M, s_sh);
+        __syncthreads();
+    }
+    if (i < p.P) preprocess_backward_one(p, i, s_sh + threadIdx.x * (3 * p.M + 1));
+    if (p.shs && p.dsh) {
+        __syncthreads();
+        stage_sh_out(p.dsh, p.P, p.M, s_sh);
+    }
+}
+
+// One Gaussian.  `sh_row` holds its SH coefficients on entry (LDS) and receives dL/dsh.
+__device__ __forceinline__ void preprocess_backward_one(const PreprocessBwdParams& p, int i, float* sh_row)
+{
     const size_t i3 = 3 * (size_t)i;
     if (!(p.radii[i] > 0)) {
         // culled: every output row is zero (upstream torch::zeros + skipped threads)
@@ -249,8 +310,8 @@ __global__ __launch_bounds__(256) void k_preprocess_backward(PreprocessBwdParams
         if (p.drots) *reinterpret_cast<float4*>(p.drots + 4 * (size_t)i) = make_float4(0.f, 0.f, 0.f, 0.f);
         if (p.dcov)
             for (int k = 0; k < 6; k++) p.dcov[6 * (size_t)i + k] = 0.f;
-        if (p.dsh)
-            for (int k = 0; k < 3 * p.M; k++) p.dsh[(size_t)i * 3 * p.M + k] = 0.f;
+        if (p.shs)
+            for (int k = 0; k < 3 * p.M; k++) sh_row[k] = 0.f;
         return;
     }
     const float4* g4 = reinterpret_cast<const float4*>(p.grad + (size_t)i * kGradStride);
@@ -271,15 +332,14 @@ __global__ __launch_bounds__(256) void k_preprocess_backward(PreprocessBwdParams
     p.dopac[i] = gb.y;
 
     const float px = p.means[i3], py = p.means[i3 + 1], pz = p.means[i3 + 2];
-    float cov_local[6];
-    const float* cov;
+    float cov[6];
     float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
     if (p.cov_pre) {
-        cov = p.cov_pre + 6 * (size_t)i;
+#pragma unroll
+        for (int k = 0; k < 6; k++) cov[k] = p.cov_pre[6 * (size_t)i + k];
     } else {
         q = *reinterpret_cast<const float4*>(p.rots + 4 * (size_t)i);
-        cov3d(p.scales[i3], p.scales[i3 + 1], p.scales[i3 + 2], p.scale_modifier, q, cov_local);
-        cov = cov_local;
+        cov3d(p.scales[i3], p.scales[i3 + 1], p.scales[i3 + 2], p.scale_modifier, q, cov);
     }
     const Cov2D cv = cov2d(px, py, pz, p.focal_x, p.focal_y, p.tanfovx, p.tanfovy, cov, p.view);
     const float limx = 1.3f * p.tanfovx, limy = 1.3f * p.tanfovy;
@@ -352,8 +412,8 @@ __global__ __launch_bounds__(256) void k_preprocess_backward(PreprocessBwdParams
 #pragma unroll
         for (int ch = 0; ch < 3; ch++) drgb[ch] = ((cb >> ch) & 1u) ? 0.0f : drgb_in[ch];
         float dm_sh[3];
-        sh_backward(p.D, p.M, p.shs + (size_t)i * p.M * 3, px - p.campos[0], py - p.campos[1],
-                    pz - p.campos[2], drgb, p.dsh + (size_t)i * p.M * 3, dm_sh);
+        sh_backward(p.D, p.M, sh_row, px - p.campos[0], py - p.campos[1], pz - p.campos[2], drgb, sh_row,
+                    dm_sh);
         dmean[0] += dm_sh[0];
         dmean[1] += dm_sh[1];
         dmean[2] += dm_sh[2];
@@ -384,7 +444,9 @@ __global__ __launch_bounds__(256) void k_preprocess_backward(PreprocessBwdParams
 hipError_t launch_preprocess_backward(const PreprocessBwdParams& p, hipStream_t s)
 {
     if (p.P == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_preprocess_backward, dim3((p.P + 255) / 256), dim3(256), 0, s, p);
+    hipError_t e = allow_lds((const void*)k_preprocess_backward, sh_lds_bytes(p.shs, p.M));
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_preprocess_backward, dim3((p.P + 255) / 256), dim3(256), sh_lds_bytes(p.shs, p.M), s, p);
     return hipGetLastError();
 }
 

@@ -1,46 +1,77 @@
 // lsr_render.hip -- per-tile compositing (forward) and its back-to-front replay (backward).
 //
-// One 256-thread workgroup per 16x16 screen tile = 4 wave64s, each wave owning 16x4 pixels.
-// The tile's depth-ordered list is streamed through LDS in batches of 256 Gaussians (48 B
-// records split into broadcast-friendly {x, y, -conic.x/2, -conic.z/2}{conic.y, opacity}
-// {r, g, b, f0}{f1, f2} arrays).  Semantics: upstream FORWARD/BACKWARD::renderCUDA extended by
+// Backward: one 128-thread workgroup per 16x16 screen tile = 2 wave64s; every lane owns TWO
+// vertically adjacent pixels, so each list entry read from LDS feeds two independent dependency
+// chains (ILP) and the per-entry fixed costs (LDS reads, loop control, the wave reduction) are
+// paid once per two pixels.  Forward: templated on pixels per lane (1 = 256 threads).  The tile's depth-ordered list is streamed through LDS in batches of 128
+// entries (48 B records split into broadcast-friendly {x, y, -conic.x/2, -conic.z/2}
+// {conic.y, opacity, power cutoff}{r, g, b, f0}{f1, f2} arrays).  Semantics: upstream FORWARD/BACKWARD::renderCUDA extended by
 // the 3-channel language feature; arithmetic order is
 // that of oracle/lsr_oracle.c render_pixel / backward_pixel.
 //
 // Backward gradient scatter: every lane of a wave visits the same list entry at the same
 // iteration, so the 12 per-Gaussian partials of a wave are reduced in registers by a
-// reduce-scatter (permlane32/16 swaps + DPP mirrors, ~35 VALU ops), the 4 waves' results are summed
+// reduce-scatter (permlane32/16 swaps + DPP mirrors, ~35 VALU ops), the 2 waves' results are summed
 // in LDS (ds_add_f32), and after each batch ONE 12-lane atomic instruction per (tile, Gaussian)
 // adds the tile's total into a 64-byte-aligned per-Gaussian record -- instead of the upstream 12
 // scattered atomics per pixel per blend.  Entries no lane contributes to are skipped by a ballot.
+#include <stdlib.h>
+
 #include "lsr_internal.h"
 
 namespace lsr {
 
-__global__ __launch_bounds__(kTilePixels) void k_render_forward(RenderParams p)
+// Exact early-out: for power < cutoff(o) = ln(1/(255 o)) - 0.01 the composited alpha
+// min(0.99, o * exp(power)) is certainly < 1/255 (1% margin >> the exp restatement's 2 ulp), so
+// the entry is skipped exactly as the full test would skip it -- without evaluating exp.
+// o < 1/255 (or o <= 0) skips always, as alpha <= o then.
+__device__ __forceinline__ float power_cutoff(float o)
 {
-    __shared__ float4 sA[kTilePixels];  // x, y, -0.5 conic.x, -0.5 conic.z
-    __shared__ float2 sB[kTilePixels];  // conic.y, opacity
-    __shared__ float4 sC[kTilePixels];  // r, g, b, f0
-    __shared__ float2 sD[kTilePixels];  // f1, f2
+    return o > (1.0f / 255.0f) ? __logf(1.0f / (255.0f * o)) - 0.01f : 3.0e38f;
+}
+
+constexpr int kRenderThreads = 128;  // 2 wave64s per 16x16 tile, 2 pixels per lane
+constexpr int kBatch = 128;           // list entries staged in LDS per round (one per thread)
+
+// One pixel's front-to-back state (upstream FORWARD::renderCUDA locals).
+struct FwdPixel {
+    float T, C0, C1, C2, F0, F1, F2;
+    uint32_t contributor, last;
+    bool done;
+};
+
+// kPix pixels per lane: lane l of the tile's (256 / kPix)-thread workgroup owns the pixels
+// (l % 16, kPix * (l / 16) + k), k < kPix -- vertically adjacent, so a wave covers a compact
+// 16 x (4 kPix) block and its lanes terminate together.
+template <int kPix>
+__global__ __launch_bounds__(kTilePixels / kPix) void k_render_forward(RenderParams p)
+{
+    constexpr int kThreads = kTilePixels / kPix;
+    __shared__ float4 sA[kThreads];  // x, y, -0.5 conic.x, -0.5 conic.z
+    __shared__ float4 sB[kThreads];  // conic.y, opacity, power cutoff, -
+    __shared__ float4 sC[kThreads];  // r, g, b, f0
+    __shared__ float2 sD[kThreads];  // f1, f2
 
     const int tile = blockIdx.x;
     const int tx = tile % p.gx, ty = tile / p.gx;
     const int t = threadIdx.x;
-    const int px = tx * kTile + (t & (kTile - 1)), py = ty * kTile + (t >> 4);
-    const bool inside = px < p.W && py < p.H;
-    const float pfx = (float)px, pfy = (float)py;
+    const int px = tx * kTile + (t & (kTile - 1));
+    const int py_base = ty * kTile + kPix * (t >> 4);
+    const float pfx = (float)px;
     const uint2 range = p.ranges[tile];
     const uint32_t start = range.x, end = range.y;
     const bool feat = p.include_feature != 0;
 
-    float T = 1.0f;
-    float C0 = 0.f, C1 = 0.f, C2 = 0.f, F0 = 0.f, F1 = 0.f, F2 = 0.f;
-    uint32_t contributor = 0, last = 0;
-    bool done = !inside;
+    FwdPixel q[kPix];
+#pragma unroll
+    for (int k = 0; k < kPix; k++)
+        q[k] = FwdPixel{1.0f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0u, 0u, !(px < p.W && py_base + k < p.H)};
 
-    for (uint32_t base = start; base < end; base += kTilePixels) {
-        if (__syncthreads_count(done) == kTilePixels) break;
+    for (uint32_t base = start; base < end; base += kThreads) {
+        bool all_done = true;
+#pragma unroll
+        for (int k = 0; k < kPix; k++) all_done = all_done && q[k].done;
+        if (__syncthreads_count(all_done) == kThreads) break;
         const uint32_t idx = base + t;
         if (idx < end) {
             const uint32_t g = p.point_list[idx];
@@ -48,59 +79,100 @@ __global__ __launch_bounds__(kTilePixels) void k_render_forward(RenderParams p)
             const float4 b = p.record[3 * (size_t)g + 1];
             const float4 c = p.record[3 * (size_t)g + 2];
             sA[t] = make_float4(a.x, a.y, -0.5f * a.z, -0.5f * b.x);
-            sB[t] = make_float2(a.w, b.y);
+            sB[t] = make_float4(a.w, b.y, power_cutoff(b.y), 0.0f);
             sC[t] = make_float4(b.z, b.w, c.x, c.y);
             sD[t] = make_float2(c.z, c.w);
         }
         __syncthreads();
-        const int cnt = (int)min((uint32_t)kTilePixels, end - base);
-        for (int j = 0; j < cnt && !done; j++) {
-            contributor++;
+        const int cnt = (int)min((uint32_t)kThreads, end - base);
+        for (int j = 0; j < cnt && !all_done; j++) {
             const float4 A = sA[j];
-            const float2 B = sB[j];
-            const float dx = A.x - pfx, dy = A.y - pfy;
-            const float power = fma_(A.z * dx, dx, fma_(A.w * dy, dy, -((B.x * dx) * dy)));
-            if (power > 0.0f) continue;
-            const float alpha = fminf(0.99f, B.y * expf_exact(power));
-            if (alpha < 1.0f / 255.0f) continue;
-            const float test_T = T * (1.0f - alpha);
-            if (test_T < 0.0001f) {
-                done = true;
-                continue;
+            const float4 B = sB[j];
+            const float dx = A.x - pfx;
+            float pw[kPix], al[kPix];
+            bool ok[kPix];
+            bool any = false;
+#pragma unroll
+            for (int k = 0; k < kPix; k++) {
+                q[k].contributor += q[k].done ? 0u : 1u;
+                const float dy = A.y - (float)(py_base + k);
+                pw[k] = fma_(A.z * dx, dx, fma_(A.w * dy, dy, -((B.x * dx) * dy)));
+                ok[k] = !q[k].done && !(pw[k] > 0.0f || pw[k] < B.z);
+                any = any || ok[k];
             }
-            const float w = alpha * T;
-            const float4 Cc = sC[j];
-            C0 = fma_(Cc.x, w, C0);
-            C1 = fma_(Cc.y, w, C1);
-            C2 = fma_(Cc.z, w, C2);
-            if (feat) {
+            if (!any) continue;
+            any = false;
+#pragma unroll
+            for (int k = 0; k < kPix; k++) {
+                al[k] = fminf(0.99f, B.y * expf_exact(pw[k]));
+                ok[k] = ok[k] && !(al[k] < 1.0f / 255.0f);
+                const float test_T = q[k].T * (1.0f - al[k]);
+                if (ok[k] && test_T < 0.0001f) {
+                    q[k].done = true;
+                    ok[k] = false;
+                }
+                pw[k] = test_T;  // reuse: the candidate transmittance
+                any = any || ok[k];
+            }
+            if (any) {
+                const float4 Cc = sC[j];
                 const float2 D = sD[j];
-                F0 = fma_(Cc.w, w, F0);
-                F1 = fma_(D.x, w, F1);
-                F2 = fma_(D.y, w, F2);
+#pragma unroll
+                for (int k = 0; k < kPix; k++) {
+                    if (!ok[k]) continue;
+                    const float w = al[k] * q[k].T;
+                    q[k].C0 = fma_(Cc.x, w, q[k].C0);
+                    q[k].C1 = fma_(Cc.y, w, q[k].C1);
+                    q[k].C2 = fma_(Cc.z, w, q[k].C2);
+                    if (feat) {
+                        q[k].F0 = fma_(Cc.w, w, q[k].F0);
+                        q[k].F1 = fma_(D.x, w, q[k].F1);
+                        q[k].F2 = fma_(D.y, w, q[k].F2);
+                    }
+                    q[k].T = pw[k];
+                    q[k].last = q[k].contributor;
+                }
             }
-            T = test_T;
-            last = contributor;
+            all_done = true;
+#pragma unroll
+            for (int k = 0; k < kPix; k++) all_done = all_done && q[k].done;
         }
     }
-    if (inside) {
-        const size_t HW = (size_t)p.W * p.H;
+    const size_t HW = (size_t)p.W * p.H;
+#pragma unroll
+    for (int k = 0; k < kPix; k++) {
+        const int py = py_base + k;
+        if (!(px < p.W && py < p.H)) continue;
         const size_t pix = (size_t)py * p.W + px;
-        p.final_T[pix] = T;
-        p.n_contrib[pix] = last;
-        p.out_color[pix] = fma_(T, p.bg[0], C0);
-        p.out_color[HW + pix] = fma_(T, p.bg[1], C1);
-        p.out_color[2 * HW + pix] = fma_(T, p.bg[2], C2);
-        p.out_lang[pix] = F0;
-        p.out_lang[HW + pix] = F1;
-        p.out_lang[2 * HW + pix] = F2;
+        p.final_T[pix] = q[k].T;
+        p.n_contrib[pix] = q[k].last;
+        p.out_color[pix] = fma_(q[k].T, p.bg[0], q[k].C0);
+        p.out_color[HW + pix] = fma_(q[k].T, p.bg[1], q[k].C1);
+        p.out_color[2 * HW + pix] = fma_(q[k].T, p.bg[2], q[k].C2);
+        p.out_lang[pix] = q[k].F0;
+        p.out_lang[HW + pix] = q[k].F1;
+        p.out_lang[2 * HW + pix] = q[k].F2;
     }
+}
+
+// LSR_FWD_PIXELS=1|2 selects the forward variant (measurement aid; default 1)
+static int fwd_pixels_per_lane()
+{
+    static int v = [] {
+        const char* e = getenv("LSR_FWD_PIXELS");
+        return (e && e[0] == '2') ? 2 : 1;
+    }();
+    return v;
 }
 
 hipError_t launch_render_forward(const RenderParams& p, int tiles, hipStream_t s)
 {
     if (tiles == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_render_forward, dim3(tiles), dim3(kTilePixels), 0, s, p);
+    const int pix = fwd_pixels_per_lane();
+    if (pix == 2)
+        hipLaunchKernelGGL(k_render_forward<2>, dim3(tiles), dim3(kTilePixels / 2), 0, s, p);
+    else
+        hipLaunchKernelGGL(k_render_forward<1>, dim3(tiles), dim3(kTilePixels), 0, s, p);
     return hipGetLastError();
 }
 
@@ -164,154 +236,192 @@ __device__ __forceinline__ int scatter_index(int lane)
     return (((lane >> 5) & 1) << 3) | (((lane >> 4) & 1) << 2) | (((lane >> 3) & 1) << 1) | ((lane >> 2) & 1);
 }
 
-__global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
+// One pixel's back-to-front state (upstream BACKWARD::renderCUDA locals).
+struct BwdPixel {
+    float T, T_final, bg_dot;
+    float dp0, dp1, dp2, dq0, dq1, dq2;
+    float acc0, acc1, acc2, accF0, accF1, accF2;
+    float lc0, lc1, lc2, lf0, lf1, lf2;
+    float last_alpha;
+    uint32_t last;
+};
+
+__device__ __forceinline__ void bwd_pixel_init(BwdPixel& q, const RenderParams& p, bool inside, size_t pix,
+                                               size_t HW, bool feat)
 {
-    __shared__ float4 sA[kTilePixels];  // x, y, -0.5 conic.x, -0.5 conic.z
-    __shared__ float2 sB[kTilePixels];  // conic.y, opacity
-    __shared__ float4 sC[kTilePixels];  // r, g, b, f0
-    __shared__ float2 sD[kTilePixels];  // f1, f2
-    __shared__ uint32_t sId[kTilePixels];
-    __shared__ float sG[kTilePixels * 12];  // per-entry gradient sums of the tile (12 floats)
+    q.T_final = inside ? p.final_T[pix] : 0.0f;
+    q.T = q.T_final;
+    q.last = inside ? p.n_contrib[pix] : 0u;
+    q.dp0 = q.dp1 = q.dp2 = q.dq0 = q.dq1 = q.dq2 = 0.f;
+    if (inside) {
+        q.dp0 = p.dL_dcolor[pix];
+        q.dp1 = p.dL_dcolor[HW + pix];
+        q.dp2 = p.dL_dcolor[2 * HW + pix];
+        if (feat && p.dL_dlang) {
+            q.dq0 = p.dL_dlang[pix];
+            q.dq1 = p.dL_dlang[HW + pix];
+            q.dq2 = p.dL_dlang[2 * HW + pix];
+        }
+    }
+    q.bg_dot = fma_(p.bg[2], q.dp2, fma_(p.bg[1], q.dp1, p.bg[0] * q.dp0));
+    q.acc0 = q.acc1 = q.acc2 = q.accF0 = q.accF1 = q.accF2 = 0.f;
+    q.lc0 = q.lc1 = q.lc2 = q.lf0 = q.lf1 = q.lf2 = 0.f;
+    q.last_alpha = 0.f;
+}
+
+// One replayed blend of one pixel: updates the pixel state and ADDS its 12 gradient partials to v
+// (order of oracle backward_pixel; alpha and the skip tests are bit-identical to the forward).
+__device__ __forceinline__ void bwd_pixel_blend(BwdPixel& q, float G, float alpha, float dx, float dy,
+                                                const float4& B, float cx, float cz, const float4& Cc,
+                                                const float2& D, bool feat, float ddelx_dx, float ddely_dy,
+                                                float (&v)[12])
+{
+    const float one_m = 1.0f - alpha;
+    // gradients need 1e-4, not bit-exactness: one v_rcp_f32 replaces the two IEEE divisions
+    // T / (1 - alpha) and T_final / (1 - alpha) (the skip decisions use power/alpha only)
+    const float inv_one_m = __builtin_amdgcn_rcpf(one_m);
+    q.T = q.T * inv_one_m;
+    const float dcd = alpha * q.T;
+    const float oml = 1.0f - q.last_alpha;
+    float dL_dalpha = 0.0f;
+    q.acc0 = fma_(q.last_alpha, q.lc0, oml * q.acc0);
+    q.lc0 = Cc.x;
+    dL_dalpha = fma_(Cc.x - q.acc0, q.dp0, dL_dalpha);
+    v[6] += dcd * q.dp0;
+    q.acc1 = fma_(q.last_alpha, q.lc1, oml * q.acc1);
+    q.lc1 = Cc.y;
+    dL_dalpha = fma_(Cc.y - q.acc1, q.dp1, dL_dalpha);
+    v[7] += dcd * q.dp1;
+    q.acc2 = fma_(q.last_alpha, q.lc2, oml * q.acc2);
+    q.lc2 = Cc.z;
+    dL_dalpha = fma_(Cc.z - q.acc2, q.dp2, dL_dalpha);
+    v[8] += dcd * q.dp2;
+    if (feat) {
+        q.accF0 = fma_(q.last_alpha, q.lf0, oml * q.accF0);
+        q.lf0 = Cc.w;
+        dL_dalpha = fma_(Cc.w - q.accF0, q.dq0, dL_dalpha);
+        v[9] += dcd * q.dq0;
+        q.accF1 = fma_(q.last_alpha, q.lf1, oml * q.accF1);
+        q.lf1 = D.x;
+        dL_dalpha = fma_(D.x - q.accF1, q.dq1, dL_dalpha);
+        v[10] += dcd * q.dq1;
+        q.accF2 = fma_(q.last_alpha, q.lf2, oml * q.accF2);
+        q.lf2 = D.y;
+        dL_dalpha = fma_(D.y - q.accF2, q.dq2, dL_dalpha);
+        v[11] += dcd * q.dq2;
+    }
+    dL_dalpha = dL_dalpha * q.T;
+    q.last_alpha = alpha;
+    dL_dalpha = fma_(-q.T_final * inv_one_m, q.bg_dot, dL_dalpha);
+    const float cy = B.x;
+    const float dL_dG = B.y * dL_dalpha;
+    const float gdx = G * dx, gdy = G * dy;
+    const float dG_ddelx = -gdx * cx - gdy * cy;
+    const float dG_ddely = -gdy * cz - gdx * cy;
+    v[0] += dL_dG * dG_ddelx * ddelx_dx;
+    v[1] += dL_dG * dG_ddely * ddely_dy;
+    v[2] += -0.5f * gdx * dx * dL_dG;
+    v[3] += -0.5f * gdx * dy * dL_dG;
+    v[4] += -0.5f * gdy * dy * dL_dG;
+    v[5] += G * dL_dalpha;
+}
+
+__global__ __launch_bounds__(kRenderThreads) void k_render_backward(RenderParams p)
+{
+    __shared__ float4 sA[kBatch];  // x, y, -0.5 conic.x, -0.5 conic.z
+    __shared__ float4 sB[kBatch];  // conic.y, opacity, power cutoff, -
+    __shared__ float4 sC[kBatch];  // r, g, b, f0
+    __shared__ float2 sD[kBatch];  // f1, f2
+    __shared__ uint32_t sId[kBatch];
+    __shared__ float sG[kBatch * 12];  // per-entry gradient sums of the tile (12 floats)
     __shared__ uint32_t s_max;
 
     const int tile = blockIdx.x;
     const int tx = tile % p.gx, ty = tile / p.gx;
     const int t = threadIdx.x, lane = t & 63;
-    const int px = tx * kTile + (t & (kTile - 1)), py = ty * kTile + (t >> 4);
-    const bool inside = px < p.W && py < p.H;
-    const float pfx = (float)px, pfy = (float)py;
+    const int px = tx * kTile + (t & (kTile - 1));
+    const int py0 = ty * kTile + 2 * (t >> 4), py1 = py0 + 1;  // vertically adjacent pair
+    const bool in0 = px < p.W && py0 < p.H, in1 = px < p.W && py1 < p.H;
+    const float pfx = (float)px, pfy0 = (float)py0, pfy1 = (float)py1;
     const size_t HW = (size_t)p.W * p.H;
-    const size_t pix = (size_t)py * p.W + px;
     const uint32_t start = p.ranges[tile].x;
     const bool feat = p.include_feature != 0;
-
-    const float T_final = inside ? p.final_T[pix] : 0.0f;
-    const uint32_t last = inside ? p.n_contrib[pix] : 0u;
-    float dp0 = 0.f, dp1 = 0.f, dp2 = 0.f, dq0 = 0.f, dq1 = 0.f, dq2 = 0.f;
-    if (inside) {
-        dp0 = p.dL_dcolor[pix];
-        dp1 = p.dL_dcolor[HW + pix];
-        dp2 = p.dL_dcolor[2 * HW + pix];
-        if (feat && p.dL_dlang) {
-            dq0 = p.dL_dlang[pix];
-            dq1 = p.dL_dlang[HW + pix];
-            dq2 = p.dL_dlang[2 * HW + pix];
-        }
-    }
-    const float bg_dot = fma_(p.bg[2], dp2, fma_(p.bg[1], dp1, p.bg[0] * dp0));
     const float ddelx_dx = 0.5f * (float)p.W, ddely_dy = 0.5f * (float)p.H;
+
+    BwdPixel q0, q1;
+    bwd_pixel_init(q0, p, in0, (size_t)py0 * p.W + px, HW, feat);
+    bwd_pixel_init(q1, p, in1, (size_t)py1 * p.W + px, HW, feat);
 
     // entries at list index >= max over the tile of n_contrib can contribute to no pixel
     if (t == 0) s_max = 0;
     __syncthreads();
-    uint32_t wmax = last;
+    uint32_t wmax = max(q0.last, q1.last);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) wmax = max(wmax, (uint32_t)__shfl_xor((int)wmax, o, 64));
     if (lane == 0) atomicMax(&s_max, wmax);
     __syncthreads();
     const int maxl = (int)s_max;
-
-    float T = T_final;
-    float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, accF0 = 0.f, accF1 = 0.f, accF2 = 0.f;
-    float lc0 = 0.f, lc1 = 0.f, lc2 = 0.f, lf0 = 0.f, lf1 = 0.f, lf2 = 0.f;
-    float last_alpha = 0.0f;
+    const int wave_max = (int)wmax;  // entries at index >= this touch no pixel of this wave
     const int vidx = scatter_index(lane);
 
-    for (int done_cnt = 0; done_cnt < maxl; done_cnt += kTilePixels) {
+    for (int done_cnt = 0; done_cnt < maxl; done_cnt += kBatch) {
         __syncthreads();
-        const int k = maxl - 1 - (done_cnt + t);
-        if (k >= 0) {
-            const uint32_t g = p.point_list[start + (uint32_t)k];
-            const float4 a = p.record[3 * (size_t)g];
-            const float4 b = p.record[3 * (size_t)g + 1];
-            const float4 c = p.record[3 * (size_t)g + 2];
-            sA[t] = make_float4(a.x, a.y, -0.5f * a.z, -0.5f * b.x);
-            sB[t] = make_float2(a.w, b.y);
-            sC[t] = make_float4(b.z, b.w, c.x, c.y);
-            sD[t] = make_float2(c.z, c.w);
-            sId[t] = g;
-        }
 #pragma unroll
-        for (int q = 0; q < 12; q++) sG[q * kTilePixels + t] = 0.f;
+        for (int h = 0; h < kBatch / kRenderThreads; h++) {
+            const int slot = t + h * kRenderThreads;
+            const int k = maxl - 1 - (done_cnt + slot);
+            if (k >= 0) {
+                const uint32_t g = p.point_list[start + (uint32_t)k];
+                const float4 a = p.record[3 * (size_t)g];
+                const float4 b = p.record[3 * (size_t)g + 1];
+                const float4 c = p.record[3 * (size_t)g + 2];
+                sA[slot] = make_float4(a.x, a.y, -0.5f * a.z, -0.5f * b.x);
+                sB[slot] = make_float4(a.w, b.y, power_cutoff(b.y), 0.0f);
+                sC[slot] = make_float4(b.z, b.w, c.x, c.y);
+                sD[slot] = make_float2(c.z, c.w);
+                sId[slot] = g;
+            }
+        }
+        for (int i = t; i < kBatch * 12; i += kRenderThreads) sG[i] = 0.f;
         __syncthreads();
-        const int cnt = min(kTilePixels, maxl - done_cnt);
+        const int cnt = min(kBatch, maxl - done_cnt);
         for (int j = 0; j < cnt; j++) {
             const int kk = maxl - 1 - (done_cnt + j);  // list index of this entry
+            if (kk >= wave_max) continue;              // wave-uniform
+            const float4 A = sA[j];
+            const float4 B = sB[j];
+            const float dx = A.x - pfx, dy0 = A.y - pfy0, dy1 = A.y - pfy1;
+            const float p0 = fma_(A.z * dx, dx, fma_(A.w * dy0, dy0, -((B.x * dx) * dy0)));
+            const float p1 = fma_(A.z * dx, dx, fma_(A.w * dy1, dy1, -((B.x * dx) * dy1)));
+            bool h0 = kk < (int)q0.last && p0 <= 0.0f && p0 >= B.z;
+            bool h1 = kk < (int)q1.last && p1 <= 0.0f && p1 >= B.z;
+            if (__ballot(h0 || h1) == 0ull) continue;  // wave-uniform skip
             float v[12];
 #pragma unroll
-            for (int q = 0; q < 12; q++) v[q] = 0.f;
-            bool hit = false;
-            if (kk < (int)last) {
-                const float4 A = sA[j];
-                const float2 B = sB[j];
-                const float dx = A.x - pfx, dy = A.y - pfy;
-                const float power = fma_(A.z * dx, dx, fma_(A.w * dy, dy, -((B.x * dx) * dy)));
-                if (power <= 0.0f) {
-                    const float G = expf_exact(power);
-                    const float alpha = fminf(0.99f, B.y * G);
-                    if (alpha >= 1.0f / 255.0f) {
-                        hit = true;
-                        const float4 Cc = sC[j];
-                        const float one_m = 1.0f - alpha;
-                        T = T / one_m;
-                        const float dchannel_dcolor = alpha * T;
-                        const float oml = 1.0f - last_alpha;
-                        float dL_dalpha = 0.0f;
-                        acc0 = fma_(last_alpha, lc0, oml * acc0);
-                        lc0 = Cc.x;
-                        dL_dalpha = fma_(Cc.x - acc0, dp0, dL_dalpha);
-                        v[6] = dchannel_dcolor * dp0;
-                        acc1 = fma_(last_alpha, lc1, oml * acc1);
-                        lc1 = Cc.y;
-                        dL_dalpha = fma_(Cc.y - acc1, dp1, dL_dalpha);
-                        v[7] = dchannel_dcolor * dp1;
-                        acc2 = fma_(last_alpha, lc2, oml * acc2);
-                        lc2 = Cc.z;
-                        dL_dalpha = fma_(Cc.z - acc2, dp2, dL_dalpha);
-                        v[8] = dchannel_dcolor * dp2;
-                        if (feat) {
-                            const float2 D = sD[j];
-                            accF0 = fma_(last_alpha, lf0, oml * accF0);
-                            lf0 = Cc.w;
-                            dL_dalpha = fma_(Cc.w - accF0, dq0, dL_dalpha);
-                            v[9] = dchannel_dcolor * dq0;
-                            accF1 = fma_(last_alpha, lf1, oml * accF1);
-                            lf1 = D.x;
-                            dL_dalpha = fma_(D.x - accF1, dq1, dL_dalpha);
-                            v[10] = dchannel_dcolor * dq1;
-                            accF2 = fma_(last_alpha, lf2, oml * accF2);
-                            lf2 = D.y;
-                            dL_dalpha = fma_(D.y - accF2, dq2, dL_dalpha);
-                            v[11] = dchannel_dcolor * dq2;
-                        }
-                        dL_dalpha = dL_dalpha * T;
-                        last_alpha = alpha;
-                        dL_dalpha = fma_(-T_final / one_m, bg_dot, dL_dalpha);
-                        const float cx = -2.0f * A.z, cz = -2.0f * A.w, cy = B.x;
-                        const float dL_dG = B.y * dL_dalpha;
-                        const float gdx = G * dx, gdy = G * dy;
-                        const float dG_ddelx = -gdx * cx - gdy * cy;
-                        const float dG_ddely = -gdy * cz - gdx * cy;
-                        v[0] = dL_dG * dG_ddelx * ddelx_dx;
-                        v[1] = dL_dG * dG_ddely * ddely_dy;
-                        v[2] = -0.5f * gdx * dx * dL_dG;
-                        v[3] = -0.5f * gdx * dy * dL_dG;
-                        v[4] = -0.5f * gdy * dy * dL_dG;
-                        v[5] = G * dL_dalpha;
-                    }
+            for (int c = 0; c < 12; c++) v[c] = 0.f;
+            if (h0 || h1) {
+                const float G0 = expf_exact(p0), G1 = expf_exact(p1);
+                const float a0 = fminf(0.99f, B.y * G0), a1 = fminf(0.99f, B.y * G1);
+                h0 = h0 && a0 >= 1.0f / 255.0f;
+                h1 = h1 && a1 >= 1.0f / 255.0f;
+                if (h0 || h1) {
+                    const float4 Cc = sC[j];
+                    const float2 D = sD[j];
+                    const float cx = -2.0f * A.z, cz = -2.0f * A.w;
+                    if (h0) bwd_pixel_blend(q0, G0, a0, dx, dy0, B, cx, cz, Cc, D, feat, ddelx_dx, ddely_dy, v);
+                    if (h1) bwd_pixel_blend(q1, G1, a1, dx, dy1, B, cx, cz, Cc, D, feat, ddelx_dx, ddely_dy, v);
                 }
             }
-            if (__ballot(hit) == 0ull) continue;  // wave-uniform skip
             const float tot = wave_reduce_scatter12(v, lane);
             if ((lane & 3) == 0 && vidx < 12) atomicAdd(&sG[j * 12 + vidx], tot);
         }
         __syncthreads();
         // flush: 16 lanes per entry (12 active) -> one 48-byte atomic row per (tile, Gaussian)
-        for (int slot = t; slot < cnt * 16; slot += kTilePixels) {
-            const int e = slot >> 4, q = slot & 15;
-            if (q < 12) {
-                const float val = sG[e * 12 + q];
-                if (val != 0.0f) atomicAdd(&p.grad[(size_t)sId[e] * kGradStride + q], val);
+        for (int slot = t; slot < cnt * 16; slot += kRenderThreads) {
+            const int e = slot >> 4, c = slot & 15;
+            if (c < 12) {
+                const float val = sG[e * 12 + c];
+                if (val != 0.0f) atomicAdd(&p.grad[(size_t)sId[e] * kGradStride + c], val);
             }
         }
     }
@@ -320,7 +430,7 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
 hipError_t launch_render_backward(const RenderParams& p, int tiles, hipStream_t s)
 {
     if (tiles == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_render_backward, dim3(tiles), dim3(kTilePixels), 0, s, p);
+    hipLaunchKernelGGL(k_render_backward, dim3(tiles), dim3(kRenderThreads), 0, s, p);
     return hipGetLastError();
 }
 
