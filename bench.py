@@ -167,8 +167,9 @@ def main():
     gen = torch.Generator().manual_seed(100 + view)
     gt = torch.nn.functional.normalize(torch.randn((3, H, W), generator=gen), dim=0).to(dev)
     mask = (torch.rand((1, H, W), generator=gen) < 0.9).float().to(dev)
+    # scene/gaussian_model.py:229 Adam(lr=0.0, eps=1e-15); fused=True runs the same update as one kernel
     optim = torch.optim.Adam([{"params": [model._language_feature], "lr": 0.0025, "name": "language_feature"}],
-                             lr=0.0, eps=1e-15)
+                             lr=0.0, eps=1e-15, fused=True)
     bucket = GradBucket(model.trainable())
 
     def step():

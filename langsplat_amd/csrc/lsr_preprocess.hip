@@ -18,6 +18,34 @@ __device__ __forceinline__ void stage_sh_in(const float* __restrict__ shs, int P
     const int g0 = blockIdx.x * blockDim.x;
     const int n = min((int)blockDim.x, P - g0) * w;
     const float* src = shs + (size_t)g0 * w;
+    if ((w & 3) == 0 && (reinterpret_cast<uintptr_t>(src) & 15) == 0) {
+        // dwordx4 loads, all issued before the first LDS write (rows are w floats, w % 4 == 0,
+        // so no float4 straddles two rows)
+        constexpr int kMaxPer = 12;  // 256 x 48 floats / (256 threads x 4): M <= 16 in one sweep
+        const float4* s4 = reinterpret_cast<const float4*>(src);
+        const int n4 = n >> 2;
+        for (int k0 = 0; k0 < n4; k0 += kMaxPer * (int)blockDim.x) {
+            float4 r[kMaxPer];
+#pragma unroll
+            for (int u = 0; u < kMaxPer; u++) {
+                const int k = k0 + u * (int)blockDim.x + (int)threadIdx.x;
+                if (k < n4) r[u] = s4[k];
+            }
+#pragma unroll
+            for (int u = 0; u < kMaxPer; u++) {
+                const int k = k0 + u * (int)blockDim.x + (int)threadIdx.x;
+                if (k < n4) {
+                    const int e = 4 * k, gi = e / w;
+                    float* d = lds + gi * ws + (e - gi * w);
+                    d[0] = r[u].x;
+                    d[1] = r[u].y;
+                    d[2] = r[u].z;
+                    d[3] = r[u].w;
+                }
+            }
+        }
+        return;
+    }
     for (int k = threadIdx.x; k < n; k += blockDim.x) {
         const int gi = k / w;
         lds[gi * ws + (k - gi * w)] = src[k];
@@ -30,6 +58,15 @@ __device__ __forceinline__ void stage_sh_out(float* __restrict__ dst_all, int P,
     const int g0 = blockIdx.x * blockDim.x;
     const int n = min((int)blockDim.x, P - g0) * w;
     float* dst = dst_all + (size_t)g0 * w;
+    if ((w & 3) == 0 && (reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+        float4* d4 = reinterpret_cast<float4*>(dst);
+        for (int k = threadIdx.x; k < (n >> 2); k += blockDim.x) {
+            const int e = 4 * k, gi = e / w;
+            const float* sr = lds + gi * ws + (e - gi * w);
+            d4[k] = make_float4(sr[0], sr[1], sr[2], sr[3]);
+        }
+        return;
+    }
     for (int k = threadIdx.x; k < n; k += blockDim.x) {
         const int gi = k / w;
         dst[k] = lds[gi * ws + (k - gi * w)];
