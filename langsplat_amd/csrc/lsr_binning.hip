@@ -148,9 +148,13 @@ static hipError_t scan_exclusive(const uint32_t* in, uint32_t* out, int n, uint3
 // ---------------------------------------------------------------- stable LSD radix sort
 
 // Per-block digit histogram; hist layout [digit][block] so one scan yields the scatter bases.
+// kItems keys per thread: 16 for large sorts, 4 for P-sized ones (so that >= ~1000 blocks run).
+template <int kItems>
 __global__ __launch_bounds__(kRadixThreads) void k_radix_hist(const uint32_t* __restrict__ keys, int n, int shift,
                                                               int nbits, uint32_t* __restrict__ hist, int nblk)
 {
+    constexpr int kRadixTile = kRadixThreads * kItems;
+    constexpr int kRadixItems = kItems;
     __shared__ uint32_t h[256];
     const int t = threadIdx.x;
     const uint32_t mask = (1u << nbits) - 1u;
@@ -172,10 +176,13 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_hist(const uint32_t* __
 // (wave64 ballot match + per-wave digit counts), the block is reordered by digit in LDS, and the
 // output is written from LDS in digit-contiguous runs, so global stores coalesce (a direct scatter
 // would send the 64 lanes of a store to up to 64 different buckets).
+template <int kItems>
 __global__ __launch_bounds__(kRadixThreads) void k_radix_scatter(
     const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in, int n, int shift, int nbits,
     const uint32_t* __restrict__ hist, int nblk, uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out)
 {
+    constexpr int kRadixTile = kRadixThreads * kItems;
+    constexpr int kRadixItems = kItems;
     __shared__ uint32_t sk[kRadixTile];
     __shared__ uint32_t sv[kRadixTile];
     __shared__ uint32_t gbase[256];     // global output position of this block's first key per digit
@@ -260,7 +267,9 @@ static hipError_t radix_sort(const uint32_t* k0, const uint32_t* v0, int n, int 
                              uint32_t* vA, uint32_t* kB, uint32_t* vB, uint32_t* hist, uint32_t* scan_scratch,
                              hipStream_t s, bool debug, int* passes_out)
 {
-    const int nblk = (n + kRadixTile - 1) / kRadixTile;
+    const bool small = n <= (1 << 21);
+    const int tile = kRadixThreads * (small ? 4 : 16);
+    const int nblk = (n + tile - 1) / tile;
     const int passes = (total_bits + 7) / 8;
     *passes_out = passes;
     const uint32_t* kin = k0;
@@ -271,12 +280,19 @@ static hipError_t radix_sort(const uint32_t* k0, const uint32_t* v0, int n, int 
         const int nbits = (total_bits - shift) < 8 ? (total_bits - shift) : 8;
         uint32_t* kout = (pass & 1) ? kA : kB;
         uint32_t* vout = (pass & 1) ? vA : vB;
-        hipLaunchKernelGGL(k_radix_hist, dim3(nblk), dim3(kRadixThreads), 0, s, kin, n, shift, nbits, hist, nblk);
+        if (small)
+            hipLaunchKernelGGL(k_radix_hist<4>, dim3(nblk), dim3(kRadixThreads), 0, s, kin, n, shift, nbits, hist, nblk);
+        else
+            hipLaunchKernelGGL(k_radix_hist<16>, dim3(nblk), dim3(kRadixThreads), 0, s, kin, n, shift, nbits, hist, nblk);
         if ((e = post(debug, s)) != hipSuccess) return e;
         if ((e = scan_exclusive(hist, hist, (1 << nbits) * nblk, scan_scratch, nullptr, s, debug)) != hipSuccess)
             return e;
-        hipLaunchKernelGGL(k_radix_scatter, dim3(nblk), dim3(kRadixThreads), 0, s, kin, vin, n, shift, nbits, hist,
-                           nblk, kout, vout);
+        if (small)
+            hipLaunchKernelGGL(k_radix_scatter<4>, dim3(nblk), dim3(kRadixThreads), 0, s, kin, vin, n, shift, nbits,
+                               hist, nblk, kout, vout);
+        else
+            hipLaunchKernelGGL(k_radix_scatter<16>, dim3(nblk), dim3(kRadixThreads), 0, s, kin, vin, n, shift, nbits,
+                               hist, nblk, kout, vout);
         if ((e = post(debug, s)) != hipSuccess) return e;
         kin = kout;
         vin = vout;
@@ -284,7 +300,8 @@ static hipError_t radix_sort(const uint32_t* k0, const uint32_t* v0, int n, int 
     return hipSuccess;
 }
 
-size_t radix_hist_words(int64_t n) { return 256 * (size_t)((n + kRadixTile - 1) / kRadixTile); }
+// sized for the smallest tile (4 keys per thread) so either variant fits
+size_t radix_hist_words(int64_t n) { return 256 * (size_t)((n + 4 * kRadixThreads - 1) / (4 * kRadixThreads)); }
 size_t scan_scratch_words(int64_t n) { return (size_t)((n + kScanChunk - 1) / kScanChunk) + 1; }
 
 // ---------------------------------------------------------------- depth order + instance offsets

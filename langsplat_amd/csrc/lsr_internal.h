@@ -18,8 +18,6 @@ enum Counter : int {
 };
 
 constexpr int kRadixThreads = 256;
-constexpr int kRadixItems = 16;
-constexpr int kRadixTile = kRadixThreads * kRadixItems;  // keys per block per pass
 constexpr int kGradStride = 16;                          // floats per Gaussian grad record
 
 size_t radix_hist_words(int64_t n);   // per-block digit histograms for n keys
