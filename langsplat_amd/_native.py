@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import threading
 from typing import Dict, Optional
 
 import torch
@@ -131,25 +132,66 @@ def _stream(device: torch.device) -> ctypes.c_void_p:
 
 
 class _Allocator:
-    """Hands out torch uint8 device tensors for the ABI's scratch requests."""
+    """Hands out torch uint8 device tensors for the ABI's scratch requests.
+
+    One process-wide ctypes callback (creating a CFUNCTYPE per call costs more than the whole
+    binding); the allocator active on this thread is published through a thread-local.
+    """
+
+    _tls = threading.local()
 
     def __init__(self, device: torch.device):
         self.device = device
         self.buffers: Dict[int, torch.Tensor] = {}
 
-        def _cb(user, which, nbytes):
-            try:
-                t = torch.empty((max(int(nbytes), 1),), dtype=torch.uint8, device=self.device)
-            except Exception:  # noqa: BLE001 -- reported to C as NULL -> LSR_ERR_ALLOC
-                return None
-            self.buffers[int(which)] = t
-            return t.data_ptr()
+    def __enter__(self):
+        self._prev = getattr(_Allocator._tls, "active", None)
+        _Allocator._tls.active = self
+        return self
 
-        self.fn = ALLOC_FN(_cb)
+    def __exit__(self, *exc):
+        _Allocator._tls.active = self._prev
 
     def get(self, which: int) -> torch.Tensor:
         t = self.buffers.get(which)
         return t if t is not None else torch.empty((0,), dtype=torch.uint8, device=self.device)
+
+
+def _alloc_cb(user, which, nbytes):
+    a = getattr(_Allocator._tls, "active", None)
+    if a is None:
+        return None
+    try:
+        t = torch.empty((max(int(nbytes), 1),), dtype=torch.uint8, device=a.device)
+    except Exception:  # noqa: BLE001 -- reported to C as NULL -> LSR_ERR_ALLOC
+        return None
+    a.buffers[int(which)] = t
+    return t.data_ptr()
+
+
+_ALLOC_CB = ALLOC_FN(_alloc_cb)
+
+
+def _f32c(t: torch.Tensor) -> torch.Tensor:
+    if t.dtype != torch.float32:
+        t = t.to(torch.float32)
+    return t if t.is_contiguous() else t.contiguous()
+
+
+class _on_device:
+    """torch.cuda.device(...) only when it is not already the current device."""
+
+    def __init__(self, device: torch.device):
+        idx = device.index if device.index is not None else torch.cuda.current_device()
+        self.ctx = None if idx == torch.cuda.current_device() else torch.cuda.device(idx)
+
+    def __enter__(self):
+        if self.ctx is not None:
+            self.ctx.__enter__()
+
+    def __exit__(self, *exc):
+        if self.ctx is not None:
+            self.ctx.__exit__(*exc)
 
 
 def make_settings(rs, keep: list) -> LsrSettings:
@@ -165,7 +207,7 @@ def make_settings(rs, keep: list) -> LsrSettings:
     s.debug = int(bool(rs.debug))
     s.include_feature = int(bool(getattr(rs, "include_feature", False)))
     for name in ("bg", "viewmatrix", "projmatrix", "campos"):
-        t = getattr(rs, name).detach().to(torch.float32).contiguous()
+        t = _f32c(getattr(rs, name).detach())
         keep.append(t)
         setattr(s, name, t.data_ptr())
     return s
@@ -199,8 +241,8 @@ def rasterize_gaussians(rs, means3D, shs, colors_precomp, language_feature, opac
     a.radii = _ptr(radii)
     alloc = _Allocator(device)
     nr = ctypes.c_int64(0)
-    with torch.cuda.device(device):
-        _check(lib.lsr_forward(ctypes.byref(s), ctypes.byref(a), alloc.fn, None, _stream(device), ctypes.byref(nr)),
+    with _on_device(device), alloc:
+        _check(lib.lsr_forward(ctypes.byref(s), ctypes.byref(a), _ALLOC_CB, None, _stream(device), ctypes.byref(nr)),
                "lsr_forward")
     return (int(nr.value), color, lang, radii, alloc.get(LSR_BUF_GEOM), alloc.get(LSR_BUF_BINNING),
             alloc.get(LSR_BUF_IMAGE))
@@ -242,11 +284,11 @@ def rasterize_gaussians_backward(rs, means3D, shs, colors_precomp, language_feat
     a.rotations = _ptr(rotations)
     a.cov3D_precomp = _ptr(cov3D_precomp)
     a.radii = _ptr(radii)
-    gc = grad_color.detach().to(torch.float32).contiguous()
+    gc = _f32c(grad_color.detach())
     a.dL_dout_color = _ptr(gc)
     gl = None
     if grad_language is not None:
-        gl = grad_language.detach().to(torch.float32).contiguous()
+        gl = _f32c(grad_language.detach())
         a.dL_dout_language_feature = _ptr(gl)
     a.geom_buffer = _ptr(geom)
     a.binning_buffer = _ptr(binning)
@@ -261,8 +303,8 @@ def rasterize_gaussians_backward(rs, means3D, shs, colors_precomp, language_feat
     a.dL_dscales = _ptr(g["scales"])
     a.dL_drotations = _ptr(g["rotations"])
     alloc = _Allocator(device)
-    with torch.cuda.device(device):
-        _check(lib.lsr_backward(ctypes.byref(s), ctypes.byref(a), alloc.fn, None, _stream(device)), "lsr_backward")
+    with _on_device(device), alloc:
+        _check(lib.lsr_backward(ctypes.byref(s), ctypes.byref(a), _ALLOC_CB, None, _stream(device)), "lsr_backward")
     return g
 
 
@@ -271,10 +313,10 @@ def mark_visible(means3D, viewmatrix, projmatrix):
     device = means3D.device
     P = int(means3D.shape[0])
     vis = torch.zeros((P,), dtype=torch.uint8, device=device)
-    m = means3D.detach().to(torch.float32).contiguous()
-    v = viewmatrix.detach().to(torch.float32).contiguous()
-    p = projmatrix.detach().to(torch.float32).contiguous()
-    with torch.cuda.device(device):
+    m = _f32c(means3D.detach())
+    v = _f32c(viewmatrix.detach())
+    p = _f32c(projmatrix.detach())
+    with _on_device(device):
         _check(lib.lsr_mark_visible(P, _ptr(m), _ptr(v), _ptr(p), _ptr(vis), _stream(device)), "lsr_mark_visible")
     return vis.bool()
 

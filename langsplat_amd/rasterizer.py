@@ -39,11 +39,11 @@ class GaussianRasterizationSettings(NamedTuple):
 
 
 def _f32(t):
-    if t is None:
-        return None
-    if t.numel() == 0:
+    if t is None or t.numel() == 0:
         return t
-    return t.to(torch.float32).contiguous()
+    if t.dtype != torch.float32:
+        t = t.to(torch.float32)
+    return t if t.is_contiguous() else t.contiguous()
 
 
 def _cpu_deep_copy(args):
