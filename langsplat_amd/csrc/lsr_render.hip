@@ -30,8 +30,6 @@ __device__ __forceinline__ float power_cutoff(float o)
     return o > (1.0f / 255.0f) ? __logf(1.0f / (255.0f * o)) - 0.01f : 3.0e38f;
 }
 
-constexpr int kRenderThreads = 128;  // 2 wave64s per 16x16 tile, 2 pixels per lane
-constexpr int kBatch = 128;           // list entries staged in LDS per round (one per thread)
 
 // One pixel's front-to-back state (upstream FORWARD::renderCUDA locals).
 struct FwdPixel {
@@ -326,36 +324,41 @@ __device__ __forceinline__ void bwd_pixel_blend(BwdPixel& q, float G, float alph
     v[5] += G * dL_dalpha;
 }
 
-__global__ __launch_bounds__(kRenderThreads) void k_render_backward(RenderParams p)
+template <int kPix>
+__global__ __launch_bounds__(kTilePixels / kPix) void k_render_backward(RenderParams p)
 {
-    __shared__ float4 sA[kBatch];  // x, y, -0.5 conic.x, -0.5 conic.z
-    __shared__ float4 sB[kBatch];  // conic.y, opacity, power cutoff, -
-    __shared__ float4 sC[kBatch];  // r, g, b, f0
-    __shared__ float2 sD[kBatch];  // f1, f2
-    __shared__ uint32_t sId[kBatch];
-    __shared__ float sG[kBatch * 12];  // per-entry gradient sums of the tile (12 floats)
+    constexpr int kThreads = kTilePixels / kPix;
+    __shared__ float4 sA[kThreads];  // x, y, -0.5 conic.x, -0.5 conic.z
+    __shared__ float4 sB[kThreads];  // conic.y, opacity, power cutoff, -
+    __shared__ float4 sC[kThreads];  // r, g, b, f0
+    __shared__ float2 sD[kThreads];  // f1, f2
+    __shared__ uint32_t sId[kThreads];
+    __shared__ float sG[kThreads * 12];  // per-entry gradient sums of the tile (12 floats)
     __shared__ uint32_t s_max;
 
     const int tile = blockIdx.x;
     const int tx = tile % p.gx, ty = tile / p.gx;
     const int t = threadIdx.x, lane = t & 63;
     const int px = tx * kTile + (t & (kTile - 1));
-    const int py0 = ty * kTile + 2 * (t >> 4), py1 = py0 + 1;  // vertically adjacent pair
-    const bool in0 = px < p.W && py0 < p.H, in1 = px < p.W && py1 < p.H;
-    const float pfx = (float)px, pfy0 = (float)py0, pfy1 = (float)py1;
+    const int py_base = ty * kTile + kPix * (t >> 4);  // kPix vertically adjacent pixels per lane
+    const float pfx = (float)px;
     const size_t HW = (size_t)p.W * p.H;
     const uint32_t start = p.ranges[tile].x;
     const bool feat = p.include_feature != 0;
     const float ddelx_dx = 0.5f * (float)p.W, ddely_dy = 0.5f * (float)p.H;
 
-    BwdPixel q0, q1;
-    bwd_pixel_init(q0, p, in0, (size_t)py0 * p.W + px, HW, feat);
-    bwd_pixel_init(q1, p, in1, (size_t)py1 * p.W + px, HW, feat);
+    BwdPixel q[kPix];
+    uint32_t wmax = 0;
+#pragma unroll
+    for (int k = 0; k < kPix; k++) {
+        const int py = py_base + k;
+        bwd_pixel_init(q[k], p, px < p.W && py < p.H, (size_t)py * p.W + px, HW, feat);
+        wmax = max(wmax, q[k].last);
+    }
 
     // entries at list index >= max over the tile of n_contrib can contribute to no pixel
     if (t == 0) s_max = 0;
     __syncthreads();
-    uint32_t wmax = max(q0.last, q1.last);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) wmax = max(wmax, (uint32_t)__shfl_xor((int)wmax, o, 64));
     if (lane == 0) atomicMax(&s_max, wmax);
@@ -364,52 +367,62 @@ __global__ __launch_bounds__(kRenderThreads) void k_render_backward(RenderParams
     const int wave_max = (int)wmax;  // entries at index >= this touch no pixel of this wave
     const int vidx = scatter_index(lane);
 
-    for (int done_cnt = 0; done_cnt < maxl; done_cnt += kBatch) {
+    for (int done_cnt = 0; done_cnt < maxl; done_cnt += kThreads) {
         __syncthreads();
-#pragma unroll
-        for (int h = 0; h < kBatch / kRenderThreads; h++) {
-            const int slot = t + h * kRenderThreads;
-            const int k = maxl - 1 - (done_cnt + slot);
-            if (k >= 0) {
-                const uint32_t g = p.point_list[start + (uint32_t)k];
-                const float4 a = p.record[3 * (size_t)g];
-                const float4 b = p.record[3 * (size_t)g + 1];
-                const float4 c = p.record[3 * (size_t)g + 2];
-                sA[slot] = make_float4(a.x, a.y, -0.5f * a.z, -0.5f * b.x);
-                sB[slot] = make_float4(a.w, b.y, power_cutoff(b.y), 0.0f);
-                sC[slot] = make_float4(b.z, b.w, c.x, c.y);
-                sD[slot] = make_float2(c.z, c.w);
-                sId[slot] = g;
-            }
+        const int kload = maxl - 1 - (done_cnt + t);
+        if (kload >= 0) {
+            const uint32_t g = p.point_list[start + (uint32_t)kload];
+            const float4 a = p.record[3 * (size_t)g];
+            const float4 b = p.record[3 * (size_t)g + 1];
+            const float4 c = p.record[3 * (size_t)g + 2];
+            sA[t] = make_float4(a.x, a.y, -0.5f * a.z, -0.5f * b.x);
+            sB[t] = make_float4(a.w, b.y, power_cutoff(b.y), 0.0f);
+            sC[t] = make_float4(b.z, b.w, c.x, c.y);
+            sD[t] = make_float2(c.z, c.w);
+            sId[t] = g;
         }
-        for (int i = t; i < kBatch * 12; i += kRenderThreads) sG[i] = 0.f;
+        for (int i = t; i < kThreads * 12; i += kThreads) sG[i] = 0.f;
         __syncthreads();
-        const int cnt = min(kBatch, maxl - done_cnt);
+        const int cnt = min(kThreads, maxl - done_cnt);
         for (int j = 0; j < cnt; j++) {
             const int kk = maxl - 1 - (done_cnt + j);  // list index of this entry
             if (kk >= wave_max) continue;              // wave-uniform
             const float4 A = sA[j];
             const float4 B = sB[j];
-            const float dx = A.x - pfx, dy0 = A.y - pfy0, dy1 = A.y - pfy1;
-            const float p0 = fma_(A.z * dx, dx, fma_(A.w * dy0, dy0, -((B.x * dx) * dy0)));
-            const float p1 = fma_(A.z * dx, dx, fma_(A.w * dy1, dy1, -((B.x * dx) * dy1)));
-            bool h0 = kk < (int)q0.last && p0 <= 0.0f && p0 >= B.z;
-            bool h1 = kk < (int)q1.last && p1 <= 0.0f && p1 >= B.z;
-            if (__ballot(h0 || h1) == 0ull) continue;  // wave-uniform skip
+            const float dx = A.x - pfx;
+            float pw[kPix];
+            bool h[kPix];
+            bool any = false;
+#pragma unroll
+            for (int k = 0; k < kPix; k++) {
+                const float dy = A.y - (float)(py_base + k);
+                pw[k] = fma_(A.z * dx, dx, fma_(A.w * dy, dy, -((B.x * dx) * dy)));
+                h[k] = kk < (int)q[k].last && pw[k] <= 0.0f && pw[k] >= B.z;
+                any = any || h[k];
+            }
+            if (__ballot(any) == 0ull) continue;  // wave-uniform skip
             float v[12];
 #pragma unroll
             for (int c = 0; c < 12; c++) v[c] = 0.f;
-            if (h0 || h1) {
-                const float G0 = expf_exact(p0), G1 = expf_exact(p1);
-                const float a0 = fminf(0.99f, B.y * G0), a1 = fminf(0.99f, B.y * G1);
-                h0 = h0 && a0 >= 1.0f / 255.0f;
-                h1 = h1 && a1 >= 1.0f / 255.0f;
-                if (h0 || h1) {
+            if (any) {
+                float G[kPix], al[kPix];
+                bool any2 = false;
+#pragma unroll
+                for (int k = 0; k < kPix; k++) {
+                    G[k] = expf_exact(pw[k]);
+                    al[k] = fminf(0.99f, B.y * G[k]);
+                    h[k] = h[k] && al[k] >= 1.0f / 255.0f;
+                    any2 = any2 || h[k];
+                }
+                if (any2) {
                     const float4 Cc = sC[j];
                     const float2 D = sD[j];
                     const float cx = -2.0f * A.z, cz = -2.0f * A.w;
-                    if (h0) bwd_pixel_blend(q0, G0, a0, dx, dy0, B, cx, cz, Cc, D, feat, ddelx_dx, ddely_dy, v);
-                    if (h1) bwd_pixel_blend(q1, G1, a1, dx, dy1, B, cx, cz, Cc, D, feat, ddelx_dx, ddely_dy, v);
+#pragma unroll
+                    for (int k = 0; k < kPix; k++)
+                        if (h[k])
+                            bwd_pixel_blend(q[k], G[k], al[k], dx, A.y - (float)(py_base + k), B, cx, cz, Cc, D,
+                                            feat, ddelx_dx, ddely_dy, v);
                 }
             }
             const float tot = wave_reduce_scatter12(v, lane);
@@ -417,7 +430,7 @@ __global__ __launch_bounds__(kRenderThreads) void k_render_backward(RenderParams
         }
         __syncthreads();
         // flush: 16 lanes per entry (12 active) -> one 48-byte atomic row per (tile, Gaussian)
-        for (int slot = t; slot < cnt * 16; slot += kRenderThreads) {
+        for (int slot = t; slot < cnt * 16; slot += kThreads) {
             const int e = slot >> 4, c = slot & 15;
             if (c < 12) {
                 const float val = sG[e * 12 + c];
@@ -427,10 +440,24 @@ __global__ __launch_bounds__(kRenderThreads) void k_render_backward(RenderParams
     }
 }
 
+// LSR_BWD_PIXELS=1|2 selects the backward variant (measurement aid; default 1: 0.52 vs 0.58 ms at
+// C3 -- with ~2300 busy tiles the chip is short of waves, so more waves per tile beat more ILP)
+static int bwd_pixels_per_lane()
+{
+    static int v = [] {
+        const char* e = getenv("LSR_BWD_PIXELS");
+        return (e && e[0] == '2') ? 2 : 1;
+    }();
+    return v;
+}
+
 hipError_t launch_render_backward(const RenderParams& p, int tiles, hipStream_t s)
 {
     if (tiles == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_render_backward, dim3(tiles), dim3(kRenderThreads), 0, s, p);
+    if (bwd_pixels_per_lane() == 1)
+        hipLaunchKernelGGL(k_render_backward<1>, dim3(tiles), dim3(kTilePixels), 0, s, p);
+    else
+        hipLaunchKernelGGL(k_render_backward<2>, dim3(tiles), dim3(kTilePixels / 2), 0, s, p);
     return hipGetLastError();
 }
 
