@@ -113,6 +113,27 @@ def algorithmic_bytes(stage, P, V, R, HW, M):
     }.get(stage)
 
 
+STAGE_KERNEL = {"render backward": "lsr::k_render_backward", "render forward": "lsr::k_render_forward",
+                "preprocess": "lsr::k_preprocess", "preprocess backward": "lsr::k_preprocess_backward"}
+
+
+def pmc_traffic(stage):
+    """HBM bytes per launch of the stage's kernel from the newest committed rocprofv3 PMC summary
+    (profiles/*_summary.json, tools/prof_summary.py: FETCH_SIZE x2 + WRITE_SIZE, gfx950 correction),
+    or (None, None) when no profile covers it."""
+    import glob
+    kern = STAGE_KERNEL.get(stage)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_summary.json")), key=os.path.getmtime)
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))["kernels"].get(kern, {})
+        except (OSError, ValueError, KeyError):
+            continue
+        if "hbm_bytes_per_launch" in d:
+            return float(d["hbm_bytes_per_launch"]), os.path.relpath(f, ROOT)
+    return None, None
+
+
 def cpu_baseline(cfg, seconds_budget=25.0):
     """Oracle (oracle/lsr_oracle.c, 1 thread) fwd+bwd on a bounded sample of the same workload:
     the first P/4 Gaussians of the C3 scene, same camera and resolution."""
@@ -241,8 +262,10 @@ def main():
     roofline = None
     if bytes_dom is not None:
         achieved = bytes_dom / (dom["avg_ms"] * 1e-3) / 1e9
+        traffic, src = pmc_traffic(dom_name)
         roofline = {"bound": "hbm", "kernel": dom_name, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+                    "traffic": None if traffic is None else int(traffic), "traffic_source": src,
                     "avg_ms": round(dom["avg_ms"], 4), "bytes_per_launch": int(bytes_dom)}
     cpu = None
     if world == 1 and not args.no_cpu_baseline:

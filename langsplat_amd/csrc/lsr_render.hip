@@ -30,6 +30,49 @@ __device__ __forceinline__ float power_cutoff(float o)
     return o > (1.0f / 255.0f) ? __logf(1.0f / (255.0f * o)) - 0.01f : 3.0e38f;
 }
 
+// Screen box of the pixels an entry can reach: power >= cut is the ellipse d^T Q d <= -2 cut
+// (Q = conic), whose half-extents are sqrt(-2 cut (Q^-1)_xx) and sqrt(-2 cut (Q^-1)_yy); widened by
+// a conservative margin (0.1% + 0.05 px >> fp32 error of the power evaluation).  Returns
+// (xmin, xmax, ymin, ymax); empty for entries that always skip, unbounded if Q is degenerate.
+// Waves cull a batch against their own pixel rectangle with it: an entry whose box misses the
+// rectangle fails the cutoff test in every lane, so skipping it is exact.
+__device__ __forceinline__ float4 entry_box(float x, float y, float cx, float cy, float cz, float cut)
+{
+    const float k = -2.0f * cut;
+    if (!(k > 0.0f)) return make_float4(3.0e38f, -3.0e38f, 3.0e38f, -3.0e38f);
+    const float detq = cx * cz - cy * cy;
+    if (!(detq > 0.0f)) return make_float4(-3.0e38f, 3.0e38f, -3.0e38f, 3.0e38f);
+    const float ex = sqrtf(k * cz / detq) * 1.001f + 0.05f;
+    const float ey = sqrtf(k * cx / detq) * 1.001f + 0.05f;
+    return make_float4(x - ex, x + ex, y - ey, y + ey);
+}
+
+__device__ __forceinline__ uint64_t lanemask_lt64(int lane)
+{
+    return lane == 0 ? 0ull : (~0ull >> (64 - lane));
+}
+
+// Compacts the batch slots [0, cnt) whose box overlaps the wave's pixel rectangle (and, for the
+// backward, whose list index is below the wave's contributor bound) into list[0, n); returns n.
+template <typename Keep>
+__device__ __forceinline__ int wave_compact(const float4* sE, int cnt, float wx0, float wx1, float wy0, float wy1,
+                                            int lane, uint16_t* list, Keep keep)
+{
+    int n = 0;
+    for (int r = 0; r < cnt; r += 64) {
+        const int e = r + lane;
+        bool ov = false;
+        if (e < cnt && keep(e)) {
+            const float4 E = sE[e];
+            ov = E.y >= wx0 && E.x <= wx1 && E.w >= wy0 && E.z <= wy1;
+        }
+        const uint64_t m = __ballot(ov);
+        if (ov) list[n + __popcll(m & lanemask_lt64(lane))] = (uint16_t)e;
+        n += __popcll(m);
+    }
+    return n;
+}
+
 
 // One pixel's front-to-back state (upstream FORWARD::renderCUDA locals).
 struct FwdPixel {
@@ -45,17 +88,23 @@ template <int kPix>
 __global__ __launch_bounds__(kTilePixels / kPix) void k_render_forward(RenderParams p)
 {
     constexpr int kThreads = kTilePixels / kPix;
+    constexpr int kWaves = kThreads / 64;
     __shared__ float4 sA[kThreads];  // x, y, -0.5 conic.x, -0.5 conic.z
     __shared__ float4 sB[kThreads];  // conic.y, opacity, power cutoff, -
     __shared__ float4 sC[kThreads];  // r, g, b, f0
     __shared__ float2 sD[kThreads];  // f1, f2
+    __shared__ float4 sE[kThreads];  // reach box (entry_box)
+    __shared__ uint16_t sL[kWaves][kThreads];  // per-wave culled slot lists
 
     const int tile = blockIdx.x;
     const int tx = tile % p.gx, ty = tile / p.gx;
-    const int t = threadIdx.x;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int px = tx * kTile + (t & (kTile - 1));
     const int py_base = ty * kTile + kPix * (t >> 4);
     const float pfx = (float)px;
+    // the wave's pixel rectangle: 16 columns x 4 kPix rows
+    const float wx0 = (float)(tx * kTile), wx1 = wx0 + (float)(kTile - 1);
+    const float wy0 = (float)(ty * kTile + 4 * kPix * wave), wy1 = wy0 + (float)(4 * kPix - 1);
     const uint2 range = p.ranges[tile];
     const uint32_t start = range.x, end = range.y;
     const bool feat = p.include_feature != 0;
@@ -76,14 +125,21 @@ __global__ __launch_bounds__(kTilePixels / kPix) void k_render_forward(RenderPar
             const float4 a = p.record[3 * (size_t)g];
             const float4 b = p.record[3 * (size_t)g + 1];
             const float4 c = p.record[3 * (size_t)g + 2];
+            const float cut = power_cutoff(b.y);
             sA[t] = make_float4(a.x, a.y, -0.5f * a.z, -0.5f * b.x);
-            sB[t] = make_float4(a.w, b.y, power_cutoff(b.y), 0.0f);
+            sB[t] = make_float4(a.w, b.y, cut, 0.0f);
             sC[t] = make_float4(b.z, b.w, c.x, c.y);
             sD[t] = make_float2(c.z, c.w);
+            sE[t] = entry_box(a.x, a.y, a.z, a.w, b.x, cut);
         }
         __syncthreads();
         const int cnt = (int)min((uint32_t)kThreads, end - base);
-        for (int j = 0; j < cnt && !all_done; j++) {
+        const int n = wave_compact(sE, cnt, wx0, wx1, wy0, wy1, lane, sL[wave], [](int) { return true; });
+        __syncthreads();  // list visible to the wave's other lanes
+        const uint32_t list_base = base - start;  // list index of slot 0
+        for (int i = 0; i < n && !all_done; i++) {
+            const int j = sL[wave][i];
+            const uint32_t contributor = list_base + (uint32_t)j + 1u;  // upstream's 1-based counter
             const float4 A = sA[j];
             const float4 B = sB[j];
             const float dx = A.x - pfx;
@@ -92,7 +148,6 @@ __global__ __launch_bounds__(kTilePixels / kPix) void k_render_forward(RenderPar
             bool any = false;
 #pragma unroll
             for (int k = 0; k < kPix; k++) {
-                q[k].contributor += q[k].done ? 0u : 1u;
                 const float dy = A.y - (float)(py_base + k);
                 pw[k] = fma_(A.z * dx, dx, fma_(A.w * dy, dy, -((B.x * dx) * dy)));
                 ok[k] = !q[k].done && !(pw[k] > 0.0f || pw[k] < B.z);
@@ -128,7 +183,7 @@ __global__ __launch_bounds__(kTilePixels / kPix) void k_render_forward(RenderPar
                         q[k].F2 = fma_(D.y, w, q[k].F2);
                     }
                     q[k].T = pw[k];
-                    q[k].last = q[k].contributor;
+                    q[k].last = contributor;
                 }
             }
             all_done = true;
@@ -334,13 +389,17 @@ __global__ __launch_bounds__(kTilePixels / kPix) void k_render_backward(RenderPa
     __shared__ float2 sD[kThreads];  // f1, f2
     __shared__ uint32_t sId[kThreads];
     __shared__ float sG[kThreads * 12];  // per-entry gradient sums of the tile (12 floats)
+    __shared__ float4 sE[kThreads];      // reach box (entry_box)
+    __shared__ uint16_t sL[kThreads / 64][kThreads];  // per-wave culled slot lists
     __shared__ uint32_t s_max;
 
     const int tile = blockIdx.x;
     const int tx = tile % p.gx, ty = tile / p.gx;
-    const int t = threadIdx.x, lane = t & 63;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int px = tx * kTile + (t & (kTile - 1));
     const int py_base = ty * kTile + kPix * (t >> 4);  // kPix vertically adjacent pixels per lane
+    const float wx0 = (float)(tx * kTile), wx1 = wx0 + (float)(kTile - 1);
+    const float wy0 = (float)(ty * kTile + 4 * kPix * wave), wy1 = wy0 + (float)(4 * kPix - 1);
     const float pfx = (float)px;
     const size_t HW = (size_t)p.W * p.H;
     const uint32_t start = p.ranges[tile].x;
@@ -375,18 +434,24 @@ __global__ __launch_bounds__(kTilePixels / kPix) void k_render_backward(RenderPa
             const float4 a = p.record[3 * (size_t)g];
             const float4 b = p.record[3 * (size_t)g + 1];
             const float4 c = p.record[3 * (size_t)g + 2];
+            const float cut = power_cutoff(b.y);
             sA[t] = make_float4(a.x, a.y, -0.5f * a.z, -0.5f * b.x);
-            sB[t] = make_float4(a.w, b.y, power_cutoff(b.y), 0.0f);
+            sB[t] = make_float4(a.w, b.y, cut, 0.0f);
             sC[t] = make_float4(b.z, b.w, c.x, c.y);
             sD[t] = make_float2(c.z, c.w);
+            sE[t] = entry_box(a.x, a.y, a.z, a.w, b.x, cut);
             sId[t] = g;
         }
         for (int i = t; i < kThreads * 12; i += kThreads) sG[i] = 0.f;
         __syncthreads();
         const int cnt = min(kThreads, maxl - done_cnt);
-        for (int j = 0; j < cnt; j++) {
+        // entries at list index >= wave_max touch no pixel of this wave
+        const int n = wave_compact(sE, cnt, wx0, wx1, wy0, wy1, lane, sL[wave],
+                                   [&](int e) { return maxl - 1 - (done_cnt + e) < wave_max; });
+        __syncthreads();  // list visible to the wave's other lanes
+        for (int i = 0; i < n; i++) {
+            const int j = sL[wave][i];
             const int kk = maxl - 1 - (done_cnt + j);  // list index of this entry
-            if (kk >= wave_max) continue;              // wave-uniform
             const float4 A = sA[j];
             const float4 B = sB[j];
             const float dx = A.x - pfx;
