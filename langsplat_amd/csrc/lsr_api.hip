@@ -209,6 +209,8 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
     pp.clamped = reinterpret_cast<uint32_t*>(geom + L.clamped);
     pp.record = reinterpret_cast<float4*>(geom + L.record);
     pp.counters = counters;
+    pp.zero = reinterpret_cast<uint32_t*>(geom + L.scan_regions);
+    pp.zero_words = (int)(kDepthScans * L.scan_region_geom);
     LSR_TRY(launch_preprocess(pp, stream), "preprocess");
     LSR_TRY(launch_depth_order(P, L, geom, counters, stream, debug), "depth order");
 
@@ -216,6 +218,7 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
     uint32_t host_cnt[4] = {0, 0, 0, 0};
     LSR_TRY(hipMemcpyAsync(host_cnt, counters, sizeof(host_cnt), hipMemcpyDeviceToHost, stream), "read counters");
     LSR_TRY(hipStreamSynchronize(stream), "synchronize");
+    if (host_cnt[kCntScanFault]) return fail(LSR_ERR_HIP, "lsr_forward: scan look-back stalled");
     if (host_cnt[kCntError] && s->prefiltered)
         return fail(LSR_ERR_PREFILTERED, "lsr_forward: prefiltered=True but a Gaussian is outside the frustum");
     const int64_t R = host_cnt[kCntRendered];

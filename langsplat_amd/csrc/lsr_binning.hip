@@ -13,7 +13,7 @@
 //   5. tile ranges from the boundaries of the sorted tile keys.
 //
 // Every step is deterministic, so point_list is bit-identical to the oracle's (tile, depth, id)
-// sort.  Scans are multi-block (reduce / scan of block sums / downsweep).
+// sort.  Scans are single-pass chained scans with decoupled look-back (one launch each).
 #include "lsr_internal.h"
 
 namespace lsr {
@@ -73,75 +73,124 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* w
     return before + x - v;
 }
 
-__global__ __launch_bounds__(kScanThreads) void k_scan_reduce(const uint32_t* __restrict__ data, int n,
-                                                              uint32_t* __restrict__ block_sums)
+// Single-pass chained scan with decoupled look-back.  Chunk ids come from an atomic ticket, so
+// every predecessor of a running chunk has already been scheduled (no dispatch-order assumption,
+// no deadlock).  Each chunk publishes {flag, value} in ONE 64-bit word (one sc1 store), so the
+// hand-off needs no fences: flag 1 = chunk aggregate, flag 2 = inclusive prefix.  Wave 0 looks
+// back over a window of 64 predecessors per hop.  The status words and the ticket must be zero
+// at launch; launch_preprocess / k_emit clear them (no memset launches).
+constexpr uint64_t kFlagAgg = 1ull << 62;
+constexpr uint64_t kFlagInc = 2ull << 62;
+constexpr uint32_t kMaxSpins = 1u << 24;  // a safety bound only; a stalled look-back flags kCntScanFault
+
+__host__ __device__ inline int scan_blocks(int n) { return (n + kScanChunk - 1) / kScanChunk; }
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v)
 {
-    __shared__ uint32_t wsum[kScanThreads / 64];
-    const int i0 = blockIdx.x * kScanChunk + threadIdx.x * kScanItems;
-    uint32_t s = 0;
 #pragma unroll
-    for (int k = 0; k < kScanItems; k++) s += (i0 + k < n) ? data[i0 + k] : 0u;
-    uint32_t tot;
-    block_exclusive_scan(s, wsum, &tot);
-    if (threadIdx.x == 0) block_sums[blockIdx.x] = tot;
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
 }
 
-// single block: exclusive scan of nb block sums in place (nb arbitrary), total to *total
-__global__ __launch_bounds__(kScanThreads) void k_scan_sums(uint32_t* __restrict__ sums, int nb,
-                                                            uint32_t* __restrict__ total)
+__global__ __launch_bounds__(kScanThreads) void k_scan(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+                                                       int n, uint64_t* __restrict__ status,
+                                                       uint32_t* __restrict__ total, uint32_t* __restrict__ fault)
 {
     __shared__ uint32_t wsum[kScanThreads / 64];
-    uint32_t carry = 0;
-    for (int base = 0; base < nb; base += kScanThreads) {
-        const int i = base + threadIdx.x;
-        const uint32_t v = i < nb ? sums[i] : 0u;
-        uint32_t tot;
-        const uint32_t ex = block_exclusive_scan(v, wsum, &tot);
-        if (i < nb) sums[i] = carry + ex;
-        carry += tot;
-    }
-    if (threadIdx.x == 0 && total) *total = carry;
-}
-
-__global__ __launch_bounds__(kScanThreads) void k_scan_down(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
-                                                            int n, const uint32_t* __restrict__ block_sums,
-                                                            uint32_t* __restrict__ last_slot)
-{
-    __shared__ uint32_t wsum[kScanThreads / 64];
-    const int i0 = blockIdx.x * kScanChunk + threadIdx.x * kScanItems;
+    __shared__ uint32_t s_chunk, s_prefix;
+    const int nchunks = scan_blocks(n);
+    uint32_t* ticket = reinterpret_cast<uint32_t*>(status + nchunks);
+    if (threadIdx.x == 0) s_chunk = atomicAdd(ticket, 1u);
+    __syncthreads();
+    const int c = (int)s_chunk;
+    const int i0 = c * kScanChunk + threadIdx.x * kScanItems;
     uint32_t v[kScanItems];
-    uint32_t s = 0;
+    if (i0 + kScanItems <= n) {
+        const uint4* src = reinterpret_cast<const uint4*>(in + i0);
 #pragma unroll
-    for (int k = 0; k < kScanItems; k++) {
-        v[k] = (i0 + k < n) ? in[i0 + k] : 0u;
-        s += v[k];
-    }
-    uint32_t tot;
-    uint32_t run = block_sums[blockIdx.x] + block_exclusive_scan(s, wsum, &tot);
+        for (int q = 0; q < kScanItems / 4; q++) {
+            const uint4 w = src[q];
+            v[4 * q] = w.x;
+            v[4 * q + 1] = w.y;
+            v[4 * q + 2] = w.z;
+            v[4 * q + 3] = w.w;
+        }
+    } else {
 #pragma unroll
-    for (int k = 0; k < kScanItems; k++) {
-        if (i0 + k < n) out[i0 + k] = run;
-        run += v[k];
+        for (int k = 0; k < kScanItems; k++) v[k] = (i0 + k < n) ? in[i0 + k] : 0u;
     }
-    if (last_slot && i0 < n && i0 + kScanItems >= n) *last_slot = run;  // = grand total
+    uint32_t sum = 0;
+#pragma unroll
+    for (int k = 0; k < kScanItems; k++) sum += v[k];
+    uint32_t agg;
+    const uint32_t ex = block_exclusive_scan(sum, wsum, &agg);
+    if (threadIdx.x < 64) {
+        const int lane = threadIdx.x;
+        uint32_t prefix = 0;
+        if (c == 0) {
+            if (lane == 0) __hip_atomic_store(&status[0], kFlagInc | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            if (lane == 0) __hip_atomic_store(&status[c], kFlagAgg | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            int top = c - 1;
+            uint32_t spins = 0;
+            for (;;) {
+                const int idx = top - lane;
+                const uint64_t w = idx >= 0
+                    ? __hip_atomic_load(&status[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kFlagInc;
+                const uint32_t flag = (uint32_t)(w >> 62);
+                const uint64_t inc = __ballot(flag == 2u);
+                const int k = inc ? __ffsll((unsigned long long)inc) - 1 : 63;  // nearest inclusive
+                const uint64_t upto = k == 63 ? ~0ull : ((2ull << k) - 1ull);
+                if (__ballot(flag == 0u) & upto) {                             // a predecessor is not ready
+                    if (++spins > kMaxSpins) {
+                        if (lane == 0) atomicOr(fault, 1u);
+                        break;
+                    }
+                    continue;
+                }
+                prefix += wave_sum(lane <= k ? (uint32_t)w : 0u);
+                if (inc) break;
+                top -= 64;
+            }
+            if (lane == 0)
+                __hip_atomic_store(&status[c], kFlagInc | (uint64_t)(prefix + agg), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (lane == 0) {
+            s_prefix = prefix;
+            if (total && c == nchunks - 1) *total = prefix + agg;
+        }
+    }
+    __syncthreads();
+    uint32_t run = s_prefix + ex;
+    if (i0 + kScanItems <= n) {
+        uint4* dst = reinterpret_cast<uint4*>(out + i0);
+#pragma unroll
+        for (int q = 0; q < kScanItems / 4; q++) {
+            uint4 w;
+            w.x = run; run += v[4 * q];
+            w.y = run; run += v[4 * q + 1];
+            w.z = run; run += v[4 * q + 2];
+            w.w = run; run += v[4 * q + 3];
+            dst[q] = w;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < kScanItems; k++) {
+            if (i0 + k < n) out[i0 + k] = run;
+            run += v[k];
+        }
+    }
 }
-
-int scan_blocks(int n) { return (n + kScanChunk - 1) / kScanChunk; }
 
 // out[i] = sum(in[0..i)); if total != null it receives the grand total.  `in` may equal `out`.
-// scratch: scan_blocks(n) words.
-static hipError_t scan_exclusive(const uint32_t* in, uint32_t* out, int n, uint32_t* scratch, uint32_t* total,
-                                 hipStream_t s, bool debug)
+// region: scan_region_words(n) zeroed words (status per chunk + ticket).
+static hipError_t scan_exclusive(const uint32_t* in, uint32_t* out, int n, uint32_t* region, uint32_t* total,
+                                 uint32_t* fault, hipStream_t s, bool debug)
 {
     if (n <= 0) return hipSuccess;
-    const int nb = scan_blocks(n);
-    hipError_t e;
-    hipLaunchKernelGGL(k_scan_reduce, dim3(nb), dim3(kScanThreads), 0, s, in, n, scratch);
-    if ((e = post(debug, s)) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(kScanThreads), 0, s, scratch, nb, total);
-    if ((e = post(debug, s)) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_scan_down, dim3(nb), dim3(kScanThreads), 0, s, in, out, n, (const uint32_t*)scratch,
-                       (uint32_t*)nullptr);
+    hipLaunchKernelGGL(k_scan, dim3(scan_blocks(n)), dim3(kScanThreads), 0, s, in, out, n,
+                       reinterpret_cast<uint64_t*>(region), total, fault);
     return post(debug, s);
 }
 
@@ -264,8 +313,8 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_scatter(
 // from (k0, v0) (v0 == null: values are the input indices) and the result lands in
 // (kA, vA) after an even number of passes, or in (kB, vB) after an odd number; returns which.
 static hipError_t radix_sort(const uint32_t* k0, const uint32_t* v0, int n, int total_bits, uint32_t* kA,
-                             uint32_t* vA, uint32_t* kB, uint32_t* vB, uint32_t* hist, uint32_t* scan_scratch,
-                             hipStream_t s, bool debug, int* passes_out)
+                             uint32_t* vA, uint32_t* kB, uint32_t* vB, uint32_t* hist, uint32_t* scan_regions,
+                             size_t region_words, uint32_t* fault, hipStream_t s, bool debug, int* passes_out)
 {
     const bool small = n <= (1 << 21);
     const int tile = kRadixThreads * (small ? 4 : 16);
@@ -285,7 +334,8 @@ static hipError_t radix_sort(const uint32_t* k0, const uint32_t* v0, int n, int 
         else
             hipLaunchKernelGGL(k_radix_hist<16>, dim3(nblk), dim3(kRadixThreads), 0, s, kin, n, shift, nbits, hist, nblk);
         if ((e = post(debug, s)) != hipSuccess) return e;
-        if ((e = scan_exclusive(hist, hist, (1 << nbits) * nblk, scan_scratch, nullptr, s, debug)) != hipSuccess)
+        if ((e = scan_exclusive(hist, hist, (1 << nbits) * nblk, scan_regions + pass * region_words, nullptr, fault,
+                                s, debug)) != hipSuccess)
             return e;
         if (small)
             hipLaunchKernelGGL(k_radix_scatter<4>, dim3(nblk), dim3(kRadixThreads), 0, s, kin, vin, n, shift, nbits,
@@ -302,7 +352,8 @@ static hipError_t radix_sort(const uint32_t* k0, const uint32_t* v0, int n, int 
 
 // sized for the smallest tile (4 keys per thread) so either variant fits
 size_t radix_hist_words(int64_t n) { return 256 * (size_t)((n + 4 * kRadixThreads - 1) / (4 * kRadixThreads)); }
-size_t scan_scratch_words(int64_t n) { return (size_t)((n + kScanChunk - 1) / kScanChunk) + 1; }
+// one u64 status word per chunk + the u64 ticket slot, in u32 words
+size_t scan_region_words(int64_t n) { return 2 * (size_t)((n + kScanChunk - 1) / kScanChunk) + 2; }
 
 // ---------------------------------------------------------------- depth order + instance offsets
 
@@ -318,21 +369,23 @@ hipError_t launch_depth_order(int P, const Layout& L, char* geom, uint32_t* coun
 {
     if (P == 0) return hipSuccess;
     uint32_t* hist = reinterpret_cast<uint32_t*>(geom + L.radix_hist);
-    uint32_t* scratch = reinterpret_cast<uint32_t*>(geom + L.scan_scratch);
+    uint32_t* regions = reinterpret_cast<uint32_t*>(geom + L.scan_regions);
+    uint32_t* fault = counters + kCntScanFault;
     uint32_t* ka = reinterpret_cast<uint32_t*>(geom + L.keys_a);
     uint32_t* kb = reinterpret_cast<uint32_t*>(geom + L.keys_b);
     uint32_t* va = reinterpret_cast<uint32_t*>(geom + L.sorted_ids);
     uint32_t* vb = reinterpret_cast<uint32_t*>(geom + L.vals_b);
     int passes = 0;
     hipError_t e = radix_sort(reinterpret_cast<const uint32_t*>(geom + L.depth_key), nullptr, P, 32, ka, va, kb, vb,
-                              hist, scratch, s, debug, &passes);
+                              hist, regions, L.scan_region_geom, fault, s, debug, &passes);
     if (e != hipSuccess) return e;
     // 4 passes: the ids are in sorted_ids (va)
     uint32_t* off = reinterpret_cast<uint32_t*>(geom + L.inst_offset);
     hipLaunchKernelGGL(k_gather_tiles, dim3((P + 255) / 256), dim3(256), 0, s, P, va,
                        reinterpret_cast<const uint32_t*>(geom + L.tiles_touched), off);
     if ((e = post(debug, s)) != hipSuccess) return e;
-    return scan_exclusive(off, off, P, scratch, counters + kCntRendered, s, debug);
+    return scan_exclusive(off, off, P, regions + passes * L.scan_region_geom, counters + kCntRendered, fault, s,
+                          debug);
 }
 
 // ---------------------------------------------------------------- emit + tile sort + ranges
@@ -340,9 +393,14 @@ hipError_t launch_depth_order(int P, const Layout& L, char* geom, uint32_t* coun
 __global__ __launch_bounds__(256) void k_emit(int P, int gx, const uint32_t* __restrict__ sorted_ids,
                                               const uint32_t* __restrict__ inst_offset,
                                               const uint32_t* __restrict__ tiles, const uint32_t* __restrict__ rect,
-                                              uint32_t* __restrict__ keys, uint32_t* __restrict__ vals)
+                                              uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
+                                              uint32_t* __restrict__ zero_a, int zero_a_words,
+                                              uint32_t* __restrict__ zero_b, int zero_b_words)
 {
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    // clear the tile ranges and the tile-sort scan status (replaces two memset launches)
+    for (int w = r; w < zero_a_words; w += gridDim.x * blockDim.x) zero_a[w] = 0u;
+    for (int w = r; w < zero_b_words; w += gridDim.x * blockDim.x) zero_b[w] = 0u;
     if (r >= P) return;
     const uint32_t g = sorted_ids[r];
     if (tiles[g] == 0) return;
@@ -370,11 +428,12 @@ hipError_t launch_binning(int P, int64_t R, const Layout& L, char* geom, char* i
                           bool debug)
 {
     uint2* ranges = reinterpret_cast<uint2*>(image + L.ranges);
-    hipError_t e = hipMemsetAsync(ranges, 0, 8 * (size_t)L.tiles, s);
-    if (e != hipSuccess || R == 0) return e;
-    int tile_bits = 1;
-    while ((1 << tile_bits) < L.tiles) tile_bits++;
-    const int passes = (tile_bits + 7) / 8;
+    if (R == 0) return hipMemsetAsync(ranges, 0, 8 * (size_t)L.tiles, s);
+    const int tile_bits = L.tile_bits;
+    const int passes = L.tile_passes;
+    uint32_t* regions = reinterpret_cast<uint32_t*>(binning + L.bin_scan_regions);
+    uint32_t* fault = reinterpret_cast<uint32_t*>(image + L.counters) + kCntScanFault;
+    hipError_t e;
     uint32_t* pl_keys = reinterpret_cast<uint32_t*>(binning + L.list_keys);
     uint32_t* pl = reinterpret_cast<uint32_t*>(binning + L.point_list);
     uint32_t* alt_keys = reinterpret_cast<uint32_t*>(binning + L.alt_keys);
@@ -393,11 +452,13 @@ hipError_t launch_binning(int P, int64_t R, const Layout& L, char* geom, char* i
                        reinterpret_cast<const uint32_t*>(geom + L.sorted_ids),
                        reinterpret_cast<const uint32_t*>(geom + L.inst_offset),
                        reinterpret_cast<const uint32_t*>(geom + L.tiles_touched),
-                       reinterpret_cast<const uint32_t*>(geom + L.rect), ek, ev);
+                       reinterpret_cast<const uint32_t*>(geom + L.rect), ek, ev,
+                       reinterpret_cast<uint32_t*>(ranges), 2 * L.tiles, regions,
+                       (int)(passes * L.scan_region_bin));
     if ((e = post(debug, s)) != hipSuccess) return e;
     int done = 0;
     e = radix_sort(ek, ev, (int)R, tile_bits, kA, vA, kB, vB, reinterpret_cast<uint32_t*>(binning + L.bin_radix_hist),
-                   reinterpret_cast<uint32_t*>(binning + L.bin_scan_scratch), s, debug, &done);
+                   regions, L.scan_region_bin, fault, s, debug, &done);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_ranges, dim3((unsigned)((R + 255) / 256)), dim3(256), 0, s, R, pl_keys, ranges);
     return post(debug, s);

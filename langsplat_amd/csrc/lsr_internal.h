@@ -14,6 +14,7 @@ namespace lsr {
 enum Counter : int {
     kCntRendered = 1,
     kCntError = 2,
+    kCntScanFault = 3,
     kCntSlots = 16
 };
 
@@ -21,20 +22,23 @@ constexpr int kRadixThreads = 256;
 constexpr int kGradStride = 16;                          // floats per Gaussian grad record
 
 size_t radix_hist_words(int64_t n);   // per-block digit histograms for n keys
-size_t scan_scratch_words(int64_t n); // block sums of a multi-block scan of n words
+size_t scan_region_words(int64_t n);  // look-back status + ticket of one scan of n words
+constexpr int kDepthScans = 5;         // 4 depth-sort passes + the instance-offset scan
 
 struct Layout {
     // geometry (per Gaussian)
     size_t depth_key, tiles_touched, rect, record, clamped, sorted_ids, inst_offset;
-    size_t keys_a, keys_b, vals_b, radix_hist, scan_scratch;
+    size_t keys_a, keys_b, vals_b, radix_hist, scan_regions;
+    size_t scan_region_geom;  // u32 words per depth-order scan region
     size_t geom_bytes;
     // image (per pixel / tile)
     size_t counters, ranges, final_T, n_contrib;
     size_t image_bytes;
     // binning (per tile instance)
-    size_t list_keys, point_list, alt_keys, alt_vals, bin_radix_hist, bin_scan_scratch;
+    size_t list_keys, point_list, alt_keys, alt_vals, bin_radix_hist, bin_scan_regions;
+    size_t scan_region_bin;   // u32 words per tile-sort scan region
     size_t binning_bytes;
-    int gx, gy, tiles;
+    int gx, gy, tiles, tile_bits, tile_passes;
 };
 
 inline size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
@@ -57,13 +61,16 @@ inline Layout make_layout(int P, int W, int H, int64_t R)
     L.vals_b = take(4 * p);
     const size_t hw_p = radix_hist_words((int64_t)p);
     L.radix_hist = take(4 * hw_p);
-    const size_t sw_p = scan_scratch_words((int64_t)(hw_p > p ? hw_p : p));
-    L.scan_scratch = take(4 * sw_p);
+    L.scan_region_geom = scan_region_words((int64_t)(hw_p > p ? hw_p : p));
+    L.scan_regions = take(4 * kDepthScans * L.scan_region_geom);
     L.geom_bytes = o;
 
     L.gx = (W + kTile - 1) / kTile;
     L.gy = (H + kTile - 1) / kTile;
     L.tiles = L.gx * L.gy;
+    L.tile_bits = 1;
+    while ((1 << L.tile_bits) < L.tiles) L.tile_bits++;
+    L.tile_passes = (L.tile_bits + 7) / 8;
     const size_t T = (size_t)(L.tiles > 0 ? L.tiles : 1);
     const size_t HW = (size_t)W * (size_t)H;
     o = 0;
@@ -81,7 +88,8 @@ inline Layout make_layout(int P, int W, int H, int64_t R)
     L.alt_vals = take(4 * r);
     const size_t hw_r = radix_hist_words((int64_t)r);
     L.bin_radix_hist = take(4 * hw_r);
-    L.bin_scan_scratch = take(4 * scan_scratch_words((int64_t)hw_r));
+    L.scan_region_bin = scan_region_words((int64_t)hw_r);
+    L.bin_scan_regions = take(4 * L.tile_passes * L.scan_region_bin);
     L.binning_bytes = o;
     return L;
 }
@@ -95,6 +103,8 @@ struct PreprocessParams {
     int32_t* radii;
     uint32_t *depth_key, *tiles, *rect, *clamped, *counters;
     float4* record;
+    uint32_t* zero;   // depth-order scan status, cleared here
+    int zero_words;
 };
 
 struct PreprocessBwdParams {

@@ -77,6 +77,7 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessParams p)
 {
     extern __shared__ float s_sh[];
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    for (int w = i; w < p.zero_words; w += gridDim.x * blockDim.x) p.zero[w] = 0u;
     if (p.shs) {
         if (blockIdx.x * blockDim.x >= p.P) return;  // block-uniform
         stage_sh_in(p.shs, p.P, p.M, s_sh);
