@@ -53,6 +53,10 @@ class Model:
         self._rotation = torch.nn.Parameter(params.rotation, requires_grad=not include_feature)
         self._opacity = torch.nn.Parameter(params.opacity, requires_grad=not include_feature)
         self._language_feature = torch.nn.Parameter(params.language_feature, requires_grad=include_feature)
+        # scene/gaussian_model.py:33-41 setup_functions; render() fuses these into the kernels
+        self.scaling_activation = torch.exp
+        self.opacity_activation = torch.sigmoid
+        self.rotation_activation = torch.nn.functional.normalize
 
     def trainable(self):
         return [p for p in (self._xyz, self._features_dc, self._features_rest, self._opacity, self._scaling,
@@ -286,7 +290,8 @@ def main():
         "config": {"workload": f"{cfg}: {P} Gaussians, {W}x{H}, SH deg 3 + 3-ch language feature, "
                                f"include_feature train step, 1 view per GPU",
                    "gaussians": P, "width": W, "height": H, "views": world, "parallelism": f"dp{world} (views)",
-                   "blends_per_step": blends_all, "num_rendered_rank0": nr, "visible_rank0": visible},
+                   "blends_per_step": blends_all, "num_rendered_rank0": nr, "visible_rank0": visible,
+                   "activation": "fused" if os.environ.get("LANGSPLAT_AMD_FUSED", "1") != "0" else "torch"},
         "raster_ms_per_step": round(raster_ms, 4),
         "stages_ms_per_step": {k: round(v["total_ms"] / args.steps, 4) for k, v in sorted(prof.items())},
         "roofline": roofline,

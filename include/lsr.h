@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define LSR_ABI_VERSION 1
+#define LSR_ABI_VERSION 2
 
 enum lsr_status {
     LSR_OK = 0,
@@ -61,6 +61,18 @@ enum lsr_buffer {
 /* Returns device memory of at least `bytes` bytes, 256-byte aligned, valid until the caller
  * releases it; NULL on failure.  Called synchronously from the calling thread. */
 typedef void* (*lsr_alloc_fn)(void* user, int32_t which, size_t bytes);
+
+/* Fused parameter activation.  Each bit set in lsr_forward_args.raw /
+ * lsr_backward_args.raw says the matching input is GaussianModel's RAW parameter; the kernels
+ * apply the model's activation (scene/gaussian_model.py:33-41 setup_functions, getters :134-161;
+ * language normalisation gaussian_renderer/__init__.py:87) and the backward returns the gradient
+ * w.r.t. the raw tensor.  raw == 0 is the reference's API: every input already activated. */
+enum lsr_raw_flags {
+    LSR_RAW_OPACITY = 1,    /* opacities = _opacity:            sigmoid(x) = 1 / (1 + exp(-x))      */
+    LSR_RAW_SCALES = 2,     /* scales = _scaling:               exp(x)                              */
+    LSR_RAW_ROTATIONS = 4,  /* rotations = _rotation:           x / max(||x||, 1e-12) (F.normalize) */
+    LSR_RAW_LANGUAGE = 8    /* language_feature = _language_feature: x / (||x|| + 1e-9)             */
+};
 
 /* GaussianRasterizationSettings (gaussian_renderer/__init__.py:37-51), device-pointer form. */
 typedef struct lsr_settings {
@@ -96,6 +108,11 @@ typedef struct lsr_forward_args {
     float* out_color;                /* 3 x H x W */
     float* out_language_feature;     /* 3 x H x W */
     int32_t* radii;                  /* P */
+    int32_t raw;                     /* lsr_raw_flags; 0 = activated inputs (reference API) */
+    int32_t reserved;
+    const float* shs_rest;           /* NULL, or P x (M-1) x 3 (_features_rest) with shs = P x 1 x 3
+                                        (_features_dc): the SH rows without torch.cat
+                                        (scene/gaussian_model.py:146-150) */
 } lsr_forward_args;
 
 /* Inputs/outputs of _C.rasterize_gaussians_backward.  Every non-NULL output is fully written
@@ -128,6 +145,10 @@ typedef struct lsr_backward_args {
     float* dL_dsh;                   /* P x M x 3 or NULL */
     float* dL_dscales;               /* P x 3 or NULL */
     float* dL_drotations;            /* P x 4 or NULL */
+    int32_t raw;                     /* as in the forward; gradients are then w.r.t. the raw inputs */
+    int32_t reserved;
+    const float* shs_rest;           /* as in the forward */
+    float* dL_dsh_rest;              /* P x (M-1) x 3 when shs_rest is set (dL_dsh is then P x 1 x 3) */
 } lsr_backward_args;
 
 /* Byte offsets of the internal state inside the forward buffers, for inspection by tests and

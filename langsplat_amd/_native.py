@@ -20,6 +20,9 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "liblsr.so")
 
 LSR_BUF_GEOM, LSR_BUF_BINNING, LSR_BUF_IMAGE, LSR_BUF_BACKWARD = 0, 1, 2, 3
+ABI_VERSION = 2
+# lsr_raw_flags (include/lsr.h): inputs are GaussianModel's raw parameters
+RAW_OPACITY, RAW_SCALES, RAW_ROTATIONS, RAW_LANGUAGE = 1, 2, 4, 8
 _vp = ctypes.c_void_p
 
 
@@ -46,7 +49,7 @@ class LsrForwardArgs(ctypes.Structure):
     _fields_ = [("P", ctypes.c_int32), ("M", ctypes.c_int32)] + [
         (n, _vp) for n in ("means3D", "shs", "colors_precomp", "language_feature", "opacities", "scales",
                            "rotations", "cov3D_precomp", "out_color", "out_language_feature", "radii")
-    ]
+    ] + [("raw", ctypes.c_int32), ("reserved", ctypes.c_int32), ("shs_rest", _vp)]
 
 
 class LsrBackwardArgs(ctypes.Structure):
@@ -56,7 +59,7 @@ class LsrBackwardArgs(ctypes.Structure):
                            "geom_buffer", "binning_buffer", "image_buffer", "dL_dmeans2D", "dL_dcolors",
                            "dL_dlanguage_feature", "dL_dopacity", "dL_dmeans3D", "dL_dcov3D", "dL_dsh",
                            "dL_dscales", "dL_drotations")
-    ]
+    ] + [("raw", ctypes.c_int32), ("reserved", ctypes.c_int32), ("shs_rest", _vp), ("dL_dsh_rest", _vp)]
 
 
 class LsrStateLayout(ctypes.Structure):
@@ -106,7 +109,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.lsr_abi_version() != 1:
+    if lib.lsr_abi_version() != ABI_VERSION:
         raise RuntimeError("liblsr.so ABI version mismatch")
     _lib = lib
     return lib
@@ -214,8 +217,11 @@ def make_settings(rs, keep: list) -> LsrSettings:
 
 
 def rasterize_gaussians(rs, means3D, shs, colors_precomp, language_feature, opacities, scales, rotations,
-                        cov3D_precomp):
-    """Native forward: returns (num_rendered, color, language_feature_image, radii, geom, binning, image)."""
+                        cov3D_precomp, raw=0, shs_rest=None):
+    """Native forward: returns (num_rendered, color, language_feature_image, radii, geom, binning, image).
+
+    raw / shs_rest: the fused-activation form (include/lsr.h lsr_raw_flags); shs is then
+    features_dc (P,1,3) and shs_rest features_rest (P,M-1,3)."""
     lib = load()
     device = means3D.device
     P = int(means3D.shape[0])
@@ -228,6 +234,10 @@ def rasterize_gaussians(rs, means3D, shs, colors_precomp, language_feature, opac
     a = LsrForwardArgs()
     a.P = P
     a.M = int(shs.shape[1]) if shs is not None and shs.numel() > 0 else 0
+    if shs_rest is not None and shs_rest.numel() > 0:
+        a.M += int(shs_rest.shape[1])
+        a.shs_rest = _ptr(shs_rest)
+    a.raw = int(raw)
     a.means3D = _ptr(means3D)
     a.shs = _ptr(shs)
     a.colors_precomp = _ptr(colors_precomp)
@@ -250,12 +260,17 @@ def rasterize_gaussians(rs, means3D, shs, colors_precomp, language_feature, opac
 
 def rasterize_gaussians_backward(rs, means3D, shs, colors_precomp, language_feature, scales, rotations,
                                  cov3D_precomp, radii, grad_color, grad_language, num_rendered, geom, binning,
-                                 image):
-    """Native backward: returns the gradient tensors keyed like the reference's inputs."""
+                                 image, raw=0, shs_rest=None, opacities=None):
+    """Native backward: returns the gradient tensors keyed like the reference's inputs (with raw
+    flags: w.r.t. the raw parameters; "shs" is then dL/dfeatures_dc and "shs_rest"
+    dL/dfeatures_rest)."""
     lib = load()
     device = means3D.device
     P = int(means3D.shape[0])
-    M = int(shs.shape[1]) if shs is not None and shs.numel() > 0 else 0
+    split = shs_rest is not None and shs_rest.numel() > 0
+    M_dc = int(shs.shape[1]) if shs is not None and shs.numel() > 0 else 0
+    M_rest = int(shs_rest.shape[1]) if split else 0
+    M = M_dc + M_rest
     keep: list = []
     s = make_settings(rs, keep)
     f32 = dict(dtype=torch.float32, device=device)
@@ -266,7 +281,8 @@ def rasterize_gaussians_backward(rs, means3D, shs, colors_precomp, language_feat
         "opacities": torch.empty((P, 1), **f32),
         "means3D": torch.empty((P, 3), **f32),
         "cov3D_precomp": torch.empty((P, 6), **f32) if _ptr(cov3D_precomp) is not None else None,
-        "shs": torch.empty((P, M, 3), **f32) if M > 0 else None,
+        "shs": torch.empty((P, M_dc, 3), **f32) if M_dc > 0 else None,
+        "shs_rest": torch.empty((P, M_rest, 3), **f32) if split else None,
         "scales": torch.empty((P, 3), **f32) if _ptr(scales) is not None else None,
         "rotations": torch.empty((P, 4), **f32) if _ptr(rotations) is not None else None,
     }
@@ -280,6 +296,11 @@ def rasterize_gaussians_backward(rs, means3D, shs, colors_precomp, language_feat
     a.shs = _ptr(shs)
     a.colors_precomp = _ptr(colors_precomp)
     a.language_feature = _ptr(language_feature)
+    a.opacities = _ptr(opacities)
+    a.raw = int(raw)
+    if split:
+        a.shs_rest = _ptr(shs_rest)
+        a.dL_dsh_rest = _ptr(g["shs_rest"])
     a.scales = _ptr(scales)
     a.rotations = _ptr(rotations)
     a.cov3D_precomp = _ptr(cov3D_precomp)

@@ -158,6 +158,10 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
         return fail(LSR_ERR_INVALID, "lsr_forward: M smaller than (sh_degree+1)^2");
     if (!s->bg || !s->viewmatrix || !s->projmatrix || !s->campos)
         return fail(LSR_ERR_INVALID, "lsr_forward: settings tensors missing");
+    if (a->raw & ~(LSR_RAW_OPACITY | LSR_RAW_SCALES | LSR_RAW_ROTATIONS | LSR_RAW_LANGUAGE))
+        return fail(LSR_ERR_INVALID, "lsr_forward: unknown raw flag");
+    if (a->shs_rest && (!a->shs || a->M < 2))
+        return fail(LSR_ERR_INVALID, "lsr_forward: shs_rest needs shs (features_dc) and M >= 2");
     hipStream_t stream = reinterpret_cast<hipStream_t>(stream_ptr);
     const bool debug = s->debug != 0;
     *num_rendered = 0;
@@ -211,6 +215,8 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
     pp.counters = counters;
     pp.zero = reinterpret_cast<uint32_t*>(geom + L.scan_regions);
     pp.zero_words = (int)(kDepthScans * L.scan_region_geom);
+    pp.raw = a->raw;
+    pp.shs_rest = a->shs_rest;
     LSR_TRY(launch_preprocess(pp, stream), "preprocess");
     LSR_TRY(launch_depth_order(P, L, geom, counters, stream, debug), "depth order");
 
@@ -256,6 +262,12 @@ int32_t lsr_backward(const lsr_settings* s, const lsr_backward_args* a, lsr_allo
         return fail(LSR_ERR_INVALID, "lsr_backward: missing output pointer");
     if ((a->shs && !a->dL_dsh) || (a->cov3D_precomp && !a->dL_dcov3D))
         return fail(LSR_ERR_INVALID, "lsr_backward: missing dL_dsh / dL_dcov3D output");
+    if (a->raw & ~(LSR_RAW_OPACITY | LSR_RAW_SCALES | LSR_RAW_ROTATIONS | LSR_RAW_LANGUAGE))
+        return fail(LSR_ERR_INVALID, "lsr_backward: unknown raw flag");
+    if (a->shs_rest && (!a->shs || a->M < 2 || !a->dL_dsh_rest))
+        return fail(LSR_ERR_INVALID, "lsr_backward: shs_rest needs shs, M >= 2 and dL_dsh_rest");
+    if ((a->raw & LSR_RAW_OPACITY) && P > 0 && !a->opacities)
+        return fail(LSR_ERR_INVALID, "lsr_backward: raw opacities missing");
     hipStream_t stream = reinterpret_cast<hipStream_t>(stream_ptr);
     const bool debug = s->debug != 0;
     if (P == 0) return LSR_OK;
@@ -317,6 +329,11 @@ int32_t lsr_backward(const lsr_settings* s, const lsr_backward_args* a, lsr_allo
     bp.dsh = a->shs ? a->dL_dsh : nullptr;
     bp.dscales = a->dL_dscales;
     bp.drots = a->dL_drotations;
+    bp.raw = a->raw;
+    bp.opac = a->opacities;
+    bp.lang = a->language_feature;
+    bp.shs_rest = a->shs_rest;
+    bp.dsh_rest = a->dL_dsh_rest;
     if (!a->shs && a->dL_dsh && a->M > 0)
         LSR_TRY(hipMemsetAsync(a->dL_dsh, 0, (size_t)P * a->M * 3 * 4, stream), "memset dsh");
     LSR_TRY(launch_preprocess_backward(bp, stream), "preprocess backward");

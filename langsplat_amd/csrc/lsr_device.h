@@ -47,6 +47,40 @@ __device__ __forceinline__ float expf_exact(float x)
 
 __device__ __forceinline__ float fma_(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
 
+// ---- parameter activations of the fused path (lsr_raw_flags; oracle lso_act_* restate them) ----
+// exp over the whole float range: expf_exact below 88, +inf above (exp(88) = 1.65e38).
+__device__ __forceinline__ float act_expf(float x) { return x > 88.0f ? __builtin_inff() : expf_exact(x); }
+__device__ __forceinline__ float act_sigmoid(float x) { return 1.0f / (1.0f + act_expf(-x)); }
+// torch.nn.functional.normalize(q, dim=1): q / max(||q||, 1e-12)
+__device__ __forceinline__ float4 act_normalize4(float4 q)
+{
+    const float d = fmaxf(sqrtf(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w), 1e-12f);
+    return make_float4(q.x / d, q.y / d, q.z / d, q.w / d);
+}
+// autograd of q / clamp_min(norm(q), 1e-12): div, clamp_min and norm backward composed
+__device__ __forceinline__ float4 act_normalize4_backward(float4 q, float4 g)
+{
+    const float n = sqrtf(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
+    const float d = fmaxf(n, 1e-12f);
+    const float gd = -(g.x * q.x + g.y * q.y + g.z * q.z + g.w * q.w) / (d * d);
+    const float k = (n >= 1e-12f && n > 0.0f) ? gd / n : 0.0f;
+    return make_float4(g.x / d + q.x * k, g.y / d + q.y * k, g.z / d + q.z * k, g.w / d + q.w * k);
+}
+// language feature: f / (||f|| + 1e-9) (gaussian_renderer/__init__.py:87)
+__device__ __forceinline__ float3 act_lang(float x, float y, float z)
+{
+    const float d = sqrtf(x * x + y * y + z * z) + 1e-9f;
+    return make_float3(x / d, y / d, z / d);
+}
+__device__ __forceinline__ float3 act_lang_backward(float x, float y, float z, float gx, float gy, float gz)
+{
+    const float n = sqrtf(x * x + y * y + z * z);
+    const float d = n + 1e-9f;
+    const float gd = -(gx * x + gy * y + gz * z) / (d * d);
+    const float k = n > 0.0f ? gd / n : 0.0f;
+    return make_float3(gx / d + x * k, gy / d + y * k, gz / d + z * k);
+}
+
 // 3-term dot in the oracle's order: fma(a2,b2, fma(a1,b1, a0*b0))
 __device__ __forceinline__ float dot3(float a0, float a1, float a2, float b0, float b1, float b2)
 {

@@ -105,6 +105,8 @@ struct PreprocessParams {
     float4* record;
     uint32_t* zero;   // depth-order scan status, cleared here
     int zero_words;
+    int raw;                  // lsr_raw_flags
+    const float* shs_rest;    // split SH rows (shs = dc only) or null
 };
 
 struct PreprocessBwdParams {
@@ -115,6 +117,9 @@ struct PreprocessBwdParams {
     const uint32_t* clamped;
     const float* grad;  // P x kGradStride
     float *dmeans2D, *dcolors, *dlang, *dopac, *dmeans3D, *dcov, *dsh, *dscales, *drots;
+    int raw;                  // lsr_raw_flags: chain the activation derivatives
+    const float *opac, *lang, *shs_rest;
+    float* dsh_rest;
 };
 
 struct RenderParams {

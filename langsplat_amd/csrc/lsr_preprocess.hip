@@ -11,65 +11,100 @@ namespace lsr {
 // SH coefficients of the block's 256 Gaussians are moved between HBM and LDS with coalesced
 // accesses (the AoS P x M x 3 layout gives each lane 12M contiguous bytes, i.e. 48 separate cache
 // lines per wave load otherwise); LDS rows are padded to 3M+1 floats, which keeps the per-lane
-// row reads bank-conflict free.
-__device__ __forceinline__ void stage_sh_in(const float* __restrict__ shs, int P, int M, float* lds)
+// row reads bank-conflict free.  A row can come from one source (shs, P x M x 3) or from two
+// (the fused path's _features_dc P x 1 x 3 into columns 0-2 and _features_rest P x (M-1) x 3
+// into columns 3..), which removes the per-step torch.cat of scene/gaussian_model.py:146-150.
+
+// rows of w floats of the block's Gaussians from src -> LDS rows (stride ws) starting at col0
+__device__ __forceinline__ void rows_in(const float* __restrict__ src, int ng, int w, float* lds, int ws, int col0)
 {
-    const int w = 3 * M, ws = w + 1;
-    const int g0 = blockIdx.x * blockDim.x;
-    const int n = min((int)blockDim.x, P - g0) * w;
-    const float* src = shs + (size_t)g0 * w;
-    if ((w & 3) == 0 && (reinterpret_cast<uintptr_t>(src) & 15) == 0) {
-        // dwordx4 loads, all issued before the first LDS write (rows are w floats, w % 4 == 0,
-        // so no float4 straddles two rows)
-        constexpr int kMaxPer = 12;  // 256 x 48 floats / (256 threads x 4): M <= 16 in one sweep
-        const float4* s4 = reinterpret_cast<const float4*>(src);
-        const int n4 = n >> 2;
-        for (int k0 = 0; k0 < n4; k0 += kMaxPer * (int)blockDim.x) {
-            float4 r[kMaxPer];
+    const int n = ng * w;
+    const int n4 = (reinterpret_cast<uintptr_t>(src) & 15) == 0 ? (n >> 2) : 0;
+    const float4* s4 = reinterpret_cast<const float4*>(src);
+    constexpr int kMaxPer = 12;  // dwordx4 loads all issued before the first LDS write
+    for (int k0 = 0; k0 < n4; k0 += kMaxPer * (int)blockDim.x) {
+        float4 r[kMaxPer];
 #pragma unroll
-            for (int u = 0; u < kMaxPer; u++) {
-                const int k = k0 + u * (int)blockDim.x + (int)threadIdx.x;
-                if (k < n4) r[u] = s4[k];
-            }
+        for (int u = 0; u < kMaxPer; u++) {
+            const int k = k0 + u * (int)blockDim.x + (int)threadIdx.x;
+            if (k < n4) r[u] = s4[k];
+        }
 #pragma unroll
-            for (int u = 0; u < kMaxPer; u++) {
-                const int k = k0 + u * (int)blockDim.x + (int)threadIdx.x;
-                if (k < n4) {
-                    const int e = 4 * k, gi = e / w;
-                    float* d = lds + gi * ws + (e - gi * w);
-                    d[0] = r[u].x;
-                    d[1] = r[u].y;
-                    d[2] = r[u].z;
-                    d[3] = r[u].w;
+        for (int u = 0; u < kMaxPer; u++) {
+            const int k = k0 + u * (int)blockDim.x + (int)threadIdx.x;
+            if (k >= n4) continue;
+            const int e = 4 * k;
+            int gi = e / w, col = e - gi * w;
+            if ((w & 3) == 0) {  // a float4 never straddles two rows
+                float* d = lds + gi * ws + col0 + col;
+                d[0] = r[u].x;
+                d[1] = r[u].y;
+                d[2] = r[u].z;
+                d[3] = r[u].w;
+            } else {
+                const float v[4] = {r[u].x, r[u].y, r[u].z, r[u].w};
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    lds[gi * ws + col0 + col] = v[j];
+                    if (++col == w) {
+                        col = 0;
+                        gi++;
+                    }
                 }
             }
         }
-        return;
     }
-    for (int k = threadIdx.x; k < n; k += blockDim.x) {
-        const int gi = k / w;
-        lds[gi * ws + (k - gi * w)] = src[k];
+    for (int e = 4 * n4 + (int)threadIdx.x; e < n; e += blockDim.x) {
+        const int gi = e / w;
+        lds[gi * ws + col0 + (e - gi * w)] = src[e];
     }
 }
 
-__device__ __forceinline__ void stage_sh_out(float* __restrict__ dst_all, int P, int M, const float* lds)
+__device__ __forceinline__ void rows_out(float* __restrict__ dst, int ng, int w, const float* lds, int ws, int col0)
 {
-    const int w = 3 * M, ws = w + 1;
-    const int g0 = blockIdx.x * blockDim.x;
-    const int n = min((int)blockDim.x, P - g0) * w;
-    float* dst = dst_all + (size_t)g0 * w;
-    if ((w & 3) == 0 && (reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
-        float4* d4 = reinterpret_cast<float4*>(dst);
-        for (int k = threadIdx.x; k < (n >> 2); k += blockDim.x) {
-            const int e = 4 * k, gi = e / w;
-            const float* sr = lds + gi * ws + (e - gi * w);
-            d4[k] = make_float4(sr[0], sr[1], sr[2], sr[3]);
+    const int n = ng * w;
+    const int n4 = (reinterpret_cast<uintptr_t>(dst) & 15) == 0 ? (n >> 2) : 0;
+    float4* d4 = reinterpret_cast<float4*>(dst);
+    for (int k = threadIdx.x; k < n4; k += blockDim.x) {
+        const int e = 4 * k;
+        int gi = e / w, col = e - gi * w;
+        float v[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            v[j] = lds[gi * ws + col0 + col];
+            if (++col == w) {
+                col = 0;
+                gi++;
+            }
         }
-        return;
+        d4[k] = make_float4(v[0], v[1], v[2], v[3]);
     }
-    for (int k = threadIdx.x; k < n; k += blockDim.x) {
-        const int gi = k / w;
-        dst[k] = lds[gi * ws + (k - gi * w)];
+    for (int e = 4 * n4 + (int)threadIdx.x; e < n; e += blockDim.x) {
+        const int gi = e / w;
+        dst[e] = lds[gi * ws + col0 + (e - gi * w)];
+    }
+}
+
+// SH rows of the block into LDS (one source, or dc + rest)
+__device__ __forceinline__ void stage_sh_in(const float* shs, const float* shs_rest, int P, int M, float* lds)
+{
+    const int g0 = blockIdx.x * blockDim.x, ng = min((int)blockDim.x, P - g0), ws = 3 * M + 1;
+    if (!shs_rest) {
+        rows_in(shs + (size_t)g0 * 3 * M, ng, 3 * M, lds, ws, 0);
+    } else {
+        rows_in(shs + (size_t)g0 * 3, ng, 3, lds, ws, 0);
+        if (M > 1) rows_in(shs_rest + (size_t)g0 * 3 * (M - 1), ng, 3 * (M - 1), lds, ws, 3);
+    }
+}
+
+__device__ __forceinline__ void stage_sh_out(float* dsh, float* dsh_rest, int P, int M, const float* lds)
+{
+    const int g0 = blockIdx.x * blockDim.x, ng = min((int)blockDim.x, P - g0), ws = 3 * M + 1;
+    if (!dsh_rest) {
+        rows_out(dsh + (size_t)g0 * 3 * M, ng, 3 * M, lds, ws, 0);
+    } else {
+        rows_out(dsh + (size_t)g0 * 3, ng, 3, lds, ws, 0);
+        if (M > 1) rows_out(dsh_rest + (size_t)g0 * 3 * (M - 1), ng, 3 * (M - 1), lds, ws, 3);
     }
 }
 
@@ -80,7 +115,7 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessParams p)
     for (int w = i; w < p.zero_words; w += gridDim.x * blockDim.x) p.zero[w] = 0u;
     if (p.shs) {
         if (blockIdx.x * blockDim.x >= p.P) return;  // block-uniform
-        stage_sh_in(p.shs, p.P, p.M, s_sh);
+        stage_sh_in(p.shs, p.shs_rest, p.P, p.M, s_sh);
         __syncthreads();
     }
     if (i >= p.P) return;
@@ -103,8 +138,15 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessParams p)
 #pragma unroll
         for (int k = 0; k < 6; k++) cov[k] = p.cov_pre[6 * (size_t)i + k];
     } else {
-        const float4 q = *reinterpret_cast<const float4*>(p.rots + 4 * (size_t)i);
-        cov3d(p.scales[3 * i], p.scales[3 * i + 1], p.scales[3 * i + 2], p.scale_modifier, q, cov);
+        float4 q = *reinterpret_cast<const float4*>(p.rots + 4 * (size_t)i);
+        float sx = p.scales[3 * i], sy = p.scales[3 * i + 1], sz = p.scales[3 * i + 2];
+        if (p.raw & LSR_RAW_ROTATIONS) q = act_normalize4(q);
+        if (p.raw & LSR_RAW_SCALES) {
+            sx = act_expf(sx);
+            sy = act_expf(sy);
+            sz = act_expf(sz);
+        }
+        cov3d(sx, sy, sz, p.scale_modifier, q, cov);
     }
     const Cov2D cv = cov2d(px, py, pz, p.focal_x, p.focal_y, p.tanfovx, p.tanfovy, cov, p.view);
     const float a = cv.a, b = cv.b, c = cv.c;
@@ -147,7 +189,14 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessParams p)
         f0 = p.lang[3 * i];
         f1 = p.lang[3 * i + 1];
         f2 = p.lang[3 * i + 2];
+        if (p.raw & LSR_RAW_LANGUAGE) {
+            const float3 f = act_lang(f0, f1, f2);
+            f0 = f.x;
+            f1 = f.y;
+            f2 = f.z;
+        }
     }
+    const float opacity = (p.raw & LSR_RAW_OPACITY) ? act_sigmoid(p.opac[i]) : p.opac[i];
     p.depth_key[i] = __float_as_uint(pv.z);
     p.radii[i] = r;
     p.tiles[i] = area;
@@ -156,7 +205,7 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessParams p)
     p.clamped[i] = clamp_bits;
     float4* rec = p.record + 3 * (size_t)i;
     rec[0] = make_float4(ix, iy, cx, cy);
-    rec[1] = make_float4(cz, p.opac[i], rgb[0], rgb[1]);
+    rec[1] = make_float4(cz, opacity, rgb[0], rgb[1]);
     rec[2] = make_float4(rgb[2], f0, f1, f2);
 }
 
@@ -321,13 +370,13 @@ __global__ __launch_bounds__(256) void k_preprocess_backward(PreprocessBwdParams
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (blockIdx.x * blockDim.x >= p.P) return;  // block-uniform
     if (p.shs) {
-        stage_sh_in(p.shs, p.P, p.M, s_sh);
+        stage_sh_in(p.shs, p.shs_rest, p.P, p.M, s_sh);
         __syncthreads();
     }
     if (i < p.P) preprocess_backward_one(p, i, s_sh + threadIdx.x * (3 * p.M + 1));
     if (p.shs && p.dsh) {
         __syncthreads();
-        stage_sh_out(p.dsh, p.P, p.M, s_sh);
+        stage_sh_out(p.dsh, p.shs_rest ? p.dsh_rest : nullptr, p.P, p.M, s_sh);
     }
 }
 
@@ -364,20 +413,39 @@ __device__ __forceinline__ void preprocess_backward_one(const PreprocessBwdParam
     p.dcolors[i3] = drgb_in[0];
     p.dcolors[i3 + 1] = drgb_in[1];
     p.dcolors[i3 + 2] = drgb_in[2];
-    p.dlang[i3] = gc.y;
-    p.dlang[i3 + 1] = gc.z;
-    p.dlang[i3 + 2] = gc.w;
-    p.dopac[i] = gb.y;
+    if ((p.raw & LSR_RAW_LANGUAGE) && p.lang) {
+        const float3 d = act_lang_backward(p.lang[i3], p.lang[i3 + 1], p.lang[i3 + 2], gc.y, gc.z, gc.w);
+        p.dlang[i3] = d.x;
+        p.dlang[i3 + 1] = d.y;
+        p.dlang[i3 + 2] = d.z;
+    } else {
+        p.dlang[i3] = gc.y;
+        p.dlang[i3 + 1] = gc.z;
+        p.dlang[i3 + 2] = gc.w;
+    }
+    if (p.raw & LSR_RAW_OPACITY) {
+        const float sg = act_sigmoid(p.opac[i]);
+        p.dopac[i] = gb.y * (1.0f - sg) * sg;  // torch sigmoid_backward: grad * (1 - y) * y
+    } else {
+        p.dopac[i] = gb.y;
+    }
 
     const float px = p.means[i3], py = p.means[i3 + 1], pz = p.means[i3 + 2];
     float cov[6];
     float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
+    float sc[3] = {0.f, 0.f, 0.f};
     if (p.cov_pre) {
 #pragma unroll
         for (int k = 0; k < 6; k++) cov[k] = p.cov_pre[6 * (size_t)i + k];
     } else {
         q = *reinterpret_cast<const float4*>(p.rots + 4 * (size_t)i);
-        cov3d(p.scales[i3], p.scales[i3 + 1], p.scales[i3 + 2], p.scale_modifier, q, cov);
+        sc[0] = p.scales[i3];
+        sc[1] = p.scales[i3 + 1];
+        sc[2] = p.scales[i3 + 2];
+        if (p.raw & LSR_RAW_ROTATIONS) q = act_normalize4(q);
+        if (p.raw & LSR_RAW_SCALES)
+            for (int k = 0; k < 3; k++) sc[k] = act_expf(sc[k]);
+        cov3d(sc[0], sc[1], sc[2], p.scale_modifier, q, cov);
     }
     const Cov2D cv = cov2d(px, py, pz, p.focal_x, p.focal_y, p.tanfovx, p.tanfovy, cov, p.view);
     const float limx = 1.3f * p.tanfovx, limy = 1.3f * p.tanfovy;
@@ -465,7 +533,17 @@ __device__ __forceinline__ void preprocess_backward_one(const PreprocessBwdParam
         for (int k = 0; k < 6; k++) p.dcov[6 * (size_t)i + k] = dcov[k];
     if (!p.cov_pre) {
         float ds[3], dr[4];
-        cov3d_backward(p.scales[i3], p.scales[i3 + 1], p.scales[i3 + 2], p.scale_modifier, q, dcov, ds, dr);
+        cov3d_backward(sc[0], sc[1], sc[2], p.scale_modifier, q, dcov, ds, dr);
+        if (p.raw & LSR_RAW_SCALES)
+            for (int k = 0; k < 3; k++) ds[k] = ds[k] * sc[k];  // torch exp backward: grad * result
+        if (p.raw & LSR_RAW_ROTATIONS) {
+            const float4 d = act_normalize4_backward(*reinterpret_cast<const float4*>(p.rots + 4 * (size_t)i),
+                                                     make_float4(dr[0], dr[1], dr[2], dr[3]));
+            dr[0] = d.x;
+            dr[1] = d.y;
+            dr[2] = d.z;
+            dr[3] = d.w;
+        }
         if (p.dscales) {
             p.dscales[i3] = ds[0];
             p.dscales[i3 + 1] = ds[1];

@@ -118,6 +118,92 @@ class _RasterizeGaussians(torch.autograd.Function):
                 want(6, g["scales"]), want(7, g["rotations"]), want(8, g["cov3D_precomp"]), None)
 
 
+def rasterize_gaussians_fused(means3D, means2D, features_dc, features_rest, opacity_raw, scaling_raw, rotation_raw,
+                              language_feature_raw, raster_settings):
+    """Fused-activation form of the rasterizer call.
+
+    Takes GaussianModel's RAW parameters -- _features_dc (P,1,3), _features_rest (P,M-1,3),
+    _opacity (P,1), _scaling (P,3), _rotation (P,4), _language_feature (P,3) or None -- and
+    returns exactly what GaussianRasterizer(...) returns for the activated inputs of
+    gaussian_renderer/__init__.py:55-91: (color, language_feature_image, radii).  The kernels
+    apply sigmoid / exp / normalize / the language normalisation and the SH concatenation
+    themselves (include/lsr.h lsr_raw_flags), so those torch passes and their backward kernels
+    disappear; gradients come back w.r.t. the raw parameters.
+    """
+    return _RasterizeGaussiansFused.apply(means3D, means2D, features_dc, features_rest, opacity_raw, scaling_raw,
+                                          rotation_raw, language_feature_raw, raster_settings)
+
+
+def _guarded(rs, dump, msg, fn, args):
+    """Run a native call; with debug=True snapshot its inputs and dump them on failure (upstream)."""
+    if not rs.debug:
+        return fn(*args)
+    cpu_args = _cpu_deep_copy(args)
+    try:
+        return fn(*args)
+    except Exception as ex:
+        torch.save(cpu_args, dump)
+        print(msg)
+        raise ex
+
+
+class _RasterizeGaussiansFused(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, means3D, means2D, features_dc, features_rest, opacity_raw, scaling_raw, rotation_raw,
+                language_feature_raw, raster_settings):
+        if means3D.device.type != "cuda":
+            raise RuntimeError("langsplat_amd rasterizer: inputs must be on a ROCm GPU device "
+                               f"(got {means3D.device}); there is no CPU implementation")
+        P = means3D.shape[0]
+        lang = language_feature_raw
+        use_lang = bool(raster_settings.include_feature) and lang is not None and lang.numel() == 3 * P and P > 0
+        raw = _native.RAW_OPACITY | _native.RAW_SCALES | _native.RAW_ROTATIONS | (
+            _native.RAW_LANGUAGE if use_lang else 0)
+        rest = _f32(features_rest) if features_rest is not None and features_rest.numel() > 0 else None
+        m3, dc, ln, op, sc, ro = (_f32(means3D), _f32(features_dc), _f32(lang) if use_lang else None,
+                                  _f32(opacity_raw), _f32(scaling_raw), _f32(rotation_raw))
+        out = _guarded(raster_settings, "snapshot_fw.dump",
+                       "\nAn error occured in forward. Please forward snapshot_fw.dump for debugging.",
+                       lambda *a: _native.rasterize_gaussians(raster_settings, *a[:8], raw=raw, shs_rest=a[8]),
+                       (m3, dc, None, ln, op, sc, ro, None, rest))
+        num_rendered, color, language_feature, radii, geom, binning, image = out
+        ctx.raster_settings = raster_settings
+        ctx.num_rendered = num_rendered
+        ctx.use_lang = use_lang
+        ctx.raw = raw
+        ctx.rest_shape = tuple(features_rest.shape) if features_rest is not None else None
+        empty = torch.empty(0)
+        ctx.save_for_backward(m3, dc, rest if rest is not None else empty, ln if ln is not None else empty, op, sc,
+                              ro, radii, geom, binning, image)
+        ctx.mark_non_differentiable(radii)
+        return color, language_feature, radii
+
+    @staticmethod
+    def backward(ctx, grad_out_color, grad_out_language_feature, _grad_radii):
+        rs = ctx.raster_settings
+        m3, dc, rest, ln, op, sc, ro, radii, geom, binning, image = ctx.saved_tensors
+        rest = rest if rest.numel() > 0 else None
+        if grad_out_color is None:
+            grad_out_color = torch.zeros((3, rs.image_height, rs.image_width), device=m3.device)
+        gl = grad_out_language_feature if ctx.use_lang else None
+        g = _guarded(rs, "snapshot_bw.dump",
+                     "\nAn error occured in backward. Writing snapshot_bw.dump for debugging.\n",
+                     lambda *a: _native.rasterize_gaussians_backward(rs, *a[:14], raw=ctx.raw, shs_rest=a[14],
+                                                                     opacities=a[15]),
+                     (m3, dc, None, ln if ctx.use_lang else None, sc, ro, None, radii, grad_out_color, gl,
+                      ctx.num_rendered, geom, binning, image, rest, op))
+
+        def want(i, t):
+            return t if ctx.needs_input_grad[i] else None
+
+        d_rest = g["shs_rest"]
+        if d_rest is None and ctx.rest_shape is not None and ctx.needs_input_grad[3]:
+            d_rest = torch.zeros(ctx.rest_shape, dtype=torch.float32, device=m3.device)
+        return (want(0, g["means3D"]), want(1, g["means2D"]), want(2, g["shs"]), want(3, d_rest),
+                want(4, g["opacities"]), want(5, g["scales"]), want(6, g["rotations"]),
+                want(7, g["language_feature_precomp"] if ctx.use_lang else None), None)
+
+
 class GaussianRasterizer(nn.Module):
     def __init__(self, raster_settings):
         super().__init__()

@@ -8,10 +8,27 @@ get_covariance, active_sh_degree, max_sh_degree).
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
-from .rasterizer import GaussianRasterizationSettings, GaussianRasterizer
+from .rasterizer import GaussianRasterizationSettings, GaussianRasterizer, rasterize_gaussians_fused
+
+
+def _fusable(pc, pipe, override_color, device) -> bool:
+    """True when render()'s inputs are GaussianModel's default activations of raw tensors
+    (scene/gaussian_model.py:33-41), so the kernels can activate them.
+    LANGSPLAT_AMD_FUSED=0 forces the reference's unfused call."""
+    if os.environ.get("LANGSPLAT_AMD_FUSED", "1") == "0" or device.type != "cuda":
+        return False
+    if override_color is not None or pipe.convert_SHs_python or pipe.compute_cov3D_python:
+        return False
+    if not all(isinstance(getattr(pc, n, None), torch.Tensor)
+               for n in ("_features_dc", "_features_rest", "_opacity", "_scaling", "_rotation")):
+        return False
+    return (getattr(pc, "scaling_activation", None) is torch.exp
+            and getattr(pc, "opacity_activation", None) is torch.sigmoid
+            and getattr(pc, "rotation_activation", None) is torch.nn.functional.normalize)
 
 
 def eval_sh(deg, sh, dirs):
@@ -66,6 +83,17 @@ def render(viewpoint_camera, pc, pipe, bg_color: torch.Tensor, opt, scaling_modi
         include_feature=opt.include_feature,
     )
     rasterizer = GaussianRasterizer(raster_settings=raster_settings)
+
+    if _fusable(pc, pipe, override_color, screenspace_points.device):
+        lang_raw = pc.get_language_feature if opt.include_feature else None
+        rendered_image, language_feature_image, radii = rasterize_gaussians_fused(
+            pc.get_xyz, screenspace_points, pc._features_dc, pc._features_rest, pc._opacity, pc._scaling,
+            pc._rotation, lang_raw, raster_settings)
+        return {"render": rendered_image,
+                "language_feature_image": language_feature_image,
+                "viewspace_points": screenspace_points,
+                "visibility_filter": radii > 0,
+                "radii": radii}
 
     means3D = pc.get_xyz
     means2D = screenspace_points

@@ -853,6 +853,78 @@ void lso_backward(const lso_state* st, const float* dL_dcolor, const float* dL_d
 /* ------------------------------------------------------------------------------------------ */
 /* state accessors (for tests)                                                                  */
 /* ------------------------------------------------------------------------------------------ */
+/* fused parameter activation (include/lsr.h lsr_raw_flags)                  */
+/* ------------------------------------------------------------------------------------------ */
+/* GaussianModel's activations (scene/gaussian_model.py:33-41 setup_functions; getters :134-161)
+ * and the language normalisation (gaussian_renderer/__init__.py:87), restated with the same
+ * operation order as the kernels (langsplat_amd/csrc/lsr_device.h act_*), so a fused GPU
+ * forward is bit-identical to this activation followed by lso_forward.  Versus torch's own
+ * sigmoid/exp/normalize these agree to a few ulp (tests/test_oracle_activation.py).  The
+ * backward follows torch autograd's formulas: sigmoid_backward grad*(1-y)*y, exp grad*result,
+ * and the composed div / clamp_min / norm backward of F.normalize. */
+#define LSO_RAW_OPACITY 1
+#define LSO_RAW_SCALES 2
+#define LSO_RAW_ROTATIONS 4
+#define LSO_RAW_LANGUAGE 8
+
+float lso_act_expf(float x) { return x > 88.0f ? INFINITY : lso_expf(x); }
+static float act_sigmoid(float x) { return 1.0f / (1.0f + lso_act_expf(-x)); }
+
+/* Activates in place-free form: each non-NULL input (P rows) is written activated to its output. */
+void lso_activate(int P, int raw, const float* opac, const float* scales, const float* rots, const float* lang,
+                  float* opac_out, float* scales_out, float* rots_out, float* lang_out)
+{
+    for (int i = 0; i < P; i++) {
+        if ((raw & LSO_RAW_OPACITY) && opac) opac_out[i] = act_sigmoid(opac[i]);
+        if ((raw & LSO_RAW_SCALES) && scales)
+            for (int k = 0; k < 3; k++) scales_out[3 * i + k] = lso_act_expf(scales[3 * i + k]);
+        if ((raw & LSO_RAW_ROTATIONS) && rots) {
+            const float* q = rots + 4 * i;
+            const float d = fmaxf(sqrtf(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]), 1e-12f);
+            for (int k = 0; k < 4; k++) rots_out[4 * i + k] = q[k] / d;
+        }
+        if ((raw & LSO_RAW_LANGUAGE) && lang) {
+            const float* f = lang + 3 * i;
+            const float d = sqrtf(f[0] * f[0] + f[1] * f[1] + f[2] * f[2]) + 1e-9f;
+            for (int k = 0; k < 3; k++) lang_out[3 * i + k] = f[k] / d;
+        }
+    }
+}
+
+/* Gradients w.r.t. the activated tensors (g_*) -> gradients w.r.t. the raw inputs (d_*). */
+void lso_activate_backward(int P, int raw, const float* opac, const float* scales, const float* rots,
+                           const float* lang, const float* g_opac, const float* g_scales, const float* g_rots,
+                           const float* g_lang, float* d_opac, float* d_scales, float* d_rots, float* d_lang)
+{
+    for (int i = 0; i < P; i++) {
+        if ((raw & LSO_RAW_OPACITY) && opac) {
+            const float y = act_sigmoid(opac[i]);
+            d_opac[i] = g_opac[i] * (1.0f - y) * y;
+        }
+        if ((raw & LSO_RAW_SCALES) && scales)
+            for (int k = 0; k < 3; k++) d_scales[3 * i + k] = g_scales[3 * i + k] * lso_act_expf(scales[3 * i + k]);
+        if ((raw & LSO_RAW_ROTATIONS) && rots) {
+            const float* q = rots + 4 * i;
+            const float* g = g_rots + 4 * i;
+            const float n = sqrtf(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+            const float d = fmaxf(n, 1e-12f);
+            const float gd = -(g[0] * q[0] + g[1] * q[1] + g[2] * q[2] + g[3] * q[3]) / (d * d);
+            const float kk = (n >= 1e-12f && n > 0.0f) ? gd / n : 0.0f;
+            for (int k = 0; k < 4; k++) d_rots[4 * i + k] = g[k] / d + q[k] * kk;
+        }
+        if ((raw & LSO_RAW_LANGUAGE) && lang) {
+            const float* f = lang + 3 * i;
+            const float* g = g_lang + 3 * i;
+            const float n = sqrtf(f[0] * f[0] + f[1] * f[1] + f[2] * f[2]);
+            const float d = n + 1e-9f;
+            const float gd = -(g[0] * f[0] + g[1] * f[1] + g[2] * f[2]) / (d * d);
+            const float kk = n > 0.0f ? gd / n : 0.0f;
+            for (int k = 0; k < 3; k++) d_lang[3 * i + k] = g[k] / d + f[k] * kk;
+        }
+    }
+}
+
+/* ------------------------------------------------------------------------------------------ */
 
 int64_t lso_num_rendered(const lso_state* st) { return st->R; }
 

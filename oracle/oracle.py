@@ -71,6 +71,12 @@ def lib():
         L.lso_sh_backward.argtypes = [ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 5
         L.lso_cov3d.restype = None
         L.lso_cov3d.argtypes = [ctypes.c_void_p, ctypes.c_float, ctypes.c_void_p, ctypes.c_void_p]
+        L.lso_act_expf.restype = ctypes.c_float
+        L.lso_act_expf.argtypes = [ctypes.c_float]
+        L.lso_activate.restype = None
+        L.lso_activate.argtypes = [ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 8
+        L.lso_activate_backward.restype = None
+        L.lso_activate_backward.argtypes = [ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 12
         L.lso_cov3d_backward.restype = None
         L.lso_cov3d_backward.argtypes = [ctypes.c_void_p, ctypes.c_float] + [ctypes.c_void_p] * 4
         _lib = L
@@ -265,3 +271,32 @@ def cov3d_backward(scales, mod, rots, dcov):
     for i in range(N):
         L.lso_cov3d_backward(_ptr(scales[i]), float(mod), _ptr(rots[i]), _ptr(dcov[i]), _ptr(ds[i]), _ptr(dr[i]))
     return ds, dr
+
+
+RAW_OPACITY, RAW_SCALES, RAW_ROTATIONS, RAW_LANGUAGE = 1, 2, 4, 8
+RAW_ALL = RAW_OPACITY | RAW_SCALES | RAW_ROTATIONS | RAW_LANGUAGE
+
+
+def activate(raw, opacity=None, scales=None, rotations=None, language=None):
+    """lso_activate: GaussianModel's activations of the raw parameters (float32 numpy out).
+    Returns (opacity, scales, rotations, language) with None for absent inputs."""
+    L = lib()
+    ins = [None if x is None else _np(x) for x in (opacity, scales, rotations, language)]
+    P = next(x.shape[0] for x in ins if x is not None)
+    outs = [None if x is None else np.zeros_like(x) for x in ins]
+    L.lso_activate(P, int(raw), *[_ptr(x) if x is not None else None for x in ins],
+                   *[_ptr(x) if x is not None else None for x in outs])
+    return tuple(outs)
+
+
+def activate_backward(raw, raw_inputs, grads):
+    """lso_activate_backward: gradients w.r.t. activated tensors -> w.r.t. the raw tensors.
+    raw_inputs, grads: 4-tuples (opacity, scales, rotations, language) with None for absent."""
+    L = lib()
+    ins = [None if x is None else _np(x) for x in raw_inputs]
+    gs = [None if g is None else _np(g) for g in grads]
+    P = next(x.shape[0] for x in ins if x is not None)
+    outs = [None if x is None else np.zeros_like(x) for x in ins]
+    p = lambda x: _ptr(x) if x is not None else None  # noqa: E731
+    L.lso_activate_backward(P, int(raw), *[p(x) for x in ins], *[p(g) for g in gs], *[p(o) for o in outs])
+    return tuple(outs)

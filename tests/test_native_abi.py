@@ -1,5 +1,6 @@
 """C-ABI library: loads without a GPU, exports every entry point include/lsr.h declares, and its
 Python front-end enforces the reference's API contract (gaussian_renderer/__init__.py:37-105)."""
+import ctypes
 import os
 import re
 
@@ -30,7 +31,7 @@ def test_library_loads_and_exports_every_declared_symbol():
     for name in _declared_functions():
         assert hasattr(lib, name), name
         assert name in _native.SIGNATURES, f"ctypes binding misses {name}"
-    assert lib.lsr_abi_version() == 1
+    assert lib.lsr_abi_version() == _native.ABI_VERSION == 2
 
 
 def test_sizes_and_layout_are_consistent():
@@ -96,3 +97,30 @@ def test_drop_in_module_name():
     import diff_gaussian_rasterization as dgr
     assert dgr.GaussianRasterizer is GaussianRasterizer
     assert dgr.GaussianRasterizationSettings is GaussianRasterizationSettings
+
+
+def test_ctypes_struct_layouts_match_header(tmp_path):
+    """Every ctypes mirror in _native.py has the C header's field offsets and sizes (gcc on lsr.h)."""
+    import subprocess
+    structs = {"lsr_settings": _native.LsrSettings, "lsr_forward_args": _native.LsrForwardArgs,
+               "lsr_backward_args": _native.LsrBackwardArgs, "lsr_state_layout": _native.LsrStateLayout,
+               "lsr_kernel_stat": _native.LsrKernelStat}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "lsr.h"', "int main(void) {"]
+    for cname, cls in structs.items():
+        lines.append(f'printf("{cname} sizeof %zu\\n", sizeof({cname}));')
+        for f in cls._fields_:
+            lines.append(f'printf("{cname} {f[0]} %zu\\n", offsetof({cname}, {f[0]}));')
+    lines.append("return 0; }")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    inc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include")
+    subprocess.run(["gcc", "-I", inc, str(src), "-o", str(exe)], check=True)
+    got = {}
+    for ln in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.splitlines():
+        s, f, v = ln.split()
+        got[(s, f)] = int(v)
+    for cname, cls in structs.items():
+        assert got[(cname, "sizeof")] == ctypes.sizeof(cls), cname
+        for f in cls._fields_:
+            assert got[(cname, f[0])] == getattr(cls, f[0]).offset, (cname, f[0])
