@@ -33,6 +33,7 @@ sys.path.insert(0, ROOT)
 
 from langsplat_amd import _native  # noqa: E402
 from langsplat_amd.distributed import GradBucket, init_from_env  # noqa: E402
+from langsplat_amd.loss import masked_l1_loss  # noqa: E402
 from langsplat_amd.render import render  # noqa: E402
 from langsplat_amd.synthetic import CONFIGS, activated_inputs, make_cameras, make_gaussians  # noqa: E402
 
@@ -191,7 +192,9 @@ def main():
     bg = torch.zeros(3, device=dev)
     gen = torch.Generator().manual_seed(100 + view)
     gt = torch.nn.functional.normalize(torch.randn((3, H, W), generator=gen), dim=0).to(dev)
-    mask = (torch.rand((1, H, W), generator=gen) < 0.9).float().to(dev)
+    # scene/cameras.py:72 builds the mask as a bool tensor (seg != -1)
+    mask = (torch.rand((1, H, W), generator=gen) < 0.9).to(dev)
+    fused = os.environ.get("LANGSPLAT_AMD_FUSED", "1") != "0"
     # scene/gaussian_model.py:229 Adam(lr=0.0, eps=1e-15); fused=True runs the same update as one kernel
     optim = torch.optim.Adam([{"params": [model._language_feature], "lr": 0.0025, "name": "language_feature"}],
                              lr=0.0, eps=1e-15, fused=True)
@@ -200,7 +203,10 @@ def main():
     def step():
         pkg = render(cam, model, Pipe, bg, Opt)
         lang = pkg["language_feature_image"]
-        loss = (lang * mask - gt * mask).abs().mean()
+        if fused:  # one kernel each way
+            loss = masked_l1_loss(lang, gt, mask)
+        else:      # train.py:98 + utils/loss_utils.py:17-18 as torch ops
+            loss = torch.abs(lang * mask - gt * mask).mean()
         loss.backward()
         if world > 1:
             bucket.all_reduce(average=True)
@@ -291,7 +297,7 @@ def main():
                                f"include_feature train step, 1 view per GPU",
                    "gaussians": P, "width": W, "height": H, "views": world, "parallelism": f"dp{world} (views)",
                    "blends_per_step": blends_all, "num_rendered_rank0": nr, "visible_rank0": visible,
-                   "activation": "fused" if os.environ.get("LANGSPLAT_AMD_FUSED", "1") != "0" else "torch"},
+                   "activation_and_loss": "fused" if fused else "torch"},
         "raster_ms_per_step": round(raster_ms, 4),
         "stages_ms_per_step": {k: round(v["total_ms"] / args.steps, 4) for k, v in sorted(prof.items())},
         "roofline": roofline,

@@ -209,6 +209,34 @@ int32_t lsr_profile_report(lsr_kernel_stat* out, int32_t capacity);
 int32_t lsr_mark_visible(int32_t P, const float* means3D, const float* viewmatrix,
                          const float* projmatrix, uint8_t* visible, void* stream);
 
+/* ---- the language-feature loss around the rasterizer ----------------
+ *
+ * lsr_masked_l1_forward replaces, in LangSplat's include_feature step (train.py:97-98),
+ *     Ll1 = l1_loss(language_feature * mask, gt_language_feature * mask)
+ * with l1_loss = torch.abs(a - b).mean() (utils/loss_utils.py:17-18): one pass over
+ * pred / gt (C x HW fp32) and mask (HW, bool bytes or fp32, broadcast over the C channels).
+ * *loss (one float, device) = sum |pred*m - gt*m| / (C*HW), summed in a fixed order
+ * (deterministic).  `scratch` holds lsr_masked_l1_scratch_bytes(C, HW) zeroed-on-exit bytes
+ * (zero it once before the first use).
+ *
+ * lsr_masked_l1_backward writes the gradient torch autograd produces for that expression:
+ *     grad_pred = sign(pred*m - gt*m) * (grad_loss[0] / (C*HW)) * m
+ * (grad_loss is the device scalar dL/dLl1), bit-identical to autograd's mean/abs/sub/mul chain.
+ *
+ * lsr_decode_language_feature restates Camera.get_language_feature (scene/cameras.py:58-92) on
+ * the GPU: seg = seg_map[level] (L x H x W int64), mask = (seg != -1), feature = feature_map[seg]
+ * (N x D fp32; index -1 reads the last row, as torch indexing does) written as D x H x W, and
+ * mask as H x W bytes -- so a training loop can decode each view's map once and keep it in HBM
+ * instead of np.load + CPU gather + H2D every step. */
+size_t lsr_masked_l1_scratch_bytes(int32_t C, int64_t HW);
+int32_t lsr_masked_l1_forward(int32_t C, int64_t HW, const float* pred, const float* gt, const void* mask,
+                              int32_t mask_is_float, float* loss, void* scratch, void* stream);
+int32_t lsr_masked_l1_backward(int32_t C, int64_t HW, const float* pred, const float* gt, const void* mask,
+                               int32_t mask_is_float, const float* grad_loss, float* grad_pred, void* stream);
+int32_t lsr_decode_language_feature(int32_t L, int32_t H, int32_t W, const int64_t* seg_map, int32_t level,
+                                    int32_t N, int32_t D, const float* feature_map, float* out_feature,
+                                    uint8_t* out_mask, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

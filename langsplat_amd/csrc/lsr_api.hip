@@ -377,4 +377,49 @@ int32_t lsr_mark_visible(int32_t P, const float* means3D, const float* viewmatri
     return LSR_OK;
 }
 
+size_t lsr_masked_l1_scratch_bytes(int32_t C, int64_t HW)
+{
+    (void)C;
+    (void)HW;
+    return masked_l1_scratch_bytes();
+}
+
+int32_t lsr_masked_l1_forward(int32_t C, int64_t HW, const float* pred, const float* gt, const void* mask,
+                              int32_t mask_is_float, float* loss, void* scratch, void* stream_ptr)
+{
+    if (C <= 0 || HW <= 0 || !pred || !gt || !mask || !loss || !scratch)
+        return fail(LSR_ERR_INVALID, "lsr_masked_l1_forward: invalid argument");
+    hipStream_t stream = reinterpret_cast<hipStream_t>(stream_ptr);
+    const bool debug = false;
+    LSR_TRY(launch_masked_l1_forward(C, HW, pred, gt, mask, mask_is_float, loss, scratch, stream), "masked l1");
+    return LSR_OK;
+}
+
+int32_t lsr_masked_l1_backward(int32_t C, int64_t HW, const float* pred, const float* gt, const void* mask,
+                               int32_t mask_is_float, const float* grad_loss, float* grad_pred, void* stream_ptr)
+{
+    if (C <= 0 || HW <= 0 || !pred || !gt || !mask || !grad_loss || !grad_pred)
+        return fail(LSR_ERR_INVALID, "lsr_masked_l1_backward: invalid argument");
+    hipStream_t stream = reinterpret_cast<hipStream_t>(stream_ptr);
+    const bool debug = false;
+    LSR_TRY(launch_masked_l1_backward(C, HW, pred, gt, mask, mask_is_float, grad_loss, grad_pred, stream),
+            "masked l1 backward");
+    return LSR_OK;
+}
+
+int32_t lsr_decode_language_feature(int32_t L, int32_t H, int32_t W, const int64_t* seg_map, int32_t level,
+                                    int32_t N, int32_t D, const float* feature_map, float* out_feature,
+                                    uint8_t* out_mask, void* stream_ptr)
+{
+    if (L <= 0 || H <= 0 || W <= 0 || level < 0 || level >= L || N <= 0 || D <= 0 || !seg_map || !feature_map ||
+        !out_feature || !out_mask)
+        return fail(LSR_ERR_INVALID, "lsr_decode_language_feature: invalid argument");
+    hipStream_t stream = reinterpret_cast<hipStream_t>(stream_ptr);
+    const bool debug = false;
+    LSR_TRY(launch_decode_language_feature(H, W, seg_map + (int64_t)level * H * W, N, D, feature_map, out_feature,
+                                           out_mask, stream),
+            "decode language feature");
+    return LSR_OK;
+}
+
 }  // extern "C"

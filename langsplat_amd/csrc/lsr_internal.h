@@ -149,6 +149,14 @@ hipError_t launch_depth_order(int P, const Layout& L, char* geom, uint32_t* coun
 hipError_t launch_binning(int P, int64_t R, const Layout& L, char* geom, char* image, char* binning,
                           hipStream_t s, bool debug);
 
+size_t masked_l1_scratch_bytes();
+hipError_t launch_masked_l1_forward(int C, int64_t HW, const float* pred, const float* gt, const void* mask,
+                                    int mask_is_float, float* loss, void* scratch, hipStream_t s);
+hipError_t launch_masked_l1_backward(int C, int64_t HW, const float* pred, const float* gt, const void* mask,
+                                     int mask_is_float, const float* grad_loss, float* grad_pred, hipStream_t s);
+hipError_t launch_decode_language_feature(int H, int W, const int64_t* seg_level, int N, int D,
+                                          const float* feature_map, float* out, uint8_t* mask, hipStream_t s);
+
 hipError_t launch_render_forward(const RenderParams& p, int tiles, hipStream_t s);
 hipError_t launch_render_backward(const RenderParams& p, int tiles, hipStream_t s);
 

@@ -1,0 +1,217 @@
+// lsr_loss.hip -- the language-feature loss around the rasterizer.
+//
+// LangSplat's include_feature step computes (train.py:97-98, utils/loss_utils.py:17-18)
+//     Ll1 = torch.abs(pred * m - gt * m).mean()        pred, gt: C x H x W, m: 1 x H x W
+// which torch runs as 5 forward + ~6 backward elementwise/reduction kernels over the 3 x H x W
+// images.  Here it is one streaming pass each way (HBM-bound: the forward reads pred + gt +
+// mask, the backward reads them again and writes grad_pred):
+//   k_masked_l1_forward  per-thread partial sums over 4-pixel quads, block sums in double, and
+//                        the last block to finish adds the block sums in a fixed order
+//                        (deterministic, no second launch);
+//   k_masked_l1_backward g * (1/N) * sign(pred*m - gt*m) * m, the operation order of autograd's
+//                        mean -> abs -> sub -> mul backward chain, hence bit-identical to it.
+// k_decode_language_feature is Camera.get_language_feature's gather (scene/cameras.py:58-92).
+#include "lsr_internal.h"
+
+namespace lsr {
+
+constexpr int kLossThreads = 256;
+constexpr int kLossMaxBlocks = 1024;
+
+// mask value of pixel p (bool bytes or fp32)
+__device__ __forceinline__ float mask_at(const void* mask, int is_float, int64_t p)
+{
+    return is_float ? static_cast<const float*>(mask)[p] : (static_cast<const uint8_t*>(mask)[p] ? 1.0f : 0.0f);
+}
+
+// V pixels starting at p of one channel (V = 4: aligned float4 path, V = 1: scalar)
+template <int V>
+__device__ __forceinline__ void load_px(const float* __restrict__ a, int64_t p, float* out)
+{
+    if (V == 4) {
+        const float4 q = *reinterpret_cast<const float4*>(a + p);
+        out[0] = q.x;
+        out[1] = q.y;
+        out[2] = q.z;
+        out[3] = q.w;
+    } else {
+        out[0] = a[p];
+    }
+}
+
+template <int V>
+__device__ __forceinline__ void load_mask(const void* mask, int is_float, int64_t p, float* m)
+{
+    if (V == 4) {
+        if (is_float) {
+            const float4 q = *reinterpret_cast<const float4*>(static_cast<const float*>(mask) + p);
+            m[0] = q.x;
+            m[1] = q.y;
+            m[2] = q.z;
+            m[3] = q.w;
+        } else {
+            const uint32_t b = *reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(mask) + p);
+#pragma unroll
+            for (int k = 0; k < 4; k++) m[k] = ((b >> (8 * k)) & 0xFFu) ? 1.0f : 0.0f;
+        }
+    } else {
+        m[0] = mask_at(mask, is_float, p);
+    }
+}
+
+__device__ __forceinline__ double block_sum_double(double v, double* wsum)
+{
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (lane == 0) wsum[wave] = v;
+    __syncthreads();
+    double t = 0.0;
+    if (threadIdx.x == 0)
+        for (int w = 0; w < kLossThreads / 64; w++) t += wsum[w];
+    return t;  // valid in thread 0
+}
+
+template <int V>
+__global__ __launch_bounds__(kLossThreads) void k_masked_l1_forward(int C, int64_t HW, const float* __restrict__ pred,
+                                                                    const float* __restrict__ gt, const void* mask,
+                                                                    int mask_is_float, float* __restrict__ loss,
+                                                                    uint32_t* __restrict__ counter,
+                                                                    double* __restrict__ partial)
+{
+    __shared__ double wsum[kLossThreads / 64];
+    __shared__ bool s_last;
+    const int64_t groups = HW / V;
+    float acc = 0.0f;
+    for (int64_t gi = (int64_t)blockIdx.x * kLossThreads + threadIdx.x; gi < groups;
+         gi += (int64_t)gridDim.x * kLossThreads) {
+        const int64_t p = gi * V;
+        float m[V];
+        load_mask<V>(mask, mask_is_float, p, m);
+        for (int c = 0; c < C; c++) {
+            float a[V], b[V];
+            load_px<V>(pred + (int64_t)c * HW, p, a);
+            load_px<V>(gt + (int64_t)c * HW, p, b);
+#pragma unroll
+            for (int k = 0; k < V; k++) acc += fabsf(a[k] * m[k] - b[k] * m[k]);
+        }
+    }
+    const double bs = block_sum_double((double)acc, wsum);
+    if (threadIdx.x == 0) {
+        partial[blockIdx.x] = bs;
+        __threadfence();  // release the block sum before counting this block done
+        const uint32_t prev = atomicAdd(counter, 1u);
+        s_last = prev == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();  // acquire: every block's partial is visible
+    double v = 0.0;
+    for (int i = threadIdx.x; i < (int)gridDim.x; i += kLossThreads)
+        v += __hip_atomic_load(&partial[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const double total = block_sum_double(v, wsum);
+    if (threadIdx.x == 0) {
+        *loss = (float)(total / (double)((int64_t)C * HW));
+        *counter = 0u;  // ready for the next launch on this scratch
+    }
+}
+
+template <int V>
+__global__ __launch_bounds__(kLossThreads) void k_masked_l1_backward(int C, int64_t HW, const float* __restrict__ pred,
+                                                                     const float* __restrict__ gt, const void* mask,
+                                                                     int mask_is_float,
+                                                                     const float* __restrict__ grad_loss,
+                                                                     float* __restrict__ grad_pred)
+{
+    // autograd: mean backward grad.div(N) (torch's GPU div by a scalar multiplies by its
+    // reciprocal), abs backward * sign, mul backward * m
+    const float gN = grad_loss[0] * (1.0f / (float)((int64_t)C * HW));
+    const int64_t groups = HW / V;
+    for (int64_t gi = (int64_t)blockIdx.x * kLossThreads + threadIdx.x; gi < groups;
+         gi += (int64_t)gridDim.x * kLossThreads) {
+        const int64_t p = gi * V;
+        float m[V];
+        load_mask<V>(mask, mask_is_float, p, m);
+        for (int c = 0; c < C; c++) {
+            float a[V], b[V], o[V];
+            load_px<V>(pred + (int64_t)c * HW, p, a);
+            load_px<V>(gt + (int64_t)c * HW, p, b);
+#pragma unroll
+            for (int k = 0; k < V; k++) {
+                const float d = a[k] * m[k] - b[k] * m[k];
+                const float sg = d > 0.0f ? 1.0f : (d < 0.0f ? -1.0f : 0.0f);
+                o[k] = gN * sg * m[k];
+            }
+            if (V == 4)
+                *reinterpret_cast<float4*>(grad_pred + (int64_t)c * HW + p) = make_float4(o[0], o[1], o[2], o[3]);
+            else
+                grad_pred[(int64_t)c * HW + p] = o[0];
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_decode_language_feature(int H, int W, const int64_t* __restrict__ seg_level,
+                                                                 int N, int D, const float* __restrict__ feature_map,
+                                                                 float* __restrict__ out, uint8_t* __restrict__ mask)
+{
+    const int64_t HW = (int64_t)H * W;
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= HW) return;
+    int64_t s = seg_level[p];
+    mask[p] = s != -1 ? 1 : 0;
+    if (s < 0) s += N;  // torch indexing: -1 is the last row
+    const bool ok = s >= 0 && s < N;
+    for (int d = 0; d < D; d++) out[(int64_t)d * HW + p] = ok ? feature_map[s * D + d] : 0.0f;
+}
+
+static bool vec4_ok(int64_t HW, const void* a, const void* b, const void* c, const void* mask, int mask_is_float)
+{
+    auto al = [](const void* q, uintptr_t m) { return (reinterpret_cast<uintptr_t>(q) & m) == 0; };
+    return (HW % 4) == 0 && al(a, 15) && al(b, 15) && (!c || al(c, 15)) && al(mask, mask_is_float ? 15 : 3);
+}
+
+static int loss_blocks(int64_t groups)
+{
+    const int64_t b = (groups + kLossThreads - 1) / kLossThreads;
+    return (int)(b < 1 ? 1 : (b > kLossMaxBlocks ? kLossMaxBlocks : b));
+}
+
+size_t masked_l1_scratch_bytes() { return 256 + 8 * (size_t)kLossMaxBlocks; }
+
+hipError_t launch_masked_l1_forward(int C, int64_t HW, const float* pred, const float* gt, const void* mask,
+                                    int mask_is_float, float* loss, void* scratch, hipStream_t s)
+{
+    uint32_t* counter = static_cast<uint32_t*>(scratch);
+    double* partial = reinterpret_cast<double*>(static_cast<char*>(scratch) + 256);
+    if (vec4_ok(HW, pred, gt, nullptr, mask, mask_is_float))
+        hipLaunchKernelGGL(k_masked_l1_forward<4>, dim3(loss_blocks(HW / 4)), dim3(kLossThreads), 0, s, C, HW, pred,
+                           gt, mask, mask_is_float, loss, counter, partial);
+    else
+        hipLaunchKernelGGL(k_masked_l1_forward<1>, dim3(loss_blocks(HW)), dim3(kLossThreads), 0, s, C, HW, pred, gt,
+                           mask, mask_is_float, loss, counter, partial);
+    return hipGetLastError();
+}
+
+hipError_t launch_masked_l1_backward(int C, int64_t HW, const float* pred, const float* gt, const void* mask,
+                                     int mask_is_float, const float* grad_loss, float* grad_pred, hipStream_t s)
+{
+    if (vec4_ok(HW, pred, gt, grad_pred, mask, mask_is_float))
+        hipLaunchKernelGGL(k_masked_l1_backward<4>, dim3(loss_blocks(HW / 4)), dim3(kLossThreads), 0, s, C, HW, pred,
+                           gt, mask, mask_is_float, grad_loss, grad_pred);
+    else
+        hipLaunchKernelGGL(k_masked_l1_backward<1>, dim3(loss_blocks(HW)), dim3(kLossThreads), 0, s, C, HW, pred, gt,
+                           mask, mask_is_float, grad_loss, grad_pred);
+    return hipGetLastError();
+}
+
+hipError_t launch_decode_language_feature(int H, int W, const int64_t* seg_level, int N, int D,
+                                          const float* feature_map, float* out, uint8_t* mask, hipStream_t s)
+{
+    const int64_t HW = (int64_t)H * W;
+    hipLaunchKernelGGL(k_decode_language_feature, dim3((unsigned)((HW + 255) / 256)), dim3(256), 0, s, H, W, seg_level,
+                       N, D, feature_map, out, mask);
+    return hipGetLastError();
+}
+
+}  // namespace lsr

@@ -15,9 +15,12 @@ namespace lsr {
 // (the fused path's _features_dc P x 1 x 3 into columns 0-2 and _features_rest P x (M-1) x 3
 // into columns 3..), which removes the per-step torch.cat of scene/gaussian_model.py:146-150.
 
-// rows of w floats of the block's Gaussians from src -> LDS rows (stride ws) starting at col0
-__device__ __forceinline__ void rows_in(const float* __restrict__ src, int ng, int w, float* lds, int ws, int col0)
+// rows of w floats of the block's Gaussians from src -> LDS rows (stride ws) starting at col0;
+// kW > 0 fixes the row width at compile time (the divisions become multiplies)
+template <int kW>
+__device__ __forceinline__ void rows_in(const float* __restrict__ src, int ng, int w_rt, float* lds, int ws, int col0)
 {
+    const int w = kW > 0 ? kW : w_rt;
     const int n = ng * w;
     const int n4 = (reinterpret_cast<uintptr_t>(src) & 15) == 0 ? (n >> 2) : 0;
     const float4* s4 = reinterpret_cast<const float4*>(src);
@@ -60,8 +63,10 @@ __device__ __forceinline__ void rows_in(const float* __restrict__ src, int ng, i
     }
 }
 
-__device__ __forceinline__ void rows_out(float* __restrict__ dst, int ng, int w, const float* lds, int ws, int col0)
+template <int kW>
+__device__ __forceinline__ void rows_out(float* __restrict__ dst, int ng, int w_rt, const float* lds, int ws, int col0)
 {
+    const int w = kW > 0 ? kW : w_rt;
     const int n = ng * w;
     const int n4 = (reinterpret_cast<uintptr_t>(dst) & 15) == 0 ? (n >> 2) : 0;
     float4* d4 = reinterpret_cast<float4*>(dst);
@@ -90,10 +95,12 @@ __device__ __forceinline__ void stage_sh_in(const float* shs, const float* shs_r
 {
     const int g0 = blockIdx.x * blockDim.x, ng = min((int)blockDim.x, P - g0), ws = 3 * M + 1;
     if (!shs_rest) {
-        rows_in(shs + (size_t)g0 * 3 * M, ng, 3 * M, lds, ws, 0);
+        if (M == 16) rows_in<48>(shs + (size_t)g0 * 48, ng, 48, lds, ws, 0);
+        else rows_in<0>(shs + (size_t)g0 * 3 * M, ng, 3 * M, lds, ws, 0);
     } else {
-        rows_in(shs + (size_t)g0 * 3, ng, 3, lds, ws, 0);
-        if (M > 1) rows_in(shs_rest + (size_t)g0 * 3 * (M - 1), ng, 3 * (M - 1), lds, ws, 3);
+        rows_in<3>(shs + (size_t)g0 * 3, ng, 3, lds, ws, 0);
+        if (M == 16) rows_in<45>(shs_rest + (size_t)g0 * 45, ng, 45, lds, ws, 3);
+        else if (M > 1) rows_in<0>(shs_rest + (size_t)g0 * 3 * (M - 1), ng, 3 * (M - 1), lds, ws, 3);
     }
 }
 
@@ -101,10 +108,12 @@ __device__ __forceinline__ void stage_sh_out(float* dsh, float* dsh_rest, int P,
 {
     const int g0 = blockIdx.x * blockDim.x, ng = min((int)blockDim.x, P - g0), ws = 3 * M + 1;
     if (!dsh_rest) {
-        rows_out(dsh + (size_t)g0 * 3 * M, ng, 3 * M, lds, ws, 0);
+        if (M == 16) rows_out<48>(dsh + (size_t)g0 * 48, ng, 48, lds, ws, 0);
+        else rows_out<0>(dsh + (size_t)g0 * 3 * M, ng, 3 * M, lds, ws, 0);
     } else {
-        rows_out(dsh + (size_t)g0 * 3, ng, 3, lds, ws, 0);
-        if (M > 1) rows_out(dsh_rest + (size_t)g0 * 3 * (M - 1), ng, 3 * (M - 1), lds, ws, 3);
+        rows_out<3>(dsh + (size_t)g0 * 3, ng, 3, lds, ws, 0);
+        if (M == 16) rows_out<45>(dsh_rest + (size_t)g0 * 45, ng, 45, lds, ws, 3);
+        else if (M > 1) rows_out<0>(dsh_rest + (size_t)g0 * 3 * (M - 1), ng, 3 * (M - 1), lds, ws, 3);
     }
 }
 
