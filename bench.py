@@ -34,6 +34,7 @@ sys.path.insert(0, ROOT)
 from langsplat_amd import _native  # noqa: E402
 from langsplat_amd.distributed import GradBucket, init_from_env  # noqa: E402
 from langsplat_amd.loss import masked_l1_loss  # noqa: E402
+from langsplat_amd.optim import Adam as AmdAdam  # noqa: E402
 from langsplat_amd.render import render  # noqa: E402
 from langsplat_amd.synthetic import CONFIGS, activated_inputs, make_cameras, make_gaussians  # noqa: E402
 
@@ -195,10 +196,15 @@ def main():
     # scene/cameras.py:72 builds the mask as a bool tensor (seg != -1)
     mask = (torch.rand((1, H, W), generator=gen) < 0.9).to(dev)
     fused = os.environ.get("LANGSPLAT_AMD_FUSED", "1") != "0"
-    # scene/gaussian_model.py:229 Adam(lr=0.0, eps=1e-15); fused=True runs the same update as one kernel
-    optim = torch.optim.Adam([{"params": [model._language_feature], "lr": 0.0025, "name": "language_feature"}],
-                             lr=0.0, eps=1e-15, fused=True)
-    bucket = GradBucket(model.trainable())
+    # scene/gaussian_model.py:229 Adam(lr=0.0, eps=1e-15) over the language-feature group (:203-217)
+    groups = [{"params": [model._language_feature], "lr": 0.0025, "name": "language_feature"}]
+    if fused:  # one HIP kernel per parameter
+        optim = AmdAdam(groups, lr=0.0, eps=1e-15)
+    else:
+        optim = torch.optim.Adam(groups, lr=0.0, eps=1e-15, fused=True)
+    # N > 1: .grad tensors are views of one flat bucket (one all-reduce); N = 1: train.py:138's
+    # zero_grad(set_to_none=True), so autograd hands the rasterizer's gradient over without a copy
+    bucket = GradBucket(model.trainable()) if world > 1 else None
 
     def step():
         pkg = render(cam, model, Pipe, bg, Opt)
@@ -208,10 +214,10 @@ def main():
         else:      # train.py:98 + utils/loss_utils.py:17-18 as torch ops
             loss = torch.abs(lang * mask - gt * mask).mean()
         loss.backward()
-        if world > 1:
+        if bucket is not None:
             bucket.all_reduce(average=True)
         optim.step()
-        optim.zero_grad(set_to_none=False)
+        optim.zero_grad(set_to_none=bucket is None)
         return loss
 
     # blends and instance counts of this view (constant over steps: geometry is frozen)

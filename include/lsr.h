@@ -216,8 +216,8 @@ int32_t lsr_mark_visible(int32_t P, const float* means3D, const float* viewmatri
  * with l1_loss = torch.abs(a - b).mean() (utils/loss_utils.py:17-18): one pass over
  * pred / gt (C x HW fp32) and mask (HW, bool bytes or fp32, broadcast over the C channels).
  * *loss (one float, device) = sum |pred*m - gt*m| / (C*HW), summed in a fixed order
- * (deterministic).  `scratch` holds lsr_masked_l1_scratch_bytes(C, HW) zeroed-on-exit bytes
- * (zero it once before the first use).
+ * (deterministic).  `scratch` holds lsr_masked_l1_scratch_bytes(C, HW) bytes, zeroed once
+ * before its first use and then reused (one stream at a time per scratch).
  *
  * lsr_masked_l1_backward writes the gradient torch autograd produces for that expression:
  *     grad_pred = sign(pred*m - gt*m) * (grad_loss[0] / (C*HW)) * m
@@ -228,6 +228,15 @@ int32_t lsr_mark_visible(int32_t P, const float* means3D, const float* viewmatri
  * (N x D fp32; index -1 reads the last row, as torch indexing does) written as D x H x W, and
  * mask as H x W bytes -- so a training loop can decode each view's map once and keep it in HBM
  * instead of np.load + CPU gather + H2D every step. */
+/* ---- optimiser step --------------------------------------------------
+ * One Adam step of torch.optim.Adam (amsgrad=False, weight_decay=0), the optimiser of
+ * scene/gaussian_model.py:229 stepped at train.py:134-137, over one fp32 parameter tensor of n
+ * elements: exp_avg / exp_avg_sq updated in place, then param.  `step` is the 1-based step count
+ * after this update (torch's state["step"]); lr may change between calls (learning-rate
+ * schedules, scene/gaussian_model.py:231-241). */
+int32_t lsr_adam_step(int64_t n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq, double lr,
+                      double beta1, double beta2, double eps, int64_t step, void* stream);
+
 size_t lsr_masked_l1_scratch_bytes(int32_t C, int64_t HW);
 int32_t lsr_masked_l1_forward(int32_t C, int64_t HW, const float* pred, const float* gt, const void* mask,
                               int32_t mask_is_float, float* loss, void* scratch, void* stream);

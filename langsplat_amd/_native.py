@@ -89,6 +89,8 @@ SIGNATURES = {
     "lsr_backward": (ctypes.c_int32, [ctypes.POINTER(LsrSettings), ctypes.POINTER(LsrBackwardArgs), ALLOC_FN, _vp,
                                       _vp]),
     "lsr_mark_visible": (ctypes.c_int32, [ctypes.c_int32, _vp, _vp, _vp, _vp, _vp]),
+    "lsr_adam_step": (ctypes.c_int32, [ctypes.c_int64, _vp, _vp, _vp, _vp, ctypes.c_double, ctypes.c_double,
+                                       ctypes.c_double, ctypes.c_double, ctypes.c_int64, _vp]),
     "lsr_masked_l1_scratch_bytes": (ctypes.c_size_t, [ctypes.c_int32, ctypes.c_int64]),
     "lsr_masked_l1_forward": (ctypes.c_int32, [ctypes.c_int32, ctypes.c_int64, _vp, _vp, _vp, ctypes.c_int32, _vp, _vp,
                                                _vp]),

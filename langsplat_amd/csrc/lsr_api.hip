@@ -4,6 +4,7 @@
 // call sites they replace): forward = preprocess -> depth sort -> tile counts/scan ->
 // [one D2H read of num_rendered] -> emit -> per-tile order -> render; backward = render
 // replay -> per-Gaussian chain rule.
+#include <math.h>
 #include <stdio.h>
 #include <string.h>
 
@@ -391,7 +392,18 @@ int32_t lsr_masked_l1_forward(int32_t C, int64_t HW, const float* pred, const fl
         return fail(LSR_ERR_INVALID, "lsr_masked_l1_forward: invalid argument");
     hipStream_t stream = reinterpret_cast<hipStream_t>(stream_ptr);
     const bool debug = false;
-    LSR_TRY(launch_masked_l1_forward(C, HW, pred, gt, mask, mask_is_float, loss, scratch, stream), "masked l1");
+    // per-scratch launch epoch (never 0, the value of freshly zeroed scratch)
+    uint32_t epoch = 0;
+    {
+        static std::mutex mu;
+        static std::map<void*, uint32_t> epochs;
+        std::lock_guard<std::mutex> g(mu);
+        uint32_t& e = epochs[scratch];
+        e = e + 1 == 0 ? 1 : e + 1;
+        epoch = e;
+    }
+    LSR_TRY(launch_masked_l1_forward(C, HW, pred, gt, mask, mask_is_float, loss, scratch, epoch, stream),
+            "masked l1");
     return LSR_OK;
 }
 
@@ -404,6 +416,27 @@ int32_t lsr_masked_l1_backward(int32_t C, int64_t HW, const float* pred, const f
     const bool debug = false;
     LSR_TRY(launch_masked_l1_backward(C, HW, pred, gt, mask, mask_is_float, grad_loss, grad_pred, stream),
             "masked l1 backward");
+    return LSR_OK;
+}
+
+int32_t lsr_adam_step(int64_t n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq, double lr,
+                      double beta1, double beta2, double eps, int64_t step, void* stream_ptr)
+{
+    if (n < 0 || (n > 0 && (!param || !grad || !exp_avg || !exp_avg_sq)) || step < 1)
+        return fail(LSR_ERR_INVALID, "lsr_adam_step: invalid argument");
+    hipStream_t stream = reinterpret_cast<hipStream_t>(stream_ptr);
+    const bool debug = false;
+    // torch/optim/adam.py _single_tensor_adam: Python-float scalars, cast where they meet tensors
+    const double bc1 = 1.0 - pow(beta1, (double)step);
+    const double bc2 = 1.0 - pow(beta2, (double)step);
+    AdamScalars a;
+    a.w1 = (float)(1.0 - beta1);
+    a.beta2 = (float)beta2;
+    a.w2 = (float)(1.0 - beta2);
+    a.inv_bc2_sqrt = 1.0f / (float)sqrt(bc2);
+    a.eps = (float)eps;
+    a.neg_step_size = (float)(-(lr / bc1));
+    LSR_TRY(launch_adam(n, param, grad, exp_avg, exp_avg_sq, a, stream), "adam");
     return LSR_OK;
 }
 

@@ -149,9 +149,19 @@ hipError_t launch_depth_order(int P, const Layout& L, char* geom, uint32_t* coun
 hipError_t launch_binning(int P, int64_t R, const Layout& L, char* geom, char* image, char* binning,
                           hipStream_t s, bool debug);
 
+struct AdamScalars {
+    float w1;             // 1 - beta1 (lerp weight)
+    float beta2, w2;      // beta2, 1 - beta2
+    float inv_bc2_sqrt;   // 1 / sqrt(1 - beta2^step)
+    float eps;
+    float neg_step_size;  // -lr / (1 - beta1^step)
+};
+hipError_t launch_adam(int64_t n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                       const AdamScalars& a, hipStream_t s);
+
 size_t masked_l1_scratch_bytes();
 hipError_t launch_masked_l1_forward(int C, int64_t HW, const float* pred, const float* gt, const void* mask,
-                                    int mask_is_float, float* loss, void* scratch, hipStream_t s);
+                                    int mask_is_float, float* loss, void* scratch, uint32_t epoch, hipStream_t s);
 hipError_t launch_masked_l1_backward(int C, int64_t HW, const float* pred, const float* gt, const void* mask,
                                      int mask_is_float, const float* grad_loss, float* grad_pred, hipStream_t s);
 hipError_t launch_decode_language_feature(int H, int W, const int64_t* seg_level, int N, int D,

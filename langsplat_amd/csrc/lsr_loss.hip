@@ -7,7 +7,7 @@
 // mask, the backward reads them again and writes grad_pred):
 //   k_masked_l1_forward  per-thread partial sums over 4-pixel quads, block sums in double, and
 //                        the last block to finish adds the block sums in a fixed order
-//                        (deterministic, no second launch);
+//                        (deterministic, no second launch, no fences);
 //   k_masked_l1_backward g * (1/N) * sign(pred*m - gt*m) * m, the operation order of autograd's
 //                        mean -> abs -> sub -> mul backward chain, hence bit-identical to it.
 // k_decode_language_feature is Camera.get_language_feature's gather (scene/cameras.py:58-92).
@@ -72,12 +72,16 @@ __device__ __forceinline__ double block_sum_double(double v, double* wsum)
     return t;  // valid in thread 0
 }
 
+// Block sums are published as ONE 64-bit word {epoch, float bits} with an sc1 store; the last
+// block (ticket) spins until every word carries this launch's epoch, then adds them in block
+// order.  No __threadfence (on gfx950 each one is an L2 writeback) and no scratch reset between
+// launches: the host passes a fresh nonzero epoch per launch.
 template <int V>
 __global__ __launch_bounds__(kLossThreads) void k_masked_l1_forward(int C, int64_t HW, const float* __restrict__ pred,
                                                                     const float* __restrict__ gt, const void* mask,
                                                                     int mask_is_float, float* __restrict__ loss,
-                                                                    uint32_t* __restrict__ counter,
-                                                                    double* __restrict__ partial)
+                                                                    uint32_t* __restrict__ ticket,
+                                                                    uint64_t* __restrict__ partial, uint32_t epoch)
 {
     __shared__ double wsum[kLossThreads / 64];
     __shared__ bool s_last;
@@ -98,22 +102,24 @@ __global__ __launch_bounds__(kLossThreads) void k_masked_l1_forward(int C, int64
     }
     const double bs = block_sum_double((double)acc, wsum);
     if (threadIdx.x == 0) {
-        partial[blockIdx.x] = bs;
-        __threadfence();  // release the block sum before counting this block done
-        const uint32_t prev = atomicAdd(counter, 1u);
-        s_last = prev == gridDim.x - 1;
+        const uint64_t word = ((uint64_t)epoch << 32) | __float_as_uint((float)bs);
+        __hip_atomic_store(&partial[blockIdx.x], word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = atomicAdd(ticket, 1u) == gridDim.x - 1;
     }
     __syncthreads();
     if (!s_last) return;
-    __threadfence();  // acquire: every block's partial is visible
     double v = 0.0;
-    for (int i = threadIdx.x; i < (int)gridDim.x; i += kLossThreads)
-        v += __hip_atomic_load(&partial[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int i = threadIdx.x; i < (int)gridDim.x; i += kLossThreads) {
+        uint64_t w = __hip_atomic_load(&partial[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (uint32_t spins = 0; (uint32_t)(w >> 32) != epoch && spins < (1u << 24); spins++)
+            w = __hip_atomic_load(&partial[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        v += (double)__uint_as_float((uint32_t)w);
+    }
     __syncthreads();
     const double total = block_sum_double(v, wsum);
     if (threadIdx.x == 0) {
         *loss = (float)(total / (double)((int64_t)C * HW));
-        *counter = 0u;  // ready for the next launch on this scratch
+        *ticket = 0u;  // the next launch on this scratch is stream-ordered after this one
     }
 }
 
@@ -180,16 +186,16 @@ static int loss_blocks(int64_t groups)
 size_t masked_l1_scratch_bytes() { return 256 + 8 * (size_t)kLossMaxBlocks; }
 
 hipError_t launch_masked_l1_forward(int C, int64_t HW, const float* pred, const float* gt, const void* mask,
-                                    int mask_is_float, float* loss, void* scratch, hipStream_t s)
+                                    int mask_is_float, float* loss, void* scratch, uint32_t epoch, hipStream_t s)
 {
     uint32_t* counter = static_cast<uint32_t*>(scratch);
-    double* partial = reinterpret_cast<double*>(static_cast<char*>(scratch) + 256);
+    uint64_t* partial = reinterpret_cast<uint64_t*>(static_cast<char*>(scratch) + 256);
     if (vec4_ok(HW, pred, gt, nullptr, mask, mask_is_float))
         hipLaunchKernelGGL(k_masked_l1_forward<4>, dim3(loss_blocks(HW / 4)), dim3(kLossThreads), 0, s, C, HW, pred,
-                           gt, mask, mask_is_float, loss, counter, partial);
+                           gt, mask, mask_is_float, loss, counter, partial, epoch);
     else
         hipLaunchKernelGGL(k_masked_l1_forward<1>, dim3(loss_blocks(HW)), dim3(kLossThreads), 0, s, C, HW, pred, gt,
-                           mask, mask_is_float, loss, counter, partial);
+                           mask, mask_is_float, loss, counter, partial, epoch);
     return hipGetLastError();
 }
 

@@ -1,0 +1,57 @@
+"""Adam for the Gaussian parameters on the GPU.
+
+Drop-in for the `torch.optim.Adam(l, lr=0.0, eps=1e-15)` of scene/gaussian_model.py:229 (and
+:203-217 in language-feature mode).  Same param_groups ("lr", "betas", "eps", "name" ...), same
+per-parameter state keys ("step", "exp_avg", "exp_avg_sq") -- so update_learning_rate
+(:231-241) and the densification code that rewrites optimizer state (:326-420) work unchanged --
+but each parameter is updated by ONE HIP kernel (liblsr.so lsr_adam_step: one HBM pass over
+param / grad / moments) instead of torch's multi-tensor kernels.  amsgrad, weight decay and
+maximize are not used by LangSplat and are not offered.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _native
+
+
+class Adam(torch.optim.Optimizer):
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8):
+        if lr < 0.0 or eps < 0.0 or not (0.0 <= betas[0] < 1.0 and 0.0 <= betas[1] < 1.0):
+            raise ValueError(f"invalid Adam hyper-parameters lr={lr} betas={betas} eps={eps}")
+        super().__init__(params, dict(lr=lr, betas=tuple(betas), eps=eps))
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        lib = _native.load()
+        for group in self.param_groups:
+            beta1, beta2 = group["betas"]
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                if p.device.type != "cuda" or p.dtype != torch.float32 or not p.is_contiguous():
+                    raise RuntimeError("langsplat_amd.optim.Adam: parameters must be contiguous fp32 tensors on a "
+                                       "ROCm GPU device (there is no CPU path)")
+                if p.grad.is_sparse:
+                    raise RuntimeError("langsplat_amd.optim.Adam does not support sparse gradients")
+                grad = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
+                state = self.state[p]
+                if len(state) == 0:
+                    state["step"] = torch.tensor(0.0)
+                    state["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    state["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                state["step"] += 1
+                step = int(state["step"].item())
+                with _native._on_device(p.device):
+                    _native._check(lib.lsr_adam_step(
+                        p.numel(), ctypes.c_void_p(p.data_ptr()), ctypes.c_void_p(grad.data_ptr()),
+                        ctypes.c_void_p(state["exp_avg"].data_ptr()), ctypes.c_void_p(state["exp_avg_sq"].data_ptr()),
+                        float(group["lr"]), float(beta1), float(beta2), float(group["eps"]), step,
+                        _native._stream(p.device)), "lsr_adam_step")
+        return loss

@@ -124,3 +124,12 @@ def test_ctypes_struct_layouts_match_header(tmp_path):
         assert got[(cname, "sizeof")] == ctypes.sizeof(cls), cname
         for f in cls._fields_:
             assert got[(cname, f[0])] == getattr(cls, f[0]).offset, (cname, f[0])
+
+
+def test_optim_adam_refuses_cpu_parameters():
+    from langsplat_amd.optim import Adam
+    p = torch.zeros(4, requires_grad=True)
+    p.grad = torch.ones(4)
+    opt = Adam([p], lr=0.1)
+    with pytest.raises(RuntimeError, match="no CPU path"):
+        opt.step()
