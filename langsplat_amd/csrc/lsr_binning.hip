@@ -196,87 +196,103 @@ static hipError_t scan_exclusive(const uint32_t* in, uint32_t* out, int n, uint3
 
 // ---------------------------------------------------------------- stable LSD radix sort
 
+// Both radix kernels use a BLOCKED arrangement: wave w of a block owns the contiguous keys
+// [w * 64 * kItems, (w + 1) * 64 * kItems) of the block's tile and walks them in rounds of 64
+// consecutive keys, counting digits in its own LDS row.  Rounds of one wave are ordered by the
+// wave's in-order LDS pipeline, so no block barrier is needed until all rounds are done; the
+// stable order (wave, round, lane) is the input order.
+
 // Per-block digit histogram; hist layout [digit][block] so one scan yields the scatter bases.
 // kItems keys per thread: 16 for large sorts, 4 for P-sized ones (so that >= ~1000 blocks run).
 template <int kItems>
 __global__ __launch_bounds__(kRadixThreads) void k_radix_hist(const uint32_t* __restrict__ keys, int n, int shift,
                                                               int nbits, uint32_t* __restrict__ hist, int nblk)
 {
-    constexpr int kRadixTile = kRadixThreads * kItems;
-    constexpr int kRadixItems = kItems;
-    __shared__ uint32_t h[256];
-    const int t = threadIdx.x;
+    constexpr int kWaves = kRadixThreads / 64;
+    __shared__ uint32_t wcnt[kWaves][256];
+    const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
     const uint32_t mask = (1u << nbits) - 1u;
-    h[t] = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; w++) wcnt[w][t] = 0;
     __syncthreads();
-    const int base = blockIdx.x * kRadixTile;
-    for (int it = 0; it < kRadixItems; it++) {
-        const int idx = base + it * kRadixThreads + t;
-        const bool valid = idx < n;
-        const uint32_t d = valid ? (keys[idx] >> shift) & mask : 0u;
-        const uint64_t peers = match_digit(d, valid, nbits);
-        if (valid && (peers & lanemask_lt()) == 0) atomicAdd(&h[d], (uint32_t)__popcll(peers));
+    const int base = blockIdx.x * kRadixThreads * kItems + wave * 64 * kItems;
+    uint32_t d[kItems];
+    bool valid[kItems];
+#pragma unroll
+    for (int it = 0; it < kItems; it++) {
+        const int idx = base + it * 64 + lane;
+        valid[it] = idx < n;
+        d[it] = valid[it] ? (keys[idx] >> shift) & mask : 0u;
+    }
+#pragma unroll
+    for (int it = 0; it < kItems; it++) {
+        const uint64_t peers = match_digit(d[it], valid[it], nbits);
+        if (valid[it] && (peers & lanemask_lt()) == 0) wcnt[wave][d[it]] += (uint32_t)__popcll(peers);
     }
     __syncthreads();
-    if (t <= (int)mask) hist[t * nblk + blockIdx.x] = h[t];
+    if (t <= (int)mask) {
+        uint32_t c = 0;
+#pragma unroll
+        for (int w = 0; w < kWaves; w++) c += wcnt[w][t];
+        hist[t * nblk + blockIdx.x] = c;
+    }
 }
 
-// Stable scatter of one block's kRadixTile keys.  Ranks are computed round by round in input order
-// (wave64 ballot match + per-wave digit counts), the block is reordered by digit in LDS, and the
-// output is written from LDS in digit-contiguous runs, so global stores coalesce (a direct scatter
-// would send the 64 lanes of a store to up to 64 different buckets).
+// Stable scatter of one block's tile.  Ranks: per wave, round by round (ballot match + the wave's
+// running digit counts); then per digit the block-local start (scan over digits) and each wave's
+// exclusive offset (sum over lower waves).  The tile is reordered by digit in LDS and written
+// from LDS in digit-contiguous runs, so global stores coalesce (a direct scatter would send the
+// 64 lanes of a store to up to 64 different buckets).
 template <int kItems>
 __global__ __launch_bounds__(kRadixThreads) void k_radix_scatter(
     const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in, int n, int shift, int nbits,
     const uint32_t* __restrict__ hist, int nblk, uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out)
 {
-    constexpr int kRadixTile = kRadixThreads * kItems;
-    constexpr int kRadixItems = kItems;
-    __shared__ uint32_t sk[kRadixTile];
-    __shared__ uint32_t sv[kRadixTile];
-    __shared__ uint32_t gbase[256];     // global output position of this block's first key per digit
-    __shared__ uint32_t dstart[256];    // block-local start of each digit in the reordered tile
-    __shared__ uint32_t run[256];       // per-digit count so far in this block
-    __shared__ uint32_t wcount[kRadixThreads / 64][256];
-    __shared__ uint32_t wsum[kRadixThreads / 64];
+    constexpr int kTile = kRadixThreads * kItems;
+    constexpr int kWaves = kRadixThreads / 64;
+    __shared__ uint32_t sk[kTile];
+    __shared__ uint32_t sv[kTile];
+    __shared__ uint32_t wcnt[kWaves][256];  // running counts, then each wave's offset within the digit
+    __shared__ uint32_t gbase[256];         // global output position of this block's first key per digit
+    __shared__ uint32_t dstart[256];        // block-local start of each digit in the reordered tile
+    __shared__ uint32_t wsum[kWaves];
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
     const uint32_t mask = (1u << nbits) - 1u;
-    gbase[t] = t <= (int)mask ? hist[t * nblk + blockIdx.x] : 0u;
-    run[t] = 0;
-    const int base = blockIdx.x * kRadixTile;
-    uint32_t key[kRadixItems], val[kRadixItems], rank[kRadixItems];
 #pragma unroll
-    for (int it = 0; it < kRadixItems; it++) {
-        const int idx = base + it * kRadixThreads + t;
+    for (int w = 0; w < kWaves; w++) wcnt[w][t] = 0;
+    gbase[t] = t <= (int)mask ? hist[t * nblk + blockIdx.x] : 0u;
+    const int tile0 = blockIdx.x * kTile;
+    const int base = tile0 + wave * 64 * kItems;
+    uint32_t key[kItems], val[kItems], rank[kItems];
+#pragma unroll
+    for (int it = 0; it < kItems; it++) {
+        const int idx = base + it * 64 + lane;
         const bool valid = idx < n;
         key[it] = valid ? keys_in[idx] : 0u;
         val[it] = valid ? (vals_in ? vals_in[idx] : (uint32_t)idx) : 0u;
     }
+    __syncthreads();
 #pragma unroll
-    for (int it = 0; it < kRadixItems; it++) {
-#pragma unroll
-        for (int w = 0; w < kRadixThreads / 64; w++) wcount[w][t] = 0;
-        __syncthreads();
-        const bool valid = base + it * kRadixThreads + t < n;
+    for (int it = 0; it < kItems; it++) {
+        const bool valid = base + it * 64 + lane < n;
         const uint32_t d = (key[it] >> shift) & mask;
         const uint64_t peers = match_digit(d, valid, nbits);
         const uint32_t r = (uint32_t)__popcll(peers & lanemask_lt());
-        if (valid && r == 0) wcount[wave][d] = (uint32_t)__popcll(peers);
-        __syncthreads();
-        uint32_t off = run[d] + r;
-        for (int w = 0; w < wave; w++) off += wcount[w][d];
-        rank[it] = off;
-        __syncthreads();
-        uint32_t add = 0;
-#pragma unroll
-        for (int w = 0; w < kRadixThreads / 64; w++) add += wcount[w][t];
-        run[t] += add;
+        const uint32_t c = wcnt[wave][d];
+        rank[it] = c + r;
+        if (valid && r == 0) wcnt[wave][d] = c + (uint32_t)__popcll(peers);
     }
     __syncthreads();
-    // block-local exclusive scan of the digit counts
+    // per digit: waves' exclusive offsets and the block-local digit start
     {
-        const uint32_t c = run[t];
-        uint32_t x = c;
+        uint32_t tot = 0;
+#pragma unroll
+        for (int w = 0; w < kWaves; w++) {
+            const uint32_t c = wcnt[w][t];
+            wcnt[w][t] = tot;
+            tot += c;
+        }
+        uint32_t x = tot;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
             const uint32_t y = __shfl_up(x, o, 64);
@@ -286,20 +302,20 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_scatter(
         __syncthreads();
         uint32_t before = 0;
         for (int w = 0; w < wave; w++) before += wsum[w];
-        dstart[t] = before + x - c;
+        dstart[t] = before + x - tot;
     }
     __syncthreads();
 #pragma unroll
-    for (int it = 0; it < kRadixItems; it++) {
-        if (base + it * kRadixThreads + t < n) {
+    for (int it = 0; it < kItems; it++) {
+        if (base + it * 64 + lane < n) {
             const uint32_t d = (key[it] >> shift) & mask;
-            const uint32_t pos = dstart[d] + rank[it];
+            const uint32_t pos = dstart[d] + wcnt[wave][d] + rank[it];
             sk[pos] = key[it];
             sv[pos] = val[it];
         }
     }
     __syncthreads();
-    const int cnt = min(kRadixTile, n - base);
+    const int cnt = min(kTile, n - tile0);
     for (int i = t; i < cnt; i += kRadixThreads) {
         const uint32_t k = sk[i];
         const uint32_t d = (k >> shift) & mask;
