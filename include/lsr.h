@@ -161,30 +161,31 @@ typedef struct lsr_state_layout {
     size_t record;         /* float4[3P] {x, y, conic.x, conic.y}{conic.z, opacity, r, g}{b, f0, f1, f2} */
     size_t clamped;        /* uint32[P]  bit c = SH colour channel c clamped */
     size_t sorted_ids;     /* uint32[P]  Gaussians by (depth, id); visible ones first */
-    size_t inst_offset;    /* uint32[P]  first tile instance of the Gaussian of depth rank r */
+    size_t super_offset;   /* uint32[P]  first super-tile entry of the Gaussian of depth rank r */
     /* image buffer */
-    size_t counters;       /* uint32[16] {reserved, num_rendered, error, ...} */
+    size_t counters;       /* uint32[16] {reserved, num_rendered, error, scan fault, super entries, ...} */
     size_t ranges;         /* uint32[2T] [start, end) of each tile in point_list */
     size_t final_T;        /* float[H*W] */
     size_t n_contrib;      /* uint32[H*W] */
     /* binning buffer */
-    size_t point_list;     /* uint32[num_rendered] Gaussian ids, tile-major, (depth, id) order */
-    size_t list_keys;      /* uint32[num_rendered] tile id of each point_list entry */
+    size_t point_list;     /* uint32[num_rendered] Gaussian ids, tile-major, (depth, id) order;
+                              entry k belongs to the tile t with ranges[t].x <= k < ranges[t].y */
 } lsr_state_layout;
 
 int32_t lsr_abi_version(void);
 const char* lsr_last_error(void);
 
-/* Sizes (bytes) of the forward scratch buffers. */
+/* Sizes (bytes) of the forward scratch buffers (binning: an upper bound for any scene with
+ * num_rendered tile instances; the forward requests the exact size). */
 size_t lsr_geom_bytes(int32_t P);
 size_t lsr_image_bytes(int32_t width, int32_t height);
-size_t lsr_binning_bytes(int64_t num_rendered);
+size_t lsr_binning_bytes(int32_t width, int32_t height, int64_t num_rendered);
 size_t lsr_backward_bytes(int32_t P);
 int32_t lsr_state_layout_of(int32_t P, int32_t width, int32_t height, int64_t num_rendered,
                             lsr_state_layout* out);
 
-/* _C.rasterize_gaussians: preprocess, depth sort, tile binning, per-tile sort, front-to-back
- * compositing.  Writes out_color, out_language_feature, radii and *num_rendered. */
+/* _C.rasterize_gaussians: preprocess, depth sort, tile binning (super-tile lists + per-tile
+ * ranks), front-to-back compositing.  Writes out_color, out_language_feature, radii and *num_rendered. */
 int32_t lsr_forward(const lsr_settings* settings, const lsr_forward_args* args,
                     lsr_alloc_fn alloc, void* alloc_user, void* stream, int64_t* num_rendered);
 

@@ -64,8 +64,8 @@ class LsrBackwardArgs(ctypes.Structure):
 
 class LsrStateLayout(ctypes.Structure):
     _fields_ = [(n, ctypes.c_size_t) for n in (
-        "depth_key", "tiles_touched", "rect", "record", "clamped", "sorted_ids", "inst_offset",
-        "counters", "ranges", "final_T", "n_contrib", "point_list", "list_keys")]
+        "depth_key", "tiles_touched", "rect", "record", "clamped", "sorted_ids", "super_offset",
+        "counters", "ranges", "final_T", "n_contrib", "point_list")]
 
 
 class LsrKernelStat(ctypes.Structure):
@@ -80,7 +80,7 @@ SIGNATURES = {
     "lsr_last_error": (ctypes.c_char_p, []),
     "lsr_geom_bytes": (ctypes.c_size_t, [ctypes.c_int32]),
     "lsr_image_bytes": (ctypes.c_size_t, [ctypes.c_int32, ctypes.c_int32]),
-    "lsr_binning_bytes": (ctypes.c_size_t, [ctypes.c_int64]),
+    "lsr_binning_bytes": (ctypes.c_size_t, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int64]),
     "lsr_backward_bytes": (ctypes.c_size_t, [ctypes.c_int32]),
     "lsr_state_layout_of": (ctypes.c_int32, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int64,
                                              ctypes.POINTER(LsrStateLayout)]),

@@ -112,11 +112,15 @@ int32_t lsr_abi_version(void) { return LSR_ABI_VERSION; }
 
 const char* lsr_last_error(void) { return g_last_error.c_str(); }
 
-size_t lsr_geom_bytes(int32_t P) { return make_layout(P, 0, 0, 0).geom_bytes; }
+size_t lsr_geom_bytes(int32_t P) { return make_layout(P, 0, 0, 0, 0).geom_bytes; }
 
-size_t lsr_image_bytes(int32_t width, int32_t height) { return make_layout(0, width, height, 0).image_bytes; }
+size_t lsr_image_bytes(int32_t width, int32_t height) { return make_layout(0, width, height, 0, 0).image_bytes; }
 
-size_t lsr_binning_bytes(int64_t num_rendered) { return make_layout(0, 0, 0, num_rendered).binning_bytes; }
+// every super-tile entry carries at least one tile instance, so E <= num_rendered
+size_t lsr_binning_bytes(int32_t width, int32_t height, int64_t num_rendered)
+{
+    return make_layout(0, width, height, num_rendered, num_rendered).binning_bytes;
+}
 
 size_t lsr_backward_bytes(int32_t P) { return 4 * (size_t)kGradStride * (size_t)(P > 0 ? P : 1); }
 
@@ -124,20 +128,19 @@ int32_t lsr_state_layout_of(int32_t P, int32_t width, int32_t height, int64_t nu
 {
     if (!out || P < 0 || width < 0 || height < 0 || num_rendered < 0)
         return fail(LSR_ERR_INVALID, "lsr_state_layout_of: invalid argument");
-    const Layout L = make_layout(P, width, height, num_rendered);
+    const Layout L = make_layout(P, width, height, num_rendered, 0);
     out->depth_key = L.depth_key;
     out->tiles_touched = L.tiles_touched;
     out->rect = L.rect;
     out->record = L.record;
     out->clamped = L.clamped;
     out->sorted_ids = L.sorted_ids;
-    out->inst_offset = L.inst_offset;
+    out->super_offset = L.super_offset;
     out->counters = L.counters;
     out->ranges = L.ranges;
     out->final_T = L.final_T;
     out->n_contrib = L.n_contrib;
     out->point_list = L.point_list;
-    out->list_keys = L.list_keys;
     return LSR_OK;
 }
 
@@ -174,7 +177,8 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
         return LSR_OK;
     }
 
-    Layout L = make_layout(P, W, H, 0);
+    Layout L = make_layout(P, W, H, 0, 0);
+    if (L.supers > 65536) return fail(LSR_ERR_INVALID, "lsr_forward: image larger than 65536 super-tiles");
     char* geom = static_cast<char*>(alloc(user, LSR_BUF_GEOM, L.geom_bytes));
     char* image = static_cast<char*>(alloc(user, LSR_BUF_IMAGE, L.image_bytes));
     if (!geom || !image) return fail(LSR_ERR_ALLOC, "lsr_forward: geometry/image buffer allocation failed");
@@ -222,7 +226,7 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
     LSR_TRY(launch_depth_order(P, L, geom, counters, stream, debug), "depth order");
 
     // the one host synchronisation: visible count, num_rendered, error flag
-    uint32_t host_cnt[4] = {0, 0, 0, 0};
+    uint32_t host_cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     LSR_TRY(hipMemcpyAsync(host_cnt, counters, sizeof(host_cnt), hipMemcpyDeviceToHost, stream), "read counters");
     LSR_TRY(hipStreamSynchronize(stream), "synchronize");
     if (host_cnt[kCntScanFault]) return fail(LSR_ERR_HIP, "lsr_forward: scan look-back stalled");
@@ -231,7 +235,7 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
     const int64_t R = host_cnt[kCntRendered];
     *num_rendered = R;
 
-    L = make_layout(P, W, H, R);
+    L = make_layout(P, W, H, R, (int64_t)host_cnt[kCntSuper]);
     char* binning = static_cast<char*>(alloc(user, LSR_BUF_BINNING, L.binning_bytes));
     if (!binning) return fail(LSR_ERR_ALLOC, "lsr_forward: binning buffer allocation failed");
     LSR_TRY(launch_binning(P, R, L, geom, image, binning, stream, debug), "binning");
@@ -274,7 +278,7 @@ int32_t lsr_backward(const lsr_settings* s, const lsr_backward_args* a, lsr_allo
     if (P == 0) return LSR_OK;
     if (!a->dL_dout_color || !a->geom_buffer || !a->image_buffer || !a->binning_buffer || !a->radii)
         return fail(LSR_ERR_INVALID, "lsr_backward: missing forward state");
-    const Layout L = make_layout(P, W, H, a->num_rendered);
+    const Layout L = make_layout(P, W, H, a->num_rendered, 0);  // point_list sits at offset 0
     char* geom = static_cast<char*>(a->geom_buffer);
     char* image = static_cast<char*>(a->image_buffer);
     char* binning = static_cast<char*>(a->binning_buffer);

@@ -1,16 +1,22 @@
 // lsr_binning.hip -- tile binning and ordering.
 //
 // The reference (upstream) emits one 64-bit key (tile << 32 | depth bits) per tile instance and
-// radix-sorts all I instances on 32+msb(T) bits.  This file reaches the SAME per-tile order
-// ((depth, Gaussian id) ascending inside each tile) with far less integer traffic:
+// radix-sorts all R instances on 32+msb(T) bits.  This file reaches the SAME per-tile order
+// ((depth, Gaussian id) ascending inside each tile) without sorting instances at all:
 //
-//   1. depth sort of the P Gaussians only (32-bit keys, stable LSD radix with wave64 ballot
-//      ranking; equal depths keep id order) -> sorted_ids;
-//   2. exclusive scan of tiles_touched in that depth order -> each Gaussian's instance offset;
-//   3. emission of every (tile, Gaussian) instance in depth order (no atomics);
-//   4. stable LSD radix sort of the instances on the TILE bits only (ceil(log2 T) bits:
-//      13 at 1080p = 2 passes) -- stability keeps depth order inside each tile;
-//   5. tile ranges from the boundaries of the sorted tile keys.
+//   1. depth sort of the P Gaussians (32-bit keys, stable LSD radix with wave64 ballot ranking;
+//      equal depths keep id order) -> sorted_ids;
+//   2. super-tiles of 8 x 8 tiles (128 x 128 px): each visible Gaussian, in depth order, emits
+//      one entry per super-tile its tile rectangle meets (about 1.5 per Gaussian vs ~8.5 tile
+//      instances), and one stable radix pass on the super-tile id (8 bits at 1080p) gives every
+//      super-tile its depth-ordered entry list;
+//   3. inside a super-tile an entry's coverage is a 64-bit tile mask.  Segments of 2048 entries
+//      are processed by one workgroup in batches of 64 per wave: a 64 x 64 bit transpose across
+//      the wave turns the batch's masks into per-tile lane columns, so a tile's stable rank
+//      among the batch is popcount(column & lanes-below) -- no keys, no atomics;
+//   4. counts per (tile, segment) are scanned once in tile-major order: that gives every
+//      segment's base inside every tile list, the tile ranges, and a point_list laid out
+//      exactly like the sorted instance list (tile, depth, id).
 //
 // Every step is deterministic, so point_list is bit-identical to the oracle's (tile, depth, id)
 // sort.  Scans are single-pass chained scans with decoupled look-back (one launch each).
@@ -371,14 +377,98 @@ size_t radix_hist_words(int64_t n) { return 256 * (size_t)((n + 4 * kRadixThread
 // one u64 status word per chunk + the u64 ticket slot, in u32 words
 size_t scan_region_words(int64_t n) { return 2 * (size_t)((n + kScanChunk - 1) / kScanChunk) + 2; }
 
-// ---------------------------------------------------------------- depth order + instance offsets
+// ---------------------------------------------------------------- super-tiles
 
-__global__ __launch_bounds__(256) void k_gather_tiles(int P, const uint32_t* __restrict__ sorted_ids,
-                                                      const uint32_t* __restrict__ tiles,
-                                                      uint32_t* __restrict__ tiles_ranked)
+// super-tile rectangle [sx0, sx1) x [sy0, sy1) of a packed tile rectangle
+__device__ __forceinline__ void super_rect(uint2 rc, int& sx0, int& sy0, int& sx1, int& sy1)
 {
+    const int x0 = rc.x & 0xFFFF, y0 = rc.x >> 16, x1 = rc.y & 0xFFFF, y1 = rc.y >> 16;
+    sx0 = x0 / kSuper;
+    sy0 = y0 / kSuper;
+    sx1 = (x1 + kSuper - 1) / kSuper;
+    sy1 = (y1 + kSuper - 1) / kSuper;
+}
+
+// An entry key: super-tile id in the low 16 bits (the only bits sorted on), the Gaussian's tile
+// rectangle clipped to the super-tile in the high 16 (lx0, lx1, ly0, ly1: 4 bits each).
+__device__ __forceinline__ uint32_t entry_key(uint2 rc, int sx, int sy, int sgx)
+{
+    const int ox = sx * kSuper, oy = sy * kSuper;
+    const int lx0 = max((int)(rc.x & 0xFFFF) - ox, 0), ly0 = max((int)(rc.x >> 16) - oy, 0);
+    const int lx1 = min((int)(rc.y & 0xFFFF) - ox, kSuper), ly1 = min((int)(rc.y >> 16) - oy, kSuper);
+    return (uint32_t)(sy * sgx + sx) | ((uint32_t)lx0 << 16) | ((uint32_t)lx1 << 20) | ((uint32_t)ly0 << 24) |
+           ((uint32_t)ly1 << 28);
+}
+
+// 64-bit mask (bit = ly * 8 + lx) of the entry's tiles inside its super-tile
+__device__ __forceinline__ uint64_t entry_mask(uint32_t key)
+{
+    const int lx0 = (key >> 16) & 15, lx1 = (key >> 20) & 15, ly0 = (key >> 24) & 15, ly1 = key >> 28;
+    if (lx0 >= lx1 || ly0 >= ly1) return 0ull;
+    const uint64_t row = (uint64_t)(((1u << (lx1 - lx0)) - 1u) << lx0);
+    uint64_t m = 0ull;
+    for (int ly = ly0; ly < ly1; ly++) m |= row << (8 * ly);
+    return m;
+}
+
+// 64 x 64 bit-matrix transpose across the wave: bit j of lane i -> bit i of lane j
+__device__ __forceinline__ uint64_t transpose64(uint64_t x)
+{
+    const int lane = threadIdx.x & 63;
+    const uint64_t M[6] = {0x00000000FFFFFFFFull, 0x0000FFFF0000FFFFull, 0x00FF00FF00FF00FFull,
+                           0x0F0F0F0F0F0F0F0Full, 0x3333333333333333ull, 0x5555555555555555ull};
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+        const int sft = 32 >> k;
+        const uint64_t y = __shfl_xor(x, sft, 64);
+        x = (lane & sft) ? (((y & ~M[k]) >> sft) | (x & ~M[k])) : ((x & M[k]) | ((y & M[k]) << sft));
+    }
+    return x;
+}
+
+// ---------------------------------------------------------------- depth order + super-tile counts
+
+// Per depth rank r: the Gaussian's tile rectangle copied into depth order (the only random
+// gather of the binning), its super-tile entry count (-> exclusive scan = entry offsets) and
+// per-block sums of its tile count (-> R; same-address atomics would serialise the blocks).
+__global__ __launch_bounds__(256) void k_super_counts(int P, const uint32_t* __restrict__ sorted_ids,
+                                                      const uint2* __restrict__ rect, uint2* __restrict__ rect_ranked,
+                                                      uint32_t* __restrict__ ns, uint32_t* __restrict__ partial)
+{
+    __shared__ uint32_t wsum[4];
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r < P) tiles_ranked[r] = tiles[sorted_ids[r]];
+    uint32_t t = 0;
+    if (r < P) {
+        const uint2 rc = rect[sorted_ids[r]];
+        rect_ranked[r] = rc;
+        const uint32_t w = (rc.y & 0xFFFF) - (rc.x & 0xFFFF), h = (rc.y >> 16) - (rc.x >> 16);
+        t = w * h;  // == tiles_touched (the rectangle is empty for culled Gaussians)
+        uint32_t n = 0;
+        if (t) {
+            int sx0, sy0, sx1, sy1;
+            super_rect(rc, sx0, sy0, sx1, sy1);
+            n = (uint32_t)((sx1 - sx0) * (sy1 - sy0));
+        }
+        ns[r] = n;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = t;
+    __syncthreads();
+    if (threadIdx.x == 0) partial[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+}
+
+// one workgroup: *out = sum of n words (fixed order)
+__global__ __launch_bounds__(256) void k_sum(int n, const uint32_t* __restrict__ v, uint32_t* __restrict__ out)
+{
+    __shared__ uint32_t wsum[4];
+    uint32_t t = 0;
+    for (int i = threadIdx.x; i < n; i += 256) t += v[i];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = t;
+    __syncthreads();
+    if (threadIdx.x == 0) *out = wsum[0] + wsum[1] + wsum[2] + wsum[3];
 }
 
 hipError_t launch_depth_order(int P, const Layout& L, char* geom, uint32_t* counters, hipStream_t s, bool debug)
@@ -396,48 +486,244 @@ hipError_t launch_depth_order(int P, const Layout& L, char* geom, uint32_t* coun
                               hist, regions, L.scan_region_geom, fault, s, debug, &passes);
     if (e != hipSuccess) return e;
     // 4 passes: the ids are in sorted_ids (va)
-    uint32_t* off = reinterpret_cast<uint32_t*>(geom + L.inst_offset);
-    hipLaunchKernelGGL(k_gather_tiles, dim3((P + 255) / 256), dim3(256), 0, s, P, va,
-                       reinterpret_cast<const uint32_t*>(geom + L.tiles_touched), off);
+    uint32_t* off = reinterpret_cast<uint32_t*>(geom + L.super_offset);
+    uint32_t* partial = reinterpret_cast<uint32_t*>(geom + L.block_partial);
+    const int nb = (P + 255) / 256;
+    hipLaunchKernelGGL(k_super_counts, dim3(nb), dim3(256), 0, s, P, va, reinterpret_cast<const uint2*>(geom + L.rect),
+                       reinterpret_cast<uint2*>(geom + L.rect_ranked), off, partial);
     if ((e = post(debug, s)) != hipSuccess) return e;
-    return scan_exclusive(off, off, P, regions + passes * L.scan_region_geom, counters + kCntRendered, fault, s,
+    hipLaunchKernelGGL(k_sum, dim3(1), dim3(256), 0, s, nb, (const uint32_t*)partial, counters + kCntRendered);
+    if ((e = post(debug, s)) != hipSuccess) return e;
+    return scan_exclusive(off, off, P, regions + passes * L.scan_region_geom, counters + kCntSuper, fault, s,
                           debug);
 }
 
-// ---------------------------------------------------------------- emit + tile sort + ranges
+// ---------------------------------------------------------------- binning
 
-__global__ __launch_bounds__(256) void k_emit(int P, int gx, const uint32_t* __restrict__ sorted_ids,
-                                              const uint32_t* __restrict__ inst_offset,
-                                              const uint32_t* __restrict__ tiles, const uint32_t* __restrict__ rect,
-                                              uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
-                                              uint32_t* __restrict__ zero_a, int zero_a_words,
-                                              uint32_t* __restrict__ zero_b, int zero_b_words)
+// Super-tile entries in depth order (keys = entry_key, vals = Gaussian id); also clears what the
+// later kernels need cleared (tile and super-tile ranges, the segment count table, scan status).
+__global__ __launch_bounds__(256) void k_emit_super(int P, int sgx, const uint32_t* __restrict__ sorted_ids,
+                                                    const uint32_t* __restrict__ offset,
+                                                    const uint2* __restrict__ rect_ranked,
+                                                    uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
+                                                    uint32_t* __restrict__ z0, int n0, uint32_t* __restrict__ z1,
+                                                    int n1, uint32_t* __restrict__ z2, int n2,
+                                                    uint32_t* __restrict__ z3, int n3)
 {
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
-    // clear the tile ranges and the tile-sort scan status (replaces two memset launches)
-    for (int w = r; w < zero_a_words; w += gridDim.x * blockDim.x) zero_a[w] = 0u;
-    for (int w = r; w < zero_b_words; w += gridDim.x * blockDim.x) zero_b[w] = 0u;
+    const int stride = gridDim.x * blockDim.x;
+    for (int w = r; w < n0; w += stride) z0[w] = 0u;
+    for (int w = r; w < n1; w += stride) z1[w] = 0u;
+    for (int w = r; w < n2; w += stride) z2[w] = 0u;
+    for (int w = r; w < n3; w += stride) z3[w] = 0u;
     if (r >= P) return;
+    const uint2 rc = rect_ranked[r];
+    if (rc.x == rc.y) return;  // culled (empty rectangle)
     const uint32_t g = sorted_ids[r];
-    if (tiles[g] == 0) return;
-    uint32_t o = inst_offset[r];
-    const uint32_t r0 = rect[2 * g], r1 = rect[2 * g + 1];
-    const int x0 = r0 & 0xFFFF, y0 = r0 >> 16, x1 = r1 & 0xFFFF, y1 = r1 >> 16;
-    for (int y = y0; y < y1; y++)
-        for (int x = x0; x < x1; x++) {
-            keys[o] = (uint32_t)(y * gx + x);
+    int sx0, sy0, sx1, sy1;
+    super_rect(rc, sx0, sy0, sx1, sy1);
+    uint32_t o = offset[r];
+    for (int y = sy0; y < sy1; y++)
+        for (int x = sx0; x < sx1; x++) {
+            keys[o] = entry_key(rc, x, y, sgx);
             vals[o] = g;
             o++;
         }
 }
 
-__global__ __launch_bounds__(256) void k_ranges(int64_t R, const uint32_t* __restrict__ keys, uint2* __restrict__ ranges)
+// [start, end) of every super-tile in the sorted entries (the low 16 key bits)
+__global__ __launch_bounds__(256) void k_super_ranges(int64_t E, const uint32_t* __restrict__ keys,
+                                                      uint2* __restrict__ ranges)
 {
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= R) return;
-    const uint32_t t = keys[k];
-    if (k == 0 || keys[k - 1] != t) ranges[t].x = (uint32_t)k;
-    if (k == R - 1 || keys[k + 1] != t) ranges[t].y = (uint32_t)(k + 1);
+    if (k >= E) return;
+    const uint32_t t = keys[k] & 0xFFFFu;
+    if (k == 0 || (keys[k - 1] & 0xFFFFu) != t) ranges[t].x = (uint32_t)k;
+    if (k == E - 1 || (keys[k + 1] & 0xFFFFu) != t) ranges[t].y = (uint32_t)(k + 1);
+}
+
+__device__ __forceinline__ uint32_t super_segments(uint2 r) { return (r.y - r.x + kSegEntries - 1) / kSegEntries; }
+
+// Positions in the tile-major (tile, segment) count table, in closed form: tile t = (tx, ty) of
+// super-tile s = (sx, sy) starts at row_prefix[ty] + col_prefix[s] + (tx - 8 sx) * nseg(s), where
+// col_prefix[s] sums nseg x width over the super-tiles left of s in its row and row_prefix[ty] sums
+// whole tile rows above ty.  One workgroup builds seg_base (segment -> super-tile map) and both
+// prefixes from the S super-tile ranges.
+__global__ __launch_bounds__(kScanThreads) void k_seg_setup(int S, int sgx, int sgy, int gx, int gy,
+                                                            const uint2* __restrict__ sranges,
+                                                            uint32_t* __restrict__ seg_base,
+                                                            uint32_t* __restrict__ col_prefix,
+                                                            uint32_t* __restrict__ row_prefix)
+{
+    __shared__ uint32_t wsum[kScanThreads / 64];
+    extern __shared__ uint32_t row_total[];  // per super-row: tiles-weighted segment count of one tile row
+    uint32_t carry = 0;
+    for (int b = 0; b < S; b += kScanThreads) {
+        const int i = b + threadIdx.x;
+        const uint32_t v = i < S ? super_segments(sranges[i]) : 0u;
+        uint32_t tot;
+        const uint32_t ex = block_exclusive_scan(v, wsum, &tot);
+        if (i < S) seg_base[i] = carry + ex;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) seg_base[S] = carry;
+    for (int sy = threadIdx.x; sy < sgy; sy += blockDim.x) {
+        uint32_t run = 0;
+        for (int sx = 0; sx < sgx; sx++) {
+            const int s = sy * sgx + sx;
+            col_prefix[s] = run;
+            run += super_segments(sranges[s]) * (uint32_t)min(kSuper, gx - sx * kSuper);
+        }
+        row_total[sy] = run;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t run = 0;
+        for (int ty = 0; ty < gy; ty++) {
+            row_prefix[ty] = run;
+            run += row_total[ty / kSuper];
+        }
+        row_prefix[gy] = run;
+    }
+}
+
+// block -> (super-tile, segment) through seg_base; false for the grid's spare blocks
+__device__ __forceinline__ bool block_segment(int S, const uint32_t* __restrict__ seg_base, int* s_out, int* seg_out)
+{
+    __shared__ int sh[2];
+    if (threadIdx.x == 0) {
+        const uint32_t b = blockIdx.x;
+        int s = -1, seg = 0;
+        if (b < seg_base[S]) {
+            int lo = 0, hi = S - 1;  // last s with seg_base[s] <= b
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (seg_base[mid] <= b) lo = mid;
+                else hi = mid - 1;
+            }
+            s = lo;
+            seg = (int)(b - seg_base[lo]);
+        }
+        sh[0] = s;
+        sh[1] = seg;
+    }
+    __syncthreads();
+    *s_out = sh[0];
+    *seg_out = sh[1];
+    return sh[0] >= 0;
+}
+
+struct SegmentCtx {
+    int s, seg, ox, oy;
+    uint32_t e0, e1, nseg, colpre;
+};
+
+__device__ __forceinline__ SegmentCtx segment_ctx(int s, int seg, int sgx, const uint2* __restrict__ sranges,
+                                                  const uint32_t* __restrict__ col_prefix)
+{
+    SegmentCtx c;
+    c.s = s;
+    c.seg = seg;
+    c.ox = (s % sgx) * kSuper;
+    c.oy = (s / sgx) * kSuper;
+    const uint2 r = sranges[s];
+    c.e0 = r.x + (uint32_t)seg * kSegEntries;
+    c.e1 = min(r.y, c.e0 + (uint32_t)kSegEntries);
+    c.nseg = super_segments(r);
+    c.colpre = col_prefix[s];
+    return c;
+}
+
+// count-table slot of (local tile l, segment 0) of the super-tile, -1 outside the image;
+// *gt = its global tile id
+__device__ __forceinline__ int64_t table_slot(const SegmentCtx& c, int l, int gx, int gy,
+                                              const uint32_t* __restrict__ row_prefix, int* gt)
+{
+    const int x = c.ox + (l & 7), y = c.oy + (l >> 3);
+    if (x >= gx || y >= gy) return -1;
+    *gt = y * gx + x;
+    return (int64_t)row_prefix[y] + c.colpre + (uint32_t)(l & 7) * c.nseg;
+}
+
+// Per (tile, segment) entry counts into the tile-major count table.
+__global__ __launch_bounds__(256) void k_bin_count(int S, int sgx, int gx, int gy, const uint32_t* __restrict__ seg_base,
+                                                   const uint2* __restrict__ sranges,
+                                                   const uint32_t* __restrict__ col_prefix,
+                                                   const uint32_t* __restrict__ row_prefix,
+                                                   const uint32_t* __restrict__ keys, uint32_t* __restrict__ table)
+{
+    __shared__ uint32_t cnt[64];
+    int s, seg;
+    if (!block_segment(S, seg_base, &s, &seg)) return;
+    const SegmentCtx c = segment_ctx(s, seg, sgx, sranges, col_prefix);
+    if (threadIdx.x < 64) cnt[threadIdx.x] = 0;
+    __syncthreads();
+    uint32_t mine = 0;  // lane l: entries of this wave covering local tile l
+    for (uint32_t b = c.e0 + (threadIdx.x & ~63u); b < c.e1; b += 256) {
+        const uint32_t e = b + (threadIdx.x & 63);
+        const uint64_t m = e < c.e1 ? entry_mask(keys[e]) : 0ull;
+        mine += (uint32_t)__popcll(transpose64(m));
+    }
+    atomicAdd(&cnt[threadIdx.x & 63], mine);
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        int gt;
+        const int64_t slot = table_slot(c, threadIdx.x, gx, gy, row_prefix, &gt);
+        if (slot >= 0) table[slot + seg] = cnt[threadIdx.x];
+    }
+}
+
+// Writes every (tile, Gaussian) pair of a segment at its final point_list position, and the tile
+// ranges (segment 0 of each super-tile).  `table` holds the scanned counts.
+__global__ __launch_bounds__(256) void k_bin_emit(int S, int sgx, int gx, int gy, const uint32_t* __restrict__ seg_base,
+                                                  const uint2* __restrict__ sranges,
+                                                  const uint32_t* __restrict__ col_prefix,
+                                                  const uint32_t* __restrict__ row_prefix,
+                                                  const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals,
+                                                  const uint32_t* __restrict__ table, uint32_t* __restrict__ point_list,
+                                                  uint2* __restrict__ ranges)
+{
+    __shared__ uint64_t colw[4][64];
+    __shared__ uint32_t pre[4][64];
+    __shared__ uint32_t cursor[64];
+    int s, seg;
+    if (!block_segment(S, seg_base, &s, &seg)) return;
+    const SegmentCtx c = segment_ctx(s, seg, sgx, sranges, col_prefix);
+    const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+    if (t < 64) {
+        int gt = 0;
+        const int64_t slot = table_slot(c, t, gx, gy, row_prefix, &gt);
+        cursor[t] = slot >= 0 ? table[slot + seg] : 0u;
+        if (seg == 0 && slot >= 0) ranges[gt] = make_uint2(table[slot], table[slot + c.nseg]);
+    }
+    const uint64_t below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    for (uint32_t b = c.e0; b < c.e1; b += 256) {
+        const uint32_t e = b + t;
+        uint32_t g = 0;
+        uint64_t m = 0ull;
+        if (e < c.e1) {
+            g = vals[e];
+            m = entry_mask(keys[e]);
+        }
+        colw[wave][lane] = transpose64(m);
+        __syncthreads();
+        if (t < 64) {
+            uint32_t run = cursor[t];
+#pragma unroll
+            for (int w = 0; w < 4; w++) {
+                pre[w][t] = run;
+                run += (uint32_t)__popcll(colw[w][t]);
+            }
+            cursor[t] = run;
+        }
+        __syncthreads();
+        while (m) {
+            const int l = __ffsll((unsigned long long)m) - 1;
+            m &= m - 1ull;
+            point_list[pre[wave][l] + (uint32_t)__popcll(colw[wave][l] & below)] = g;
+        }
+        __syncthreads();
+    }
 }
 
 hipError_t launch_binning(int P, int64_t R, const Layout& L, char* geom, char* image, char* binning, hipStream_t s,
@@ -445,38 +731,49 @@ hipError_t launch_binning(int P, int64_t R, const Layout& L, char* geom, char* i
 {
     uint2* ranges = reinterpret_cast<uint2*>(image + L.ranges);
     if (R == 0) return hipMemsetAsync(ranges, 0, 8 * (size_t)L.tiles, s);
-    const int tile_bits = L.tile_bits;
-    const int passes = L.tile_passes;
+    const int64_t E = L.super_entries;
     uint32_t* regions = reinterpret_cast<uint32_t*>(binning + L.bin_scan_regions);
     uint32_t* fault = reinterpret_cast<uint32_t*>(image + L.counters) + kCntScanFault;
-    hipError_t e;
-    uint32_t* pl_keys = reinterpret_cast<uint32_t*>(binning + L.list_keys);
+    uint32_t* kA = reinterpret_cast<uint32_t*>(binning + L.super_keys);
+    uint32_t* vA = reinterpret_cast<uint32_t*>(binning + L.super_vals);
+    uint32_t* kB = reinterpret_cast<uint32_t*>(binning + L.alt_keys);
+    uint32_t* vB = reinterpret_cast<uint32_t*>(binning + L.alt_vals);
+    uint2* sranges = reinterpret_cast<uint2*>(binning + L.super_ranges);
+    uint32_t* seg_base = reinterpret_cast<uint32_t*>(binning + L.seg_base);
+    uint32_t* colpre = reinterpret_cast<uint32_t*>(binning + L.col_prefix);
+    uint32_t* rowpre = reinterpret_cast<uint32_t*>(binning + L.row_prefix);
+    uint32_t* table = reinterpret_cast<uint32_t*>(binning + L.seg_table);
     uint32_t* pl = reinterpret_cast<uint32_t*>(binning + L.point_list);
-    uint32_t* alt_keys = reinterpret_cast<uint32_t*>(binning + L.alt_keys);
-    uint32_t* alt_vals = reinterpret_cast<uint32_t*>(binning + L.alt_vals);
-    // emit so that the sorted result lands in (list_keys, point_list): odd pass counts start in the
-    // (list) buffers and end in alt... radix_sort writes pass 0 to B, so start in A for even passes
-    uint32_t *ek, *ev, *kA, *vA, *kB, *vB;
-    if (passes % 2 == 0) {
-        ek = pl_keys; ev = pl;            // A -> B -> A
-        kA = pl_keys; vA = pl; kB = alt_keys; vB = alt_vals;
-    } else {
-        ek = alt_keys; ev = alt_vals;     // A' -> B' with B' = list buffers
-        kA = alt_keys; vA = alt_vals; kB = pl_keys; vB = pl;
-    }
-    hipLaunchKernelGGL(k_emit, dim3((P + 255) / 256), dim3(256), 0, s, P, L.gx,
+    hipError_t e;
+    hipLaunchKernelGGL(k_emit_super, dim3((P + 255) / 256), dim3(256), 0, s, P, L.sgx,
                        reinterpret_cast<const uint32_t*>(geom + L.sorted_ids),
-                       reinterpret_cast<const uint32_t*>(geom + L.inst_offset),
-                       reinterpret_cast<const uint32_t*>(geom + L.tiles_touched),
-                       reinterpret_cast<const uint32_t*>(geom + L.rect), ek, ev,
-                       reinterpret_cast<uint32_t*>(ranges), 2 * L.tiles, regions,
-                       (int)(passes * L.scan_region_bin));
+                       reinterpret_cast<const uint32_t*>(geom + L.super_offset),
+                       reinterpret_cast<const uint2*>(geom + L.rect_ranked), kA, vA,
+                       reinterpret_cast<uint32_t*>(ranges), 2 * L.tiles, reinterpret_cast<uint32_t*>(sranges),
+                       2 * L.supers, table, (int)L.seg_table_words, regions,
+                       (int)((L.super_passes + 1) * L.scan_region_bin));
     if ((e = post(debug, s)) != hipSuccess) return e;
-    int done = 0;
-    e = radix_sort(ek, ev, (int)R, tile_bits, kA, vA, kB, vB, reinterpret_cast<uint32_t*>(binning + L.bin_radix_hist),
-                   regions, L.scan_region_bin, fault, s, debug, &done);
+    int passes = 0;
+    e = radix_sort(kA, vA, (int)E, L.super_bits, kA, vA, kB, vB, reinterpret_cast<uint32_t*>(binning + L.bin_radix_hist),
+                   regions, L.scan_region_bin, fault, s, debug, &passes);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_ranges, dim3((unsigned)((R + 255) / 256)), dim3(256), 0, s, R, pl_keys, ranges);
+    const uint32_t* skeys = (passes & 1) ? kB : kA;
+    const uint32_t* svals = (passes & 1) ? vB : vA;
+    hipLaunchKernelGGL(k_super_ranges, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, s, E, skeys, sranges);
+    if ((e = post(debug, s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_seg_setup, dim3(1), dim3(kScanThreads), 4 * (size_t)L.sgy, s, L.supers, L.sgx, L.sgy, L.gx,
+                       L.gy, (const uint2*)sranges, seg_base, colpre, rowpre);
+    if ((e = post(debug, s)) != hipSuccess) return e;
+    const unsigned grid = (unsigned)L.seg_blocks;
+    hipLaunchKernelGGL(k_bin_count, dim3(grid), dim3(256), 0, s, L.supers, L.sgx, L.gx, L.gy, (const uint32_t*)seg_base,
+                       (const uint2*)sranges, (const uint32_t*)colpre, (const uint32_t*)rowpre, skeys, table);
+    if ((e = post(debug, s)) != hipSuccess) return e;
+    if ((e = scan_exclusive(table, table, (int)L.seg_table_words, regions + L.super_passes * L.scan_region_bin,
+                            nullptr, fault, s, debug)) != hipSuccess)
+        return e;
+    hipLaunchKernelGGL(k_bin_emit, dim3(grid), dim3(256), 0, s, L.supers, L.sgx, L.gx, L.gy, (const uint32_t*)seg_base,
+                       (const uint2*)sranges, (const uint32_t*)colpre, (const uint32_t*)rowpre, skeys, svals,
+                       (const uint32_t*)table, pl, ranges);
     return post(debug, s);
 }
 

@@ -15,10 +15,13 @@ enum Counter : int {
     kCntRendered = 1,
     kCntError = 2,
     kCntScanFault = 3,
+    kCntSuper = 4,       // super-tile entries E (binning)
     kCntSlots = 16
 };
 
 constexpr int kRadixThreads = 256;
+constexpr int kSuper = 8;          // super-tile = kSuper x kSuper tiles (64-bit tile masks)
+constexpr int kSegEntries = 2048;  // super-tile list entries per binning workgroup
 constexpr int kGradStride = 16;                          // floats per Gaussian grad record
 
 size_t radix_hist_words(int64_t n);   // per-block digit histograms for n keys
@@ -27,23 +30,27 @@ constexpr int kDepthScans = 5;         // 4 depth-sort passes + the instance-off
 
 struct Layout {
     // geometry (per Gaussian)
-    size_t depth_key, tiles_touched, rect, record, clamped, sorted_ids, inst_offset;
-    size_t keys_a, keys_b, vals_b, radix_hist, scan_regions;
+    size_t depth_key, tiles_touched, rect, record, clamped, sorted_ids, super_offset;
+    size_t keys_a, keys_b, vals_b, radix_hist, scan_regions, rect_ranked, block_partial;
     size_t scan_region_geom;  // u32 words per depth-order scan region
     size_t geom_bytes;
     // image (per pixel / tile)
     size_t counters, ranges, final_T, n_contrib;
     size_t image_bytes;
-    // binning (per tile instance)
-    size_t list_keys, point_list, alt_keys, alt_vals, bin_radix_hist, bin_scan_regions;
-    size_t scan_region_bin;   // u32 words per tile-sort scan region
+    // binning (point_list per tile instance, the rest per super-tile entry / segment)
+    size_t point_list, super_keys, super_vals, alt_keys, alt_vals, bin_radix_hist, bin_scan_regions;
+    size_t super_ranges, seg_base, col_prefix, row_prefix, seg_table;
+    size_t scan_region_bin;   // u32 words per binning scan region
+    size_t seg_table_words;   // (tile, segment) count table incl. one trailing slot
+    int64_t super_entries;    // E
+    int64_t seg_blocks;       // upper bound on segments = binning grid
     size_t binning_bytes;
-    int gx, gy, tiles, tile_bits, tile_passes;
+    int gx, gy, tiles, sgx, sgy, supers, super_bits, super_passes;
 };
 
 inline size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
 
-inline Layout make_layout(int P, int W, int H, int64_t R)
+inline Layout make_layout(int P, int W, int H, int64_t R, int64_t E)
 {
     Layout L{};
     size_t o = 0;
@@ -55,7 +62,7 @@ inline Layout make_layout(int P, int W, int H, int64_t R)
     L.record = take(48 * p);
     L.clamped = take(4 * p);
     L.sorted_ids = take(4 * p);
-    L.inst_offset = take(4 * (p + 1));
+    L.super_offset = take(4 * (p + 1));
     L.keys_a = take(4 * p);
     L.keys_b = take(4 * p);
     L.vals_b = take(4 * p);
@@ -63,14 +70,19 @@ inline Layout make_layout(int P, int W, int H, int64_t R)
     L.radix_hist = take(4 * hw_p);
     L.scan_region_geom = scan_region_words((int64_t)(hw_p > p ? hw_p : p));
     L.scan_regions = take(4 * kDepthScans * L.scan_region_geom);
+    L.rect_ranked = take(8 * p);
+    L.block_partial = take(4 * ((p + 255) / 256));
     L.geom_bytes = o;
 
     L.gx = (W + kTile - 1) / kTile;
     L.gy = (H + kTile - 1) / kTile;
     L.tiles = L.gx * L.gy;
-    L.tile_bits = 1;
-    while ((1 << L.tile_bits) < L.tiles) L.tile_bits++;
-    L.tile_passes = (L.tile_bits + 7) / 8;
+    L.sgx = (L.gx + kSuper - 1) / kSuper;
+    L.sgy = (L.gy + kSuper - 1) / kSuper;
+    L.supers = L.sgx * L.sgy;
+    L.super_bits = 1;  // <= 16: the entry key keeps the super-tile id in its low 16 bits
+    while ((1 << L.super_bits) < L.supers) L.super_bits++;
+    L.super_passes = (L.super_bits + 7) / 8;
     const size_t T = (size_t)(L.tiles > 0 ? L.tiles : 1);
     const size_t HW = (size_t)W * (size_t)H;
     o = 0;
@@ -82,14 +94,24 @@ inline Layout make_layout(int P, int W, int H, int64_t R)
 
     o = 0;
     const size_t r = (size_t)(R > 0 ? R : 1);
-    L.list_keys = take(4 * r);
+    const size_t e = (size_t)(E > 0 ? E : 1);
+    L.super_entries = E;
+    L.seg_blocks = (int64_t)((e + kSegEntries - 1) / kSegEntries) + L.supers;
+    L.seg_table_words = 64 * (size_t)L.seg_blocks + 1;
     L.point_list = take(4 * r);
-    L.alt_keys = take(4 * r);
-    L.alt_vals = take(4 * r);
-    const size_t hw_r = radix_hist_words((int64_t)r);
-    L.bin_radix_hist = take(4 * hw_r);
-    L.scan_region_bin = scan_region_words((int64_t)hw_r);
-    L.bin_scan_regions = take(4 * L.tile_passes * L.scan_region_bin);
+    L.super_keys = take(4 * e);
+    L.super_vals = take(4 * e);
+    L.alt_keys = take(4 * e);
+    L.alt_vals = take(4 * e);
+    const size_t hw_e = radix_hist_words((int64_t)e);
+    L.bin_radix_hist = take(4 * hw_e);
+    L.scan_region_bin = scan_region_words((int64_t)(hw_e > L.seg_table_words ? hw_e : L.seg_table_words));
+    L.bin_scan_regions = take(4 * (L.super_passes + 1) * L.scan_region_bin);
+    L.super_ranges = take(8 * (size_t)L.supers);
+    L.seg_base = take(4 * ((size_t)L.supers + 1));
+    L.col_prefix = take(4 * (size_t)L.supers);
+    L.row_prefix = take(4 * ((size_t)L.gy + 1));
+    L.seg_table = take(4 * L.seg_table_words);
     L.binning_bytes = o;
     return L;
 }
@@ -141,11 +163,11 @@ hipError_t launch_preprocess_backward(const PreprocessBwdParams& p, hipStream_t 
 hipError_t launch_mark_visible(int P, const float* means, const float* view, const float* proj,
                                uint8_t* visible, hipStream_t s);
 
-// depth sort of all P Gaussians by (depth key, id) -> sorted_ids; per-Gaussian instance offsets in
-// that order; counters[kCntRendered] = number of tile instances
+// depth sort of all P Gaussians by (depth key, id) -> sorted_ids; per-Gaussian super-tile entry
+// offsets in that order; counters[kCntRendered] = tile instances R, counters[kCntSuper] = entries E
 hipError_t launch_depth_order(int P, const Layout& L, char* geom, uint32_t* counters, hipStream_t s,
                               bool debug);
-// emit instances in depth order, stable sort on tile bits -> point_list; tile ranges
+// super-tile lists, per-(tile, segment) counts, scanned bases -> point_list and tile ranges
 hipError_t launch_binning(int P, int64_t R, const Layout& L, char* geom, char* image, char* binning,
                           hipStream_t s, bool debug);
 

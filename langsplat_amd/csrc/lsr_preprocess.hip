@@ -131,6 +131,7 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessParams p)
     p.radii[i] = 0;
     p.tiles[i] = 0;
     p.depth_key[i] = 0xFFFFFFFFu;
+    *reinterpret_cast<uint2*>(p.rect + 2 * (size_t)i) = make_uint2(0u, 0u);  // empty: culled
     const float px = p.means[3 * i], py = p.means[3 * i + 1], pz = p.means[3 * i + 2];
     const float3 pv = xform4x3(p.view, px, py, pz);
     if (pv.z <= 0.2f) {
@@ -209,8 +210,8 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessParams p)
     p.depth_key[i] = __float_as_uint(pv.z);
     p.radii[i] = r;
     p.tiles[i] = area;
-    p.rect[2 * i] = (uint32_t)r4[0] | ((uint32_t)r4[1] << 16);
-    p.rect[2 * i + 1] = (uint32_t)r4[2] | ((uint32_t)r4[3] << 16);
+    *reinterpret_cast<uint2*>(p.rect + 2 * (size_t)i) =
+        make_uint2((uint32_t)r4[0] | ((uint32_t)r4[1] << 16), (uint32_t)r4[2] | ((uint32_t)r4[3] << 16));
     p.clamped[i] = clamp_bits;
     float4* rec = p.record + 3 * (size_t)i;
     rec[0] = make_float4(ix, iy, cx, cy);

@@ -40,7 +40,7 @@ def test_sizes_and_layout_are_consistent():
     lay = _native.state_layout(P, W, H, R)
     assert lay["record"] % 16 == 0 and lay["record"] + 48 * P <= lib.lsr_geom_bytes(P)
     assert lay["n_contrib"] + 4 * W * H <= lib.lsr_image_bytes(W, H)
-    assert lay["point_list"] + 4 * R <= lib.lsr_binning_bytes(R)
+    assert lay["point_list"] + 4 * R <= lib.lsr_binning_bytes(W, H, R)
     assert lib.lsr_backward_bytes(P) == 64 * P
     assert lib.lsr_geom_bytes(2 * P) > lib.lsr_geom_bytes(P)
 
