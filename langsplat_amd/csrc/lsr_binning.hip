@@ -674,7 +674,12 @@ __global__ __launch_bounds__(256) void k_bin_count(int S, int sgx, int gx, int g
 }
 
 // Writes every (tile, Gaussian) pair of a segment at its final point_list position, and the tile
-// ranges (segment 0 of each super-tile).  `table` holds the scanned counts.
+// ranges (segment 0 of each super-tile).  `table` holds the scanned counts.  Per batch of 256
+// entries: each wave transposes its 64 masks (lane l <- column of local tile l), lane l of wave w
+// computes tile l's base for the wave (cursor + columns of lower waves), and each entry's lane
+// stores its tiles at base + popcount(column & lanes below).  The last wave advances the cursors;
+// two barriers per batch; the next batch is prefetched.  (Storing tile by tile, one contiguous
+// run per store, measured slower: 64 wave-uniform iterations cost more than the scatter.)
 __global__ __launch_bounds__(256) void k_bin_emit(int S, int sgx, int gx, int gy, const uint32_t* __restrict__ seg_base,
                                                   const uint2* __restrict__ sranges,
                                                   const uint32_t* __restrict__ col_prefix,
@@ -697,32 +702,31 @@ __global__ __launch_bounds__(256) void k_bin_emit(int S, int sgx, int gx, int gy
         if (seg == 0 && slot >= 0) ranges[gt] = make_uint2(table[slot], table[slot + c.nseg]);
     }
     const uint64_t below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    uint32_t kn = 0, gn = 0;
+    if (c.e0 + t < c.e1) {
+        kn = keys[c.e0 + t];
+        gn = vals[c.e0 + t];
+    }
     for (uint32_t b = c.e0; b < c.e1; b += 256) {
-        const uint32_t e = b + t;
-        uint32_t g = 0;
-        uint64_t m = 0ull;
-        if (e < c.e1) {
-            g = vals[e];
-            m = entry_mask(keys[e]);
+        uint64_t m = b + t < c.e1 ? entry_mask(kn) : 0ull;
+        const uint32_t g = gn;
+        if (b + 256 + t < c.e1) {  // prefetch the next batch
+            kn = keys[b + 256 + t];
+            gn = vals[b + 256 + t];
         }
-        colw[wave][lane] = transpose64(m);
+        const uint64_t col = transpose64(m);
+        colw[wave][lane] = col;
         __syncthreads();
-        if (t < 64) {
-            uint32_t run = cursor[t];
-#pragma unroll
-            for (int w = 0; w < 4; w++) {
-                pre[w][t] = run;
-                run += (uint32_t)__popcll(colw[w][t]);
-            }
-            cursor[t] = run;
-        }
+        uint32_t base = cursor[lane];
+        for (int w = 0; w < wave; w++) base += (uint32_t)__popcll(colw[w][lane]);
+        pre[wave][lane] = base;  // read back only by this wave
         __syncthreads();
+        if (wave == 3) cursor[lane] = base + (uint32_t)__popcll(col);
         while (m) {
             const int l = __ffsll((unsigned long long)m) - 1;
             m &= m - 1ull;
             point_list[pre[wave][l] + (uint32_t)__popcll(colw[wave][l] & below)] = g;
         }
-        __syncthreads();
     }
 }
 

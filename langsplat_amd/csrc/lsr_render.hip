@@ -139,9 +139,9 @@ __global__ __launch_bounds__(kTilePixels / kPix) void k_render_forward(RenderPar
         const uint32_t list_base = base - start;  // list index of slot 0
         for (int i = 0; i < n && !all_done; i++) {
             const int j = sL[wave][i];
-            const uint32_t contributor = list_base + (uint32_t)j + 1u;  // upstream's 1-based counter
             const float4 A = sA[j];
             const float4 B = sB[j];
+            const uint32_t contributor = list_base + (uint32_t)j + 1u;  // upstream's 1-based counter
             const float dx = A.x - pfx;
             float pw[kPix], al[kPix];
             bool ok[kPix];
@@ -451,9 +451,9 @@ __global__ __launch_bounds__(kTilePixels / kPix) void k_render_backward(RenderPa
         __syncthreads();  // list visible to the wave's other lanes
         for (int i = 0; i < n; i++) {
             const int j = sL[wave][i];
-            const int kk = maxl - 1 - (done_cnt + j);  // list index of this entry
             const float4 A = sA[j];
             const float4 B = sB[j];
+            const int kk = maxl - 1 - (done_cnt + j);  // list index of this entry
             const float dx = A.x - pfx;
             float pw[kPix];
             bool h[kPix];
@@ -465,21 +465,26 @@ __global__ __launch_bounds__(kTilePixels / kPix) void k_render_backward(RenderPa
                 h[k] = kk < (int)q[k].last && pw[k] <= 0.0f && pw[k] >= B.z;
                 any = any || h[k];
             }
-            if (__ballot(any) == 0ull) continue;  // wave-uniform skip
-            float v[12];
+            if (__ballot(any) != 0ull) {  // wave-uniform skip otherwise
+                float v[12];
 #pragma unroll
-            for (int c = 0; c < 12; c++) v[c] = 0.f;
-            if (any) {
+                for (int c = 0; c < 12; c++) v[c] = 0.f;
                 float G[kPix], al[kPix];
-                bool any2 = false;
+                bool hit = false;
 #pragma unroll
                 for (int k = 0; k < kPix; k++) {
-                    G[k] = expf_exact(pw[k]);
+                    // hardware exp (a few ulp): gradients need 1e-4.  Only the 1/255 skip decision
+                    // must equal the forward's, so alphas within 1e-6 of it use the exact exp.
+                    G[k] = __expf(pw[k]);
                     al[k] = fminf(0.99f, B.y * G[k]);
+                    if (fabsf(al[k] - 1.0f / 255.0f) < 1e-6f) {
+                        G[k] = expf_exact(pw[k]);
+                        al[k] = fminf(0.99f, B.y * G[k]);
+                    }
                     h[k] = h[k] && al[k] >= 1.0f / 255.0f;
-                    any2 = any2 || h[k];
+                    hit = hit || h[k];
                 }
-                if (any2) {
+                if (hit) {
                     const float4 Cc = sC[j];
                     const float2 D = sD[j];
                     const float cx = -2.0f * A.z, cz = -2.0f * A.w;
@@ -489,9 +494,9 @@ __global__ __launch_bounds__(kTilePixels / kPix) void k_render_backward(RenderPa
                             bwd_pixel_blend(q[k], G[k], al[k], dx, A.y - (float)(py_base + k), B, cx, cz, Cc, D,
                                             feat, ddelx_dx, ddely_dy, v);
                 }
+                const float tot = wave_reduce_scatter12(v, lane);
+                if ((lane & 3) == 0 && vidx < 12) atomicAdd(&sG[j * 12 + vidx], tot);
             }
-            const float tot = wave_reduce_scatter12(v, lane);
-            if ((lane & 3) == 0 && vidx < 12) atomicAdd(&sG[j * 12 + vidx], tot);
         }
         __syncthreads();
         // flush: 16 lanes per entry (12 active) -> one 48-byte atomic row per (tile, Gaussian)
