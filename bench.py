@@ -142,11 +142,11 @@ def pmc_traffic(stage):
 
 def cpu_baseline(cfg, seconds_budget=25.0):
     """Oracle (oracle/lsr_oracle.c, 1 thread) fwd+bwd on a bounded sample of the same workload:
-    the first P/4 Gaussians of the C3 scene, same camera and resolution."""
+    the first P/2 Gaussians of the C3 scene, same camera and resolution (~15 s single-threaded)."""
     from oracle import oracle
     from tests.scenes import settings_for
     c = CONFIGS[cfg]
-    frac = 4
+    frac = 2
     Ps = c["P"] // frac
     g = make_gaussians(c["P"], seed=0)
     cam = make_cameras(1, c["width"], c["height"])[0]
