@@ -74,6 +74,33 @@ __device__ __forceinline__ int wave_compact(const float4* sE, int cnt, float wx0
 }
 
 
+// Pixel ownership.  kPix = 1: wave w of the tile's 4 owns the 8 x 8 pixel block
+// (8 (w & 1), 8 (w >> 1)) -- a compact block meets fewer reach boxes than a 16 x 4 strip.
+// kPix = 2: lane l owns the vertically adjacent pixels (l % 16, 2 (l / 16) + k) and a wave a
+// 16 x 8 strip.  (wx0, wx1, wy0, wy1) is the wave's pixel rectangle, for culling.
+template <int kPix>
+__device__ __forceinline__ void pixel_map(int tx, int ty, int t, int& px, int& py_base, float& wx0, float& wx1,
+                                          float& wy0, float& wy1)
+{
+    const int lane = t & 63, wave = t >> 6;
+    if (kPix == 1) {
+        const int bx = tx * kTile + 8 * (wave & 1), by = ty * kTile + 8 * (wave >> 1);
+        px = bx + (lane & 7);
+        py_base = by + (lane >> 3);
+        wx0 = (float)bx;
+        wx1 = wx0 + 7.0f;
+        wy0 = (float)by;
+        wy1 = wy0 + 7.0f;
+    } else {
+        px = tx * kTile + (t & (kTile - 1));
+        py_base = ty * kTile + kPix * (t >> 4);
+        wx0 = (float)(tx * kTile);
+        wx1 = wx0 + (float)(kTile - 1);
+        wy0 = (float)(ty * kTile + 4 * kPix * wave);
+        wy1 = wy0 + (float)(4 * kPix - 1);
+    }
+}
+
 // One pixel's front-to-back state (upstream FORWARD::renderCUDA locals).
 struct FwdPixel {
     float T, C0, C1, C2, F0, F1, F2;
@@ -81,9 +108,7 @@ struct FwdPixel {
     bool done;
 };
 
-// kPix pixels per lane: lane l of the tile's (256 / kPix)-thread workgroup owns the pixels
-// (l % 16, kPix * (l / 16) + k), k < kPix -- vertically adjacent, so a wave covers a compact
-// 16 x (4 kPix) block and its lanes terminate together.
+// kPix pixels per lane (pixel_map).
 template <int kPix>
 __global__ __launch_bounds__(kTilePixels / kPix) void k_render_forward(RenderParams p)
 {
@@ -99,12 +124,10 @@ __global__ __launch_bounds__(kTilePixels / kPix) void k_render_forward(RenderPar
     const int tile = blockIdx.x;
     const int tx = tile % p.gx, ty = tile / p.gx;
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    const int px = tx * kTile + (t & (kTile - 1));
-    const int py_base = ty * kTile + kPix * (t >> 4);
+    int px, py_base;
+    float wx0, wx1, wy0, wy1;
+    pixel_map<kPix>(tx, ty, t, px, py_base, wx0, wx1, wy0, wy1);
     const float pfx = (float)px;
-    // the wave's pixel rectangle: 16 columns x 4 kPix rows
-    const float wx0 = (float)(tx * kTile), wx1 = wx0 + (float)(kTile - 1);
-    const float wy0 = (float)(ty * kTile + 4 * kPix * wave), wy1 = wy0 + (float)(4 * kPix - 1);
     const uint2 range = p.ranges[tile];
     const uint32_t start = range.x, end = range.y;
     const bool feat = p.include_feature != 0;
@@ -396,10 +419,9 @@ __global__ __launch_bounds__(kTilePixels / kPix) void k_render_backward(RenderPa
     const int tile = blockIdx.x;
     const int tx = tile % p.gx, ty = tile / p.gx;
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    const int px = tx * kTile + (t & (kTile - 1));
-    const int py_base = ty * kTile + kPix * (t >> 4);  // kPix vertically adjacent pixels per lane
-    const float wx0 = (float)(tx * kTile), wx1 = wx0 + (float)(kTile - 1);
-    const float wy0 = (float)(ty * kTile + 4 * kPix * wave), wy1 = wy0 + (float)(4 * kPix - 1);
+    int px, py_base;
+    float wx0, wx1, wy0, wy1;
+    pixel_map<kPix>(tx, ty, t, px, py_base, wx0, wx1, wy0, wy1);
     const float pfx = (float)px;
     const size_t HW = (size_t)p.W * p.H;
     const uint32_t start = p.ranges[tile].x;
