@@ -675,11 +675,12 @@ __global__ __launch_bounds__(256) void k_bin_count(int S, int sgx, int gx, int g
 
 // Writes every (tile, Gaussian) pair of a segment at its final point_list position, and the tile
 // ranges (segment 0 of each super-tile).  `table` holds the scanned counts.  Per batch of 256
-// entries: each wave transposes its 64 masks (lane l <- column of local tile l), lane l of wave w
-// computes tile l's base for the wave (cursor + columns of lower waves), and each entry's lane
-// stores its tiles at base + popcount(column & lanes below).  The last wave advances the cursors;
-// two barriers per batch; the next batch is prefetched.  (Storing tile by tile, one contiguous
-// run per store, measured slower: 64 wave-uniform iterations cost more than the scatter.)
+// entries: each wave transposes its 64 masks (lane l <- column of local tile l), so an entry's
+// rank in tile l is popcount(column & lanes below) past the lower waves' columns.  The batch's
+// output is up to 64 contiguous runs (one per tile); it is staged in LDS tile-major and written
+// with consecutive lanes on consecutive addresses (batches over kStage instances store directly).
+constexpr int kStage = 4096;
+
 __global__ __launch_bounds__(256) void k_bin_emit(int S, int sgx, int gx, int gy, const uint32_t* __restrict__ seg_base,
                                                   const uint2* __restrict__ sranges,
                                                   const uint32_t* __restrict__ col_prefix,
@@ -689,8 +690,11 @@ __global__ __launch_bounds__(256) void k_bin_emit(int S, int sgx, int gx, int gy
                                                   uint2* __restrict__ ranges)
 {
     __shared__ uint64_t colw[4][64];
-    __shared__ uint32_t pre[4][64];
-    __shared__ uint32_t cursor[64];
+    __shared__ uint32_t pre[4][64];    // per wave: rank base of tile l inside the batch's staging
+    __shared__ uint32_t cursor[64];    // global position of tile l's next instance
+    __shared__ uint32_t toff[65];      // batch staging offset of tile l (exclusive scan), total
+    __shared__ uint32_t stage_g[kStage];
+    __shared__ uint8_t stage_t[kStage];
     int s, seg;
     if (!block_segment(S, seg_base, &s, &seg)) return;
     const SegmentCtx c = segment_ctx(s, seg, sgx, sranges, col_prefix);
@@ -702,31 +706,56 @@ __global__ __launch_bounds__(256) void k_bin_emit(int S, int sgx, int gx, int gy
         if (seg == 0 && slot >= 0) ranges[gt] = make_uint2(table[slot], table[slot + c.nseg]);
     }
     const uint64_t below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    uint32_t kn = 0, gn = 0;
-    if (c.e0 + t < c.e1) {
-        kn = keys[c.e0 + t];
-        gn = vals[c.e0 + t];
-    }
     for (uint32_t b = c.e0; b < c.e1; b += 256) {
-        uint64_t m = b + t < c.e1 ? entry_mask(kn) : 0ull;
-        const uint32_t g = gn;
-        if (b + 256 + t < c.e1) {  // prefetch the next batch
-            kn = keys[b + 256 + t];
-            gn = vals[b + 256 + t];
+        const uint32_t e = b + t;
+        uint32_t g = 0;
+        uint64_t m = 0ull;
+        if (e < c.e1) {
+            g = vals[e];
+            m = entry_mask(keys[e]);
         }
-        const uint64_t col = transpose64(m);
-        colw[wave][lane] = col;
+        colw[wave][lane] = transpose64(m);
         __syncthreads();
-        uint32_t base = cursor[lane];
-        for (int w = 0; w < wave; w++) base += (uint32_t)__popcll(colw[w][lane]);
-        pre[wave][lane] = base;  // read back only by this wave
-        __syncthreads();
-        if (wave == 3) cursor[lane] = base + (uint32_t)__popcll(col);
-        while (m) {
-            const int l = __ffsll((unsigned long long)m) - 1;
-            m &= m - 1ull;
-            point_list[pre[wave][l] + (uint32_t)__popcll(colw[wave][l] & below)] = g;
+        if (t < 64) {  // wave 0, lane l = tile l: per-wave bases and the tile-major staging scan
+            uint32_t run = 0;
+#pragma unroll
+            for (int w = 0; w < 4; w++) {
+                pre[w][t] = run;
+                run += (uint32_t)__popcll(colw[w][t]);
+            }
+            uint32_t x = run;  // inclusive scan of the tile totals over the 64 lanes
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(x, o, 64);
+                if (t >= o) x += y;
+            }
+            toff[t] = x - run;
+            if (t == 63) toff[64] = x;
         }
+        __syncthreads();
+        const uint32_t total = toff[64];
+        if (total <= (uint32_t)kStage) {
+            while (m) {
+                const int l = __ffsll((unsigned long long)m) - 1;
+                m &= m - 1ull;
+                const uint32_t i = toff[l] + pre[wave][l] + (uint32_t)__popcll(colw[wave][l] & below);
+                stage_g[i] = g;
+                stage_t[i] = (uint8_t)l;
+            }
+            __syncthreads();
+            for (uint32_t i = t; i < total; i += 256) {
+                const int l = stage_t[i];
+                point_list[cursor[l] + (i - toff[l])] = stage_g[i];
+            }
+        } else {
+            while (m) {
+                const int l = __ffsll((unsigned long long)m) - 1;
+                m &= m - 1ull;
+                point_list[cursor[l] + pre[wave][l] + (uint32_t)__popcll(colw[wave][l] & below)] = g;
+            }
+        }
+        __syncthreads();
+        if (t < 64) cursor[t] += toff[t + 1] - toff[t];
     }
 }
 

@@ -21,7 +21,7 @@ enum Counter : int {
 
 constexpr int kRadixThreads = 256;
 constexpr int kSuper = 8;          // super-tile = kSuper x kSuper tiles (64-bit tile masks)
-constexpr int kSegEntries = 2048;  // super-tile list entries per binning workgroup
+constexpr int kSegEntries = 512;   // super-tile list entries per binning workgroup
 constexpr int kGradStride = 16;                          // floats per Gaussian grad record
 
 size_t radix_hist_words(int64_t n);   // per-block digit histograms for n keys
