@@ -210,6 +210,13 @@ int32_t lsr_profile_report(lsr_kernel_stat* out, int32_t capacity);
 int32_t lsr_mark_visible(int32_t P, const float* means3D, const float* viewmatrix,
                          const float* projmatrix, uint8_t* visible, void* stream);
 
+/* Measurement hook, not part of the reference interface: with LSR_RENDER_STATS=1 in the
+ * environment the render backward counts, per wave-iteration over a culled list entry, [0]
+ * entries, [1] entries passing the power test in some lane, [2] entries some lane blends, [3]
+ * lanes blending, [8 + c] a histogram of lanes blending (c = 0..64).  Copies min(n, 73) counters
+ * to host memory and clears them (synchronous). */
+int32_t lsr_debug_render_stats(uint64_t* out, int32_t n);
+
 /* ---- the language-feature loss around the rasterizer ----------------
  *
  * lsr_masked_l1_forward replaces, in LangSplat's include_feature step (train.py:97-98),

@@ -99,6 +99,7 @@ SIGNATURES = {
     "lsr_decode_language_feature": (ctypes.c_int32, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _vp,
                                                      ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _vp, _vp, _vp,
                                                      _vp]),
+    "lsr_debug_render_stats": (ctypes.c_int32, [ctypes.POINTER(ctypes.c_uint64), ctypes.c_int32]),
     "lsr_profile_enable": (ctypes.c_int32, [ctypes.c_int32]),
     "lsr_profile_report": (ctypes.c_int32, [ctypes.POINTER(LsrKernelStat), ctypes.c_int32]),
 }
@@ -374,3 +375,11 @@ def profile_report() -> Dict[str, Dict[str, float]]:
         out[k] = {"launches": int(arr[i].launches), "total_ms": float(arr[i].total_ms),
                   "avg_ms": float(arr[i].total_ms) / max(int(arr[i].launches), 1)}
     return out
+
+
+def debug_render_stats():
+    """Counters of the LSR_RENDER_STATS=1 backward (include/lsr.h lsr_debug_render_stats); clears them."""
+    arr = (ctypes.c_uint64 * 73)()
+    _check(load().lsr_debug_render_stats(arr, 73), "lsr_debug_render_stats")
+    v = list(arr)
+    return {"entries": v[0], "power_hit": v[1], "alpha_hit": v[2], "lanes_hit": v[3], "hist": v[8:8 + 65]}

@@ -371,6 +371,16 @@ int32_t lsr_profile_report(lsr_kernel_stat* out, int32_t capacity)
     return n;
 }
 
+int32_t lsr_debug_render_stats(uint64_t* out, int32_t n)
+{
+    if (!out || n <= 0) return fail(LSR_ERR_INVALID, "lsr_debug_render_stats: invalid argument");
+    const bool debug = false;
+    hipStream_t stream = nullptr;
+    (void)stream;
+    LSR_TRY(render_stats_read(reinterpret_cast<unsigned long long*>(out), n), "render stats");
+    return LSR_OK;
+}
+
 int32_t lsr_mark_visible(int32_t P, const float* means3D, const float* viewmatrix, const float* projmatrix,
                          uint8_t* visible, void* stream_ptr)
 {

@@ -191,5 +191,6 @@ hipError_t launch_decode_language_feature(int H, int W, const int64_t* seg_level
 
 hipError_t launch_render_forward(const RenderParams& p, int tiles, hipStream_t s);
 hipError_t launch_render_backward(const RenderParams& p, int tiles, hipStream_t s);
+hipError_t render_stats_read(unsigned long long* out, int n);  // reads and clears
 
 }  // namespace lsr

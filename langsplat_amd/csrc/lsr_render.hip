@@ -402,10 +402,16 @@ __device__ __forceinline__ void bwd_pixel_blend(BwdPixel& q, float G, float alph
     v[5] += G * dL_dalpha;
 }
 
-template <int kPix>
+// Measurement hook (LSR_RENDER_STATS=1, lsr_debug_render_stats): per wave-iteration counters of
+// the backward -- [0] compacted entries, [1] entries passing the power test in some lane, [2] with
+// an alpha hit, [3] lanes hit, [8 + c] histogram of lanes hit (c = 0..64).  Off by default.
+__device__ unsigned long long g_render_stats[8 + 65];
+
+template <int kPix, bool kStats = false>
 __global__ __launch_bounds__(kTilePixels / kPix) void k_render_backward(RenderParams p)
 {
     constexpr int kThreads = kTilePixels / kPix;
+    __shared__ uint32_t s_stat[kStats ? 8 + 65 : 1];
     __shared__ float4 sA[kThreads];  // x, y, -0.5 conic.x, -0.5 conic.z
     __shared__ float4 sB[kThreads];  // conic.y, opacity, power cutoff, -
     __shared__ float4 sC[kThreads];  // r, g, b, f0
@@ -437,6 +443,8 @@ __global__ __launch_bounds__(kTilePixels / kPix) void k_render_backward(RenderPa
         wmax = max(wmax, q[k].last);
     }
 
+    if (kStats)
+        for (int i = t; i < 8 + 65; i += kThreads) s_stat[i] = 0;
     // entries at list index >= max over the tile of n_contrib can contribute to no pixel
     if (t == 0) s_max = 0;
     __syncthreads();
@@ -471,6 +479,7 @@ __global__ __launch_bounds__(kTilePixels / kPix) void k_render_backward(RenderPa
         const int n = wave_compact(sE, cnt, wx0, wx1, wy0, wy1, lane, sL[wave],
                                    [&](int e) { return maxl - 1 - (done_cnt + e) < wave_max; });
         __syncthreads();  // list visible to the wave's other lanes
+        if (kStats && lane == 0) atomicAdd(&s_stat[0], (uint32_t)n);
         for (int i = 0; i < n; i++) {
             const int j = sL[wave][i];
             const float4 A = sA[j];
@@ -499,12 +508,26 @@ __global__ __launch_bounds__(kTilePixels / kPix) void k_render_backward(RenderPa
                     // must equal the forward's, so alphas within 1e-6 of it use the exact exp.
                     G[k] = __expf(pw[k]);
                     al[k] = fminf(0.99f, B.y * G[k]);
-                    if (fabsf(al[k] - 1.0f / 255.0f) < 1e-6f) {
-                        G[k] = expf_exact(pw[k]);
-                        al[k] = fminf(0.99f, B.y * G[k]);
+                    const bool near = fabsf(al[k] - 1.0f / 255.0f) < 1e-6f;
+                    if (__ballot(near) != 0ull) {  // wave-uniform: keeps the exact exp off the hot path
+                        if (near) {
+                            G[k] = expf_exact(pw[k]);
+                            al[k] = fminf(0.99f, B.y * G[k]);
+                        }
                     }
                     h[k] = h[k] && al[k] >= 1.0f / 255.0f;
                     hit = hit || h[k];
+                }
+                if (kStats) {
+                    const int nh = __popcll(__ballot(hit));
+                    if (lane == 0) {
+                        atomicAdd(&s_stat[1], 1u);
+                        if (nh) {
+                            atomicAdd(&s_stat[2], 1u);
+                            atomicAdd(&s_stat[3], (uint32_t)nh);
+                        }
+                        atomicAdd(&s_stat[8 + nh], 1u);
+                    }
                 }
                 if (hit) {
                     const float4 Cc = sC[j];
@@ -530,6 +553,30 @@ __global__ __launch_bounds__(kTilePixels / kPix) void k_render_backward(RenderPa
             }
         }
     }
+    if (kStats) {
+        __syncthreads();
+        for (int i = t; i < 8 + 65; i += kThreads)
+            if (s_stat[i]) atomicAdd(&g_render_stats[i], (unsigned long long)s_stat[i]);
+    }
+}
+
+static bool render_stats_on()
+{
+    static bool v = [] {
+        const char* e = getenv("LSR_RENDER_STATS");
+        return e && e[0] == '1';
+    }();
+    return v;
+}
+
+hipError_t render_stats_read(unsigned long long* out, int n)
+{
+    if (n > 8 + 65) n = 8 + 65;
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_render_stats), sizeof(unsigned long long) * n, 0,
+                                       hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return e;
+    static const unsigned long long zeros[8 + 65] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_render_stats), zeros, sizeof(zeros), 0, hipMemcpyHostToDevice);
 }
 
 // LSR_BWD_PIXELS=1|2 selects the backward variant (measurement aid; default 1: 0.52 vs 0.58 ms at
@@ -546,7 +593,9 @@ static int bwd_pixels_per_lane()
 hipError_t launch_render_backward(const RenderParams& p, int tiles, hipStream_t s)
 {
     if (tiles == 0) return hipSuccess;
-    if (bwd_pixels_per_lane() == 1)
+    if (render_stats_on())
+        hipLaunchKernelGGL((k_render_backward<1, true>), dim3(tiles), dim3(kTilePixels), 0, s, p);
+    else if (bwd_pixels_per_lane() == 1)
         hipLaunchKernelGGL(k_render_backward<1>, dim3(tiles), dim3(kTilePixels), 0, s, p);
     else
         hipLaunchKernelGGL(k_render_backward<2>, dim3(tiles), dim3(kTilePixels / 2), 0, s, p);
