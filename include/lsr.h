@@ -245,6 +245,14 @@ int32_t lsr_debug_render_stats(uint64_t* out, int32_t n);
 int32_t lsr_adam_step(int64_t n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq, double lr,
                       double beta1, double beta2, double eps, int64_t step, void* stream);
 
+/* ---- point-cloud initialisation --------------------------------------
+ * simple-knn's distCUDA2 (scene/gaussian_model.py:20,180): for each of the N points (N x 3 fp32),
+ * the mean of the squared distances to its 3 nearest OTHER points (exact; a duplicate of a point
+ * counts at distance 0; with N < 4 the missing neighbours count as FLT_MAX).  Scratch is requested
+ * once through `alloc` (which = LSR_BUF_BACKWARD). */
+int32_t lsr_dist_cuda2(int64_t N, const float* points, float* out_mean_dist, lsr_alloc_fn alloc, void* alloc_user,
+                       void* stream);
+
 size_t lsr_masked_l1_scratch_bytes(int32_t C, int64_t HW);
 int32_t lsr_masked_l1_forward(int32_t C, int64_t HW, const float* pred, const float* gt, const void* mask,
                               int32_t mask_is_float, float* loss, void* scratch, void* stream);

@@ -21,7 +21,7 @@ CSRC = os.path.join(HERE, "csrc")
 ROOT = os.path.dirname(HERE)
 BUILD_DIR = os.path.join(ROOT, "build", "lsr")
 LIB_PATH = os.path.join(HERE, "liblsr.so")
-SOURCES = ["lsr_preprocess.hip", "lsr_binning.hip", "lsr_render.hip", "lsr_loss.hip", "lsr_optim.hip", "lsr_api.hip"]
+SOURCES = ["lsr_preprocess.hip", "lsr_binning.hip", "lsr_render.hip", "lsr_loss.hip", "lsr_optim.hip", "lsr_knn.hip", "lsr_api.hip"]
 HEADERS = ["lsr_device.h", "lsr_internal.h"]
 ARCH = os.environ.get("LSR_OFFLOAD_ARCH", "gfx950")
 

@@ -454,6 +454,20 @@ int32_t lsr_adam_step(int64_t n, float* param, const float* grad, float* exp_avg
     return LSR_OK;
 }
 
+int32_t lsr_dist_cuda2(int64_t N, const float* points, float* out_mean_dist, lsr_alloc_fn alloc, void* user,
+                       void* stream_ptr)
+{
+    if (N < 0 || (N > 0 && (!points || !out_mean_dist || !alloc)) || N > 0x3FFFFFFF)
+        return fail(LSR_ERR_INVALID, "lsr_dist_cuda2: invalid argument");
+    if (N == 0) return LSR_OK;
+    hipStream_t stream = reinterpret_cast<hipStream_t>(stream_ptr);
+    const bool debug = false;
+    void* scratch = alloc(user, LSR_BUF_BACKWARD, knn_scratch_bytes(N));
+    if (!scratch) return fail(LSR_ERR_ALLOC, "lsr_dist_cuda2: scratch allocation failed");
+    LSR_TRY(launch_knn_mean_dist3(N, points, out_mean_dist, scratch, stream), "dist_cuda2");
+    return LSR_OK;
+}
+
 int32_t lsr_decode_language_feature(int32_t L, int32_t H, int32_t W, const int64_t* seg_map, int32_t level,
                                     int32_t N, int32_t D, const float* feature_map, float* out_feature,
                                     uint8_t* out_mask, void* stream_ptr)

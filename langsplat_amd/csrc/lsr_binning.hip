@@ -200,6 +200,12 @@ static hipError_t scan_exclusive(const uint32_t* in, uint32_t* out, int n, uint3
     return post(debug, s);
 }
 
+hipError_t scan_exclusive_u32(const uint32_t* in, uint32_t* out, int n, uint32_t* region, uint32_t* fault,
+                              hipStream_t s)
+{
+    return scan_exclusive(in, out, n, region, nullptr, fault, s, false);
+}
+
 // ---------------------------------------------------------------- stable LSD radix sort
 
 // Both radix kernels use a BLOCKED arrangement: wave w of a block owns the contiguous keys

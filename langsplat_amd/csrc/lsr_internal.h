@@ -181,6 +181,12 @@ struct AdamScalars {
 hipError_t launch_adam(int64_t n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
                        const AdamScalars& a, hipStream_t s);
 
+// out[i] = sum(in[0..i)); region: scan_region_words(n) zeroed words (single-pass look-back scan)
+hipError_t scan_exclusive_u32(const uint32_t* in, uint32_t* out, int n, uint32_t* region, uint32_t* fault,
+                              hipStream_t s);
+size_t knn_scratch_bytes(int64_t N);
+hipError_t launch_knn_mean_dist3(int64_t N, const float* pts, float* out, void* scratch, hipStream_t s);
+
 size_t masked_l1_scratch_bytes();
 hipError_t launch_masked_l1_forward(int C, int64_t HW, const float* pred, const float* gt, const void* mask,
                                     int mask_is_float, float* loss, void* scratch, uint32_t epoch, hipStream_t s);

@@ -925,6 +925,35 @@ void lso_activate_backward(int P, int raw, const float* opac, const float* scale
 }
 
 /* ------------------------------------------------------------------------------------------ */
+/* distCUDA2 (simple-knn, scene/gaussian_model.py:20,180)                     */
+/* ------------------------------------------------------------------------------------------ */
+/* Brute force O(N^2): for each point, the 3 smallest squared distances to OTHER points (by
+ * index), each fmaf(dz, dz, fmaf(dy, dy, dx * dx)), mean (d0 + d1 + d2) / 3 with d0 <= d1 <= d2;
+ * missing neighbours (N < 4) are FLT_MAX -- simple-knn's published semantics (exact 3-NN). */
+#include <float.h>
+void lso_knn_mean_dist3(int64_t N, const float* pts, float* out)
+{
+    for (int64_t i = 0; i < N; i++) {
+        float b0 = FLT_MAX, b1 = FLT_MAX, b2 = FLT_MAX;
+        const float px = pts[3 * i], py = pts[3 * i + 1], pz = pts[3 * i + 2];
+        for (int64_t j = 0; j < N; j++) {
+            if (j == i) continue;
+            const float dx = px - pts[3 * j], dy = py - pts[3 * j + 1], dz = pz - pts[3 * j + 2];
+            const float d = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
+            if (d < b2) {
+                if (d < b1) {
+                    b2 = b1;
+                    if (d < b0) { b1 = b0; b0 = d; } else { b1 = d; }
+                } else {
+                    b2 = d;
+                }
+            }
+        }
+        out[i] = (b0 + b1 + b2) / 3.0f;
+    }
+}
+
+/* ------------------------------------------------------------------------------------------ */
 
 int64_t lso_num_rendered(const lso_state* st) { return st->R; }
 

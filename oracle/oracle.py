@@ -77,6 +77,8 @@ def lib():
         L.lso_activate.argtypes = [ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 8
         L.lso_activate_backward.restype = None
         L.lso_activate_backward.argtypes = [ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 12
+        L.lso_knn_mean_dist3.restype = None
+        L.lso_knn_mean_dist3.argtypes = [ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]
         L.lso_cov3d_backward.restype = None
         L.lso_cov3d_backward.argtypes = [ctypes.c_void_p, ctypes.c_float] + [ctypes.c_void_p] * 4
         _lib = L
@@ -300,3 +302,11 @@ def activate_backward(raw, raw_inputs, grads):
     p = lambda x: _ptr(x) if x is not None else None  # noqa: E731
     L.lso_activate_backward(P, int(raw), *[p(x) for x in ins], *[p(g) for g in gs], *[p(o) for o in outs])
     return tuple(outs)
+
+
+def knn_mean_dist3(points) -> np.ndarray:
+    """lso_knn_mean_dist3: brute-force distCUDA2 (mean squared distance to the 3 nearest others)."""
+    p = _np(points)
+    out = np.zeros((p.shape[0],), np.float32)
+    lib().lso_knn_mean_dist3(p.shape[0], _ptr(p), _ptr(out))
+    return out
