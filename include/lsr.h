@@ -131,7 +131,7 @@ typedef struct lsr_backward_args {
     const float* rotations;
     const float* cov3D_precomp;
     const int32_t* radii;
-    const float* dL_dout_color;             /* 3 x H x W */
+    const float* dL_dout_color;             /* 3 x H x W or NULL (treated as zeros) */
     const float* dL_dout_language_feature;  /* 3 x H x W or NULL (treated as zeros) */
     void* geom_buffer;
     void* binning_buffer;
@@ -205,6 +205,9 @@ typedef struct lsr_kernel_stat {
 
 int32_t lsr_profile_enable(int32_t on);
 int32_t lsr_profile_report(lsr_kernel_stat* out, int32_t capacity);
+/* Restricts profiling to the comma-separated stage names (NULL or "" = every stage), so a timed
+ * run can time its dominant kernel live without event overhead around the other stages. */
+int32_t lsr_profile_select(const char* stages);
 
 /* _C.mark_visible: visible[i] = 1 iff Gaussian i passes the near-plane frustum test. */
 int32_t lsr_mark_visible(int32_t P, const float* means3D, const float* viewmatrix,

@@ -10,6 +10,7 @@ There is no CPU fallback: if liblsr.so cannot be loaded the import of this modul
 from __future__ import annotations
 
 import ctypes
+import math
 import os
 import threading
 from typing import Dict, Optional
@@ -103,6 +104,7 @@ SIGNATURES = {
     "lsr_debug_render_stats": (ctypes.c_int32, [ctypes.POINTER(ctypes.c_uint64), ctypes.c_int32]),
     "lsr_profile_enable": (ctypes.c_int32, [ctypes.c_int32]),
     "lsr_profile_report": (ctypes.c_int32, [ctypes.POINTER(LsrKernelStat), ctypes.c_int32]),
+    "lsr_profile_select": (ctypes.c_int32, [ctypes.c_char_p]),
 }
 
 _lib: Optional[ctypes.CDLL] = None
@@ -209,8 +211,28 @@ class _on_device:
             self.ctx.__exit__(*exc)
 
 
+_SETTINGS_CACHE: Dict[int, tuple] = {}
+
+
 def make_settings(rs, keep: list) -> LsrSettings:
-    """lsr_settings from a GaussianRasterizationSettings (gaussian_renderer/__init__.py:37-51)."""
+    """lsr_settings from a GaussianRasterizationSettings (gaussian_renderer/__init__.py:37-51).
+
+    Cached per settings object (a NamedTuple, so immutable): render() builds one per view and the
+    forward and backward both convert it.  The cache holds the object, so its id stays unique."""
+    hit = _SETTINGS_CACHE.get(id(rs))
+    if hit is not None and hit[0] is rs:
+        keep.append(hit[2])
+        return hit[1]
+    mine: list = []
+    s = _build_settings(rs, mine)
+    if len(_SETTINGS_CACHE) >= 16:
+        _SETTINGS_CACHE.clear()
+    _SETTINGS_CACHE[id(rs)] = (rs, s, mine)
+    keep.append(mine)
+    return s
+
+
+def _build_settings(rs, keep: list) -> LsrSettings:
     s = LsrSettings()
     s.image_height = int(rs.image_height)
     s.image_width = int(rs.image_width)
@@ -285,19 +307,28 @@ def rasterize_gaussians_backward(rs, means3D, shs, colors_precomp, language_feat
     M = M_dc + M_rest
     keep: list = []
     s = make_settings(rs, keep)
-    f32 = dict(dtype=torch.float32, device=device)
-    g = {
-        "means2D": torch.empty((P, 3), **f32),
-        "colors_precomp": torch.empty((P, 3), **f32),
-        "language_feature_precomp": torch.empty((P, 3), **f32),
-        "opacities": torch.empty((P, 1), **f32),
-        "means3D": torch.empty((P, 3), **f32),
-        "cov3D_precomp": torch.empty((P, 6), **f32) if _ptr(cov3D_precomp) is not None else None,
-        "shs": torch.empty((P, M_dc, 3), **f32) if M_dc > 0 else None,
-        "shs_rest": torch.empty((P, M_rest, 3), **f32) if split else None,
-        "scales": torch.empty((P, 3), **f32) if _ptr(scales) is not None else None,
-        "rotations": torch.empty((P, 4), **f32) if _ptr(rotations) is not None else None,
-    }
+    # every gradient output is a view of ONE allocation (one caching-allocator call per backward)
+    shapes = [("means2D", (P, 3)), ("colors_precomp", (P, 3)), ("language_feature_precomp", (P, 3)),
+              ("opacities", (P, 1)), ("means3D", (P, 3))]
+    if _ptr(cov3D_precomp) is not None:
+        shapes.append(("cov3D_precomp", (P, 6)))
+    if M_dc > 0:
+        shapes.append(("shs", (P, M_dc, 3)))
+    if split:
+        shapes.append(("shs_rest", (P, M_rest, 3)))
+    if _ptr(scales) is not None:
+        shapes.append(("scales", (P, 3)))
+    if _ptr(rotations) is not None:
+        shapes.append(("rotations", (P, 4)))
+    sizes = [math.prod(sh) for _, sh in shapes]
+    aligned = [(n + 63) // 64 * 64 for n in sizes]  # 256-B aligned views (vector loads/stores)
+    flat = torch.empty((max(sum(aligned), 1),), dtype=torch.float32, device=device)
+    g = dict.fromkeys(("means2D", "colors_precomp", "language_feature_precomp", "opacities", "means3D",
+                       "cov3D_precomp", "shs", "shs_rest", "scales", "rotations"))
+    off = 0
+    for (name, sh), n, na in zip(shapes, sizes, aligned):
+        g[name] = flat[off:off + n].view(sh)
+        off += na
     if P == 0:
         return {k: (v.zero_() if v is not None else None) for k, v in g.items()}
     a = LsrBackwardArgs()
@@ -317,7 +348,7 @@ def rasterize_gaussians_backward(rs, means3D, shs, colors_precomp, language_feat
     a.rotations = _ptr(rotations)
     a.cov3D_precomp = _ptr(cov3D_precomp)
     a.radii = _ptr(radii)
-    gc = _f32c(grad_color.detach())
+    gc = _f32c(grad_color.detach()) if grad_color is not None else None  # None: zero colour gradient
     a.dL_dout_color = _ptr(gc)
     gl = None
     if grad_language is not None:
@@ -360,8 +391,12 @@ def state_layout(P: int, W: int, H: int, num_rendered: int) -> Dict[str, int]:
     return {name: int(getattr(lay, name)) for name, _ in LsrStateLayout._fields_}
 
 
-def profile_enable(on: bool = True):
-    load().lsr_profile_enable(1 if on else 0)
+def profile_enable(on: bool = True, stages=None):
+    """Start (clearing) / stop the per-stage HIP-event profiler; `stages` restricts it to those
+    stage names (lsr_profile_select)."""
+    lib = load()
+    lib.lsr_profile_select(",".join(stages).encode() if stages else None)
+    lib.lsr_profile_enable(1 if on else 0)
 
 
 def profile_report() -> Dict[str, Dict[str, float]]:

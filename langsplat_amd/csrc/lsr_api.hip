@@ -28,6 +28,7 @@ struct Pending {
 struct Profiler {
     std::mutex mu;
     bool on = false;
+    std::vector<std::string> select;  // empty: every stage
     std::vector<Pending> pending;
     std::vector<hipEvent_t> pool;
     std::map<std::string, std::pair<int64_t, double>> stats;
@@ -69,6 +70,11 @@ struct Scope {
     {
         std::lock_guard<std::mutex> g(g_prof.mu);
         if (!g_prof.on) return;
+        if (!g_prof.select.empty()) {
+            bool hit = false;
+            for (const auto& x : g_prof.select) hit = hit || x == n;
+            if (!hit) return;
+        }
         a = g_prof.get();
         b = g_prof.get();
         if (a && b) (void)hipEventRecord(a, s);
@@ -83,7 +89,39 @@ struct Scope {
 };
 }  // namespace
 
-static int32_t fail(int32_t code, const char* what, hipError_t e = hipSuccess)
+// ------------------------------------------------------------------ counter hand-off to the host
+// The forward's one host wait: a one-thread kernel publishes the counters into pinned host memory
+// (system-scope stores, then a sequence number) and the host spins on the sequence number -- no
+// pageable device-to-host copy (which is synchronous) and no stream-synchronise wake-up latency.
+namespace {
+struct HostCounters {
+    uint32_t vals[8];
+    uint32_t seq;
+};
+thread_local HostCounters* t_hc = nullptr;
+thread_local uint32_t t_seq = 0;
+}  // namespace
+
+static int32_t fail(int32_t code, const char* what, hipError_t e = hipSuccess);
+
+// Waits until the counters published with `seq` arrived; false (and a HIP error) on failure.
+static hipError_t wait_counters(HostCounters* hc, uint32_t seq, hipStream_t stream)
+{
+    for (uint64_t spin = 0;; spin++) {
+        if (__atomic_load_n(&hc->seq, __ATOMIC_ACQUIRE) == seq) return hipSuccess;
+        if ((spin & 1023) == 1023) {
+            const hipError_t q = hipStreamQuery(stream);
+            if (q != hipSuccess && q != hipErrorNotReady) return q;
+            if (q == hipSuccess) {  // stream idle: the store must be visible now
+                if (__atomic_load_n(&hc->seq, __ATOMIC_ACQUIRE) == seq) return hipSuccess;
+                return hipErrorUnknown;
+            }
+        }
+        __builtin_ia32_pause();
+    }
+}
+
+static int32_t fail(int32_t code, const char* what, hipError_t e)
 {
     char buf[512];
     if (e != hipSuccess)
@@ -225,10 +263,18 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
     LSR_TRY(launch_preprocess(pp, stream), "preprocess");
     LSR_TRY(launch_depth_order(P, L, geom, counters, stream, debug), "depth order");
 
-    // the one host synchronisation: visible count, num_rendered, error flag
-    uint32_t host_cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    LSR_TRY(hipMemcpyAsync(host_cnt, counters, sizeof(host_cnt), hipMemcpyDeviceToHost, stream), "read counters");
-    LSR_TRY(hipStreamSynchronize(stream), "synchronize");
+    // the one host wait: num_rendered, super-tile entries, error flags
+    if (!t_hc) {
+        void* h = nullptr;
+        LSR_TRY(hipHostMalloc(&h, sizeof(HostCounters), hipHostMallocCoherent), "pinned counters");
+        t_hc = static_cast<HostCounters*>(h);
+        t_hc->seq = 0;
+    }
+    const uint32_t seq = ++t_seq == 0 ? ++t_seq : t_seq;
+    LSR_TRY(launch_publish_counters(counters, t_hc->vals, &t_hc->seq, seq, stream), "publish counters");
+    LSR_TRY(wait_counters(t_hc, seq, stream), "wait counters");
+    uint32_t host_cnt[8];
+    for (int i = 0; i < 8; i++) host_cnt[i] = t_hc->vals[i];
     if (host_cnt[kCntScanFault]) return fail(LSR_ERR_HIP, "lsr_forward: scan look-back stalled");
     if (host_cnt[kCntError] && s->prefiltered)
         return fail(LSR_ERR_PREFILTERED, "lsr_forward: prefiltered=True but a Gaussian is outside the frustum");
@@ -276,7 +322,7 @@ int32_t lsr_backward(const lsr_settings* s, const lsr_backward_args* a, lsr_allo
     hipStream_t stream = reinterpret_cast<hipStream_t>(stream_ptr);
     const bool debug = s->debug != 0;
     if (P == 0) return LSR_OK;
-    if (!a->dL_dout_color || !a->geom_buffer || !a->image_buffer || !a->binning_buffer || !a->radii)
+    if (!a->geom_buffer || !a->image_buffer || !a->binning_buffer || !a->radii)
         return fail(LSR_ERR_INVALID, "lsr_backward: missing forward state");
     const Layout L = make_layout(P, W, H, a->num_rendered, 0);  // point_list sits at offset 0
     char* geom = static_cast<char*>(a->geom_buffer);
@@ -349,8 +395,34 @@ int32_t lsr_profile_enable(int32_t on)
 {
     std::lock_guard<std::mutex> g(g_prof.mu);
     g_prof.drain();
-    if (on) g_prof.stats.clear();
+    if (on) {
+        g_prof.stats.clear();
+        // events come from a pool filled here, not created inside the measured launches
+        while (g_prof.pool.size() < 512) {
+            hipEvent_t e = nullptr;
+            if (hipEventCreate(&e) != hipSuccess) break;
+            g_prof.pool.push_back(e);
+        }
+    }
     g_prof.on = on != 0;
+    return LSR_OK;
+}
+
+int32_t lsr_profile_select(const char* stages)
+{
+    std::lock_guard<std::mutex> g(g_prof.mu);
+    g_prof.select.clear();
+    if (!stages) return LSR_OK;
+    std::string cur;
+    for (const char* c = stages;; c++) {
+        if (*c == ',' || *c == 0) {
+            if (!cur.empty()) g_prof.select.push_back(cur);
+            cur.clear();
+            if (*c == 0) break;
+        } else {
+            cur.push_back(*c);
+        }
+    }
     return LSR_OK;
 }
 

@@ -200,6 +200,22 @@ static hipError_t scan_exclusive(const uint32_t* in, uint32_t* out, int n, uint3
     return post(debug, s);
 }
 
+// one thread: counters -> pinned host memory (system scope), then the sequence number
+__global__ void k_publish_counters(const uint32_t* __restrict__ counters, uint32_t* host_vals, uint32_t* host_seq,
+                                   uint32_t seq)
+{
+    for (int i = 0; i < 8; i++)
+        __hip_atomic_store(&host_vals[i], counters[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(host_seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+hipError_t launch_publish_counters(const uint32_t* counters, uint32_t* host_vals, uint32_t* host_seq, uint32_t seq,
+                                   hipStream_t s)
+{
+    hipLaunchKernelGGL(k_publish_counters, dim3(1), dim3(1), 0, s, counters, host_vals, host_seq, seq);
+    return hipGetLastError();
+}
+
 hipError_t scan_exclusive_u32(const uint32_t* in, uint32_t* out, int n, uint32_t* region, uint32_t* fault,
                               hipStream_t s)
 {

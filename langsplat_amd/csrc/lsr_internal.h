@@ -184,6 +184,8 @@ hipError_t launch_adam(int64_t n, float* param, const float* grad, float* exp_av
 // out[i] = sum(in[0..i)); region: scan_region_words(n) zeroed words (single-pass look-back scan)
 hipError_t scan_exclusive_u32(const uint32_t* in, uint32_t* out, int n, uint32_t* region, uint32_t* fault,
                               hipStream_t s);
+hipError_t launch_publish_counters(const uint32_t* counters, uint32_t* host_vals, uint32_t* host_seq, uint32_t seq,
+                                   hipStream_t s);
 size_t knn_scratch_bytes(int64_t N);
 hipError_t launch_knn_mean_dist3(int64_t N, const float* pts, float* out, void* scratch, hipStream_t s);
 

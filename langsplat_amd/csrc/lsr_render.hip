@@ -330,9 +330,11 @@ __device__ __forceinline__ void bwd_pixel_init(BwdPixel& q, const RenderParams& 
     q.last = inside ? p.n_contrib[pix] : 0u;
     q.dp0 = q.dp1 = q.dp2 = q.dq0 = q.dq1 = q.dq2 = 0.f;
     if (inside) {
-        q.dp0 = p.dL_dcolor[pix];
-        q.dp1 = p.dL_dcolor[HW + pix];
-        q.dp2 = p.dL_dcolor[2 * HW + pix];
+        if (p.dL_dcolor) {  // null: the colour image does not reach the loss (zero gradient)
+            q.dp0 = p.dL_dcolor[pix];
+            q.dp1 = p.dL_dcolor[HW + pix];
+            q.dp2 = p.dL_dcolor[2 * HW + pix];
+        }
         if (feat && p.dL_dlang) {
             q.dq0 = p.dL_dlang[pix];
             q.dq1 = p.dL_dlang[HW + pix];

@@ -94,9 +94,7 @@ class _RasterizeGaussians(torch.autograd.Function):
         rs = ctx.raster_settings
         means3D, sh, colors_precomp, lang, scales, rotations, cov3Ds_precomp, radii, geom, binning, image = \
             ctx.saved_tensors
-        if grad_out_color is None:
-            grad_out_color = torch.zeros((3, rs.image_height, rs.image_width), device=means3D.device)
-        gl = grad_out_language_feature if ctx.use_lang else None
+        gl = grad_out_language_feature if ctx.use_lang else None  # grad_out_color None: zero colour gradient
         args = (means3D, sh, colors_precomp, lang if ctx.use_lang else None, scales, rotations, cov3Ds_precomp,
                 radii, grad_out_color, gl, ctx.num_rendered, geom, binning, image)
         if rs.debug:
@@ -182,9 +180,7 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
     def backward(ctx, grad_out_color, grad_out_language_feature, _grad_radii):
         rs = ctx.raster_settings
         m3, dc, rest, ln, op, sc, ro, radii, geom, binning, image = ctx.saved_tensors
-        rest = rest if rest.numel() > 0 else None
-        if grad_out_color is None:
-            grad_out_color = torch.zeros((3, rs.image_height, rs.image_width), device=m3.device)
+        rest = rest if rest.numel() > 0 else None  # grad_out_color None: zero colour gradient
         gl = grad_out_language_feature if ctx.use_lang else None
         g = _guarded(rs, "snapshot_bw.dump",
                      "\nAn error occured in backward. Writing snapshot_bw.dump for debugging.\n",
