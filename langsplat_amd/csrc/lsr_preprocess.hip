@@ -122,17 +122,44 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessParams p)
     extern __shared__ float s_sh[];
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     for (int w = i; w < p.zero_words; w += gridDim.x * blockDim.x) p.zero[w] = 0u;
+    // Per-Gaussian inputs are loaded first, so their latency overlaps the SH staging below
+    // (issued after the barrier they would add a second memory round trip to every block).
+    const bool live = i < p.P;
+    float px = 0.f, py = 0.f, pz = 0.f, sx = 0.f, sy = 0.f, sz = 0.f, opac = 0.f;
+    float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
+    float cov[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    float f0 = 0.f, f1 = 0.f, f2 = 0.f;
+    const bool feat = p.include_feature && p.lang;
+    if (live) {
+        px = p.means[3 * i];
+        py = p.means[3 * i + 1];
+        pz = p.means[3 * i + 2];
+        if (p.cov_pre) {
+#pragma unroll
+            for (int k = 0; k < 6; k++) cov[k] = p.cov_pre[6 * (size_t)i + k];
+        } else {
+            q = *reinterpret_cast<const float4*>(p.rots + 4 * (size_t)i);
+            sx = p.scales[3 * i];
+            sy = p.scales[3 * i + 1];
+            sz = p.scales[3 * i + 2];
+        }
+        opac = p.opac[i];
+        if (feat) {
+            f0 = p.lang[3 * i];
+            f1 = p.lang[3 * i + 1];
+            f2 = p.lang[3 * i + 2];
+        }
+    }
     if (p.shs) {
         if (blockIdx.x * blockDim.x >= p.P) return;  // block-uniform
         stage_sh_in(p.shs, p.shs_rest, p.P, p.M, s_sh);
         __syncthreads();
     }
-    if (i >= p.P) return;
+    if (!live) return;
     p.radii[i] = 0;
     p.tiles[i] = 0;
     p.depth_key[i] = 0xFFFFFFFFu;
     *reinterpret_cast<uint2*>(p.rect + 2 * (size_t)i) = make_uint2(0u, 0u);  // empty: culled
-    const float px = p.means[3 * i], py = p.means[3 * i + 1], pz = p.means[3 * i + 2];
     const float3 pv = xform4x3(p.view, px, py, pz);
     if (pv.z <= 0.2f) {
         if (p.prefiltered) atomicOr(&p.counters[kCntError], 1u);
@@ -143,13 +170,7 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessParams p)
     const float p_w = 1.0f / (hw + 0.0000001f);
     const float proj_x = hom.x * p_w, proj_y = hom.y * p_w;
 
-    float cov[6];
-    if (p.cov_pre) {
-#pragma unroll
-        for (int k = 0; k < 6; k++) cov[k] = p.cov_pre[6 * (size_t)i + k];
-    } else {
-        float4 q = *reinterpret_cast<const float4*>(p.rots + 4 * (size_t)i);
-        float sx = p.scales[3 * i], sy = p.scales[3 * i + 1], sz = p.scales[3 * i + 2];
+    if (!p.cov_pre) {
         if (p.raw & LSR_RAW_ROTATIONS) q = act_normalize4(q);
         if (p.raw & LSR_RAW_SCALES) {
             sx = act_expf(sx);
@@ -194,19 +215,13 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessParams p)
         rgb[1] = p.colors[3 * i + 1];
         rgb[2] = p.colors[3 * i + 2];
     }
-    float f0 = 0.f, f1 = 0.f, f2 = 0.f;
-    if (p.include_feature && p.lang) {
-        f0 = p.lang[3 * i];
-        f1 = p.lang[3 * i + 1];
-        f2 = p.lang[3 * i + 2];
-        if (p.raw & LSR_RAW_LANGUAGE) {
-            const float3 f = act_lang(f0, f1, f2);
-            f0 = f.x;
-            f1 = f.y;
-            f2 = f.z;
-        }
+    if (feat && (p.raw & LSR_RAW_LANGUAGE)) {
+        const float3 f = act_lang(f0, f1, f2);
+        f0 = f.x;
+        f1 = f.y;
+        f2 = f.z;
     }
-    const float opacity = (p.raw & LSR_RAW_OPACITY) ? act_sigmoid(p.opac[i]) : p.opac[i];
+    const float opacity = (p.raw & LSR_RAW_OPACITY) ? act_sigmoid(opac) : opac;
     p.depth_key[i] = __float_as_uint(pv.z);
     p.radii[i] = r;
     p.tiles[i] = area;
@@ -372,18 +387,61 @@ __device__ void cov3d_backward(float sx, float sy, float sz, float mod, float4 q
               2.f * y * (dR[2][1] + dR[1][2]) - 4.f * z * (dR[1][1] + dR[0][0]);
 }
 
-__device__ __forceinline__ void preprocess_backward_one(const PreprocessBwdParams& p, int i, float* sh_row);
+// The per-Gaussian inputs of the backward, loaded before the SH staging so that the two memory
+// round trips overlap.
+struct BwdIn {
+    int radius;
+    uint32_t clamp;
+    float4 ga, gb, gc;  // the 12 accumulated gradients (render backward record)
+    float px, py, pz, opac;
+    float4 q;
+    float sc[3], lang[3], cov[6];
+};
+
+__device__ __forceinline__ void load_bwd_in(const PreprocessBwdParams& p, int i, BwdIn& in)
+{
+    const size_t i3 = 3 * (size_t)i;
+    in.radius = p.radii[i];
+    const float4* g4 = reinterpret_cast<const float4*>(p.grad + (size_t)i * kGradStride);
+    in.ga = g4[0];
+    in.gb = g4[1];
+    in.gc = g4[2];
+    in.px = p.means[i3];
+    in.py = p.means[i3 + 1];
+    in.pz = p.means[i3 + 2];
+    in.clamp = p.shs ? p.clamped[i] : 0u;
+    in.opac = (p.raw & LSR_RAW_OPACITY) ? p.opac[i] : 0.f;
+    in.q = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int k = 0; k < 3; k++) in.sc[k] = 0.f;
+    for (int k = 0; k < 6; k++) in.cov[k] = 0.f;
+    if (p.cov_pre) {
+#pragma unroll
+        for (int k = 0; k < 6; k++) in.cov[k] = p.cov_pre[6 * (size_t)i + k];
+    } else {
+        in.q = *reinterpret_cast<const float4*>(p.rots + 4 * (size_t)i);
+        in.sc[0] = p.scales[i3];
+        in.sc[1] = p.scales[i3 + 1];
+        in.sc[2] = p.scales[i3 + 2];
+    }
+    const bool lang = (p.raw & LSR_RAW_LANGUAGE) && p.lang;
+    for (int k = 0; k < 3; k++) in.lang[k] = lang ? p.lang[i3 + k] : 0.f;
+}
+
+__device__ __forceinline__ void preprocess_backward_one(const PreprocessBwdParams& p, int i, const BwdIn& in,
+                                                        float* sh_row);
 
 __global__ __launch_bounds__(256) void k_preprocess_backward(PreprocessBwdParams p)
 {
     extern __shared__ float s_sh[];
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (blockIdx.x * blockDim.x >= p.P) return;  // block-uniform
+    BwdIn in;
+    if (i < p.P) load_bwd_in(p, i, in);
     if (p.shs) {
         stage_sh_in(p.shs, p.shs_rest, p.P, p.M, s_sh);
         __syncthreads();
     }
-    if (i < p.P) preprocess_backward_one(p, i, s_sh + threadIdx.x * (3 * p.M + 1));
+    if (i < p.P) preprocess_backward_one(p, i, in, s_sh + threadIdx.x * (3 * p.M + 1));
     if (p.shs && p.dsh) {
         __syncthreads();
         stage_sh_out(p.dsh, p.shs_rest ? p.dsh_rest : nullptr, p.P, p.M, s_sh);
@@ -391,10 +449,11 @@ __global__ __launch_bounds__(256) void k_preprocess_backward(PreprocessBwdParams
 }
 
 // One Gaussian.  `sh_row` holds its SH coefficients on entry (LDS) and receives dL/dsh.
-__device__ __forceinline__ void preprocess_backward_one(const PreprocessBwdParams& p, int i, float* sh_row)
+__device__ __forceinline__ void preprocess_backward_one(const PreprocessBwdParams& p, int i, const BwdIn& in,
+                                                        float* sh_row)
 {
     const size_t i3 = 3 * (size_t)i;
-    if (!(p.radii[i] > 0)) {
+    if (!(in.radius > 0)) {
         // culled: every output row is zero (upstream torch::zeros + skipped threads)
         for (int k = 0; k < 3; k++) {
             p.dmeans2D[i3 + k] = 0.f;
@@ -411,8 +470,7 @@ __device__ __forceinline__ void preprocess_backward_one(const PreprocessBwdParam
             for (int k = 0; k < 3 * p.M; k++) sh_row[k] = 0.f;
         return;
     }
-    const float4* g4 = reinterpret_cast<const float4*>(p.grad + (size_t)i * kGradStride);
-    const float4 ga = g4[0], gb = g4[1], gc = g4[2];
+    const float4 ga = in.ga, gb = in.gb, gc = in.gc;
     // record: [0] dx [1] dy [2] dconic.x [3] dconic.y [4] dconic.w [5] dopacity [6..8] drgb [9..11] dlang
     const float dxy0 = ga.x, dxy1 = ga.y;
     const float dcx = ga.z, dcy = ga.w, dcz = gb.x;
@@ -424,7 +482,7 @@ __device__ __forceinline__ void preprocess_backward_one(const PreprocessBwdParam
     p.dcolors[i3 + 1] = drgb_in[1];
     p.dcolors[i3 + 2] = drgb_in[2];
     if ((p.raw & LSR_RAW_LANGUAGE) && p.lang) {
-        const float3 d = act_lang_backward(p.lang[i3], p.lang[i3 + 1], p.lang[i3 + 2], gc.y, gc.z, gc.w);
+        const float3 d = act_lang_backward(in.lang[0], in.lang[1], in.lang[2], gc.y, gc.z, gc.w);
         p.dlang[i3] = d.x;
         p.dlang[i3 + 1] = d.y;
         p.dlang[i3 + 2] = d.z;
@@ -434,24 +492,20 @@ __device__ __forceinline__ void preprocess_backward_one(const PreprocessBwdParam
         p.dlang[i3 + 2] = gc.w;
     }
     if (p.raw & LSR_RAW_OPACITY) {
-        const float sg = act_sigmoid(p.opac[i]);
+        const float sg = act_sigmoid(in.opac);
         p.dopac[i] = gb.y * (1.0f - sg) * sg;  // torch sigmoid_backward: grad * (1 - y) * y
     } else {
         p.dopac[i] = gb.y;
     }
 
-    const float px = p.means[i3], py = p.means[i3 + 1], pz = p.means[i3 + 2];
+    const float px = in.px, py = in.py, pz = in.pz;
     float cov[6];
-    float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
-    float sc[3] = {0.f, 0.f, 0.f};
+    float4 q = in.q;
+    float sc[3] = {in.sc[0], in.sc[1], in.sc[2]};
     if (p.cov_pre) {
 #pragma unroll
-        for (int k = 0; k < 6; k++) cov[k] = p.cov_pre[6 * (size_t)i + k];
+        for (int k = 0; k < 6; k++) cov[k] = in.cov[k];
     } else {
-        q = *reinterpret_cast<const float4*>(p.rots + 4 * (size_t)i);
-        sc[0] = p.scales[i3];
-        sc[1] = p.scales[i3 + 1];
-        sc[2] = p.scales[i3 + 2];
         if (p.raw & LSR_RAW_ROTATIONS) q = act_normalize4(q);
         if (p.raw & LSR_RAW_SCALES)
             for (int k = 0; k < 3; k++) sc[k] = act_expf(sc[k]);
@@ -523,7 +577,7 @@ __device__ __forceinline__ void preprocess_backward_one(const PreprocessBwdParam
     dmean[2] += (m[8] * m_w - m[11] * mul1) * dxy0 + (m[9] * m_w - m[11] * mul2) * dxy1;
 
     if (p.shs) {
-        const uint32_t cb = p.clamped[i];
+        const uint32_t cb = in.clamp;
         float drgb[3];
 #pragma unroll
         for (int ch = 0; ch < 3; ch++) drgb[ch] = ((cb >> ch) & 1u) ? 0.0f : drgb_in[ch];
@@ -547,8 +601,7 @@ __device__ __forceinline__ void preprocess_backward_one(const PreprocessBwdParam
         if (p.raw & LSR_RAW_SCALES)
             for (int k = 0; k < 3; k++) ds[k] = ds[k] * sc[k];  // torch exp backward: grad * result
         if (p.raw & LSR_RAW_ROTATIONS) {
-            const float4 d = act_normalize4_backward(*reinterpret_cast<const float4*>(p.rots + 4 * (size_t)i),
-                                                     make_float4(dr[0], dr[1], dr[2], dr[3]));
+            const float4 d = act_normalize4_backward(in.q, make_float4(dr[0], dr[1], dr[2], dr[3]));
             dr[0] = d.x;
             dr[1] = d.y;
             dr[2] = d.z;
