@@ -117,7 +117,11 @@ __device__ __forceinline__ void stage_sh_out(float* dsh, float* dsh_rest, int P,
     }
 }
 
-__global__ __launch_bounds__(256) void k_preprocess(PreprocessParams p)
+// 128-thread blocks: the SH staging takes 4 (3M + 1) bytes of LDS per thread, so smaller blocks let
+// more of them share a CU and overlap one block's loads with another's arithmetic.
+constexpr int kPreThreads = 128;
+
+__global__ __launch_bounds__(kPreThreads) void k_preprocess(PreprocessParams p)
 {
     extern __shared__ float s_sh[];
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -234,7 +238,7 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessParams p)
     rec[2] = make_float4(rgb[2], f0, f1, f2);
 }
 
-static size_t sh_lds_bytes(const float* shs, int M) { return shs ? 256 * (size_t)(3 * M + 1) * 4 : 0; }
+static size_t sh_lds_bytes(const float* shs, int M) { return shs ? kPreThreads * (size_t)(3 * M + 1) * 4 : 0; }
 
 // dynamic LDS beyond the 64 KiB default (M > 20 stored SH coefficients) must be opted into
 static hipError_t allow_lds(const void* fn, size_t bytes)
@@ -249,7 +253,8 @@ hipError_t launch_preprocess(const PreprocessParams& p, hipStream_t s)
     if (p.P == 0) return hipSuccess;
     hipError_t e = allow_lds((const void*)k_preprocess, sh_lds_bytes(p.shs, p.M));
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_preprocess, dim3((p.P + 255) / 256), dim3(256), sh_lds_bytes(p.shs, p.M), s, p);
+    hipLaunchKernelGGL(k_preprocess, dim3((p.P + kPreThreads - 1) / kPreThreads), dim3(kPreThreads),
+                       sh_lds_bytes(p.shs, p.M), s, p);
     return hipGetLastError();
 }
 
@@ -430,7 +435,7 @@ __device__ __forceinline__ void load_bwd_in(const PreprocessBwdParams& p, int i,
 __device__ __forceinline__ void preprocess_backward_one(const PreprocessBwdParams& p, int i, const BwdIn& in,
                                                         float* sh_row);
 
-__global__ __launch_bounds__(256) void k_preprocess_backward(PreprocessBwdParams p)
+__global__ __launch_bounds__(kPreThreads) void k_preprocess_backward(PreprocessBwdParams p)
 {
     extern __shared__ float s_sh[];
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -625,7 +630,8 @@ hipError_t launch_preprocess_backward(const PreprocessBwdParams& p, hipStream_t 
     if (p.P == 0) return hipSuccess;
     hipError_t e = allow_lds((const void*)k_preprocess_backward, sh_lds_bytes(p.shs, p.M));
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_preprocess_backward, dim3((p.P + 255) / 256), dim3(256), sh_lds_bytes(p.shs, p.M), s, p);
+    hipLaunchKernelGGL(k_preprocess_backward, dim3((p.P + kPreThreads - 1) / kPreThreads), dim3(kPreThreads),
+                       sh_lds_bytes(p.shs, p.M), s, p);
     return hipGetLastError();
 }
 
