@@ -17,14 +17,14 @@ namespace lsr {
 
 // rows of w floats of the block's Gaussians from src -> LDS rows (stride ws) starting at col0;
 // kW > 0 fixes the row width at compile time (the divisions become multiplies)
-template <int kW>
+template <int kW, int kMaxPer>
 __device__ __forceinline__ void rows_in(const float* __restrict__ src, int ng, int w_rt, float* lds, int ws, int col0)
 {
     const int w = kW > 0 ? kW : w_rt;
     const int n = ng * w;
     const int n4 = (reinterpret_cast<uintptr_t>(src) & 15) == 0 ? (n >> 2) : 0;
     const float4* s4 = reinterpret_cast<const float4*>(src);
-    constexpr int kMaxPer = 12;  // dwordx4 loads all issued before the first LDS write
+    // kMaxPer dwordx4 loads per thread are issued before the first LDS write
     for (int k0 = 0; k0 < n4; k0 += kMaxPer * (int)blockDim.x) {
         float4 r[kMaxPer];
 #pragma unroll
@@ -90,17 +90,20 @@ __device__ __forceinline__ void rows_out(float* __restrict__ dst, int ng, int w_
     }
 }
 
-// SH rows of the block into LDS (one source, or dc + rest)
+// SH rows of the block into LDS (one source, or dc + rest); kDepth dwordx4 loads in flight per
+// thread (deep for the forward, whose waves have registers to spare; shallower for the
+// backward, whose arithmetic already limits its occupancy)
+template <int kDepth>
 __device__ __forceinline__ void stage_sh_in(const float* shs, const float* shs_rest, int P, int M, float* lds)
 {
     const int g0 = blockIdx.x * blockDim.x, ng = min((int)blockDim.x, P - g0), ws = 3 * M + 1;
     if (!shs_rest) {
-        if (M == 16) rows_in<48>(shs + (size_t)g0 * 48, ng, 48, lds, ws, 0);
-        else rows_in<0>(shs + (size_t)g0 * 3 * M, ng, 3 * M, lds, ws, 0);
+        if (M == 16) rows_in<48, kDepth>(shs + (size_t)g0 * 48, ng, 48, lds, ws, 0);
+        else rows_in<0, kDepth>(shs + (size_t)g0 * 3 * M, ng, 3 * M, lds, ws, 0);
     } else {
-        rows_in<3>(shs + (size_t)g0 * 3, ng, 3, lds, ws, 0);
-        if (M == 16) rows_in<45>(shs_rest + (size_t)g0 * 45, ng, 45, lds, ws, 3);
-        else if (M > 1) rows_in<0>(shs_rest + (size_t)g0 * 3 * (M - 1), ng, 3 * (M - 1), lds, ws, 3);
+        rows_in<3, kDepth>(shs + (size_t)g0 * 3, ng, 3, lds, ws, 0);
+        if (M == 16) rows_in<45, kDepth>(shs_rest + (size_t)g0 * 45, ng, 45, lds, ws, 3);
+        else if (M > 1) rows_in<0, kDepth>(shs_rest + (size_t)g0 * 3 * (M - 1), ng, 3 * (M - 1), lds, ws, 3);
     }
 }
 
@@ -156,7 +159,7 @@ __global__ __launch_bounds__(kPreThreads) void k_preprocess(PreprocessParams p)
     }
     if (p.shs) {
         if (blockIdx.x * blockDim.x >= p.P) return;  // block-uniform
-        stage_sh_in(p.shs, p.shs_rest, p.P, p.M, s_sh);
+        stage_sh_in<12>(p.shs, p.shs_rest, p.P, p.M, s_sh);
         __syncthreads();
     }
     if (!live) return;
@@ -443,7 +446,7 @@ __global__ __launch_bounds__(kPreThreads) void k_preprocess_backward(PreprocessB
     BwdIn in;
     if (i < p.P) load_bwd_in(p, i, in);
     if (p.shs) {
-        stage_sh_in(p.shs, p.shs_rest, p.P, p.M, s_sh);
+        stage_sh_in<6>(p.shs, p.shs_rest, p.P, p.M, s_sh);
         __syncthreads();
     }
     if (i < p.P) preprocess_backward_one(p, i, in, s_sh + threadIdx.x * (3 * p.M + 1));
