@@ -160,7 +160,7 @@ typedef struct lsr_state_layout {
     size_t rect;           /* uint32[2P] (minx | miny << 16, maxx | maxy << 16) */
     size_t record;         /* float4[3P] {x, y, conic.x, conic.y}{conic.z, opacity, r, g}{b, f0, f1, f2} */
     size_t clamped;        /* uint32[P]  bit c = SH colour channel c clamped */
-    size_t sorted_ids;     /* uint32[P]  Gaussians by (depth, id); visible ones first */
+    size_t sorted_ids;     /* uint32[P]  Gaussians by (depth, id); culled ones tie with the farthest */
     size_t super_offset;   /* uint32[P]  first super-tile entry of the Gaussian of depth rank r */
     /* image buffer */
     size_t counters;       /* uint32[16] {reserved, num_rendered, error, scan fault, super entries, ...} */

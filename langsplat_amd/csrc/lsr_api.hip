@@ -260,10 +260,11 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
     pp.zero_words = (int)(kDepthScans * L.scan_region_geom);
     pp.raw = a->raw;
     pp.shs_rest = a->shs_rest;
+    pp.partial = reinterpret_cast<uint4*>(geom + L.pre_partial);
     LSR_TRY(launch_preprocess(pp, stream), "preprocess");
-    LSR_TRY(launch_depth_order(P, L, geom, counters, stream, debug), "depth order");
 
-    // the one host wait: num_rendered, super-tile entries, error flags
+    // The one host wait, right after preprocess: num_rendered R and the super-tile entries E size
+    // the binning buffer, and the visible depth-key range fixes the number of sort passes.
     if (!t_hc) {
         void* h = nullptr;
         LSR_TRY(hipHostMalloc(&h, sizeof(HostCounters), hipHostMallocCoherent), "pinned counters");
@@ -271,7 +272,9 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
         t_hc->seq = 0;
     }
     const uint32_t seq = ++t_seq == 0 ? ++t_seq : t_seq;
-    LSR_TRY(launch_publish_counters(counters, t_hc->vals, &t_hc->seq, seq, stream), "publish counters");
+    LSR_TRY(launch_publish_counters((P + kPreThreads - 1) / kPreThreads, pp.partial, counters, t_hc->vals, &t_hc->seq,
+                                    seq, stream),
+            "publish counters");
     LSR_TRY(wait_counters(t_hc, seq, stream), "wait counters");
     uint32_t host_cnt[8];
     for (int i = 0; i < 8; i++) host_cnt[i] = t_hc->vals[i];
@@ -280,6 +283,14 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
         return fail(LSR_ERR_PREFILTERED, "lsr_forward: prefiltered=True but a Gaussian is outside the frustum");
     const int64_t R = host_cnt[kCntRendered];
     *num_rendered = R;
+    if (R > 0) {
+        // sort only the bits the visible keys span (key - min <= max - min)
+        const uint32_t span = host_cnt[kCntKeyMax] - host_cnt[kCntKeyMin];
+        int bits = 0;
+        while (bits < 32 && (span >> bits) != 0) bits++;
+        const int passes = bits <= 8 ? 1 : (bits + 7) / 8;
+        LSR_TRY(launch_depth_order(P, passes, L, geom, counters, stream, debug), "depth order");
+    }
 
     L = make_layout(P, W, H, R, (int64_t)host_cnt[kCntSuper]);
     char* binning = static_cast<char*>(alloc(user, LSR_BUF_BINNING, L.binning_bytes));

@@ -200,19 +200,57 @@ static hipError_t scan_exclusive(const uint32_t* in, uint32_t* out, int n, uint3
     return post(debug, s);
 }
 
-// one thread: counters -> pinned host memory (system scope), then the sequence number
-__global__ void k_publish_counters(const uint32_t* __restrict__ counters, uint32_t* host_vals, uint32_t* host_seq,
-                                   uint32_t seq)
+// One workgroup: reduces the preprocess block partials into the counters (R, E, visible depth-key
+// min / max), then publishes counters[0..7] to pinned host memory (system scope) followed by the
+// sequence number the host spins on.
+__global__ __launch_bounds__(256) void k_publish_counters(int nb, const uint4* __restrict__ partial,
+                                                          uint32_t* __restrict__ counters, uint32_t* host_vals,
+                                                          uint32_t* host_seq, uint32_t seq)
 {
+    __shared__ uint32_t red[4][4];
+    uint32_t t = 0, e = 0, kmin = 0xFFFFFFFFu, kmax = 0;
+    for (int b = threadIdx.x; b < nb; b += 256) {
+        const uint4 v = partial[b];
+        t += v.x;
+        e += v.y;
+        kmin = min(kmin, v.z);
+        kmax = max(kmax, v.w);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        t += __shfl_xor(t, o, 64);
+        e += __shfl_xor(e, o, 64);
+        kmin = min(kmin, (uint32_t)__shfl_xor((int)kmin, o, 64));
+        kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, o, 64));
+    }
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        red[0][w] = t;
+        red[1][w] = e;
+        red[2][w] = kmin;
+        red[3][w] = kmax;
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    for (int k = 1; k < 4; k++) {
+        red[0][0] += red[0][k];
+        red[1][0] += red[1][k];
+        red[2][0] = min(red[2][0], red[2][k]);
+        red[3][0] = max(red[3][0], red[3][k]);
+    }
+    counters[kCntRendered] = red[0][0];
+    counters[kCntSuper] = red[1][0];
+    counters[kCntKeyMin] = red[2][0];
+    counters[kCntKeyMax] = red[3][0];
     for (int i = 0; i < 8; i++)
         __hip_atomic_store(&host_vals[i], counters[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(host_seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-hipError_t launch_publish_counters(const uint32_t* counters, uint32_t* host_vals, uint32_t* host_seq, uint32_t seq,
-                                   hipStream_t s)
+hipError_t launch_publish_counters(int nb, const uint4* partial, uint32_t* counters, uint32_t* host_vals,
+                                   uint32_t* host_seq, uint32_t seq, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_publish_counters, dim3(1), dim3(1), 0, s, counters, host_vals, host_seq, seq);
+    hipLaunchKernelGGL(k_publish_counters, dim3(1), dim3(256), 0, s, nb, partial, counters, host_vals, host_seq, seq);
     return hipGetLastError();
 }
 
@@ -232,9 +270,18 @@ hipError_t scan_exclusive_u32(const uint32_t* in, uint32_t* out, int n, uint32_t
 
 // Per-block digit histogram; hist layout [digit][block] so one scan yields the scatter bases.
 // kItems keys per thread: 16 for large sorts, 4 for P-sized ones (so that >= ~1000 blocks run).
+// First pass of the depth sort only (kxf != null): key' = key - kxf[0] (the smallest visible depth
+// key), and culled keys (0xFFFFFFFF) -> kxf[1] - kxf[0], the largest visible one (their position
+// among equal keys is irrelevant: they emit nothing).  Order among visible keys is unchanged.
+__device__ __forceinline__ uint32_t key_xf(uint32_t k, const uint32_t* kxf)
+{
+    return k == 0xFFFFFFFFu ? kxf[1] - kxf[0] : k - kxf[0];
+}
+
 template <int kItems>
 __global__ __launch_bounds__(kRadixThreads) void k_radix_hist(const uint32_t* __restrict__ keys, int n, int shift,
-                                                              int nbits, uint32_t* __restrict__ hist, int nblk)
+                                                              int nbits, uint32_t* __restrict__ hist, int nblk,
+                                                              const uint32_t* __restrict__ kxf)
 {
     constexpr int kWaves = kRadixThreads / 64;
     __shared__ uint32_t wcnt[kWaves][256];
@@ -250,7 +297,9 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_hist(const uint32_t* __
     for (int it = 0; it < kItems; it++) {
         const int idx = base + it * 64 + lane;
         valid[it] = idx < n;
-        d[it] = valid[it] ? (keys[idx] >> shift) & mask : 0u;
+        uint32_t k = valid[it] ? keys[idx] : 0u;
+        if (kxf) k = key_xf(k, kxf);
+        d[it] = valid[it] ? (k >> shift) & mask : 0u;
     }
 #pragma unroll
     for (int it = 0; it < kItems; it++) {
@@ -274,7 +323,8 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_hist(const uint32_t* __
 template <int kItems>
 __global__ __launch_bounds__(kRadixThreads) void k_radix_scatter(
     const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in, int n, int shift, int nbits,
-    const uint32_t* __restrict__ hist, int nblk, uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out)
+    const uint32_t* __restrict__ hist, int nblk, uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
+    const uint32_t* __restrict__ kxf)
 {
     constexpr int kTile = kRadixThreads * kItems;
     constexpr int kWaves = kRadixThreads / 64;
@@ -297,6 +347,7 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_scatter(
         const int idx = base + it * 64 + lane;
         const bool valid = idx < n;
         key[it] = valid ? keys_in[idx] : 0u;
+        if (kxf) key[it] = key_xf(key[it], kxf);
         val[it] = valid ? (vals_in ? vals_in[idx] : (uint32_t)idx) : 0u;
     }
     __syncthreads();
@@ -358,7 +409,8 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_scatter(
 // (kA, vA) after an even number of passes, or in (kB, vB) after an odd number; returns which.
 static hipError_t radix_sort(const uint32_t* k0, const uint32_t* v0, int n, int total_bits, uint32_t* kA,
                              uint32_t* vA, uint32_t* kB, uint32_t* vB, uint32_t* hist, uint32_t* scan_regions,
-                             size_t region_words, uint32_t* fault, hipStream_t s, bool debug, int* passes_out)
+                             size_t region_words, uint32_t* fault, hipStream_t s, bool debug, int* passes_out,
+                             const uint32_t* kxf = nullptr)
 {
     const bool small = n <= (1 << 21);
     const int tile = kRadixThreads * (small ? 4 : 16);
@@ -374,19 +426,21 @@ static hipError_t radix_sort(const uint32_t* k0, const uint32_t* v0, int n, int 
         uint32_t* kout = (pass & 1) ? kA : kB;
         uint32_t* vout = (pass & 1) ? vA : vB;
         if (small)
-            hipLaunchKernelGGL(k_radix_hist<4>, dim3(nblk), dim3(kRadixThreads), 0, s, kin, n, shift, nbits, hist, nblk);
+            hipLaunchKernelGGL(k_radix_hist<4>, dim3(nblk), dim3(kRadixThreads), 0, s, kin, n, shift, nbits, hist, nblk,
+                               pass == 0 ? kxf : nullptr);
         else
-            hipLaunchKernelGGL(k_radix_hist<16>, dim3(nblk), dim3(kRadixThreads), 0, s, kin, n, shift, nbits, hist, nblk);
+            hipLaunchKernelGGL(k_radix_hist<16>, dim3(nblk), dim3(kRadixThreads), 0, s, kin, n, shift, nbits, hist,
+                               nblk, pass == 0 ? kxf : nullptr);
         if ((e = post(debug, s)) != hipSuccess) return e;
         if ((e = scan_exclusive(hist, hist, (1 << nbits) * nblk, scan_regions + pass * region_words, nullptr, fault,
                                 s, debug)) != hipSuccess)
             return e;
         if (small)
             hipLaunchKernelGGL(k_radix_scatter<4>, dim3(nblk), dim3(kRadixThreads), 0, s, kin, vin, n, shift, nbits,
-                               hist, nblk, kout, vout);
+                               hist, nblk, kout, vout, pass == 0 ? kxf : nullptr);
         else
             hipLaunchKernelGGL(k_radix_scatter<16>, dim3(nblk), dim3(kRadixThreads), 0, s, kin, vin, n, shift, nbits,
-                               hist, nblk, kout, vout);
+                               hist, nblk, kout, vout, pass == 0 ? kxf : nullptr);
         if ((e = post(debug, s)) != hipSuccess) return e;
         kin = kout;
         vin = vout;
@@ -451,49 +505,26 @@ __device__ __forceinline__ uint64_t transpose64(uint64_t x)
 // ---------------------------------------------------------------- depth order + super-tile counts
 
 // Per depth rank r: the Gaussian's tile rectangle copied into depth order (the only random
-// gather of the binning), its super-tile entry count (-> exclusive scan = entry offsets) and
-// per-block sums of its tile count (-> R; same-address atomics would serialise the blocks).
+// gather of the binning) and its super-tile entry count (-> exclusive scan = entry offsets).
 __global__ __launch_bounds__(256) void k_super_counts(int P, const uint32_t* __restrict__ sorted_ids,
                                                       const uint2* __restrict__ rect, uint2* __restrict__ rect_ranked,
-                                                      uint32_t* __restrict__ ns, uint32_t* __restrict__ partial)
+                                                      uint32_t* __restrict__ ns)
 {
-    __shared__ uint32_t wsum[4];
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
-    uint32_t t = 0;
-    if (r < P) {
-        const uint2 rc = rect[sorted_ids[r]];
-        rect_ranked[r] = rc;
-        const uint32_t w = (rc.y & 0xFFFF) - (rc.x & 0xFFFF), h = (rc.y >> 16) - (rc.x >> 16);
-        t = w * h;  // == tiles_touched (the rectangle is empty for culled Gaussians)
-        uint32_t n = 0;
-        if (t) {
-            int sx0, sy0, sx1, sy1;
-            super_rect(rc, sx0, sy0, sx1, sy1);
-            n = (uint32_t)((sx1 - sx0) * (sy1 - sy0));
-        }
-        ns[r] = n;
+    if (r >= P) return;
+    const uint2 rc = rect[sorted_ids[r]];
+    rect_ranked[r] = rc;
+    uint32_t n = 0;
+    if (rc.x != rc.y) {  // empty rectangle: culled
+        int sx0, sy0, sx1, sy1;
+        super_rect(rc, sx0, sy0, sx1, sy1);
+        n = (uint32_t)((sx1 - sx0) * (sy1 - sy0));
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
-    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = t;
-    __syncthreads();
-    if (threadIdx.x == 0) partial[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    ns[r] = n;
 }
 
-// one workgroup: *out = sum of n words (fixed order)
-__global__ __launch_bounds__(256) void k_sum(int n, const uint32_t* __restrict__ v, uint32_t* __restrict__ out)
-{
-    __shared__ uint32_t wsum[4];
-    uint32_t t = 0;
-    for (int i = threadIdx.x; i < n; i += 256) t += v[i];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
-    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = t;
-    __syncthreads();
-    if (threadIdx.x == 0) *out = wsum[0] + wsum[1] + wsum[2] + wsum[3];
-}
-
-hipError_t launch_depth_order(int P, const Layout& L, char* geom, uint32_t* counters, hipStream_t s, bool debug)
+hipError_t launch_depth_order(int P, int passes, const Layout& L, char* geom, uint32_t* counters, hipStream_t s,
+                              bool debug)
 {
     if (P == 0) return hipSuccess;
     uint32_t* hist = reinterpret_cast<uint32_t*>(geom + L.radix_hist);
@@ -503,18 +534,20 @@ hipError_t launch_depth_order(int P, const Layout& L, char* geom, uint32_t* coun
     uint32_t* kb = reinterpret_cast<uint32_t*>(geom + L.keys_b);
     uint32_t* va = reinterpret_cast<uint32_t*>(geom + L.sorted_ids);
     uint32_t* vb = reinterpret_cast<uint32_t*>(geom + L.vals_b);
-    int passes = 0;
-    hipError_t e = radix_sort(reinterpret_cast<const uint32_t*>(geom + L.depth_key), nullptr, P, 32, ka, va, kb, vb,
-                              hist, regions, L.scan_region_geom, fault, s, debug, &passes);
+    // radix_sort ends in its (kA, vA) pair after an even number of passes and in (kB, vB) after an
+    // odd one: swap the roles so the ids always end in sorted_ids
+    int done = 0;
+    const uint32_t* keys = reinterpret_cast<const uint32_t*>(geom + L.depth_key);
+    hipError_t e = (passes & 1)
+        ? radix_sort(keys, nullptr, P, 8 * passes, kb, vb, ka, va, hist, regions, L.scan_region_geom, fault, s, debug,
+                     &done, counters + kCntKeyMin)
+        : radix_sort(keys, nullptr, P, 8 * passes, ka, va, kb, vb, hist, regions, L.scan_region_geom, fault, s, debug,
+                     &done, counters + kCntKeyMin);
     if (e != hipSuccess) return e;
-    // 4 passes: the ids are in sorted_ids (va)
     uint32_t* off = reinterpret_cast<uint32_t*>(geom + L.super_offset);
-    uint32_t* partial = reinterpret_cast<uint32_t*>(geom + L.block_partial);
-    const int nb = (P + 255) / 256;
-    hipLaunchKernelGGL(k_super_counts, dim3(nb), dim3(256), 0, s, P, va, reinterpret_cast<const uint2*>(geom + L.rect),
-                       reinterpret_cast<uint2*>(geom + L.rect_ranked), off, partial);
-    if ((e = post(debug, s)) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_sum, dim3(1), dim3(256), 0, s, nb, (const uint32_t*)partial, counters + kCntRendered);
+    hipLaunchKernelGGL(k_super_counts, dim3((P + 255) / 256), dim3(256), 0, s, P, (const uint32_t*)va,
+                       reinterpret_cast<const uint2*>(geom + L.rect), reinterpret_cast<uint2*>(geom + L.rect_ranked),
+                       off);
     if ((e = post(debug, s)) != hipSuccess) return e;
     return scan_exclusive(off, off, P, regions + passes * L.scan_region_geom, counters + kCntSuper, fault, s,
                           debug);

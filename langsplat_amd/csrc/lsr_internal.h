@@ -16,10 +16,15 @@ enum Counter : int {
     kCntError = 2,
     kCntScanFault = 3,
     kCntSuper = 4,       // super-tile entries E (binning)
+    kCntKeyMin = 5,      // smallest visible depth key (float bits)
+    kCntKeyMax = 6,      // largest visible depth key
     kCntSlots = 16
 };
 
 constexpr int kRadixThreads = 256;
+// preprocess workgroups: the SH staging takes 4 (3M + 1) bytes of LDS per thread, so 128-thread
+// blocks let more of them share a CU and overlap one block's loads with another's arithmetic
+constexpr int kPreThreads = 128;
 constexpr int kSuper = 8;          // super-tile = kSuper x kSuper tiles (64-bit tile masks)
 constexpr int kSegEntries = 512;   // super-tile list entries per binning workgroup
 constexpr int kGradStride = 16;                          // floats per Gaussian grad record
@@ -31,7 +36,7 @@ constexpr int kDepthScans = 5;         // 4 depth-sort passes + the instance-off
 struct Layout {
     // geometry (per Gaussian)
     size_t depth_key, tiles_touched, rect, record, clamped, sorted_ids, super_offset;
-    size_t keys_a, keys_b, vals_b, radix_hist, scan_regions, rect_ranked, block_partial;
+    size_t keys_a, keys_b, vals_b, radix_hist, scan_regions, rect_ranked, pre_partial;
     size_t scan_region_geom;  // u32 words per depth-order scan region
     size_t geom_bytes;
     // image (per pixel / tile)
@@ -71,7 +76,7 @@ inline Layout make_layout(int P, int W, int H, int64_t R, int64_t E)
     L.scan_region_geom = scan_region_words((int64_t)(hw_p > p ? hw_p : p));
     L.scan_regions = take(4 * kDepthScans * L.scan_region_geom);
     L.rect_ranked = take(8 * p);
-    L.block_partial = take(4 * ((p + 255) / 256));
+    L.pre_partial = take(16 * ((p + kPreThreads - 1) / kPreThreads));
     L.geom_bytes = o;
 
     L.gx = (W + kTile - 1) / kTile;
@@ -127,6 +132,7 @@ struct PreprocessParams {
     float4* record;
     uint32_t* zero;   // depth-order scan status, cleared here
     int zero_words;
+    uint4* partial;   // per block {tile instances, super-tile entries, min / max visible depth key}
     int raw;                  // lsr_raw_flags
     const float* shs_rest;    // split SH rows (shs = dc only) or null
 };
@@ -163,9 +169,10 @@ hipError_t launch_preprocess_backward(const PreprocessBwdParams& p, hipStream_t 
 hipError_t launch_mark_visible(int P, const float* means, const float* view, const float* proj,
                                uint8_t* visible, hipStream_t s);
 
-// depth sort of all P Gaussians by (depth key, id) -> sorted_ids; per-Gaussian super-tile entry
-// offsets in that order; counters[kCntRendered] = tile instances R, counters[kCntSuper] = entries E
-hipError_t launch_depth_order(int P, const Layout& L, char* geom, uint32_t* counters, hipStream_t s,
+// depth sort of all P Gaussians by (depth key, id) on `passes` 8-bit digits of the key minus the
+// smallest visible key (counters[kCntKeyMin/Max], from launch_preprocess) -> sorted_ids; per-Gaussian
+// super-tile entry offsets in that order
+hipError_t launch_depth_order(int P, int passes, const Layout& L, char* geom, uint32_t* counters, hipStream_t s,
                               bool debug);
 // super-tile lists, per-(tile, segment) counts, scanned bases -> point_list and tile ranges
 hipError_t launch_binning(int P, int64_t R, const Layout& L, char* geom, char* image, char* binning,
@@ -184,8 +191,9 @@ hipError_t launch_adam(int64_t n, float* param, const float* grad, float* exp_av
 // out[i] = sum(in[0..i)); region: scan_region_words(n) zeroed words (single-pass look-back scan)
 hipError_t scan_exclusive_u32(const uint32_t* in, uint32_t* out, int n, uint32_t* region, uint32_t* fault,
                               hipStream_t s);
-hipError_t launch_publish_counters(const uint32_t* counters, uint32_t* host_vals, uint32_t* host_seq, uint32_t seq,
-                                   hipStream_t s);
+// reduces the preprocess block partials into counters and publishes counters[0..7] + seq to the host
+hipError_t launch_publish_counters(int nb, const uint4* partial, uint32_t* counters, uint32_t* host_vals,
+                                   uint32_t* host_seq, uint32_t seq, hipStream_t s);
 size_t knn_scratch_bytes(int64_t N);
 hipError_t launch_knn_mean_dist3(int64_t N, const float* pts, float* out, void* scratch, hipStream_t s);
 

@@ -120,10 +120,6 @@ __device__ __forceinline__ void stage_sh_out(float* dsh, float* dsh_rest, int P,
     }
 }
 
-// 128-thread blocks: the SH staging takes 4 (3M + 1) bytes of LDS per thread, so smaller blocks let
-// more of them share a CU and overlap one block's loads with another's arithmetic.
-constexpr int kPreThreads = 128;
-
 __global__ __launch_bounds__(kPreThreads) void k_preprocess(PreprocessParams p)
 {
     extern __shared__ float s_sh[];
@@ -162,7 +158,9 @@ __global__ __launch_bounds__(kPreThreads) void k_preprocess(PreprocessParams p)
         stage_sh_in<12>(p.shs, p.shs_rest, p.P, p.M, s_sh);
         __syncthreads();
     }
-    if (!live) return;
+    // per-thread contributions to the block partials: tile instances, super-tile entries, depth key
+    uint32_t my_tiles = 0, my_supers = 0, my_key = 0xFFFFFFFFu;
+    if (live) do {  // `break` = culled
     p.radii[i] = 0;
     p.tiles[i] = 0;
     p.depth_key[i] = 0xFFFFFFFFu;
@@ -170,7 +168,7 @@ __global__ __launch_bounds__(kPreThreads) void k_preprocess(PreprocessParams p)
     const float3 pv = xform4x3(p.view, px, py, pz);
     if (pv.z <= 0.2f) {
         if (p.prefiltered) atomicOr(&p.counters[kCntError], 1u);
-        return;
+        break;
     }
     const float3 hom = xform4x3(p.proj, px, py, pz);
     const float hw = xform4w(p.proj, px, py, pz);
@@ -189,7 +187,7 @@ __global__ __launch_bounds__(kPreThreads) void k_preprocess(PreprocessParams p)
     const Cov2D cv = cov2d(px, py, pz, p.focal_x, p.focal_y, p.tanfovx, p.tanfovy, cov, p.view);
     const float a = cv.a, b = cv.b, c = cv.c;
     const float det = a * c - b * b;
-    if (det == 0.0f) return;
+    if (det == 0.0f) break;
     const float det_inv = 1.f / det;
     const float cx = c * det_inv, cy = -b * det_inv, cz = a * det_inv;
     const float mid = 0.5f * (a + c);
@@ -202,7 +200,7 @@ __global__ __launch_bounds__(kPreThreads) void k_preprocess(PreprocessParams p)
     int r4[4];
     tile_rect(ix, iy, r, p.gx, p.gy, r4);
     const uint32_t area = (uint32_t)((r4[2] - r4[0]) * (r4[3] - r4[1]));
-    if (area == 0) return;
+    if (area == 0) break;
 
     float rgb[3];
     uint32_t clamp_bits = 0;
@@ -239,6 +237,41 @@ __global__ __launch_bounds__(kPreThreads) void k_preprocess(PreprocessParams p)
     rec[0] = make_float4(ix, iy, cx, cy);
     rec[1] = make_float4(cz, opacity, rgb[0], rgb[1]);
     rec[2] = make_float4(rgb[2], f0, f1, f2);
+    my_tiles = area;
+    my_supers = (uint32_t)(((r4[2] + kSuper - 1) / kSuper - r4[0] / kSuper) *
+                           ((r4[3] + kSuper - 1) / kSuper - r4[1] / kSuper));
+    my_key = __float_as_uint(pv.z);
+    } while (0);
+    // block partials {R, E, min visible depth key, max visible depth key}: the host learns R, E and
+    // the depth-key range before the depth sort (k_pre_reduce; the sort then needs only the bits
+    // the visible keys actually span)
+    __shared__ uint32_t red[4][kPreThreads / 64];
+    uint32_t kmin = my_key, kmax = my_key == 0xFFFFFFFFu ? 0u : my_key;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        my_tiles += __shfl_xor(my_tiles, o, 64);
+        my_supers += __shfl_xor(my_supers, o, 64);
+        kmin = min(kmin, (uint32_t)__shfl_xor((int)kmin, o, 64));
+        kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, o, 64));
+    }
+    const int wave = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        red[0][wave] = my_tiles;
+        red[1][wave] = my_supers;
+        red[2][wave] = kmin;
+        red[3][wave] = kmax;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint4 v = make_uint4(0u, 0u, 0xFFFFFFFFu, 0u);
+        for (int w = 0; w < kPreThreads / 64; w++) {
+            v.x += red[0][w];
+            v.y += red[1][w];
+            v.z = min(v.z, red[2][w]);
+            v.w = max(v.w, red[3][w]);
+        }
+        p.partial[blockIdx.x] = v;
+    }
 }
 
 static size_t sh_lds_bytes(const float* shs, int M) { return shs ? kPreThreads * (size_t)(3 * M + 1) * 4 : 0; }
@@ -256,9 +289,9 @@ hipError_t launch_preprocess(const PreprocessParams& p, hipStream_t s)
     if (p.P == 0) return hipSuccess;
     hipError_t e = allow_lds((const void*)k_preprocess, sh_lds_bytes(p.shs, p.M));
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_preprocess, dim3((p.P + kPreThreads - 1) / kPreThreads), dim3(kPreThreads),
-                       sh_lds_bytes(p.shs, p.M), s, p);
-    return hipGetLastError();
+    const int nb = (p.P + kPreThreads - 1) / kPreThreads;
+    hipLaunchKernelGGL(k_preprocess, dim3(nb), dim3(kPreThreads), sh_lds_bytes(p.shs, p.M), s, p);
+    return hipGetLastError();  // the block partials are reduced by launch_publish_counters
 }
 
 // ------------------------------------------------------------------------------------------

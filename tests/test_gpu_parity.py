@@ -282,3 +282,32 @@ def test_full_size_properties(cfg):
         rhs = ga[k].double() + gb[k].double()
         scale = rhs.abs().max().item() + 1e-30
         assert (lhs - rhs).abs().max().item() <= 1e-3 * scale, k
+
+
+@pytest.mark.parametrize("kind", ["wide", "narrow", "ties"])
+def test_depth_sort_pass_counts(kind):
+    """The depth sort radix-sorts only the bits the visible keys span (key - min): a depth range
+    of 0.3..80 needs 4 passes, a sliver 1 pass, exact ties 1 pass and fall back to id order.  The
+    per-tile order (and everything downstream) must stay bit-identical to the oracle's."""
+    g = torch.Generator().manual_seed({"wide": 31, "narrow": 32, "ties": 33}[kind])
+    P, W, H = 3000, 96, 64
+    cam = make_cameras(1, W, H)[0]  # at (0, 0, -4) looking along +z: view depth = z + 4
+    if kind == "wide":
+        d = torch.exp(torch.rand(P, generator=g) * (math.log(80.0) - math.log(0.3)) + math.log(0.3))
+    elif kind == "narrow":
+        d = 4.0 + torch.rand(P, generator=g) * 1e-3
+    else:
+        d = torch.full((P,), 4.0)
+    u, v = torch.rand(P, generator=g) * 2 - 1, torch.rand(P, generator=g) * 2 - 1
+    means = torch.stack([u * d * 0.4, v * d * 0.3, d - 4.0], 1)
+    if kind == "ties":
+        means[P // 2:] = means[:P - P // 2]  # exact duplicates: equal keys, order by id
+    inp = dict(means3D=means, opacities=torch.rand((P, 1), generator=g) * 0.6 + 0.05,
+               colors_precomp=torch.rand((P, 3), generator=g),
+               language_feature_precomp=torch.nn.functional.normalize(torch.randn((P, 3), generator=g)),
+               scales=torch.full((P, 3), 0.02) * d[:, None] / 4.0,
+               rotations=torch.nn.functional.normalize(torch.randn((P, 4), generator=g)))
+    st = settings_for(cam, sh_degree=0)
+    run, std, ind, out = check_forward_exact(st, inp)
+    assert out[0] > 0
+    check_backward(st, inp, run, out)
