@@ -244,10 +244,32 @@ def _build_settings(rs, keep: list) -> LsrSettings:
     s.debug = int(bool(rs.debug))
     s.include_feature = int(bool(getattr(rs, "include_feature", False)))
     for name in ("bg", "viewmatrix", "projmatrix", "campos"):
-        t = _f32c(getattr(rs, name).detach())
+        t = _f32c_cached(getattr(rs, name))
         keep.append(t)
         setattr(s, name, t.data_ptr())
     return s
+
+
+_CONTIG_CACHE: Dict[int, tuple] = {}
+
+
+def _f32c_cached(src: torch.Tensor) -> torch.Tensor:
+    """_f32c of a camera tensor, reused while the source object and its version are unchanged.
+
+    render() builds new settings every step from the same camera tensors, and the reference's
+    world_view_transform is a transposed view (scene/cameras.py:47): without the cache every step
+    pays a small copy kernel for it."""
+    t = src.detach()
+    if t.dtype == torch.float32 and t.is_contiguous():
+        return t
+    hit = _CONTIG_CACHE.get(id(src))
+    if hit is not None and hit[0] is src and hit[1] == src._version:
+        return hit[2]
+    c = _f32c(t)
+    if len(_CONTIG_CACHE) >= 64:
+        _CONTIG_CACHE.clear()
+    _CONTIG_CACHE[id(src)] = (src, src._version, c)
+    return c
 
 
 def rasterize_gaussians(rs, means3D, shs, colors_precomp, language_feature, opacities, scales, rotations,
@@ -264,7 +286,7 @@ def rasterize_gaussians(rs, means3D, shs, colors_precomp, language_feature, opac
     s = make_settings(rs, keep)
     color = torch.empty((3, H, W), dtype=torch.float32, device=device)
     lang = torch.empty((3, H, W), dtype=torch.float32, device=device)
-    radii = torch.zeros((P,), dtype=torch.int32, device=device)
+    radii = torch.empty((P,), dtype=torch.int32, device=device)  # preprocess writes every entry
     a = LsrForwardArgs()
     a.P = P
     a.M = int(shs.shape[1]) if shs is not None and shs.numel() > 0 else 0

@@ -221,7 +221,7 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
     char* image = static_cast<char*>(alloc(user, LSR_BUF_IMAGE, L.image_bytes));
     if (!geom || !image) return fail(LSR_ERR_ALLOC, "lsr_forward: geometry/image buffer allocation failed");
     uint32_t* counters = reinterpret_cast<uint32_t*>(image + L.counters);
-    LSR_TRY(hipMemsetAsync(counters, 0, 4 * kCntSlots, stream), "memset counters");
+    LSR_TRY(hipMemsetAsync(counters, 0, 4 * kCntWords, stream), "memset counters");
 
     PreprocessParams pp{};
     pp.P = P;
@@ -308,6 +308,8 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
     rp.bg = s->bg;
     rp.final_T = reinterpret_cast<float*>(image + L.final_T);
     rp.n_contrib = reinterpret_cast<uint32_t*>(image + L.n_contrib);
+    rp.sched_counts = reinterpret_cast<uint32_t*>(image + L.counters);
+    rp.sched_lists = reinterpret_cast<uint32_t*>(image + L.tile_lists);
     rp.out_color = a->out_color;
     rp.out_lang = a->out_language_feature;
     LSR_TRY(launch_render_forward(rp, L.tiles, stream), "render forward");
@@ -355,6 +357,8 @@ int32_t lsr_backward(const lsr_settings* s, const lsr_backward_args* a, lsr_allo
     rp.bg = s->bg;
     rp.final_T = reinterpret_cast<float*>(image + L.final_T);
     rp.n_contrib = reinterpret_cast<uint32_t*>(image + L.n_contrib);
+    rp.sched_counts = reinterpret_cast<uint32_t*>(image + L.counters);
+    rp.sched_lists = reinterpret_cast<uint32_t*>(image + L.tile_lists);
     rp.dL_dcolor = a->dL_dout_color;
     rp.dL_dlang = a->dL_dout_language_feature;
     rp.grad = grad;

@@ -742,7 +742,8 @@ __global__ __launch_bounds__(256) void k_bin_emit(int S, int sgx, int gx, int gy
                                                   const uint32_t* __restrict__ row_prefix,
                                                   const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals,
                                                   const uint32_t* __restrict__ table, uint32_t* __restrict__ point_list,
-                                                  uint2* __restrict__ ranges)
+                                                  uint2* __restrict__ ranges, uint32_t* __restrict__ sched_counts,
+                                                  uint32_t* __restrict__ sched_lists)
 {
     __shared__ uint64_t colw[4][64];
     __shared__ uint32_t pre[4][64];    // per wave: rank base of tile l inside the batch's staging
@@ -758,7 +759,12 @@ __global__ __launch_bounds__(256) void k_bin_emit(int S, int sgx, int gx, int gy
         int gt = 0;
         const int64_t slot = table_slot(c, t, gx, gy, row_prefix, &gt);
         cursor[t] = slot >= 0 ? table[slot + seg] : 0u;
-        if (seg == 0 && slot >= 0) ranges[gt] = make_uint2(table[slot], table[slot + c.nseg]);
+        if (seg == 0 && slot >= 0) {
+            const uint2 r = make_uint2(table[slot], table[slot + c.nseg]);
+            ranges[gt] = r;
+            // the forward's longest-first schedule: work = list length
+            if (r.y > r.x) schedule_tile(sched_counts, sched_lists, gx * gy, gt, r.y - r.x);
+        }
     }
     const uint64_t below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     for (uint32_t b = c.e0; b < c.e1; b += 256) {
@@ -861,7 +867,9 @@ hipError_t launch_binning(int P, int64_t R, const Layout& L, char* geom, char* i
         return e;
     hipLaunchKernelGGL(k_bin_emit, dim3(grid), dim3(256), 0, s, L.supers, L.sgx, L.gx, L.gy, (const uint32_t*)seg_base,
                        (const uint2*)sranges, (const uint32_t*)colpre, (const uint32_t*)rowpre, skeys, svals,
-                       (const uint32_t*)table, pl, ranges);
+                       (const uint32_t*)table, pl, ranges,
+                       reinterpret_cast<uint32_t*>(image + L.counters) + kCntFwdClass,
+                       reinterpret_cast<uint32_t*>(image + L.tile_lists));
     return post(debug, s);
 }
 

@@ -20,6 +20,12 @@ enum Counter : int {
     kCntKeyMax = 6,      // largest visible depth key
     kCntSlots = 16
 };
+// longest-first tile schedule (lsr_render.hip): tiles per work class, forward and backward,
+// right after the counters so one memset clears both
+constexpr int kWorkClasses = 64;
+constexpr int kCntFwdClass = kCntSlots;
+constexpr int kCntBwdClass = kCntSlots + kWorkClasses;
+constexpr int kCntWords = kCntSlots + 2 * kWorkClasses;
 
 constexpr int kRadixThreads = 256;
 // preprocess workgroups: the SH staging takes 4 (3M + 1) bytes of LDS per thread, so 128-thread
@@ -40,7 +46,7 @@ struct Layout {
     size_t scan_region_geom;  // u32 words per depth-order scan region
     size_t geom_bytes;
     // image (per pixel / tile)
-    size_t counters, ranges, final_T, n_contrib;
+    size_t counters, ranges, final_T, n_contrib, tile_lists;
     size_t image_bytes;
     // binning (point_list per tile instance, the rest per super-tile entry / segment)
     size_t point_list, super_keys, super_vals, alt_keys, alt_vals, bin_radix_hist, bin_scan_regions;
@@ -91,10 +97,11 @@ inline Layout make_layout(int P, int W, int H, int64_t R, int64_t E)
     const size_t T = (size_t)(L.tiles > 0 ? L.tiles : 1);
     const size_t HW = (size_t)W * (size_t)H;
     o = 0;
-    L.counters = take(4 * kCntSlots);
+    L.counters = take(4 * kCntWords);
     L.ranges = take(8 * T);
     L.final_T = take(4 * (HW > 0 ? HW : 1));
     L.n_contrib = take(4 * (HW > 0 ? HW : 1));
+    L.tile_lists = take(4 * 2 * kWorkClasses * T);  // [fwd | bwd][class][T]
     L.image_bytes = o;
 
     o = 0;
@@ -159,6 +166,10 @@ struct RenderParams {
     float* final_T;
     uint32_t* n_contrib;
     float *out_color, *out_lang;
+    // longest-first schedule: class counts (counters + kCntFwdClass / kCntBwdClass) and lists
+    // (class c of pass d at tile_lists[(d * kWorkClasses + c) * tiles]); null: launch order
+    uint32_t* sched_counts;
+    uint32_t* sched_lists;
     // backward
     const float *dL_dcolor, *dL_dlang;
     float* grad;
@@ -177,6 +188,23 @@ hipError_t launch_depth_order(int P, int passes, const Layout& L, char* geom, ui
 // super-tile lists, per-(tile, segment) counts, scanned bases -> point_list and tile ranges
 hipError_t launch_binning(int P, int64_t R, const Layout& L, char* geom, char* image, char* binning,
                           hipStream_t s, bool debug);
+
+// work class of a tile with w >= 1 units of work: quarter-octaves, monotone in w, 0..63 (w >= 2^16
+// shares the top class)
+__device__ __forceinline__ int work_class(uint32_t w)
+{
+    if (w >= 65536u) return kWorkClasses - 1;
+    const int lg = 31 - __clz(w);
+    const int frac = lg >= 2 ? (int)((w >> (lg - 2)) & 3u) : (lg == 1 ? (int)((w & 1u) << 1) : 0);
+    return 4 * lg + frac;
+}
+
+// appends tile t with w >= 1 units of work to class lists (counts[c], lists[c * T + i])
+__device__ __forceinline__ void schedule_tile(uint32_t* counts, uint32_t* lists, int T, int t, uint32_t w)
+{
+    const int c = work_class(w);
+    lists[(size_t)c * T + atomicAdd(&counts[c], 1u)] = (uint32_t)t;
+}
 
 struct AdamScalars {
     float w1;             // 1 - beta1 (lerp weight)

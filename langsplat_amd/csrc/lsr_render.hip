@@ -1,17 +1,22 @@
 // lsr_render.hip -- per-tile compositing (forward) and its back-to-front replay (backward).
 //
-// Backward: one 128-thread workgroup per 16x16 screen tile = 2 wave64s; every lane owns TWO
-// vertically adjacent pixels, so each list entry read from LDS feeds two independent dependency
-// chains (ILP) and the per-entry fixed costs (LDS reads, loop control, the wave reduction) are
-// paid once per two pixels.  Forward: templated on pixels per lane (1 = 256 threads).  The tile's depth-ordered list is streamed through LDS in batches of 128
-// entries (48 B records split into broadcast-friendly {x, y, -conic.x/2, -conic.z/2}
-// {conic.y, opacity, power cutoff}{r, g, b, f0}{f1, f2} arrays).  Semantics: upstream FORWARD/BACKWARD::renderCUDA extended by
-// the 3-channel language feature; arithmetic order is
-// that of oracle/lsr_oracle.c render_pixel / backward_pixel.
+// One 256-thread workgroup per 16x16 screen tile; wave w of its 4 owns the 8x8 pixel block
+// (8 (w & 1), 8 (w >> 1)) and every lane one pixel.  Workgroups take tiles longest first
+// (scheduled_tile).  The tile's depth-ordered list is streamed through LDS in batches of 256
+// entries (one per thread: {x, y, -conic.x/2, -conic.z/2}{conic.y, opacity, power cutoff, f1}
+// {r, g, b, f0}{f2}); the loading thread also computes the screen box the entry can reach
+// (entry_box), and a wave skips the entries whose box misses its block:
+//   forward:  each wave compacts the batch into a slot list (wave_compact);
+//   backward: the loader stores a 4-bit mask of the wave blocks the box meets and each wave walks
+//             the set bits of a ballot over it -- no list, 26.9 KB of LDS, so 5 workgroups per CU.
+// (Measured both ways at C3: the list is faster in the forward, the mask in the backward.)
+// Semantics: upstream FORWARD/BACKWARD::renderCUDA extended by the 3-channel language feature
+// (SURVEY.md §8a a10-a11, App. A.4-A.5); arithmetic order is that of oracle/lsr_oracle.c
+// render_pixel / backward_pixel.
 //
 // Backward gradient scatter: every lane of a wave visits the same list entry at the same
 // iteration, so the 12 per-Gaussian partials of a wave are reduced in registers by a
-// reduce-scatter (permlane32/16 swaps + DPP mirrors, ~35 VALU ops), the 2 waves' results are summed
+// reduce-scatter (permlane32/16 swaps + DPP mirrors, ~35 VALU ops), the 4 waves' results are summed
 // in LDS (ds_add_f32), and after each batch ONE 12-lane atomic instruction per (tile, Gaussian)
 // adds the tile's total into a 64-byte-aligned per-Gaussian record -- instead of the upstream 12
 // scattered atomics per pixel per blend.  Entries no lane contributes to are skipped by a ballot.
@@ -47,16 +52,24 @@ __device__ __forceinline__ float4 entry_box(float x, float y, float cx, float cy
     return make_float4(x - ex, x + ex, y - ey, y + ey);
 }
 
-__device__ __forceinline__ uint64_t lanemask_lt64(int lane)
+// 4-bit mask of the tile's wave blocks an entry's reach box E meets: wave w owns the pixels
+// [x0 + 8 (w & 1), +7] x [y0 + 8 (w >> 1), +7].  An entry whose box misses a block fails the
+// cutoff test in every pixel of it, so skipping it there is exact.
+__device__ __forceinline__ uint32_t wave_cover(const float4& E, float x0, float y0)
 {
-    return lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    const bool xa = E.y >= x0 && E.x <= x0 + 7.0f;
+    const bool xb = E.y >= x0 + 8.0f && E.x <= x0 + 15.0f;
+    const bool ya = E.w >= y0 && E.z <= y0 + 7.0f;
+    const bool yb = E.w >= y0 + 8.0f && E.z <= y0 + 15.0f;
+    return (xa && ya ? 1u : 0u) | (xb && ya ? 2u : 0u) | (xa && yb ? 4u : 0u) | (xb && yb ? 8u : 0u);
 }
 
-// Compacts the batch slots [0, cnt) whose box overlaps the wave's pixel rectangle (and, for the
-// backward, whose list index is below the wave's contributor bound) into list[0, n); returns n.
+// Compacts the batch slots [0, cnt) whose reach box overlaps the wave's 8 x 8 pixel block at
+// (wx0, wy0) (and pass `keep`) into list[0, n); returns n.  An entry whose box misses the block
+// fails the cutoff test in every pixel of it, so skipping it is exact.
 template <typename Keep>
-__device__ __forceinline__ int wave_compact(const float4* sE, int cnt, float wx0, float wx1, float wy0, float wy1,
-                                            int lane, uint16_t* list, Keep keep)
+__device__ __forceinline__ int wave_compact(const float4* sE, int cnt, float wx0, float wy0, int lane, uint8_t* list,
+                                            Keep keep)
 {
     int n = 0;
     for (int r = 0; r < cnt; r += 64) {
@@ -64,41 +77,49 @@ __device__ __forceinline__ int wave_compact(const float4* sE, int cnt, float wx0
         bool ov = false;
         if (e < cnt && keep(e)) {
             const float4 E = sE[e];
-            ov = E.y >= wx0 && E.x <= wx1 && E.w >= wy0 && E.z <= wy1;
+            ov = E.y >= wx0 && E.x <= wx0 + 7.0f && E.w >= wy0 && E.z <= wy0 + 7.0f;
         }
         const uint64_t m = __ballot(ov);
-        if (ov) list[n + __popcll(m & lanemask_lt64(lane))] = (uint16_t)e;
+        if (ov) list[n + __popcll(m & ((1ull << lane) - 1ull))] = (uint8_t)e;
         n += __popcll(m);
     }
     return n;
 }
 
-
-// Pixel ownership.  kPix = 1: wave w of the tile's 4 owns the 8 x 8 pixel block
-// (8 (w & 1), 8 (w >> 1)) -- a compact block meets fewer reach boxes than a 16 x 4 strip.
-// kPix = 2: lane l owns the vertically adjacent pixels (l % 16, 2 (l / 16) + k) and a wave a
-// 16 x 8 strip.  (wx0, wx1, wy0, wy1) is the wave's pixel rectangle, for culling.
-template <int kPix>
-__device__ __forceinline__ void pixel_map(int tx, int ty, int t, int& px, int& py_base, float& wx0, float& wx1,
-                                          float& wy0, float& wy1)
+// Pixel of lane t of the tile (wave w owns the 8 x 8 block (8 (w & 1), 8 (w >> 1)): a compact
+// block meets fewer reach boxes than a 16 x 4 strip).
+__device__ __forceinline__ void pixel_map(int tx, int ty, int t, int& px, int& py)
 {
     const int lane = t & 63, wave = t >> 6;
-    if (kPix == 1) {
-        const int bx = tx * kTile + 8 * (wave & 1), by = ty * kTile + 8 * (wave >> 1);
-        px = bx + (lane & 7);
-        py_base = by + (lane >> 3);
-        wx0 = (float)bx;
-        wx1 = wx0 + 7.0f;
-        wy0 = (float)by;
-        wy1 = wy0 + 7.0f;
-    } else {
-        px = tx * kTile + (t & (kTile - 1));
-        py_base = ty * kTile + kPix * (t >> 4);
-        wx0 = (float)(tx * kTile);
-        wx1 = wx0 + (float)(kTile - 1);
-        wy0 = (float)(ty * kTile + 4 * kPix * wave);
-        wy1 = wy0 + (float)(4 * kPix - 1);
+    px = tx * kTile + 8 * (wave & 1) + (lane & 7);
+    py = ty * kTile + 8 * (wave >> 1) + (lane >> 3);
+}
+
+// Longest-first (LPT) tile schedule.  Tile work is very uneven -- at C3 2.8k of the 8.2k tiles
+// hold entries and their replay lengths run from 1 to ~700 -- and the hardware hands workgroups
+// to CUs in launch order, so in tile order the longest tiles may start last and the kernel ends
+// on a tail.  Whoever learns a tile's work appends the tile to the list of its work class
+// (work_class: half-octaves; k_bin_emit for the forward's list lengths, the forward for the
+// backward's replay lengths); workgroup b then takes the b-th tile in descending class order.
+// The order changes no result.
+//
+// Tile of workgroup b (every wave computes it, wave-uniform), or -1 - (scheduled tiles) when b is
+// past them.
+__device__ __forceinline__ int scheduled_tile(int b, const uint32_t* counts, const uint32_t* lists, int T)
+{
+    const int lane = threadIdx.x & 63;
+    const uint32_t n = counts[kWorkClasses - 1 - lane];  // lane 0: the heaviest class
+    uint32_t x = n;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
+        if (lane >= o) x += y;
     }
+    const uint32_t total = (uint32_t)__shfl((int)x, 63, 64);
+    if ((uint32_t)b >= total) return -1 - (int)total;
+    const int l = (int)__builtin_ctzll(__ballot(x > (uint32_t)b));
+    const uint32_t first = (uint32_t)__shfl((int)(x - n), l, 64);
+    return (int)lists[(size_t)(kWorkClasses - 1 - l) * T + ((uint32_t)b - first)];
 }
 
 // One pixel's front-to-back state (upstream FORWARD::renderCUDA locals).
@@ -108,40 +129,66 @@ struct FwdPixel {
     bool done;
 };
 
-// kPix pixels per lane (pixel_map).
-template <int kPix>
-__global__ __launch_bounds__(kTilePixels / kPix) void k_render_forward(RenderParams p)
+// Output of the tiles without entries among u = j, j + M, ... (background colour, T = 1, no
+// contributors); tiles with entries are skipped (their own workgroups render them).
+__device__ void render_empty_tiles(const RenderParams& p, int j, int M)
 {
-    constexpr int kThreads = kTilePixels / kPix;
-    constexpr int kWaves = kThreads / 64;
-    __shared__ float4 sA[kThreads];  // x, y, -0.5 conic.x, -0.5 conic.z
-    __shared__ float4 sB[kThreads];  // conic.y, opacity, power cutoff, -
-    __shared__ float4 sC[kThreads];  // r, g, b, f0
-    __shared__ float2 sD[kThreads];  // f1, f2
-    __shared__ float4 sE[kThreads];  // reach box (entry_box)
-    __shared__ uint16_t sL[kWaves][kThreads];  // per-wave culled slot lists
+    const int T = p.gx * p.gy;
+    const size_t HW = (size_t)p.W * p.H;
+    for (int u = j; u < T; u += M) {
+        const uint2 r = p.ranges[u];
+        if (r.x != r.y) continue;
+        int px, py;
+        pixel_map(u % p.gx, u / p.gx, (int)threadIdx.x, px, py);
+        if (!(px < p.W && py < p.H)) continue;
+        const size_t pix = (size_t)py * p.W + px;
+        p.final_T[pix] = 1.0f;
+        p.n_contrib[pix] = 0u;
+        p.out_color[pix] = fma_(1.0f, p.bg[0], 0.0f);
+        p.out_color[HW + pix] = fma_(1.0f, p.bg[1], 0.0f);
+        p.out_color[2 * HW + pix] = fma_(1.0f, p.bg[2], 0.0f);
+        p.out_lang[pix] = 0.0f;
+        p.out_lang[HW + pix] = 0.0f;
+        p.out_lang[2 * HW + pix] = 0.0f;
+    }
+}
 
-    const int tile = blockIdx.x;
+__global__ __launch_bounds__(kTilePixels) void k_render_forward(RenderParams p)
+{
+    constexpr int kThreads = kTilePixels;
+    __shared__ float4 sA[kThreads];  // x, y, -0.5 conic.x, -0.5 conic.z
+    __shared__ float4 sB[kThreads];  // conic.y, opacity, power cutoff, f1
+    __shared__ float4 sC[kThreads];  // r, g, b, f0
+    __shared__ float sF[kThreads];   // f2
+    __shared__ float4 sE[kThreads];  // reach box (entry_box)
+    __shared__ uint8_t sL[kThreads / 64][kThreads];  // per-wave culled slot lists
+    __shared__ uint32_t s_last;
+
+    const int T = p.gx * p.gy;
+    int tile = (int)blockIdx.x;
+    if (p.sched_counts) {
+        tile = scheduled_tile((int)blockIdx.x, p.sched_counts + kCntFwdClass, p.sched_lists, T);
+        if (tile < 0) {  // past the tiles with entries: fill the empty ones, strided
+            const int listed = -1 - tile;
+            render_empty_tiles(p, (int)blockIdx.x - listed, T - listed);
+            return;
+        }
+    }
     const int tx = tile % p.gx, ty = tile / p.gx;
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    int px, py_base;
-    float wx0, wx1, wy0, wy1;
-    pixel_map<kPix>(tx, ty, t, px, py_base, wx0, wx1, wy0, wy1);
-    const float pfx = (float)px;
+    int px, py;
+    pixel_map(tx, ty, t, px, py);
+    const float pfx = (float)px, pfy = (float)py;
+    const float wx0 = (float)(tx * kTile + 8 * (wave & 1)), wy0 = (float)(ty * kTile + 8 * (wave >> 1));
     const uint2 range = p.ranges[tile];
     const uint32_t start = range.x, end = range.y;
     const bool feat = p.include_feature != 0;
+    const bool inside = px < p.W && py < p.H;
+    if (t == 0) s_last = 0;
 
-    FwdPixel q[kPix];
-#pragma unroll
-    for (int k = 0; k < kPix; k++)
-        q[k] = FwdPixel{1.0f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0u, 0u, !(px < p.W && py_base + k < p.H)};
-
+    FwdPixel q{1.0f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0u, 0u, !inside};
     for (uint32_t base = start; base < end; base += kThreads) {
-        bool all_done = true;
-#pragma unroll
-        for (int k = 0; k < kPix; k++) all_done = all_done && q[k].done;
-        if (__syncthreads_count(all_done) == kThreads) break;
+        if (__syncthreads_count(q.done) == kThreads) break;
         const uint32_t idx = base + t;
         if (idx < end) {
             const uint32_t g = p.point_list[idx];
@@ -150,105 +197,82 @@ __global__ __launch_bounds__(kTilePixels / kPix) void k_render_forward(RenderPar
             const float4 c = p.record[3 * (size_t)g + 2];
             const float cut = power_cutoff(b.y);
             sA[t] = make_float4(a.x, a.y, -0.5f * a.z, -0.5f * b.x);
-            sB[t] = make_float4(a.w, b.y, cut, 0.0f);
+            sB[t] = make_float4(a.w, b.y, cut, c.z);
             sC[t] = make_float4(b.z, b.w, c.x, c.y);
-            sD[t] = make_float2(c.z, c.w);
+            sF[t] = c.w;
             sE[t] = entry_box(a.x, a.y, a.z, a.w, b.x, cut);
         }
         __syncthreads();
         const int cnt = (int)min((uint32_t)kThreads, end - base);
-        const int n = wave_compact(sE, cnt, wx0, wx1, wy0, wy1, lane, sL[wave], [](int) { return true; });
+        const int n = wave_compact(sE, cnt, wx0, wy0, lane, sL[wave], [](int) { return true; });
         __syncthreads();  // list visible to the wave's other lanes
         const uint32_t list_base = base - start;  // list index of slot 0
-        for (int i = 0; i < n && !all_done; i++) {
+        for (int i = 0; i < n && !q.done; i++) {
             const int j = sL[wave][i];
             const float4 A = sA[j];
             const float4 B = sB[j];
-            const uint32_t contributor = list_base + (uint32_t)j + 1u;  // upstream's 1-based counter
-            const float dx = A.x - pfx;
-            float pw[kPix], al[kPix];
-            bool ok[kPix];
-            bool any = false;
-#pragma unroll
-            for (int k = 0; k < kPix; k++) {
-                const float dy = A.y - (float)(py_base + k);
-                pw[k] = fma_(A.z * dx, dx, fma_(A.w * dy, dy, -((B.x * dx) * dy)));
-                ok[k] = !q[k].done && !(pw[k] > 0.0f || pw[k] < B.z);
-                any = any || ok[k];
+            const float dx = A.x - pfx, dy = A.y - pfy;
+            const float pw = fma_(A.z * dx, dx, fma_(A.w * dy, dy, -((B.x * dx) * dy)));
+            if (pw > 0.0f || pw < B.z) continue;
+            const float al = fminf(0.99f, B.y * expf_exact(pw));
+            if (al < 1.0f / 255.0f) continue;
+            const float test_T = q.T * (1.0f - al);
+            if (test_T < 0.0001f) {
+                q.done = true;
+                continue;
             }
-            if (!any) continue;
-            any = false;
-#pragma unroll
-            for (int k = 0; k < kPix; k++) {
-                al[k] = fminf(0.99f, B.y * expf_exact(pw[k]));
-                ok[k] = ok[k] && !(al[k] < 1.0f / 255.0f);
-                const float test_T = q[k].T * (1.0f - al[k]);
-                if (ok[k] && test_T < 0.0001f) {
-                    q[k].done = true;
-                    ok[k] = false;
-                }
-                pw[k] = test_T;  // reuse: the candidate transmittance
-                any = any || ok[k];
+            const float4 Cc = sC[j];
+            const float w = al * q.T;
+            q.C0 = fma_(Cc.x, w, q.C0);
+            q.C1 = fma_(Cc.y, w, q.C1);
+            q.C2 = fma_(Cc.z, w, q.C2);
+            if (feat) {
+                q.F0 = fma_(Cc.w, w, q.F0);
+                q.F1 = fma_(B.w, w, q.F1);
+                q.F2 = fma_(sF[j], w, q.F2);
             }
-            if (any) {
-                const float4 Cc = sC[j];
-                const float2 D = sD[j];
-#pragma unroll
-                for (int k = 0; k < kPix; k++) {
-                    if (!ok[k]) continue;
-                    const float w = al[k] * q[k].T;
-                    q[k].C0 = fma_(Cc.x, w, q[k].C0);
-                    q[k].C1 = fma_(Cc.y, w, q[k].C1);
-                    q[k].C2 = fma_(Cc.z, w, q[k].C2);
-                    if (feat) {
-                        q[k].F0 = fma_(Cc.w, w, q[k].F0);
-                        q[k].F1 = fma_(D.x, w, q[k].F1);
-                        q[k].F2 = fma_(D.y, w, q[k].F2);
-                    }
-                    q[k].T = pw[k];
-                    q[k].last = contributor;
-                }
-            }
-            all_done = true;
-#pragma unroll
-            for (int k = 0; k < kPix; k++) all_done = all_done && q[k].done;
+            q.T = test_T;
+            q.last = list_base + (uint32_t)j + 1u;  // upstream's 1-based contributor counter
         }
     }
-    const size_t HW = (size_t)p.W * p.H;
+    // the tile's replay length, for the backward's launch order
+    uint32_t wl = q.last;
 #pragma unroll
-    for (int k = 0; k < kPix; k++) {
-        const int py = py_base + k;
-        if (!(px < p.W && py < p.H)) continue;
-        const size_t pix = (size_t)py * p.W + px;
-        p.final_T[pix] = q[k].T;
-        p.n_contrib[pix] = q[k].last;
-        p.out_color[pix] = fma_(q[k].T, p.bg[0], q[k].C0);
-        p.out_color[HW + pix] = fma_(q[k].T, p.bg[1], q[k].C1);
-        p.out_color[2 * HW + pix] = fma_(q[k].T, p.bg[2], q[k].C2);
-        p.out_lang[pix] = q[k].F0;
-        p.out_lang[HW + pix] = q[k].F1;
-        p.out_lang[2 * HW + pix] = q[k].F2;
-    }
+    for (int o = 32; o > 0; o >>= 1) wl = max(wl, (uint32_t)__shfl_xor((int)wl, o, 64));
+    __syncthreads();
+    if (lane == 0) atomicMax(&s_last, wl);
+    __syncthreads();
+    if (t == 0 && p.sched_counts && s_last > 0)
+        schedule_tile(p.sched_counts + kCntBwdClass, p.sched_lists + (size_t)kWorkClasses * T, T, tile, s_last);
+    if (!inside) return;
+    const size_t HW = (size_t)p.W * p.H;
+    const size_t pix = (size_t)py * p.W + px;
+    p.final_T[pix] = q.T;
+    p.n_contrib[pix] = q.last;
+    p.out_color[pix] = fma_(q.T, p.bg[0], q.C0);
+    p.out_color[HW + pix] = fma_(q.T, p.bg[1], q.C1);
+    p.out_color[2 * HW + pix] = fma_(q.T, p.bg[2], q.C2);
+    p.out_lang[pix] = q.F0;
+    p.out_lang[HW + pix] = q.F1;
+    p.out_lang[2 * HW + pix] = q.F2;
 }
 
-// LSR_FWD_PIXELS=1|2 selects the forward variant (measurement aid; default 1)
-static int fwd_pixels_per_lane()
+// LSR_ORDER=0 launches the tiles in tile order (measurement aid)
+static bool scheduled()
 {
-    static int v = [] {
-        const char* e = getenv("LSR_FWD_PIXELS");
-        return (e && e[0] == '2') ? 2 : 1;
+    static const bool v = [] {
+        const char* e = getenv("LSR_ORDER");
+        return !(e && e[0] == '0');
     }();
     return v;
 }
 
-hipError_t launch_render_forward(const RenderParams& p, int tiles, hipStream_t s)
+hipError_t launch_render_forward(const RenderParams& pin, int tiles, hipStream_t s)
 {
     if (tiles == 0) return hipSuccess;
-    const int pix = fwd_pixels_per_lane();
-    if (pix == 2)
-        hipLaunchKernelGGL(k_render_forward<2>, dim3(tiles), dim3(kTilePixels / 2), 0, s, p);
-    else
-        hipLaunchKernelGGL(k_render_forward<1>, dim3(tiles), dim3(kTilePixels), 0, s, p);
+    RenderParams p = pin;
+    if (!scheduled()) p.sched_counts = p.sched_lists = nullptr;
+    hipLaunchKernelGGL(k_render_forward, dim3(tiles), dim3(kTilePixels), 0, s, p);
     return hipGetLastError();
 }
 
@@ -409,58 +433,57 @@ __device__ __forceinline__ void bwd_pixel_blend(BwdPixel& q, float G, float alph
 // an alpha hit, [3] lanes hit, [8 + c] histogram of lanes hit (c = 0..64).  Off by default.
 __device__ unsigned long long g_render_stats[8 + 65];
 
-template <int kPix, bool kStats = false>
-__global__ __launch_bounds__(kTilePixels / kPix) void k_render_backward(RenderParams p)
+template <bool kStats>
+__global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
 {
-    constexpr int kThreads = kTilePixels / kPix;
+    constexpr int kThreads = kTilePixels;
     __shared__ uint32_t s_stat[kStats ? 8 + 65 : 1];
-    __shared__ float4 sA[kThreads];  // x, y, -0.5 conic.x, -0.5 conic.z
-    __shared__ float4 sB[kThreads];  // conic.y, opacity, power cutoff, -
-    __shared__ float4 sC[kThreads];  // r, g, b, f0
-    __shared__ float2 sD[kThreads];  // f1, f2
+    __shared__ float4 sA[kThreads];      // x, y, -0.5 conic.x, -0.5 conic.z
+    __shared__ float4 sB[kThreads];      // conic.y, opacity, power cutoff, f1
+    __shared__ float4 sC[kThreads];      // r, g, b, f0
+    __shared__ float sF[kThreads];       // f2
     __shared__ uint32_t sId[kThreads];
     __shared__ float sG[kThreads * 12];  // per-entry gradient sums of the tile (12 floats)
-    __shared__ float4 sE[kThreads];      // reach box (entry_box)
-    __shared__ uint16_t sL[kThreads / 64][kThreads];  // per-wave culled slot lists
-    __shared__ uint32_t s_max;
+    __shared__ uint8_t sM[kThreads];     // wave_cover mask (& the waves' contributor bounds)
+    __shared__ uint32_t s_wmax[kThreads / 64];
 
-    const int tile = blockIdx.x;
+    int tile = (int)blockIdx.x;
+    if (p.sched_counts) {  // tiles without contributors are not scheduled: nothing to do
+        const int T = p.gx * p.gy;
+        tile = scheduled_tile((int)blockIdx.x, p.sched_counts + kCntBwdClass,
+                              p.sched_lists + (size_t)kWorkClasses * T, T);
+        if (tile < 0) return;
+    }
     const int tx = tile % p.gx, ty = tile / p.gx;
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    int px, py_base;
-    float wx0, wx1, wy0, wy1;
-    pixel_map<kPix>(tx, ty, t, px, py_base, wx0, wx1, wy0, wy1);
-    const float pfx = (float)px;
+    int px, py;
+    pixel_map(tx, ty, t, px, py);
+    const float pfx = (float)px, pfy = (float)py;
+    const float tx0 = (float)(tx * kTile), ty0 = (float)(ty * kTile);
     const size_t HW = (size_t)p.W * p.H;
     const uint32_t start = p.ranges[tile].x;
     const bool feat = p.include_feature != 0;
     const float ddelx_dx = 0.5f * (float)p.W, ddely_dy = 0.5f * (float)p.H;
 
-    BwdPixel q[kPix];
-    uint32_t wmax = 0;
-#pragma unroll
-    for (int k = 0; k < kPix; k++) {
-        const int py = py_base + k;
-        bwd_pixel_init(q[k], p, px < p.W && py < p.H, (size_t)py * p.W + px, HW, feat);
-        wmax = max(wmax, q[k].last);
-    }
+    BwdPixel q;
+    bwd_pixel_init(q, p, px < p.W && py < p.H, (size_t)py * p.W + px, HW, feat);
+    uint32_t wmax = q.last;
 
     if (kStats)
         for (int i = t; i < 8 + 65; i += kThreads) s_stat[i] = 0;
-    // entries at list index >= max over the tile of n_contrib can contribute to no pixel
-    if (t == 0) s_max = 0;
-    __syncthreads();
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) wmax = max(wmax, (uint32_t)__shfl_xor((int)wmax, o, 64));
-    if (lane == 0) atomicMax(&s_max, wmax);
+    if (lane == 0) s_wmax[wave] = wmax;  // entries at list index >= this touch no pixel of the wave
     __syncthreads();
-    const int maxl = (int)s_max;
-    const int wave_max = (int)wmax;  // entries at index >= this touch no pixel of this wave
+    const uint32_t w0 = s_wmax[0], w1 = s_wmax[1], w2 = s_wmax[2], w3 = s_wmax[3];
+    // entries at list index >= max over the tile of n_contrib can contribute to no pixel
+    const int maxl = (int)max(max(w0, w1), max(w2, w3));
     const int vidx = scatter_index(lane);
 
     for (int done_cnt = 0; done_cnt < maxl; done_cnt += kThreads) {
         __syncthreads();
         const int kload = maxl - 1 - (done_cnt + t);
+        uint32_t cover = 0;
         if (kload >= 0) {
             const uint32_t g = p.point_list[start + (uint32_t)kload];
             const float4 a = p.record[3 * (size_t)g];
@@ -468,60 +491,50 @@ __global__ __launch_bounds__(kTilePixels / kPix) void k_render_backward(RenderPa
             const float4 c = p.record[3 * (size_t)g + 2];
             const float cut = power_cutoff(b.y);
             sA[t] = make_float4(a.x, a.y, -0.5f * a.z, -0.5f * b.x);
-            sB[t] = make_float4(a.w, b.y, cut, 0.0f);
+            sB[t] = make_float4(a.w, b.y, cut, c.z);
             sC[t] = make_float4(b.z, b.w, c.x, c.y);
-            sD[t] = make_float2(c.z, c.w);
-            sE[t] = entry_box(a.x, a.y, a.z, a.w, b.x, cut);
+            sF[t] = c.w;
             sId[t] = g;
+            const uint32_t k = (uint32_t)kload;
+            const uint32_t live = (k < w0 ? 1u : 0u) | (k < w1 ? 2u : 0u) | (k < w2 ? 4u : 0u) | (k < w3 ? 8u : 0u);
+            cover = wave_cover(entry_box(a.x, a.y, a.z, a.w, b.x, cut), tx0, ty0) & live;
         }
+        sM[t] = (uint8_t)cover;
         for (int i = t; i < kThreads * 12; i += kThreads) sG[i] = 0.f;
         __syncthreads();
         const int cnt = min(kThreads, maxl - done_cnt);
-        // entries at list index >= wave_max touch no pixel of this wave
-        const int n = wave_compact(sE, cnt, wx0, wx1, wy0, wy1, lane, sL[wave],
-                                   [&](int e) { return maxl - 1 - (done_cnt + e) < wave_max; });
-        __syncthreads();  // list visible to the wave's other lanes
-        if (kStats && lane == 0) atomicAdd(&s_stat[0], (uint32_t)n);
-        for (int i = 0; i < n; i++) {
-            const int j = sL[wave][i];
-            const float4 A = sA[j];
-            const float4 B = sB[j];
-            const int kk = maxl - 1 - (done_cnt + j);  // list index of this entry
-            const float dx = A.x - pfx;
-            float pw[kPix];
-            bool h[kPix];
-            bool any = false;
-#pragma unroll
-            for (int k = 0; k < kPix; k++) {
-                const float dy = A.y - (float)(py_base + k);
-                pw[k] = fma_(A.z * dx, dx, fma_(A.w * dy, dy, -((B.x * dx) * dy)));
-                h[k] = kk < (int)q[k].last && pw[k] <= 0.0f && pw[k] >= B.z;
-                any = any || h[k];
-            }
-            if (__ballot(any) != 0ull) {  // wave-uniform skip otherwise
+        // the wave walks the set bits of a ballot over the cover masks (no list, no barrier)
+        for (int r = 0; r < cnt; r += 64) {
+            const int e = r + lane;
+            uint64_t m = __ballot(e < cnt && ((sM[e] >> wave) & 1u));
+            if (kStats && lane == 0) atomicAdd(&s_stat[0], (uint32_t)__popcll(m));
+            while (m != 0ull) {
+                const int j = r + (int)__builtin_ctzll(m);
+                m &= m - 1ull;
+                const float4 A = sA[j];
+                const float4 B = sB[j];
+                const int kk = maxl - 1 - (done_cnt + j);  // list index of this entry
+                const float dx = A.x - pfx, dy = A.y - pfy;
+                const float pw = fma_(A.z * dx, dx, fma_(A.w * dy, dy, -((B.x * dx) * dy)));
+                bool h = kk < (int)q.last && pw <= 0.0f && pw >= B.z;
+                if (__ballot(h) == 0ull) continue;  // wave-uniform skip
                 float v[12];
 #pragma unroll
                 for (int c = 0; c < 12; c++) v[c] = 0.f;
-                float G[kPix], al[kPix];
-                bool hit = false;
-#pragma unroll
-                for (int k = 0; k < kPix; k++) {
-                    // hardware exp (a few ulp): gradients need 1e-4.  Only the 1/255 skip decision
-                    // must equal the forward's, so alphas within 1e-6 of it use the exact exp.
-                    G[k] = __expf(pw[k]);
-                    al[k] = fminf(0.99f, B.y * G[k]);
-                    const bool near = fabsf(al[k] - 1.0f / 255.0f) < 1e-6f;
-                    if (__ballot(near) != 0ull) {  // wave-uniform: keeps the exact exp off the hot path
-                        if (near) {
-                            G[k] = expf_exact(pw[k]);
-                            al[k] = fminf(0.99f, B.y * G[k]);
-                        }
+                // hardware exp (a few ulp): gradients need 1e-4.  Only the 1/255 skip decision
+                // must equal the forward's, so alphas within 1e-6 of it use the exact exp.
+                float G = __expf(pw);
+                float al = fminf(0.99f, B.y * G);
+                const bool near = fabsf(al - 1.0f / 255.0f) < 1e-6f;
+                if (__ballot(near) != 0ull) {  // wave-uniform: keeps the exact exp off the hot path
+                    if (near) {
+                        G = expf_exact(pw);
+                        al = fminf(0.99f, B.y * G);
                     }
-                    h[k] = h[k] && al[k] >= 1.0f / 255.0f;
-                    hit = hit || h[k];
                 }
+                h = h && al >= 1.0f / 255.0f;
                 if (kStats) {
-                    const int nh = __popcll(__ballot(hit));
+                    const int nh = __popcll(__ballot(h));
                     if (lane == 0) {
                         atomicAdd(&s_stat[1], 1u);
                         if (nh) {
@@ -531,15 +544,11 @@ __global__ __launch_bounds__(kTilePixels / kPix) void k_render_backward(RenderPa
                         atomicAdd(&s_stat[8 + nh], 1u);
                     }
                 }
-                if (hit) {
+                if (h) {
                     const float4 Cc = sC[j];
-                    const float2 D = sD[j];
-                    const float cx = -2.0f * A.z, cz = -2.0f * A.w;
-#pragma unroll
-                    for (int k = 0; k < kPix; k++)
-                        if (h[k])
-                            bwd_pixel_blend(q[k], G[k], al[k], dx, A.y - (float)(py_base + k), B, cx, cz, Cc, D,
-                                            feat, ddelx_dx, ddely_dy, v);
+                    const float2 D = make_float2(B.w, sF[j]);
+                    bwd_pixel_blend(q, G, al, dx, dy, B, -2.0f * A.z, -2.0f * A.w, Cc, D, feat, ddelx_dx, ddely_dy,
+                                    v);
                 }
                 const float tot = wave_reduce_scatter12(v, lane);
                 if ((lane & 3) == 0 && vidx < 12) atomicAdd(&sG[j * 12 + vidx], tot);
@@ -581,26 +590,15 @@ hipError_t render_stats_read(unsigned long long* out, int n)
     return hipMemcpyToSymbol(HIP_SYMBOL(g_render_stats), zeros, sizeof(zeros), 0, hipMemcpyHostToDevice);
 }
 
-// LSR_BWD_PIXELS=1|2 selects the backward variant (measurement aid; default 1: 0.52 vs 0.58 ms at
-// C3 -- with ~2300 busy tiles the chip is short of waves, so more waves per tile beat more ILP)
-static int bwd_pixels_per_lane()
-{
-    static int v = [] {
-        const char* e = getenv("LSR_BWD_PIXELS");
-        return (e && e[0] == '2') ? 2 : 1;
-    }();
-    return v;
-}
-
-hipError_t launch_render_backward(const RenderParams& p, int tiles, hipStream_t s)
+hipError_t launch_render_backward(const RenderParams& pin, int tiles, hipStream_t s)
 {
     if (tiles == 0) return hipSuccess;
+    RenderParams p = pin;
+    if (!scheduled()) p.sched_counts = p.sched_lists = nullptr;
     if (render_stats_on())
-        hipLaunchKernelGGL((k_render_backward<1, true>), dim3(tiles), dim3(kTilePixels), 0, s, p);
-    else if (bwd_pixels_per_lane() == 1)
-        hipLaunchKernelGGL(k_render_backward<1>, dim3(tiles), dim3(kTilePixels), 0, s, p);
+        hipLaunchKernelGGL(k_render_backward<true>, dim3(tiles), dim3(kTilePixels), 0, s, p);
     else
-        hipLaunchKernelGGL(k_render_backward<2>, dim3(tiles), dim3(kTilePixels / 2), 0, s, p);
+        hipLaunchKernelGGL(k_render_backward<false>, dim3(tiles), dim3(kTilePixels), 0, s, p);
     return hipGetLastError();
 }
 

@@ -87,6 +87,7 @@ class _RasterizeGaussians(torch.autograd.Function):
         ctx.save_for_backward(m3, shs_, cp, ln if ln is not None else torch.empty(0), sc, ro, cv, radii, geom,
                               binning, image)
         ctx.mark_non_differentiable(radii)
+        ctx.set_materialize_grads(False)  # an output off the loss path arrives as None (= zeros)
         return color, language_feature, radii
 
     @staticmethod
@@ -174,6 +175,7 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
         ctx.save_for_backward(m3, dc, rest if rest is not None else empty, ln if ln is not None else empty, op, sc,
                               ro, radii, geom, binning, image)
         ctx.mark_non_differentiable(radii)
+        ctx.set_materialize_grads(False)  # an output off the loss path arrives as None (= zeros)
         return color, language_feature, radii
 
     @staticmethod

@@ -57,13 +57,28 @@ def eval_sh(deg, sh, dirs):
     return result
 
 
+_ZEROS: dict = {}
+
+
+def _screenspace_points(xyz: torch.Tensor) -> torch.Tensor:
+    """viewspace_points of gaussian_renderer/__init__.py:24-28: a zero (P,3) tensor that requires
+    grad and whose .grad receives dL/dmeans2D after backward.
+
+    The reference builds `zeros_like(xyz, requires_grad=True) + 0` and retain_grad()s it: per step
+    a fill, an add, and a clone of the incoming gradient.  Here it is a fresh leaf over a cached
+    zero buffer.  It has the same values and the same .grad, and autograd hands the rasterizer's
+    gradient to .grad without a copy."""
+    key = (xyz.device, xyz.dtype, int(xyz.shape[0]))
+    z = _ZEROS.get(key)
+    if z is None:
+        _ZEROS.clear()
+        z = torch.zeros((int(xyz.shape[0]), 3), dtype=xyz.dtype, device=xyz.device)
+        _ZEROS[key] = z
+    return z.detach().requires_grad_(True)
+
+
 def render(viewpoint_camera, pc, pipe, bg_color: torch.Tensor, opt, scaling_modifier=1.0, override_color=None):
-    screenspace_points = torch.zeros_like(pc.get_xyz, dtype=pc.get_xyz.dtype, requires_grad=True,
-                                          device=pc.get_xyz.device) + 0
-    try:
-        screenspace_points.retain_grad()
-    except Exception:  # noqa: BLE001 -- same tolerance as the reference
-        pass
+    screenspace_points = _screenspace_points(pc.get_xyz)
 
     tanfovx = math.tan(viewpoint_camera.FoVx * 0.5)
     tanfovy = math.tan(viewpoint_camera.FoVy * 0.5)
