@@ -440,4 +440,5 @@ def debug_render_stats():
     arr = (ctypes.c_uint64 * 73)()
     _check(load().lsr_debug_render_stats(arr, 73), "lsr_debug_render_stats")
     v = list(arr)
-    return {"entries": v[0], "power_hit": v[1], "alpha_hit": v[2], "lanes_hit": v[3], "hist": v[8:8 + 65]}
+    return {"entries": v[0], "power_hit": v[1], "alpha_hit": v[2], "lanes_hit": v[3], "barrier_slots": v[4],
+            "batches": v[6], "hist": v[8:8 + 65]}

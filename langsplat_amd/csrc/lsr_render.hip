@@ -438,6 +438,7 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
 {
     constexpr int kThreads = kTilePixels;
     __shared__ uint32_t s_stat[kStats ? 8 + 65 : 1];
+    __shared__ uint32_t s_bmax;  // kStats: the batch's largest per-wave entry count
     __shared__ float4 sA[kThreads];      // x, y, -0.5 conic.x, -0.5 conic.z
     __shared__ float4 sB[kThreads];      // conic.y, opacity, power cutoff, f1
     __shared__ float4 sC[kThreads];      // r, g, b, f0
@@ -469,8 +470,10 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
     bwd_pixel_init(q, p, px < p.W && py < p.H, (size_t)py * p.W + px, HW, feat);
     uint32_t wmax = q.last;
 
-    if (kStats)
+    if (kStats) {
         for (int i = t; i < 8 + 65; i += kThreads) s_stat[i] = 0;
+        if (t == 0) s_bmax = 0;
+    }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) wmax = max(wmax, (uint32_t)__shfl_xor((int)wmax, o, 64));
     if (lane == 0) s_wmax[wave] = wmax;  // entries at list index >= this touch no pixel of the wave
@@ -504,9 +507,11 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
         __syncthreads();
         const int cnt = min(kThreads, maxl - done_cnt);
         // the wave walks the set bits of a ballot over the cover masks (no list, no barrier)
+        uint32_t nw = 0;  // kStats
         for (int r = 0; r < cnt; r += 64) {
             const int e = r + lane;
             uint64_t m = __ballot(e < cnt && ((sM[e] >> wave) & 1u));
+            if (kStats) nw += (uint32_t)__popcll(m);
             if (kStats && lane == 0) atomicAdd(&s_stat[0], (uint32_t)__popcll(m));
             while (m != 0ull) {
                 const int j = r + (int)__builtin_ctzll(m);
@@ -554,7 +559,13 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
                 if ((lane & 3) == 0 && vidx < 12) atomicAdd(&sG[j * 12 + vidx], tot);
             }
         }
+        if (kStats && lane == 0) atomicMax(&s_bmax, nw);
         __syncthreads();
+        if (kStats && t == 0) {
+            s_stat[4] += 4u * s_bmax;  // wave-entry slots the batch's barrier holds (4 x the busiest wave)
+            s_stat[6] += 1u;           // batches
+            s_bmax = 0u;
+        }
         // flush: 16 lanes per entry (12 active) -> one 48-byte atomic row per (tile, Gaussian)
         for (int slot = t; slot < cnt * 16; slot += kThreads) {
             const int e = slot >> 4, c = slot & 15;

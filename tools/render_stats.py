@@ -43,6 +43,8 @@ def main():
     e, ph, ah, lh = s["entries"], s["power_hit"], s["alpha_hit"], s["lanes_hit"]
     print(f"{cfg}: R={nr} wave-entries={e} power-hit={ph} ({ph / max(e, 1):.3f}) alpha-hit={ah} "
           f"({ah / max(e, 1):.3f}) lanes/alpha-hit={lh / max(ah, 1):.2f} blends={lh}")
+    print(f"  batches={s['batches']} wave-entry slots held by batch barriers (4 x busiest wave)="
+          f"{s['barrier_slots']} -> wave utilisation {e / max(s['barrier_slots'], 1):.3f}")
     hist = s["hist"]
     tot = sum(hist)
     acc = 0
