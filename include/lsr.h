@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define LSR_ABI_VERSION 2
+#define LSR_ABI_VERSION 3
 
 enum lsr_status {
     LSR_OK = 0,
@@ -113,6 +113,8 @@ typedef struct lsr_forward_args {
     const float* shs_rest;           /* NULL, or P x (M-1) x 3 (_features_rest) with shs = P x 1 x 3
                                         (_features_dc): the SH rows without torch.cat
                                         (scene/gaussian_model.py:146-150) */
+    uint8_t* visible;                /* NULL, or P bytes: radii > 0 (render()'s visibility_filter,
+                                        gaussian_renderer/__init__.py:99), written by preprocess */
 } lsr_forward_args;
 
 /* Inputs/outputs of _C.rasterize_gaussians_backward.  Every non-NULL output is fully written

@@ -21,7 +21,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "liblsr.so")
 
 LSR_BUF_GEOM, LSR_BUF_BINNING, LSR_BUF_IMAGE, LSR_BUF_BACKWARD = 0, 1, 2, 3
-ABI_VERSION = 2
+ABI_VERSION = 3
 # lsr_raw_flags (include/lsr.h): inputs are GaussianModel's raw parameters
 RAW_OPACITY, RAW_SCALES, RAW_ROTATIONS, RAW_LANGUAGE = 1, 2, 4, 8
 _vp = ctypes.c_void_p
@@ -50,7 +50,7 @@ class LsrForwardArgs(ctypes.Structure):
     _fields_ = [("P", ctypes.c_int32), ("M", ctypes.c_int32)] + [
         (n, _vp) for n in ("means3D", "shs", "colors_precomp", "language_feature", "opacities", "scales",
                            "rotations", "cov3D_precomp", "out_color", "out_language_feature", "radii")
-    ] + [("raw", ctypes.c_int32), ("reserved", ctypes.c_int32), ("shs_rest", _vp)]
+    ] + [("raw", ctypes.c_int32), ("reserved", ctypes.c_int32), ("shs_rest", _vp), ("visible", _vp)]
 
 
 class LsrBackwardArgs(ctypes.Structure):
@@ -273,11 +273,12 @@ def _f32c_cached(src: torch.Tensor) -> torch.Tensor:
 
 
 def rasterize_gaussians(rs, means3D, shs, colors_precomp, language_feature, opacities, scales, rotations,
-                        cov3D_precomp, raw=0, shs_rest=None):
+                        cov3D_precomp, raw=0, shs_rest=None, visible=None):
     """Native forward: returns (num_rendered, color, language_feature_image, radii, geom, binning, image).
 
     raw / shs_rest: the fused-activation form (include/lsr.h lsr_raw_flags); shs is then
-    features_dc (P,1,3) and shs_rest features_rest (P,M-1,3)."""
+    features_dc (P,1,3) and shs_rest features_rest (P,M-1,3).  visible: optional (P,) bool tensor
+    that receives radii > 0."""
     lib = load()
     device = means3D.device
     P = int(means3D.shape[0])
@@ -305,6 +306,10 @@ def rasterize_gaussians(rs, means3D, shs, colors_precomp, language_feature, opac
     a.out_color = _ptr(color)
     a.out_language_feature = _ptr(lang)
     a.radii = _ptr(radii)
+    if visible is not None:
+        if visible.dtype != torch.bool or visible.numel() != P or not visible.is_contiguous():
+            raise ValueError("visible must be a contiguous (P,) bool tensor")
+        a.visible = _ptr(visible)
     alloc = _Allocator(device)
     nr = ctypes.c_int64(0)
     with _on_device(device), alloc:

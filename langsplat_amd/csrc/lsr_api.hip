@@ -220,8 +220,8 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
     char* geom = static_cast<char*>(alloc(user, LSR_BUF_GEOM, L.geom_bytes));
     char* image = static_cast<char*>(alloc(user, LSR_BUF_IMAGE, L.image_bytes));
     if (!geom || !image) return fail(LSR_ERR_ALLOC, "lsr_forward: geometry/image buffer allocation failed");
+    // no memset: k_publish_counters initialises every counter word before anything reads it
     uint32_t* counters = reinterpret_cast<uint32_t*>(image + L.counters);
-    LSR_TRY(hipMemsetAsync(counters, 0, 4 * kCntWords, stream), "memset counters");
 
     PreprocessParams pp{};
     pp.P = P;
@@ -250,6 +250,7 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
     pp.proj = s->projmatrix;
     pp.campos = s->campos;
     pp.radii = a->radii;
+    pp.visible = a->visible;
     pp.depth_key = reinterpret_cast<uint32_t*>(geom + L.depth_key);
     pp.tiles = reinterpret_cast<uint32_t*>(geom + L.tiles_touched);
     pp.rect = reinterpret_cast<uint32_t*>(geom + L.rect);
@@ -278,7 +279,6 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
     LSR_TRY(wait_counters(t_hc, seq, stream), "wait counters");
     uint32_t host_cnt[8];
     for (int i = 0; i < 8; i++) host_cnt[i] = t_hc->vals[i];
-    if (host_cnt[kCntScanFault]) return fail(LSR_ERR_HIP, "lsr_forward: scan look-back stalled");
     if (host_cnt[kCntError] && s->prefiltered)
         return fail(LSR_ERR_PREFILTERED, "lsr_forward: prefiltered=True but a Gaussian is outside the frustum");
     const int64_t R = host_cnt[kCntRendered];
@@ -296,6 +296,12 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
     char* binning = static_cast<char*>(alloc(user, LSR_BUF_BINNING, L.binning_bytes));
     if (!binning) return fail(LSR_ERR_ALLOC, "lsr_forward: binning buffer allocation failed");
     LSR_TRY(launch_binning(P, R, L, geom, image, binning, stream, debug), "binning");
+    if (debug) {  // the look-back scans' safety bound (kMaxSpins) flags a stall here
+        uint32_t fault = 0;
+        LSR_TRY(hipMemcpyAsync(&fault, counters + kCntScanFault, 4, hipMemcpyDeviceToHost, stream), "read fault");
+        LSR_TRY(hipStreamSynchronize(stream), "sync");
+        if (fault) return fail(LSR_ERR_HIP, "lsr_forward: scan look-back stalled");
+    }
     RenderParams rp{};
     rp.W = W;
     rp.H = H;

@@ -201,21 +201,30 @@ static hipError_t scan_exclusive(const uint32_t* in, uint32_t* out, int n, uint3
 }
 
 // One workgroup: reduces the preprocess block partials into the counters (R, E, visible depth-key
-// min / max), then publishes counters[0..7] to pinned host memory (system scope) followed by the
+// min / max, the prefiltered error flag: bit 31 of the max key), clears the other counter words
+// (scan fault, the tile schedule's class counts) -- so the counters need no memset before the
+// forward -- then publishes counters[0..7] to pinned host memory (system scope) followed by the
 // sequence number the host spins on.
-__global__ __launch_bounds__(256) void k_publish_counters(int nb, const uint4* __restrict__ partial,
-                                                          uint32_t* __restrict__ counters, uint32_t* host_vals,
-                                                          uint32_t* host_seq, uint32_t seq)
+constexpr int kPublishThreads = 1024;
+
+__global__ __launch_bounds__(kPublishThreads) void k_publish_counters(int nb, const uint4* __restrict__ partial,
+                                                                      uint32_t* __restrict__ counters,
+                                                                      uint32_t* host_vals, uint32_t* host_seq,
+                                                                      uint32_t seq)
 {
-    __shared__ uint32_t red[4][4];
+    constexpr int kWaves = kPublishThreads / 64;
+    __shared__ uint32_t red[4][kWaves];
     uint32_t t = 0, e = 0, kmin = 0xFFFFFFFFu, kmax = 0;
-    for (int b = threadIdx.x; b < nb; b += 256) {
+    for (int b = threadIdx.x; b < nb; b += kPublishThreads) {
         const uint4 v = partial[b];
         t += v.x;
         e += v.y;
         kmin = min(kmin, v.z);
-        kmax = max(kmax, v.w);
+        kmax = max(kmax, v.w);  // the error bit, if set anywhere, survives the max
     }
+    for (int i = threadIdx.x; i < kCntWords; i += kPublishThreads)
+        if (i != kCntRendered && i != kCntSuper && i != kCntKeyMin && i != kCntKeyMax && i != kCntError)
+            counters[i] = 0u;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         t += __shfl_xor(t, o, 64);
@@ -232,7 +241,7 @@ __global__ __launch_bounds__(256) void k_publish_counters(int nb, const uint4* _
     }
     __syncthreads();
     if (threadIdx.x != 0) return;
-    for (int k = 1; k < 4; k++) {
+    for (int k = 1; k < kWaves; k++) {
         red[0][0] += red[0][k];
         red[1][0] += red[1][k];
         red[2][0] = min(red[2][0], red[2][k]);
@@ -241,7 +250,8 @@ __global__ __launch_bounds__(256) void k_publish_counters(int nb, const uint4* _
     counters[kCntRendered] = red[0][0];
     counters[kCntSuper] = red[1][0];
     counters[kCntKeyMin] = red[2][0];
-    counters[kCntKeyMax] = red[3][0];
+    counters[kCntKeyMax] = red[3][0] & 0x7FFFFFFFu;
+    counters[kCntError] = red[3][0] >> 31;
     for (int i = 0; i < 8; i++)
         __hip_atomic_store(&host_vals[i], counters[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(host_seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -250,7 +260,8 @@ __global__ __launch_bounds__(256) void k_publish_counters(int nb, const uint4* _
 hipError_t launch_publish_counters(int nb, const uint4* partial, uint32_t* counters, uint32_t* host_vals,
                                    uint32_t* host_seq, uint32_t seq, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_publish_counters, dim3(1), dim3(256), 0, s, nb, partial, counters, host_vals, host_seq, seq);
+    hipLaunchKernelGGL(k_publish_counters, dim3(1), dim3(kPublishThreads), 0, s, nb, partial, counters, host_vals,
+                       host_seq, seq);
     return hipGetLastError();
 }
 

@@ -142,6 +142,7 @@ struct PreprocessParams {
     uint4* partial;   // per block {tile instances, super-tile entries, min / max visible depth key}
     int raw;                  // lsr_raw_flags
     const float* shs_rest;    // split SH rows (shs = dc only) or null
+    uint8_t* visible;         // optional radii > 0 bytes
 };
 
 struct PreprocessBwdParams {

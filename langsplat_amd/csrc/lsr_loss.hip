@@ -5,7 +5,8 @@
 // which torch runs as 5 forward + ~6 backward elementwise/reduction kernels over the 3 x H x W
 // images.  Here it is one streaming pass each way (HBM-bound: the forward reads pred + gt +
 // mask, the backward reads them again and writes grad_pred):
-//   k_masked_l1_forward  per-thread partial sums over 4-pixel quads, block sums in double, and
+//   k_masked_l1_forward  per-thread partial sums over 4-pixel quads (one 512-thread block per CU),
+//                        block sums in double, and
 //                        the last block to finish adds the block sums in a fixed order
 //                        (deterministic, no second launch, no fences);
 //   k_masked_l1_backward g * (1/N) * sign(pred*m - gt*m) * m, the operation order of autograd's
@@ -17,6 +18,10 @@ namespace lsr {
 
 constexpr int kLossThreads = 256;
 constexpr int kLossMaxBlocks = 1024;
+// the forward's blocks each take a ticket on ONE word (which saturates near 90 adds per us), so it
+// runs on one 512-thread block per CU
+constexpr int kFwdThreads = 512;
+constexpr int kFwdBlocks = 256;
 
 // mask value of pixel p (bool bytes or fp32)
 __device__ __forceinline__ float mask_at(const void* mask, int is_float, int64_t p)
@@ -59,6 +64,7 @@ __device__ __forceinline__ void load_mask(const void* mask, int is_float, int64_
     }
 }
 
+template <int kThreads>
 __device__ __forceinline__ double block_sum_double(double v, double* wsum)
 {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -68,7 +74,7 @@ __device__ __forceinline__ double block_sum_double(double v, double* wsum)
     __syncthreads();
     double t = 0.0;
     if (threadIdx.x == 0)
-        for (int w = 0; w < kLossThreads / 64; w++) t += wsum[w];
+        for (int w = 0; w < kThreads / 64; w++) t += wsum[w];
     return t;  // valid in thread 0
 }
 
@@ -77,18 +83,18 @@ __device__ __forceinline__ double block_sum_double(double v, double* wsum)
 // order.  No __threadfence (on gfx950 each one is an L2 writeback) and no scratch reset between
 // launches: the host passes a fresh nonzero epoch per launch.
 template <int V>
-__global__ __launch_bounds__(kLossThreads) void k_masked_l1_forward(int C, int64_t HW, const float* __restrict__ pred,
+__global__ __launch_bounds__(kFwdThreads) void k_masked_l1_forward(int C, int64_t HW, const float* __restrict__ pred,
                                                                     const float* __restrict__ gt, const void* mask,
                                                                     int mask_is_float, float* __restrict__ loss,
                                                                     uint32_t* __restrict__ ticket,
                                                                     uint64_t* __restrict__ partial, uint32_t epoch)
 {
-    __shared__ double wsum[kLossThreads / 64];
+    __shared__ double wsum[kFwdThreads / 64];
     __shared__ bool s_last;
     const int64_t groups = HW / V;
     float acc = 0.0f;
-    for (int64_t gi = (int64_t)blockIdx.x * kLossThreads + threadIdx.x; gi < groups;
-         gi += (int64_t)gridDim.x * kLossThreads) {
+    for (int64_t gi = (int64_t)blockIdx.x * kFwdThreads + threadIdx.x; gi < groups;
+         gi += (int64_t)gridDim.x * kFwdThreads) {
         const int64_t p = gi * V;
         float m[V];
         load_mask<V>(mask, mask_is_float, p, m);
@@ -100,7 +106,7 @@ __global__ __launch_bounds__(kLossThreads) void k_masked_l1_forward(int C, int64
             for (int k = 0; k < V; k++) acc += fabsf(a[k] * m[k] - b[k] * m[k]);
         }
     }
-    const double bs = block_sum_double((double)acc, wsum);
+    const double bs = block_sum_double<kFwdThreads>((double)acc, wsum);
     if (threadIdx.x == 0) {
         const uint64_t word = ((uint64_t)epoch << 32) | __float_as_uint((float)bs);
         __hip_atomic_store(&partial[blockIdx.x], word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -109,14 +115,14 @@ __global__ __launch_bounds__(kLossThreads) void k_masked_l1_forward(int C, int64
     __syncthreads();
     if (!s_last) return;
     double v = 0.0;
-    for (int i = threadIdx.x; i < (int)gridDim.x; i += kLossThreads) {
+    for (int i = threadIdx.x; i < (int)gridDim.x; i += kFwdThreads) {
         uint64_t w = __hip_atomic_load(&partial[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         for (uint32_t spins = 0; (uint32_t)(w >> 32) != epoch && spins < (1u << 24); spins++)
             w = __hip_atomic_load(&partial[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         v += (double)__uint_as_float((uint32_t)w);
     }
     __syncthreads();
-    const double total = block_sum_double(v, wsum);
+    const double total = block_sum_double<kFwdThreads>(v, wsum);
     if (threadIdx.x == 0) {
         *loss = (float)(total / (double)((int64_t)C * HW));
         *ticket = 0u;  // the next launch on this scratch is stream-ordered after this one
@@ -190,12 +196,16 @@ hipError_t launch_masked_l1_forward(int C, int64_t HW, const float* pred, const 
 {
     uint32_t* counter = static_cast<uint32_t*>(scratch);
     uint64_t* partial = reinterpret_cast<uint64_t*>(static_cast<char*>(scratch) + 256);
+    auto blocks = [](int64_t groups) {
+        const int64_t b = (groups + kFwdThreads - 1) / kFwdThreads;
+        return (int)(b < 1 ? 1 : (b > kFwdBlocks ? kFwdBlocks : b));
+    };
     if (vec4_ok(HW, pred, gt, nullptr, mask, mask_is_float))
-        hipLaunchKernelGGL(k_masked_l1_forward<4>, dim3(loss_blocks(HW / 4)), dim3(kLossThreads), 0, s, C, HW, pred,
-                           gt, mask, mask_is_float, loss, counter, partial, epoch);
-    else
-        hipLaunchKernelGGL(k_masked_l1_forward<1>, dim3(loss_blocks(HW)), dim3(kLossThreads), 0, s, C, HW, pred, gt,
+        hipLaunchKernelGGL(k_masked_l1_forward<4>, dim3(blocks(HW / 4)), dim3(kFwdThreads), 0, s, C, HW, pred, gt,
                            mask, mask_is_float, loss, counter, partial, epoch);
+    else
+        hipLaunchKernelGGL(k_masked_l1_forward<1>, dim3(blocks(HW)), dim3(kFwdThreads), 0, s, C, HW, pred, gt, mask,
+                           mask_is_float, loss, counter, partial, epoch);
     return hipGetLastError();
 }
 

@@ -159,15 +159,16 @@ __global__ __launch_bounds__(kPreThreads) void k_preprocess(PreprocessParams p)
         __syncthreads();
     }
     // per-thread contributions to the block partials: tile instances, super-tile entries, depth key
-    uint32_t my_tiles = 0, my_supers = 0, my_key = 0xFFFFFFFFu;
+    uint32_t my_tiles = 0, my_supers = 0, my_key = 0xFFFFFFFFu, my_err = 0;
     if (live) do {  // `break` = culled
     p.radii[i] = 0;
+    if (p.visible) p.visible[i] = 0;
     p.tiles[i] = 0;
     p.depth_key[i] = 0xFFFFFFFFu;
     *reinterpret_cast<uint2*>(p.rect + 2 * (size_t)i) = make_uint2(0u, 0u);  // empty: culled
     const float3 pv = xform4x3(p.view, px, py, pz);
     if (pv.z <= 0.2f) {
-        if (p.prefiltered) atomicOr(&p.counters[kCntError], 1u);
+        if (p.prefiltered) my_err = 0x80000000u;
         break;
     }
     const float3 hom = xform4x3(p.proj, px, py, pz);
@@ -229,6 +230,7 @@ __global__ __launch_bounds__(kPreThreads) void k_preprocess(PreprocessParams p)
     const float opacity = (p.raw & LSR_RAW_OPACITY) ? act_sigmoid(opac) : opac;
     p.depth_key[i] = __float_as_uint(pv.z);
     p.radii[i] = r;
+    if (p.visible) p.visible[i] = r > 0 ? 1 : 0;
     p.tiles[i] = area;
     *reinterpret_cast<uint2*>(p.rect + 2 * (size_t)i) =
         make_uint2((uint32_t)r4[0] | ((uint32_t)r4[1] << 16), (uint32_t)r4[2] | ((uint32_t)r4[3] << 16));
@@ -242,11 +244,12 @@ __global__ __launch_bounds__(kPreThreads) void k_preprocess(PreprocessParams p)
                            ((r4[3] + kSuper - 1) / kSuper - r4[1] / kSuper));
     my_key = __float_as_uint(pv.z);
     } while (0);
-    // block partials {R, E, min visible depth key, max visible depth key}: the host learns R, E and
+    // block partials {R, E, min visible depth key, max visible depth key | error}: the host learns R, E and
     // the depth-key range before the depth sort (k_pre_reduce; the sort then needs only the bits
     // the visible keys actually span)
     __shared__ uint32_t red[4][kPreThreads / 64];
-    uint32_t kmin = my_key, kmax = my_key == 0xFFFFFFFFu ? 0u : my_key;
+    // bit 31 of the max key carries the prefiltered error (visible keys are positive floats)
+    uint32_t kmin = my_key, kmax = (my_key == 0xFFFFFFFFu ? 0u : my_key) | my_err;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         my_tiles += __shfl_xor(my_tiles, o, 64);

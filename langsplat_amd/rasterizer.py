@@ -118,7 +118,7 @@ class _RasterizeGaussians(torch.autograd.Function):
 
 
 def rasterize_gaussians_fused(means3D, means2D, features_dc, features_rest, opacity_raw, scaling_raw, rotation_raw,
-                              language_feature_raw, raster_settings):
+                              language_feature_raw, raster_settings, with_visibility=False):
     """Fused-activation form of the rasterizer call.
 
     Takes GaussianModel's RAW parameters -- _features_dc (P,1,3), _features_rest (P,M-1,3),
@@ -127,10 +127,13 @@ def rasterize_gaussians_fused(means3D, means2D, features_dc, features_rest, opac
     gaussian_renderer/__init__.py:55-91: (color, language_feature_image, radii).  The kernels
     apply sigmoid / exp / normalize / the language normalisation and the SH concatenation
     themselves (include/lsr.h lsr_raw_flags), so those torch passes and their backward kernels
-    disappear; gradients come back w.r.t. the raw parameters.
+    disappear; gradients come back w.r.t. the raw parameters.  with_visibility=True appends
+    render()'s visibility_filter (radii > 0, written by the preprocess kernel).
     """
-    return _RasterizeGaussiansFused.apply(means3D, means2D, features_dc, features_rest, opacity_raw, scaling_raw,
-                                          rotation_raw, language_feature_raw, raster_settings)
+    color, lang, radii, visible = _RasterizeGaussiansFused.apply(
+        means3D, means2D, features_dc, features_rest, opacity_raw, scaling_raw, rotation_raw, language_feature_raw,
+        raster_settings)
+    return (color, lang, radii, visible) if with_visibility else (color, lang, radii)
 
 
 def _guarded(rs, dump, msg, fn, args):
@@ -161,10 +164,12 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
         rest = _f32(features_rest) if features_rest is not None and features_rest.numel() > 0 else None
         m3, dc, ln, op, sc, ro = (_f32(means3D), _f32(features_dc), _f32(lang) if use_lang else None,
                                   _f32(opacity_raw), _f32(scaling_raw), _f32(rotation_raw))
+        visible = torch.empty((P,), dtype=torch.bool, device=m3.device)  # radii > 0, written by preprocess
         out = _guarded(raster_settings, "snapshot_fw.dump",
                        "\nAn error occured in forward. Please forward snapshot_fw.dump for debugging.",
-                       lambda *a: _native.rasterize_gaussians(raster_settings, *a[:8], raw=raw, shs_rest=a[8]),
-                       (m3, dc, None, ln, op, sc, ro, None, rest))
+                       lambda *a: _native.rasterize_gaussians(raster_settings, *a[:8], raw=raw, shs_rest=a[8],
+                                                              visible=a[9]),
+                       (m3, dc, None, ln, op, sc, ro, None, rest, visible))
         num_rendered, color, language_feature, radii, geom, binning, image = out
         ctx.raster_settings = raster_settings
         ctx.num_rendered = num_rendered
@@ -174,12 +179,12 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
         empty = torch.empty(0)
         ctx.save_for_backward(m3, dc, rest if rest is not None else empty, ln if ln is not None else empty, op, sc,
                               ro, radii, geom, binning, image)
-        ctx.mark_non_differentiable(radii)
+        ctx.mark_non_differentiable(radii, visible)
         ctx.set_materialize_grads(False)  # an output off the loss path arrives as None (= zeros)
-        return color, language_feature, radii
+        return color, language_feature, radii, visible
 
     @staticmethod
-    def backward(ctx, grad_out_color, grad_out_language_feature, _grad_radii):
+    def backward(ctx, grad_out_color, grad_out_language_feature, _grad_radii, _grad_visible):
         rs = ctx.raster_settings
         m3, dc, rest, ln, op, sc, ro, radii, geom, binning, image = ctx.saved_tensors
         rest = rest if rest.numel() > 0 else None  # grad_out_color None: zero colour gradient

@@ -101,13 +101,13 @@ def render(viewpoint_camera, pc, pipe, bg_color: torch.Tensor, opt, scaling_modi
 
     if _fusable(pc, pipe, override_color, screenspace_points.device):
         lang_raw = pc.get_language_feature if opt.include_feature else None
-        rendered_image, language_feature_image, radii = rasterize_gaussians_fused(
+        rendered_image, language_feature_image, radii, visible = rasterize_gaussians_fused(
             pc.get_xyz, screenspace_points, pc._features_dc, pc._features_rest, pc._opacity, pc._scaling,
-            pc._rotation, lang_raw, raster_settings)
+            pc._rotation, lang_raw, raster_settings, with_visibility=True)
         return {"render": rendered_image,
                 "language_feature_image": language_feature_image,
                 "viewspace_points": screenspace_points,
-                "visibility_filter": radii > 0,
+                "visibility_filter": visible,  # radii > 0, from the preprocess kernel
                 "radii": radii}
 
     means3D = pc.get_xyz

@@ -133,6 +133,9 @@ def _render_grads(g, cam, fused, monkeypatch, gc, gl):
     grads = {n: getattr(m, "_" + n).grad.detach().cpu().numpy()
              for n in ("xyz", "features_dc", "features_rest", "scaling", "rotation", "opacity", "language_feature")}
     grads["viewspace"] = pkg["viewspace_points"].grad.detach().cpu().numpy()
+    # the fused path's visibility_filter comes from the preprocess kernel: same as radii > 0
+    assert pkg["visibility_filter"].dtype == torch.bool
+    assert torch.equal(pkg["visibility_filter"], pkg["radii"] > 0)
     return pkg["render"].detach(), pkg["language_feature_image"].detach(), pkg["radii"], grads
 
 
