@@ -311,19 +311,19 @@ __device__ __forceinline__ float mirror_add(float lo, float hi, bool upper)
     return keep + dpp<kCtrl>(send);
 }
 
-// Reduce-scatter of 12 per-lane values (slots 12..15 implicit zeros) over the wave: afterwards
-// lane l holds the wave total of value index bitrev(l>>2) (4 consecutive lanes hold the same one).
+// Reduce-scatter of 12 per-lane values over the wave, 6 pairs wide: lane bit 5 picks v[k] / v[k + 6]
+// (permlane32 swap), bit 4 r[m] / r[m + 3] (permlane16 swap), bit 3 s0 / s1 (row_mirror; s2 is
+// summed on both sides), bit 2 t0 / t1 (row_half_mirror), then bits 1, 0 (quad_perm).  Afterwards
+// lane l holds the wave total of value scatter_index(l); quads with bits 3 and 2 both set duplicate
+// the quads with bit 3 clear (scatter_writer).
 __device__ __forceinline__ float wave_reduce_scatter12(const float (&v)[12], int lane)
 {
-    const float r0 = swap32_add(v[0], v[8]), r1 = swap32_add(v[1], v[9]);
-    const float r2 = swap32_add(v[2], v[10]), r3 = swap32_add(v[3], v[11]);
-    const float r4 = swap32_add(v[4], 0.0f), r5 = swap32_add(v[5], 0.0f);
-    const float r6 = swap32_add(v[6], 0.0f), r7 = swap32_add(v[7], 0.0f);
-    const float s0 = swap16_add(r0, r4), s1 = swap16_add(r1, r5);
-    const float s2 = swap16_add(r2, r6), s3 = swap16_add(r3, r7);
+    const float r0 = swap32_add(v[0], v[6]), r1 = swap32_add(v[1], v[7]), r2 = swap32_add(v[2], v[8]);
+    const float r3 = swap32_add(v[3], v[9]), r4 = swap32_add(v[4], v[10]), r5 = swap32_add(v[5], v[11]);
+    const float s0 = swap16_add(r0, r3), s1 = swap16_add(r1, r4), s2 = swap16_add(r2, r5);
     const bool u8 = (lane & 8) != 0, u4 = (lane & 4) != 0;
-    const float t0 = mirror_add<0x140>(s0, s2, u8);  // row_mirror
-    const float t1 = mirror_add<0x140>(s1, s3, u8);
+    const float t0 = mirror_add<0x140>(s0, s1, u8);  // row_mirror
+    const float t1 = s2 + dpp<0x140>(s2);
     float w = mirror_add<0x141>(t0, t1, u4);         // row_half_mirror
     w += dpp<0x4E>(w);                               // quad_perm [2,3,0,1]
     w += dpp<0xB1>(w);                               // quad_perm [1,0,3,2]
@@ -332,17 +332,24 @@ __device__ __forceinline__ float wave_reduce_scatter12(const float (&v)[12], int
 
 __device__ __forceinline__ int scatter_index(int lane)
 {
-    // bits 5,4,3,2 of the lane select value bits 3,2,1,0
-    return (((lane >> 5) & 1) << 3) | (((lane >> 4) & 1) << 2) | (((lane >> 3) & 1) << 1) | ((lane >> 2) & 1);
+    const int m = (lane & 4) ? 2 : ((lane >> 3) & 1);
+    return m + 3 * ((lane >> 4) & 1) + 6 * ((lane >> 5) & 1);
 }
 
-// One pixel's back-to-front state (upstream BACKWARD::renderCUDA locals).
+// One lane per distinct reduced value (12 of 64).
+__device__ __forceinline__ bool scatter_writer(int lane)
+{
+    return (lane & 3) == 0 && (lane & 12) != 12;
+}
+
+// One pixel's back-to-front state (upstream BACKWARD::renderCUDA locals).  acc* is the colour /
+// feature composited behind the current entry; upstream updates it at the start of the NEXT blend
+// from (last_alpha, last_color) -- updating it at the end of this blend with (alpha, color) is the
+// same expression on the same operands, one blend earlier, and needs no last_* registers.
 struct BwdPixel {
     float T, T_final, bg_dot;
     float dp0, dp1, dp2, dq0, dq1, dq2;
     float acc0, acc1, acc2, accF0, accF1, accF2;
-    float lc0, lc1, lc2, lf0, lf1, lf2;
-    float last_alpha;
     uint32_t last;
 };
 
@@ -367,16 +374,17 @@ __device__ __forceinline__ void bwd_pixel_init(BwdPixel& q, const RenderParams& 
     }
     q.bg_dot = fma_(p.bg[2], q.dp2, fma_(p.bg[1], q.dp1, p.bg[0] * q.dp0));
     q.acc0 = q.acc1 = q.acc2 = q.accF0 = q.accF1 = q.accF2 = 0.f;
-    q.lc0 = q.lc1 = q.lc2 = q.lf0 = q.lf1 = q.lf2 = 0.f;
-    q.last_alpha = 0.f;
 }
 
-// One replayed blend of one pixel: updates the pixel state and ADDS its 12 gradient partials to v
+// One replayed blend of one pixel: updates the pixel state and WRITES its 12 gradient partials to v
 // (order of oracle backward_pixel; alpha and the skip tests are bit-identical to the forward).
+// Branch-free: a lane without this blend passes alpha = G = 0, which leaves T and acc* unchanged
+// (1 / (1 - 0) = 1, fma(0, c, 1 * acc) = acc) and makes every partial 0 (each carries a factor
+// alpha or G) -- so the wave needs no exec-mask split and no zero-fill of v.
+template <bool kFeat>
 __device__ __forceinline__ void bwd_pixel_blend(BwdPixel& q, float G, float alpha, float dx, float dy,
                                                 const float4& B, float cx, float cz, const float4& Cc,
-                                                const float2& D, bool feat, float ddelx_dx, float ddely_dy,
-                                                float (&v)[12])
+                                                const float2& D, float ddelx_dx, float ddely_dy, float (&v)[12])
 {
     const float one_m = 1.0f - alpha;
     // gradients need 1e-4, not bit-exactness: one v_rcp_f32 replaces the two IEEE divisions
@@ -384,48 +392,41 @@ __device__ __forceinline__ void bwd_pixel_blend(BwdPixel& q, float G, float alph
     const float inv_one_m = __builtin_amdgcn_rcpf(one_m);
     q.T = q.T * inv_one_m;
     const float dcd = alpha * q.T;
-    const float oml = 1.0f - q.last_alpha;
-    float dL_dalpha = 0.0f;
-    q.acc0 = fma_(q.last_alpha, q.lc0, oml * q.acc0);
-    q.lc0 = Cc.x;
-    dL_dalpha = fma_(Cc.x - q.acc0, q.dp0, dL_dalpha);
-    v[6] += dcd * q.dp0;
-    q.acc1 = fma_(q.last_alpha, q.lc1, oml * q.acc1);
-    q.lc1 = Cc.y;
+    float dL_dalpha = fma_(Cc.x - q.acc0, q.dp0, 0.0f);
+    q.acc0 = fma_(alpha, Cc.x, one_m * q.acc0);
+    v[6] = dcd * q.dp0;
     dL_dalpha = fma_(Cc.y - q.acc1, q.dp1, dL_dalpha);
-    v[7] += dcd * q.dp1;
-    q.acc2 = fma_(q.last_alpha, q.lc2, oml * q.acc2);
-    q.lc2 = Cc.z;
+    q.acc1 = fma_(alpha, Cc.y, one_m * q.acc1);
+    v[7] = dcd * q.dp1;
     dL_dalpha = fma_(Cc.z - q.acc2, q.dp2, dL_dalpha);
-    v[8] += dcd * q.dp2;
-    if (feat) {
-        q.accF0 = fma_(q.last_alpha, q.lf0, oml * q.accF0);
-        q.lf0 = Cc.w;
+    q.acc2 = fma_(alpha, Cc.z, one_m * q.acc2);
+    v[8] = dcd * q.dp2;
+    if (kFeat) {
         dL_dalpha = fma_(Cc.w - q.accF0, q.dq0, dL_dalpha);
-        v[9] += dcd * q.dq0;
-        q.accF1 = fma_(q.last_alpha, q.lf1, oml * q.accF1);
-        q.lf1 = D.x;
+        q.accF0 = fma_(alpha, Cc.w, one_m * q.accF0);
+        v[9] = dcd * q.dq0;
         dL_dalpha = fma_(D.x - q.accF1, q.dq1, dL_dalpha);
-        v[10] += dcd * q.dq1;
-        q.accF2 = fma_(q.last_alpha, q.lf2, oml * q.accF2);
-        q.lf2 = D.y;
+        q.accF1 = fma_(alpha, D.x, one_m * q.accF1);
+        v[10] = dcd * q.dq1;
         dL_dalpha = fma_(D.y - q.accF2, q.dq2, dL_dalpha);
-        v[11] += dcd * q.dq2;
+        q.accF2 = fma_(alpha, D.y, one_m * q.accF2);
+        v[11] = dcd * q.dq2;
+    } else {
+        v[9] = v[10] = v[11] = 0.0f;
     }
     dL_dalpha = dL_dalpha * q.T;
-    q.last_alpha = alpha;
     dL_dalpha = fma_(-q.T_final * inv_one_m, q.bg_dot, dL_dalpha);
     const float cy = B.x;
     const float dL_dG = B.y * dL_dalpha;
     const float gdx = G * dx, gdy = G * dy;
     const float dG_ddelx = -gdx * cx - gdy * cy;
     const float dG_ddely = -gdy * cz - gdx * cy;
-    v[0] += dL_dG * dG_ddelx * ddelx_dx;
-    v[1] += dL_dG * dG_ddely * ddely_dy;
-    v[2] += -0.5f * gdx * dx * dL_dG;
-    v[3] += -0.5f * gdx * dy * dL_dG;
-    v[4] += -0.5f * gdy * dy * dL_dG;
-    v[5] += G * dL_dalpha;
+    v[0] = dL_dG * dG_ddelx * ddelx_dx;
+    v[1] = dL_dG * dG_ddely * ddely_dy;
+    v[2] = -0.5f * gdx * dx * dL_dG;
+    v[3] = -0.5f * gdx * dy * dL_dG;
+    v[4] = -0.5f * gdy * dy * dL_dG;
+    v[5] = G * dL_dalpha;
 }
 
 // Measurement hook (LSR_RENDER_STATS=1, lsr_debug_render_stats): per wave-iteration counters of
@@ -433,7 +434,7 @@ __device__ __forceinline__ void bwd_pixel_blend(BwdPixel& q, float G, float alph
 // an alpha hit, [3] lanes hit, [8 + c] histogram of lanes hit (c = 0..64).  Off by default.
 __device__ unsigned long long g_render_stats[8 + 65];
 
-template <bool kStats>
+template <bool kStats, bool kFeat>
 __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
 {
     constexpr int kThreads = kTilePixels;
@@ -443,7 +444,6 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
     __shared__ float4 sB[kThreads];      // conic.y, opacity, power cutoff, f1
     __shared__ float4 sC[kThreads];      // r, g, b, f0
     __shared__ float sF[kThreads];       // f2
-    __shared__ uint32_t sId[kThreads];
     __shared__ float sG[kThreads * 12];  // per-entry gradient sums of the tile (12 floats)
     __shared__ uint8_t sM[kThreads];     // wave_cover mask (& the waves' contributor bounds)
     __shared__ uint32_t s_wmax[kThreads / 64];
@@ -463,11 +463,10 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
     const float tx0 = (float)(tx * kTile), ty0 = (float)(ty * kTile);
     const size_t HW = (size_t)p.W * p.H;
     const uint32_t start = p.ranges[tile].x;
-    const bool feat = p.include_feature != 0;
     const float ddelx_dx = 0.5f * (float)p.W, ddely_dy = 0.5f * (float)p.H;
 
     BwdPixel q;
-    bwd_pixel_init(q, p, px < p.W && py < p.H, (size_t)py * p.W + px, HW, feat);
+    bwd_pixel_init(q, p, px < p.W && py < p.H, (size_t)py * p.W + px, HW, kFeat);
     uint32_t wmax = q.last;
 
     if (kStats) {
@@ -497,7 +496,6 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
             sB[t] = make_float4(a.w, b.y, cut, c.z);
             sC[t] = make_float4(b.z, b.w, c.x, c.y);
             sF[t] = c.w;
-            sId[t] = g;
             const uint32_t k = (uint32_t)kload;
             const uint32_t live = (k < w0 ? 1u : 0u) | (k < w1 ? 2u : 0u) | (k < w2 ? 4u : 0u) | (k < w3 ? 8u : 0u);
             cover = wave_cover(entry_box(a.x, a.y, a.z, a.w, b.x, cut), tx0, ty0) & live;
@@ -523,9 +521,6 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
                 const float pw = fma_(A.z * dx, dx, fma_(A.w * dy, dy, -((B.x * dx) * dy)));
                 bool h = kk < (int)q.last && pw <= 0.0f && pw >= B.z;
                 if (__ballot(h) == 0ull) continue;  // wave-uniform skip
-                float v[12];
-#pragma unroll
-                for (int c = 0; c < 12; c++) v[c] = 0.f;
                 // hardware exp (a few ulp): gradients need 1e-4.  Only the 1/255 skip decision
                 // must equal the forward's, so alphas within 1e-6 of it use the exact exp.
                 float G = __expf(pw);
@@ -549,14 +544,13 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
                         atomicAdd(&s_stat[8 + nh], 1u);
                     }
                 }
-                if (h) {
-                    const float4 Cc = sC[j];
-                    const float2 D = make_float2(B.w, sF[j]);
-                    bwd_pixel_blend(q, G, al, dx, dy, B, -2.0f * A.z, -2.0f * A.w, Cc, D, feat, ddelx_dx, ddely_dy,
-                                    v);
-                }
+                if (!h) al = G = 0.0f;
+                const float4 Cc = sC[j];
+                const float2 D = kFeat ? make_float2(B.w, sF[j]) : make_float2(0.f, 0.f);
+                float v[12];
+                bwd_pixel_blend<kFeat>(q, G, al, dx, dy, B, -2.0f * A.z, -2.0f * A.w, Cc, D, ddelx_dx, ddely_dy, v);
                 const float tot = wave_reduce_scatter12(v, lane);
-                if ((lane & 3) == 0 && vidx < 12) atomicAdd(&sG[j * 12 + vidx], tot);
+                if (scatter_writer(lane)) atomicAdd(&sG[j * 12 + vidx], tot);
             }
         }
         if (kStats && lane == 0) atomicMax(&s_bmax, nw);
@@ -571,7 +565,10 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
             const int e = slot >> 4, c = slot & 15;
             if (c < 12) {
                 const float val = sG[e * 12 + c];
-                if (val != 0.0f) atomicAdd(&p.grad[(size_t)sId[e] * kGradStride + c], val);
+                if (val != 0.0f) {  // the id again from point_list (an L2 hit; saves 1 KB of LDS)
+                    const uint32_t g = p.point_list[start + (uint32_t)(maxl - 1 - (done_cnt + e))];
+                    atomicAdd(&p.grad[(size_t)g * kGradStride + c], val);
+                }
             }
         }
     }
@@ -606,10 +603,17 @@ hipError_t launch_render_backward(const RenderParams& pin, int tiles, hipStream_
     if (tiles == 0) return hipSuccess;
     RenderParams p = pin;
     if (!scheduled()) p.sched_counts = p.sched_lists = nullptr;
-    if (render_stats_on())
-        hipLaunchKernelGGL(k_render_backward<true>, dim3(tiles), dim3(kTilePixels), 0, s, p);
-    else
-        hipLaunchKernelGGL(k_render_backward<false>, dim3(tiles), dim3(kTilePixels), 0, s, p);
+    const bool feat = p.include_feature != 0;
+    if (render_stats_on()) {
+        if (feat)
+            hipLaunchKernelGGL((k_render_backward<true, true>), dim3(tiles), dim3(kTilePixels), 0, s, p);
+        else
+            hipLaunchKernelGGL((k_render_backward<true, false>), dim3(tiles), dim3(kTilePixels), 0, s, p);
+    } else if (feat) {
+        hipLaunchKernelGGL((k_render_backward<false, true>), dim3(tiles), dim3(kTilePixels), 0, s, p);
+    } else {
+        hipLaunchKernelGGL((k_render_backward<false, false>), dim3(tiles), dim3(kTilePixels), 0, s, p);
+    }
     return hipGetLastError();
 }
 
