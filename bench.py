@@ -182,7 +182,8 @@ def main():
     args = ap.parse_args()
 
     rank, world = init_from_env()
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # one GPU per rank; the modulo only matters for a gloo rehearsal of N ranks on fewer GPUs
+    local_rank = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     cfg = args.config or ("C3" if world == 1 else "C4")

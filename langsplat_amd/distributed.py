@@ -22,8 +22,8 @@ def init_from_env(backend: str = None):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world <= 1 or dist.is_initialized():
         return dist.get_rank() if dist.is_initialized() else 0, world
-    if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    if backend is None:  # LSR_DIST_BACKEND=gloo: a rehearsal with several ranks on one GPU
+        backend = os.environ.get("LSR_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     dist.init_process_group(backend=backend)
     return dist.get_rank(), dist.get_world_size()
