@@ -78,19 +78,29 @@ def check_forward_exact(st, inp, run=None):
     return run, std, ind, out
 
 
-def assert_grad_close(name, gpu, ref):
+def assert_grad_close(name, gpu, ref, outliers=0.0):
+    """|gpu - ref| <= 1e-4 (|ref| + floor) everywhere, or -- `outliers` > 0, the full-size tests --
+    on all but that fraction of the entries, which must still be within 1e-3.
+
+    Why full size needs the allowance: the scale/rotation gradients sum many per-pixel terms that
+    cancel, so they move by ~1e-4 of the floored scale under ANY 1-ulp change of the fp32
+    evaluation.  Measured on the C3 scene with the oracle itself: T * (1/(1-alpha)) instead of
+    T / (1-alpha) moves 2 of 4M rotation entries past 1e-4 (worst 1.26e-4); G one ulp up moves the
+    worst rotation entry by 7.8e-5.  The GPU's float atomics and v_rcp_f32 are such changes."""
     gpu = np.asarray(gpu, dtype=np.float64)
     ref = np.asarray(ref, dtype=np.float64)
     assert gpu.shape == ref.shape, name
     floor = GRAD_FLOOR * (np.max(np.abs(ref)) if ref.size else 0.0) + 1e-30
     bad = np.abs(gpu - ref) > GRAD_RTOL * (np.abs(ref) + floor)
+    if outliers > 0.0 and bad.sum() <= outliers * bad.size:
+        bad = np.abs(gpu - ref) > 10 * GRAD_RTOL * (np.abs(ref) + floor)
     if bad.any():
         i = np.argmax(np.abs(gpu - ref) / (np.abs(ref) + floor))
         raise AssertionError(f"{name}: {bad.sum()} / {bad.size} entries off; worst gpu={gpu.flat[i]} "
                              f"ref={ref.flat[i]} floor={floor}")
 
 
-def check_backward(st, inp, run, out, seed=7):
+def check_backward(st, inp, run, out, seed=7, outliers=0.0):
     W, H = st.image_width, st.image_height
     gc, gl = grad_seed(H, W, seed=seed)
     ref = run.backward(gc, gl if st.include_feature else None)
@@ -112,7 +122,7 @@ def check_backward(st, inp, run, out, seed=7):
     else:
         names += ["scales", "rotations"]
     for n in names:
-        assert_grad_close(n, g[n].cpu().numpy(), ref[n])
+        assert_grad_close(n, g[n].cpu().numpy(), ref[n], outliers)
     return g, ref
 
 
@@ -234,6 +244,23 @@ def test_forward_is_deterministic():
 
 
 @pytest.mark.parametrize("cfg", ["C2", "C3"])
+def test_full_size_oracle_parity(cfg):
+    """BASELINE.json configs[1] and [2] at full size against the C oracle (~10-20 s of oracle time):
+    forward bit-exact (images, radii, tile ranges, per-tile order, final T, contributor counts),
+    every gradient within the 1e-4 relative tolerance on all but 1e-5 of its entries (and those
+    within 1e-3: assert_grad_close)."""
+    c = CONFIGS[cfg]
+    g = make_gaussians(c["P"], seed=0)
+    cam = make_cameras(1, c["width"], c["height"])[0]
+    st = settings_for(cam, sh_degree=3)
+    with torch.no_grad():
+        inp = {k: v.contiguous() for k, v in activated_inputs(g).items()}
+    run, std, ind, out = check_forward_exact(st, inp)
+    assert run.blends > 0
+    check_backward(st, inp, run, out, seed=3, outliers=1e-5)
+
+
+@pytest.mark.parametrize("cfg", ["C2", "C3", "C5"])
 def test_full_size_properties(cfg):
     """BASELINE.json full sizes: per-tile lists sorted by (depth, id), instance accounting, and the
     backward is linear in the upstream gradient (size-independent properties)."""
