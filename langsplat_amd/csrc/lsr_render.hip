@@ -347,7 +347,7 @@ __device__ __forceinline__ bool scatter_writer(int lane)
 // from (last_alpha, last_color) -- updating it at the end of this blend with (alpha, color) is the
 // same expression on the same operands, one blend earlier, and needs no last_* registers.
 struct BwdPixel {
-    float T, T_final, bg_dot;
+    float T, T_final, bg_term;
     float dp0, dp1, dp2, dq0, dq1, dq2;
     float acc0, acc1, acc2, accF0, accF1, accF2;
     uint32_t last;
@@ -372,61 +372,75 @@ __device__ __forceinline__ void bwd_pixel_init(BwdPixel& q, const RenderParams& 
             q.dq2 = p.dL_dlang[2 * HW + pix];
         }
     }
-    q.bg_dot = fma_(p.bg[2], q.dp2, fma_(p.bg[1], q.dp1, p.bg[0] * q.dp0));
+    q.bg_term = -q.T_final * fma_(p.bg[2], q.dp2, fma_(p.bg[1], q.dp1, p.bg[0] * q.dp0));
     q.acc0 = q.acc1 = q.acc2 = q.accF0 = q.accF1 = q.accF2 = 0.f;
 }
 
 // One replayed blend of one pixel: updates the pixel state and WRITES its 12 gradient partials to v
-// (order of oracle backward_pixel; alpha and the skip tests are bit-identical to the forward).
+// (alpha and the skip tests are bit-identical to the forward; the gradient arithmetic is that of
+// oracle backward_pixel, regrouped to fewer operations -- gradients need 1e-4, not bit-exactness).
 // Branch-free: a lane without this blend passes alpha = G = 0, which leaves T and acc* unchanged
-// (1 / (1 - 0) = 1, fma(0, c, 1 * acc) = acc) and makes every partial 0 (each carries a factor
+// (1 / (1 - 0) = 1, acc + 0 * (c - acc) = acc) and makes every partial 0 (each carries a factor
 // alpha or G) -- so the wave needs no exec-mask split and no zero-fill of v.
+// Constant factors are applied once per (tile, Gaussian) at the flush instead of per pixel
+// (flush_scale): v[0] = dL/dmean2D.x / (2 ddelx_dx), v[1] likewise, v[2..4] = -2 dL/dconic.
+// A = {x, y, -conic.x / 2, -conic.z / 2}, B = {conic.y, opacity, .., ..}.
 template <bool kFeat>
 __device__ __forceinline__ void bwd_pixel_blend(BwdPixel& q, float G, float alpha, float dx, float dy,
-                                                const float4& B, float cx, float cz, const float4& Cc,
-                                                const float2& D, float ddelx_dx, float ddely_dy, float (&v)[12])
+                                                const float4& A, const float4& B, const float4& Cc,
+                                                const float2& D, float (&v)[12])
 {
     const float one_m = 1.0f - alpha;
-    // gradients need 1e-4, not bit-exactness: one v_rcp_f32 replaces the two IEEE divisions
-    // T / (1 - alpha) and T_final / (1 - alpha) (the skip decisions use power/alpha only)
+    // one v_rcp_f32 replaces the two IEEE divisions T / (1 - alpha) and T_final / (1 - alpha)
     const float inv_one_m = __builtin_amdgcn_rcpf(one_m);
     q.T = q.T * inv_one_m;
     const float dcd = alpha * q.T;
-    float dL_dalpha = fma_(Cc.x - q.acc0, q.dp0, 0.0f);
-    q.acc0 = fma_(alpha, Cc.x, one_m * q.acc0);
+    // per channel: dL/dalpha += (c - acc) dL/dpix; acc <- acc + alpha (c - acc) (= alpha c + (1 - alpha) acc)
+    float e = Cc.x - q.acc0;
+    float dL_dalpha = e * q.dp0;
+    q.acc0 = fma_(alpha, e, q.acc0);
     v[6] = dcd * q.dp0;
-    dL_dalpha = fma_(Cc.y - q.acc1, q.dp1, dL_dalpha);
-    q.acc1 = fma_(alpha, Cc.y, one_m * q.acc1);
+    e = Cc.y - q.acc1;
+    dL_dalpha = fma_(e, q.dp1, dL_dalpha);
+    q.acc1 = fma_(alpha, e, q.acc1);
     v[7] = dcd * q.dp1;
-    dL_dalpha = fma_(Cc.z - q.acc2, q.dp2, dL_dalpha);
-    q.acc2 = fma_(alpha, Cc.z, one_m * q.acc2);
+    e = Cc.z - q.acc2;
+    dL_dalpha = fma_(e, q.dp2, dL_dalpha);
+    q.acc2 = fma_(alpha, e, q.acc2);
     v[8] = dcd * q.dp2;
     if (kFeat) {
-        dL_dalpha = fma_(Cc.w - q.accF0, q.dq0, dL_dalpha);
-        q.accF0 = fma_(alpha, Cc.w, one_m * q.accF0);
+        e = Cc.w - q.accF0;
+        dL_dalpha = fma_(e, q.dq0, dL_dalpha);
+        q.accF0 = fma_(alpha, e, q.accF0);
         v[9] = dcd * q.dq0;
-        dL_dalpha = fma_(D.x - q.accF1, q.dq1, dL_dalpha);
-        q.accF1 = fma_(alpha, D.x, one_m * q.accF1);
+        e = D.x - q.accF1;
+        dL_dalpha = fma_(e, q.dq1, dL_dalpha);
+        q.accF1 = fma_(alpha, e, q.accF1);
         v[10] = dcd * q.dq1;
-        dL_dalpha = fma_(D.y - q.accF2, q.dq2, dL_dalpha);
-        q.accF2 = fma_(alpha, D.y, one_m * q.accF2);
+        e = D.y - q.accF2;
+        dL_dalpha = fma_(e, q.dq2, dL_dalpha);
+        q.accF2 = fma_(alpha, e, q.accF2);
         v[11] = dcd * q.dq2;
     } else {
         v[9] = v[10] = v[11] = 0.0f;
     }
-    dL_dalpha = dL_dalpha * q.T;
-    dL_dalpha = fma_(-q.T_final * inv_one_m, q.bg_dot, dL_dalpha);
-    const float cy = B.x;
+    // dL/dalpha = T (sum) - T_final / (1 - alpha) (bg . dL/dpix); bg_term = -T_final (bg . dL/dpix)
+    dL_dalpha = fma_(q.bg_term, inv_one_m, dL_dalpha * q.T);
     const float dL_dG = B.y * dL_dalpha;
-    const float gdx = G * dx, gdy = G * dy;
-    const float dG_ddelx = -gdx * cx - gdy * cy;
-    const float dG_ddely = -gdy * cz - gdx * cy;
-    v[0] = dL_dG * dG_ddelx * ddelx_dx;
-    v[1] = dL_dG * dG_ddely * ddely_dy;
-    v[2] = -0.5f * gdx * dx * dL_dG;
-    v[3] = -0.5f * gdx * dy * dL_dG;
-    v[4] = -0.5f * gdy * dy * dL_dG;
+    const float ga = (G * dx) * dL_dG, gb = (G * dy) * dL_dG;
+    // dG/ddelx dL/dG = -(ga conic.x + gb conic.y) = 2 (ga A.z - gb conic.y / 2), likewise y
+    v[0] = fma_(-0.5f, gb * B.x, ga * A.z);
+    v[1] = fma_(-0.5f, ga * B.x, gb * A.w);
+    v[2] = ga * dx;
+    v[3] = ga * dy;
+    v[4] = gb * dy;
     v[5] = G * dL_dalpha;
+}
+
+// Factor of gradient slot c applied at the flush (see bwd_pixel_blend).
+__device__ __forceinline__ float flush_scale(int c, int W, int H)
+{
+    return c == 0 ? (float)W : c == 1 ? (float)H : (c >= 2 && c <= 4) ? -0.5f : 1.0f;
 }
 
 // Measurement hook (LSR_RENDER_STATS=1, lsr_debug_render_stats): per wave-iteration counters of
@@ -463,7 +477,7 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
     const float tx0 = (float)(tx * kTile), ty0 = (float)(ty * kTile);
     const size_t HW = (size_t)p.W * p.H;
     const uint32_t start = p.ranges[tile].x;
-    const float ddelx_dx = 0.5f * (float)p.W, ddely_dy = 0.5f * (float)p.H;
+    const float fscale = flush_scale(t & 15, p.W, p.H);  // this thread's flush slot is always t & 15
 
     BwdPixel q;
     bwd_pixel_init(q, p, px < p.W && py < p.H, (size_t)py * p.W + px, HW, kFeat);
@@ -548,7 +562,7 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
                 const float4 Cc = sC[j];
                 const float2 D = kFeat ? make_float2(B.w, sF[j]) : make_float2(0.f, 0.f);
                 float v[12];
-                bwd_pixel_blend<kFeat>(q, G, al, dx, dy, B, -2.0f * A.z, -2.0f * A.w, Cc, D, ddelx_dx, ddely_dy, v);
+                bwd_pixel_blend<kFeat>(q, G, al, dx, dy, A, B, Cc, D, v);
                 const float tot = wave_reduce_scatter12(v, lane);
                 if (scatter_writer(lane)) atomicAdd(&sG[j * 12 + vidx], tot);
             }
@@ -564,7 +578,7 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
         for (int slot = t; slot < cnt * 16; slot += kThreads) {
             const int e = slot >> 4, c = slot & 15;
             if (c < 12) {
-                const float val = sG[e * 12 + c];
+                const float val = sG[e * 12 + c] * fscale;
                 if (val != 0.0f) {  // the id again from point_list (an L2 hit; saves 1 KB of LDS)
                     const uint32_t g = p.point_list[start + (uint32_t)(maxl - 1 - (done_cnt + e))];
                     atomicAdd(&p.grad[(size_t)g * kGradStride + c], val);
