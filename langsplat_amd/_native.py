@@ -102,6 +102,7 @@ SIGNATURES = {
                                                      ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _vp, _vp, _vp,
                                                      _vp]),
     "lsr_debug_render_stats": (ctypes.c_int32, [ctypes.POINTER(ctypes.c_uint64), ctypes.c_int32]),
+    "lsr_debug_render_timeline": (ctypes.c_int32, [ctypes.c_int32, ctypes.POINTER(ctypes.c_uint32), ctypes.c_int32]),
     "lsr_profile_enable": (ctypes.c_int32, [ctypes.c_int32]),
     "lsr_profile_report": (ctypes.c_int32, [ctypes.POINTER(LsrKernelStat), ctypes.c_int32]),
     "lsr_profile_select": (ctypes.c_int32, [ctypes.c_char_p]),
@@ -447,3 +448,13 @@ def debug_render_stats():
     v = list(arr)
     return {"entries": v[0], "power_hit": v[1], "alpha_hit": v[2], "lanes_hit": v[3], "barrier_slots": v[4],
             "batches": v[6], "hist": v[8:8 + 65]}
+
+
+def debug_render_timeline(kernel, n):
+    """Per-workgroup timeline of the LSR_RENDER_STATS=1 render kernels (kernel 0 forward, 1 backward;
+    include/lsr.h lsr_debug_render_timeline): list of (start, end, tile, hw_slot) for workgroups < n."""
+    arr = (ctypes.c_uint32 * (4 * n))()
+    _check(load().lsr_debug_render_timeline(kernel, arr, n), "lsr_debug_render_timeline")
+    v = list(arr)
+    return [(v[4 * i], v[4 * i + 1], v[4 * i + 2] if v[4 * i + 2] < 2 ** 31 else v[4 * i + 2] - 2 ** 32, v[4 * i + 3])
+            for i in range(n)]

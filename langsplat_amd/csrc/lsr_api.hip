@@ -474,6 +474,17 @@ int32_t lsr_debug_render_stats(uint64_t* out, int32_t n)
     return LSR_OK;
 }
 
+int32_t lsr_debug_render_timeline(int32_t kernel, uint32_t* out, int32_t n)
+{
+    if (!out || n <= 0 || kernel < 0 || kernel > 1)
+        return fail(LSR_ERR_INVALID, "lsr_debug_render_timeline: invalid argument");
+    const bool debug = false;
+    hipStream_t stream = nullptr;
+    (void)stream;
+    LSR_TRY(render_timeline_read(out, kernel, n), "render timeline");
+    return LSR_OK;
+}
+
 int32_t lsr_mark_visible(int32_t P, const float* means3D, const float* viewmatrix, const float* projmatrix,
                          uint8_t* visible, void* stream_ptr)
 {

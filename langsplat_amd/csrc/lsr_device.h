@@ -45,6 +45,52 @@ __device__ __forceinline__ float expf_exact(float x)
     return p * __uint_as_float((uint32_t)(e + 127) << 23);
 }
 
+// expf_exact without the underflow branch, for the render loops: every alpha they use comes from a
+// power >= the cutoff of power_cutoff (> -6), where the two are the same operation sequence; the
+// clamp only keeps lanes whose result is discarded finite.  Branch-free, so the chains of
+// neighbouring list entries interleave.
+__device__ __forceinline__ float expf_exact_render(float x)
+{
+    x = __builtin_fmaxf(x, -87.0f);
+    float n = __builtin_rintf(x * 1.44269504088896341f);
+    float r = __builtin_fmaf(n, -0.693145751953125f, x);
+    r = __builtin_fmaf(n, -1.42860682030941723212e-6f, r);
+    float p = 1.98412698e-4f;
+    p = __builtin_fmaf(p, r, 1.38888889e-3f);
+    p = __builtin_fmaf(p, r, 8.33333333e-3f);
+    p = __builtin_fmaf(p, r, 4.16666667e-2f);
+    p = __builtin_fmaf(p, r, 1.66666667e-1f);
+    p = __builtin_fmaf(p, r, 0.5f);
+    p = __builtin_fmaf(p, r, 1.0f);
+    p = __builtin_fmaf(p, r, 1.0f);
+    int e = (int)n;
+    return p * __uint_as_float((uint32_t)(e + 127) << 23);
+}
+
+// expf_exact_render of two values at once: the polynomial as packed fp32 (v_pk_fma_f32), i.e. the
+// same IEEE operations per element in about half the instructions.
+typedef float lsr_f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ lsr_f2 expf_exact_render2(lsr_f2 x)
+{
+    x = __builtin_elementwise_max(x, (lsr_f2)(-87.0f));
+    lsr_f2 n = __builtin_elementwise_rint(x * 1.44269504088896341f);
+    lsr_f2 r = __builtin_elementwise_fma(n, (lsr_f2)(-0.693145751953125f), x);
+    r = __builtin_elementwise_fma(n, (lsr_f2)(-1.42860682030941723212e-6f), r);
+    lsr_f2 p = (lsr_f2)(1.98412698e-4f);
+    p = __builtin_elementwise_fma(p, r, (lsr_f2)(1.38888889e-3f));
+    p = __builtin_elementwise_fma(p, r, (lsr_f2)(8.33333333e-3f));
+    p = __builtin_elementwise_fma(p, r, (lsr_f2)(4.16666667e-2f));
+    p = __builtin_elementwise_fma(p, r, (lsr_f2)(1.66666667e-1f));
+    p = __builtin_elementwise_fma(p, r, (lsr_f2)(0.5f));
+    p = __builtin_elementwise_fma(p, r, (lsr_f2)(1.0f));
+    p = __builtin_elementwise_fma(p, r, (lsr_f2)(1.0f));
+    const int e0 = (int)n.x, e1 = (int)n.y;
+    lsr_f2 sc;
+    sc.x = __uint_as_float((uint32_t)(e0 + 127) << 23);
+    sc.y = __uint_as_float((uint32_t)(e1 + 127) << 23);
+    return p * sc;
+}
+
 __device__ __forceinline__ float fma_(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
 
 // ---- parameter activations of the fused path (lsr_raw_flags; oracle lso_act_* restate them) ----

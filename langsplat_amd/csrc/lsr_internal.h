@@ -171,6 +171,7 @@ struct RenderParams {
     // (class c of pass d at tile_lists[(d * kWorkClasses + c) * tiles]); null: launch order
     uint32_t* sched_counts;
     uint32_t* sched_lists;
+    int prio;  // wave priority by launch position (longest tiles highest), 0: off
     // backward
     const float *dL_dcolor, *dL_dlang;
     float* grad;
@@ -237,5 +238,6 @@ hipError_t launch_decode_language_feature(int H, int W, const int64_t* seg_level
 hipError_t launch_render_forward(const RenderParams& p, int tiles, hipStream_t s);
 hipError_t launch_render_backward(const RenderParams& p, int tiles, hipStream_t s);
 hipError_t render_stats_read(unsigned long long* out, int n);  // reads and clears
+hipError_t render_timeline_read(uint32_t* out, int kernel, int n);
 
 }  // namespace lsr

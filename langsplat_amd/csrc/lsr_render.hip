@@ -122,12 +122,74 @@ __device__ __forceinline__ int scheduled_tile(int b, const uint32_t* counts, con
     return (int)lists[(size_t)(kWorkClasses - 1 - l) * T + ((uint32_t)b - first)];
 }
 
+// Measurement hook (LSR_RENDER_STATS=1, lsr_debug_render_timeline): per workgroup of the two render
+// kernels {start, end} (s_memrealtime, 100 MHz), the tile and the hardware slot (XCC_ID << 16 |
+// HW_ID bits 8..15: cu, sh, se).  Off by default.
+constexpr int kTimelineMax = 1 << 15;
+__device__ uint32_t g_render_timeline[2][kTimelineMax * 4];
+
+__device__ __forceinline__ uint32_t hw_slot()
+{
+    const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID
+    const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+    return ((xcc & 0xFu) << 16) | ((hw >> 8) & 0xFFu);
+}
+
+__device__ __forceinline__ void timeline_put(int kernel, uint64_t t0, int tile)
+{
+    const int b = (int)blockIdx.x;
+    if (threadIdx.x != 0 || b >= kTimelineMax) return;
+    uint32_t* o = g_render_timeline[kernel] + 4 * b;
+    o[0] = (uint32_t)t0;
+    o[1] = (uint32_t)wall_clock64();
+    o[2] = (uint32_t)tile;
+    o[3] = hw_slot();
+}
+
+// Wave priority by launch position.  A tile's compositing is one serial chain per pixel, so the
+// kernel can end no earlier than its longest tile's chain -- and the longest tiles (launched first)
+// share their SIMDs with up to 7 other waves, which round-robin issue would give an equal share.
+// Raising the first-launched (longest) workgroups' priority lets their chains run at close to
+// their own latency while shorter tiles fill the issue gaps.  Changes no result.
+__device__ __forceinline__ void launch_priority(int b, int prio)
+{
+    if (!prio) return;
+    if (b < 256) __builtin_amdgcn_s_setprio(3);
+    else if (b < 768) __builtin_amdgcn_s_setprio(2);
+    else if (b < 1536) __builtin_amdgcn_s_setprio(1);
+}
+
 // One pixel's front-to-back state (upstream FORWARD::renderCUDA locals).
 struct FwdPixel {
     float T, C0, C1, C2, F0, F1, F2;
     uint32_t contributor, last;
     bool done;
 };
+
+// One front-to-back blend of list slot j with alpha al (upstream FORWARD::renderCUDA; the operation
+// order of oracle render_pixel): stop before the entry once T would fall below 1e-4.
+template <bool kFeat>
+__device__ __forceinline__ void fwd_pixel_blend(FwdPixel& q, float al, int j, uint32_t list_base, const float4* sC,
+                                                const float* sF, float f1)
+{
+    const float test_T = q.T * (1.0f - al);
+    if (test_T < 0.0001f) {
+        q.done = true;
+        return;
+    }
+    const float4 Cc = sC[j];
+    const float w = al * q.T;
+    q.C0 = fma_(Cc.x, w, q.C0);
+    q.C1 = fma_(Cc.y, w, q.C1);
+    q.C2 = fma_(Cc.z, w, q.C2);
+    if (kFeat) {
+        q.F0 = fma_(Cc.w, w, q.F0);
+        q.F1 = fma_(f1, w, q.F1);
+        q.F2 = fma_(sF[j], w, q.F2);
+    }
+    q.T = test_T;
+    q.last = list_base + (uint32_t)j + 1u;  // upstream's 1-based contributor counter
+}
 
 // Output of the tiles without entries among u = j, j + M, ... (background colour, T = 1, no
 // contributors); tiles with entries are skipped (their own workgroups render them).
@@ -153,8 +215,10 @@ __device__ void render_empty_tiles(const RenderParams& p, int j, int M)
     }
 }
 
+template <bool kStats, bool kFeat>
 __global__ __launch_bounds__(kTilePixels) void k_render_forward(RenderParams p)
 {
+    const uint64_t t_start = kStats ? wall_clock64() : 0;
     constexpr int kThreads = kTilePixels;
     __shared__ float4 sA[kThreads];  // x, y, -0.5 conic.x, -0.5 conic.z
     __shared__ float4 sB[kThreads];  // conic.y, opacity, power cutoff, f1
@@ -171,9 +235,11 @@ __global__ __launch_bounds__(kTilePixels) void k_render_forward(RenderParams p)
         if (tile < 0) {  // past the tiles with entries: fill the empty ones, strided
             const int listed = -1 - tile;
             render_empty_tiles(p, (int)blockIdx.x - listed, T - listed);
+            if (kStats) timeline_put(0, t_start, -1);
             return;
         }
     }
+    launch_priority((int)blockIdx.x, p.prio);
     const int tx = tile % p.gx, ty = tile / p.gx;
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     int px, py;
@@ -182,7 +248,6 @@ __global__ __launch_bounds__(kTilePixels) void k_render_forward(RenderParams p)
     const float wx0 = (float)(tx * kTile + 8 * (wave & 1)), wy0 = (float)(ty * kTile + 8 * (wave >> 1));
     const uint2 range = p.ranges[tile];
     const uint32_t start = range.x, end = range.y;
-    const bool feat = p.include_feature != 0;
     const bool inside = px < p.W && py < p.H;
     if (t == 0) s_last = 0;
 
@@ -204,35 +269,34 @@ __global__ __launch_bounds__(kTilePixels) void k_render_forward(RenderParams p)
         }
         __syncthreads();
         const int cnt = (int)min((uint32_t)kThreads, end - base);
-        const int n = wave_compact(sE, cnt, wx0, wy0, lane, sL[wave], [](int) { return true; });
+        const int n = __builtin_amdgcn_readfirstlane(
+            wave_compact(sE, cnt, wx0, wy0, lane, sL[wave], [](int) { return true; }));
         __syncthreads();  // list visible to the wave's other lanes
         const uint32_t list_base = base - start;  // list index of slot 0
-        for (int i = 0; i < n && !q.done; i++) {
-            const int j = sL[wave][i];
-            const float4 A = sA[j];
-            const float4 B = sB[j];
-            const float dx = A.x - pfx, dy = A.y - pfy;
-            const float pw = fma_(A.z * dx, dx, fma_(A.w * dy, dy, -((B.x * dx) * dy)));
-            if (pw > 0.0f || pw < B.z) continue;
-            const float al = fminf(0.99f, B.y * expf_exact(pw));
-            if (al < 1.0f / 255.0f) continue;
-            const float test_T = q.T * (1.0f - al);
-            if (test_T < 0.0001f) {
-                q.done = true;
-                continue;
-            }
-            const float4 Cc = sC[j];
-            const float w = al * q.T;
-            q.C0 = fma_(Cc.x, w, q.C0);
-            q.C1 = fma_(Cc.y, w, q.C1);
-            q.C2 = fma_(Cc.z, w, q.C2);
-            if (feat) {
-                q.F0 = fma_(Cc.w, w, q.F0);
-                q.F1 = fma_(B.w, w, q.F1);
-                q.F2 = fma_(sF[j], w, q.F2);
-            }
-            q.T = test_T;
-            q.last = list_base + (uint32_t)j + 1u;  // upstream's 1-based contributor counter
+        // two list entries per iteration: their power / exp / alpha do not depend on the pixel state,
+        // so the two chains interleave; only the transmittance test and the blend are sequential.
+        // Same operations per entry as one at a time (bit-identical results).
+        for (int i = 0; i < n; i += 2) {
+            if (__ballot(!q.done) == 0ull) break;
+            const int j0 = sL[wave][i];
+            const bool has1 = i + 1 < n;
+            const int j1 = has1 ? sL[wave][i + 1] : j0;
+            const float4 A0 = sA[j0], B0 = sB[j0];
+            const float4 A1 = sA[j1], B1 = sB[j1];
+            const float dx0 = A0.x - pfx, dy0 = A0.y - pfy;
+            const float dx1 = A1.x - pfx, dy1 = A1.y - pfy;
+            const float pw0 = fma_(A0.z * dx0, dx0, fma_(A0.w * dy0, dy0, -((B0.x * dx0) * dy0)));
+            const float pw1 = fma_(A1.z * dx1, dx1, fma_(A1.w * dy1, dy1, -((B1.x * dx1) * dy1)));
+            lsr_f2 pw2;
+            pw2.x = pw0;
+            pw2.y = pw1;
+            const lsr_f2 G2 = expf_exact_render2(pw2);
+            const float al0 = fminf(0.99f, B0.y * G2.x);
+            const float al1 = fminf(0.99f, B1.y * G2.y);
+            const bool ok0 = !(pw0 > 0.0f || pw0 < B0.z) && !(al0 < 1.0f / 255.0f);
+            const bool ok1 = has1 && !(pw1 > 0.0f || pw1 < B1.z) && !(al1 < 1.0f / 255.0f);
+            if (ok0 && !q.done) fwd_pixel_blend<kFeat>(q, al0, j0, list_base, sC, sF, B0.w);
+            if (ok1 && !q.done) fwd_pixel_blend<kFeat>(q, al1, j1, list_base, sC, sF, B1.w);
         }
     }
     // the tile's replay length, for the backward's launch order
@@ -244,6 +308,7 @@ __global__ __launch_bounds__(kTilePixels) void k_render_forward(RenderParams p)
     __syncthreads();
     if (t == 0 && p.sched_counts && s_last > 0)
         schedule_tile(p.sched_counts + kCntBwdClass, p.sched_lists + (size_t)kWorkClasses * T, T, tile, s_last);
+    if (kStats) timeline_put(0, t_start, tile);
     if (!inside) return;
     const size_t HW = (size_t)p.W * p.H;
     const size_t pix = (size_t)py * p.W + px;
@@ -255,6 +320,36 @@ __global__ __launch_bounds__(kTilePixels) void k_render_forward(RenderParams p)
     p.out_lang[pix] = q.F0;
     p.out_lang[HW + pix] = q.F1;
     p.out_lang[2 * HW + pix] = q.F2;
+}
+
+static bool render_stats_on()
+{
+    static bool v = [] {
+        const char* e = getenv("LSR_RENDER_STATS");
+        return e && e[0] == '1';
+    }();
+    return v;
+}
+
+// LSR_PRIO=0 turns the launch-position wave priority off (measurement aid)
+static int prio_levels()
+{
+    static const int v = [] {
+        const char* e = getenv("LSR_PRIO");
+        return (e && e[0] == '0') ? 0 : 1;
+    }();
+    return v;
+}
+
+// LSR_DEBUG_GRID=n launches only the first n workgroups of each render kernel (measurement aid for
+// the timeline: a long tile's time alone vs among others; the outputs are then incomplete)
+static int debug_grid(int tiles)
+{
+    static const int v = [] {
+        const char* e = getenv("LSR_DEBUG_GRID");
+        return e ? atoi(e) : 0;
+    }();
+    return v > 0 && v < tiles ? v : tiles;
 }
 
 // LSR_ORDER=0 launches the tiles in tile order (measurement aid)
@@ -272,7 +367,19 @@ hipError_t launch_render_forward(const RenderParams& pin, int tiles, hipStream_t
     if (tiles == 0) return hipSuccess;
     RenderParams p = pin;
     if (!scheduled()) p.sched_counts = p.sched_lists = nullptr;
-    hipLaunchKernelGGL(k_render_forward, dim3(tiles), dim3(kTilePixels), 0, s, p);
+    p.prio = p.sched_counts ? prio_levels() : 0;
+    const bool feat = p.include_feature != 0;
+    if (render_stats_on()) {
+        tiles = debug_grid(tiles);
+        if (feat)
+            hipLaunchKernelGGL((k_render_forward<true, true>), dim3(tiles), dim3(kTilePixels), 0, s, p);
+        else
+            hipLaunchKernelGGL((k_render_forward<true, false>), dim3(tiles), dim3(kTilePixels), 0, s, p);
+    } else if (feat) {
+        hipLaunchKernelGGL((k_render_forward<false, true>), dim3(tiles), dim3(kTilePixels), 0, s, p);
+    } else {
+        hipLaunchKernelGGL((k_render_forward<false, false>), dim3(tiles), dim3(kTilePixels), 0, s, p);
+    }
     return hipGetLastError();
 }
 
@@ -353,26 +460,26 @@ struct BwdPixel {
     uint32_t last;
 };
 
-__device__ __forceinline__ void bwd_pixel_init(BwdPixel& q, const RenderParams& p, bool inside, size_t pix,
-                                               size_t HW, bool feat)
+template <bool kFeat, bool kColor>
+__device__ __forceinline__ void bwd_pixel_init(BwdPixel& q, const RenderParams& p, bool inside, size_t pix, size_t HW)
 {
     q.T_final = inside ? p.final_T[pix] : 0.0f;
     q.T = q.T_final;
     q.last = inside ? p.n_contrib[pix] : 0u;
     q.dp0 = q.dp1 = q.dp2 = q.dq0 = q.dq1 = q.dq2 = 0.f;
     if (inside) {
-        if (p.dL_dcolor) {  // null: the colour image does not reach the loss (zero gradient)
+        if (kColor) {
             q.dp0 = p.dL_dcolor[pix];
             q.dp1 = p.dL_dcolor[HW + pix];
             q.dp2 = p.dL_dcolor[2 * HW + pix];
         }
-        if (feat && p.dL_dlang) {
+        if (kFeat && p.dL_dlang) {
             q.dq0 = p.dL_dlang[pix];
             q.dq1 = p.dL_dlang[HW + pix];
             q.dq2 = p.dL_dlang[2 * HW + pix];
         }
     }
-    q.bg_term = -q.T_final * fma_(p.bg[2], q.dp2, fma_(p.bg[1], q.dp1, p.bg[0] * q.dp0));
+    q.bg_term = kColor ? -q.T_final * fma_(p.bg[2], q.dp2, fma_(p.bg[1], q.dp1, p.bg[0] * q.dp0)) : 0.0f;
     q.acc0 = q.acc1 = q.acc2 = q.accF0 = q.accF1 = q.accF2 = 0.f;
 }
 
@@ -385,10 +492,10 @@ __device__ __forceinline__ void bwd_pixel_init(BwdPixel& q, const RenderParams& 
 // Constant factors are applied once per (tile, Gaussian) at the flush instead of per pixel
 // (flush_scale): v[0] = dL/dmean2D.x / (2 ddelx_dx), v[1] likewise, v[2..4] = -2 dL/dconic.
 // A = {x, y, -conic.x / 2, -conic.z / 2}, B = {conic.y, opacity, .., ..}.
-template <bool kFeat>
+template <bool kFeat, bool kColor>
 __device__ __forceinline__ void bwd_pixel_blend(BwdPixel& q, float G, float alpha, float dx, float dy,
-                                                const float4& A, const float4& B, const float4& Cc,
-                                                const float2& D, float (&v)[12])
+                                                const float4& A, const float4& B, const float3& C, const float3& F,
+                                                float (&v)[12])
 {
     const float one_m = 1.0f - alpha;
     // one v_rcp_f32 replaces the two IEEE divisions T / (1 - alpha) and T_final / (1 - alpha)
@@ -396,28 +503,34 @@ __device__ __forceinline__ void bwd_pixel_blend(BwdPixel& q, float G, float alph
     q.T = q.T * inv_one_m;
     const float dcd = alpha * q.T;
     // per channel: dL/dalpha += (c - acc) dL/dpix; acc <- acc + alpha (c - acc) (= alpha c + (1 - alpha) acc)
-    float e = Cc.x - q.acc0;
-    float dL_dalpha = e * q.dp0;
-    q.acc0 = fma_(alpha, e, q.acc0);
-    v[6] = dcd * q.dp0;
-    e = Cc.y - q.acc1;
-    dL_dalpha = fma_(e, q.dp1, dL_dalpha);
-    q.acc1 = fma_(alpha, e, q.acc1);
-    v[7] = dcd * q.dp1;
-    e = Cc.z - q.acc2;
-    dL_dalpha = fma_(e, q.dp2, dL_dalpha);
-    q.acc2 = fma_(alpha, e, q.acc2);
-    v[8] = dcd * q.dp2;
+    float dL_dalpha = 0.0f;
+    float e;
+    if (kColor) {
+        e = C.x - q.acc0;
+        dL_dalpha = e * q.dp0;
+        q.acc0 = fma_(alpha, e, q.acc0);
+        v[6] = dcd * q.dp0;
+        e = C.y - q.acc1;
+        dL_dalpha = fma_(e, q.dp1, dL_dalpha);
+        q.acc1 = fma_(alpha, e, q.acc1);
+        v[7] = dcd * q.dp1;
+        e = C.z - q.acc2;
+        dL_dalpha = fma_(e, q.dp2, dL_dalpha);
+        q.acc2 = fma_(alpha, e, q.acc2);
+        v[8] = dcd * q.dp2;
+    } else {  // the colour image does not reach the loss: its terms are exactly zero
+        v[6] = v[7] = v[8] = 0.0f;
+    }
     if (kFeat) {
-        e = Cc.w - q.accF0;
-        dL_dalpha = fma_(e, q.dq0, dL_dalpha);
+        e = F.x - q.accF0;
+        dL_dalpha = kColor ? fma_(e, q.dq0, dL_dalpha) : e * q.dq0;
         q.accF0 = fma_(alpha, e, q.accF0);
         v[9] = dcd * q.dq0;
-        e = D.x - q.accF1;
+        e = F.y - q.accF1;
         dL_dalpha = fma_(e, q.dq1, dL_dalpha);
         q.accF1 = fma_(alpha, e, q.accF1);
         v[10] = dcd * q.dq1;
-        e = D.y - q.accF2;
+        e = F.z - q.accF2;
         dL_dalpha = fma_(e, q.dq2, dL_dalpha);
         q.accF2 = fma_(alpha, e, q.accF2);
         v[11] = dcd * q.dq2;
@@ -425,7 +538,7 @@ __device__ __forceinline__ void bwd_pixel_blend(BwdPixel& q, float G, float alph
         v[9] = v[10] = v[11] = 0.0f;
     }
     // dL/dalpha = T (sum) - T_final / (1 - alpha) (bg . dL/dpix); bg_term = -T_final (bg . dL/dpix)
-    dL_dalpha = fma_(q.bg_term, inv_one_m, dL_dalpha * q.T);
+    dL_dalpha = kColor ? fma_(q.bg_term, inv_one_m, dL_dalpha * q.T) : dL_dalpha * q.T;
     const float dL_dG = B.y * dL_dalpha;
     const float ga = (G * dx) * dL_dG, gb = (G * dy) * dL_dG;
     // dG/ddelx dL/dG = -(ga conic.x + gb conic.y) = 2 (ga A.z - gb conic.y / 2), likewise y
@@ -435,6 +548,13 @@ __device__ __forceinline__ void bwd_pixel_blend(BwdPixel& q, float G, float alph
     v[3] = ga * dy;
     v[4] = gb * dy;
     v[5] = G * dL_dalpha;
+}
+
+// LDS slot of gradient value c: without the colour gradient values 6..8 are not stored.
+template <bool kColor>
+__device__ __forceinline__ int gslot(int c)
+{
+    return kColor || c < 6 ? c : c - 3;
 }
 
 // Factor of gradient slot c applied at the flush (see bwd_pixel_blend).
@@ -448,7 +568,7 @@ __device__ __forceinline__ float flush_scale(int c, int W, int H)
 // an alpha hit, [3] lanes hit, [8 + c] histogram of lanes hit (c = 0..64).  Off by default.
 __device__ unsigned long long g_render_stats[8 + 65];
 
-template <bool kStats, bool kFeat>
+template <bool kStats, bool kFeat, bool kColor>
 __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
 {
     constexpr int kThreads = kTilePixels;
@@ -456,12 +576,16 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
     __shared__ uint32_t s_bmax;  // kStats: the batch's largest per-wave entry count
     __shared__ float4 sA[kThreads];      // x, y, -0.5 conic.x, -0.5 conic.z
     __shared__ float4 sB[kThreads];      // conic.y, opacity, power cutoff, f1
-    __shared__ float4 sC[kThreads];      // r, g, b, f0
-    __shared__ float sF[kThreads];       // f2
-    __shared__ float sG[kThreads * 12];  // per-entry gradient sums of the tile (12 floats)
+    // kColor: sC = {r, g, b, f0}, sF = {f2}; otherwise (the colour gradient is zero) only the language
+    // feature is staged, sF = {f0, f2}, and the tile sums hold 9 slots per entry (no colour slots)
+    constexpr int kGS = kColor ? 12 : 9;
+    __shared__ float4 sC[kColor ? kThreads : 1];
+    __shared__ float sF[kThreads * (kColor ? 1 : 2)];
+    __shared__ float sG[kThreads * kGS];  // per-entry gradient sums of the tile
     __shared__ uint8_t sM[kThreads];     // wave_cover mask (& the waves' contributor bounds)
     __shared__ uint32_t s_wmax[kThreads / 64];
 
+    const uint64_t t_start = kStats ? wall_clock64() : 0;
     int tile = (int)blockIdx.x;
     if (p.sched_counts) {  // tiles without contributors are not scheduled: nothing to do
         const int T = p.gx * p.gy;
@@ -469,6 +593,7 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
                               p.sched_lists + (size_t)kWorkClasses * T, T);
         if (tile < 0) return;
     }
+    launch_priority((int)blockIdx.x, p.prio);
     const int tx = tile % p.gx, ty = tile / p.gx;
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     int px, py;
@@ -480,7 +605,7 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
     const float fscale = flush_scale(t & 15, p.W, p.H);  // this thread's flush slot is always t & 15
 
     BwdPixel q;
-    bwd_pixel_init(q, p, px < p.W && py < p.H, (size_t)py * p.W + px, HW, kFeat);
+    bwd_pixel_init<kFeat, kColor>(q, p, px < p.W && py < p.H, (size_t)py * p.W + px, HW);
     uint32_t wmax = q.last;
 
     if (kStats) {
@@ -508,14 +633,19 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
             const float cut = power_cutoff(b.y);
             sA[t] = make_float4(a.x, a.y, -0.5f * a.z, -0.5f * b.x);
             sB[t] = make_float4(a.w, b.y, cut, c.z);
-            sC[t] = make_float4(b.z, b.w, c.x, c.y);
-            sF[t] = c.w;
+            if (kColor) {
+                sC[t] = make_float4(b.z, b.w, c.x, c.y);
+                sF[t] = c.w;
+            } else {
+                sF[2 * t] = c.y;
+                sF[2 * t + 1] = c.w;
+            }
             const uint32_t k = (uint32_t)kload;
             const uint32_t live = (k < w0 ? 1u : 0u) | (k < w1 ? 2u : 0u) | (k < w2 ? 4u : 0u) | (k < w3 ? 8u : 0u);
             cover = wave_cover(entry_box(a.x, a.y, a.z, a.w, b.x, cut), tx0, ty0) & live;
         }
         sM[t] = (uint8_t)cover;
-        for (int i = t; i < kThreads * 12; i += kThreads) sG[i] = 0.f;
+        for (int i = t; i < kThreads * kGS; i += kThreads) sG[i] = 0.f;
         __syncthreads();
         const int cnt = min(kThreads, maxl - done_cnt);
         // the wave walks the set bits of a ballot over the cover masks (no list, no barrier)
@@ -559,12 +689,20 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
                     }
                 }
                 if (!h) al = G = 0.0f;
-                const float4 Cc = sC[j];
-                const float2 D = kFeat ? make_float2(B.w, sF[j]) : make_float2(0.f, 0.f);
+                float3 C = make_float3(0.f, 0.f, 0.f), F = make_float3(0.f, 0.f, 0.f);
+                if (kColor) {
+                    const float4 Cc = sC[j];
+                    C = make_float3(Cc.x, Cc.y, Cc.z);
+                    if (kFeat) F = make_float3(Cc.w, B.w, sF[j]);
+                } else if (kFeat) {
+                    const float2 f02 = *reinterpret_cast<const float2*>(&sF[2 * j]);
+                    F = make_float3(f02.x, B.w, f02.y);
+                }
                 float v[12];
-                bwd_pixel_blend<kFeat>(q, G, al, dx, dy, A, B, Cc, D, v);
+                bwd_pixel_blend<kFeat, kColor>(q, G, al, dx, dy, A, B, C, F, v);
                 const float tot = wave_reduce_scatter12(v, lane);
-                if (scatter_writer(lane)) atomicAdd(&sG[j * 12 + vidx], tot);
+                if (scatter_writer(lane) && (kColor || vidx < 6 || vidx >= 9))
+                    atomicAdd(&sG[j * kGS + gslot<kColor>(vidx)], tot);
             }
         }
         if (kStats && lane == 0) atomicMax(&s_bmax, nw);
@@ -578,7 +716,8 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
         for (int slot = t; slot < cnt * 16; slot += kThreads) {
             const int e = slot >> 4, c = slot & 15;
             if (c < 12) {
-                const float val = sG[e * 12 + c] * fscale;
+                if (!kColor && c >= 6 && c < 9) continue;  // zero colour gradient
+                const float val = sG[e * kGS + gslot<kColor>(c)] * fscale;
                 if (val != 0.0f) {  // the id again from point_list (an L2 hit; saves 1 KB of LDS)
                     const uint32_t g = p.point_list[start + (uint32_t)(maxl - 1 - (done_cnt + e))];
                     atomicAdd(&p.grad[(size_t)g * kGradStride + c], val);
@@ -590,16 +729,8 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
         __syncthreads();
         for (int i = t; i < 8 + 65; i += kThreads)
             if (s_stat[i]) atomicAdd(&g_render_stats[i], (unsigned long long)s_stat[i]);
+        timeline_put(1, t_start, tile);
     }
-}
-
-static bool render_stats_on()
-{
-    static bool v = [] {
-        const char* e = getenv("LSR_RENDER_STATS");
-        return e && e[0] == '1';
-    }();
-    return v;
 }
 
 hipError_t render_stats_read(unsigned long long* out, int n)
@@ -612,22 +743,43 @@ hipError_t render_stats_read(unsigned long long* out, int n)
     return hipMemcpyToSymbol(HIP_SYMBOL(g_render_stats), zeros, sizeof(zeros), 0, hipMemcpyHostToDevice);
 }
 
+hipError_t render_timeline_read(uint32_t* out, int kernel, int n)
+{
+    if (kernel < 0 || kernel > 1) return hipErrorInvalidValue;
+    if (n > kTimelineMax) n = kTimelineMax;
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_render_timeline), sizeof(uint32_t) * 4 * n,
+                                       sizeof(uint32_t) * 4 * kTimelineMax * kernel, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return e;
+    return hipSuccess;
+}
+
 hipError_t launch_render_backward(const RenderParams& pin, int tiles, hipStream_t s)
 {
     if (tiles == 0) return hipSuccess;
     RenderParams p = pin;
     if (!scheduled()) p.sched_counts = p.sched_lists = nullptr;
+    p.prio = p.sched_counts ? prio_levels() : 0;
     const bool feat = p.include_feature != 0;
+    const bool color = p.dL_dcolor != nullptr;  // null: the colour image does not reach the loss
+    const int variant = (feat ? 1 : 0) | (color ? 2 : 0);
+    if (render_stats_on()) tiles = debug_grid(tiles);
+#define LSR_BWD(S, F, C) hipLaunchKernelGGL((k_render_backward<S, F, C>), dim3(tiles), dim3(kTilePixels), 0, s, p)
     if (render_stats_on()) {
-        if (feat)
-            hipLaunchKernelGGL((k_render_backward<true, true>), dim3(tiles), dim3(kTilePixels), 0, s, p);
-        else
-            hipLaunchKernelGGL((k_render_backward<true, false>), dim3(tiles), dim3(kTilePixels), 0, s, p);
-    } else if (feat) {
-        hipLaunchKernelGGL((k_render_backward<false, true>), dim3(tiles), dim3(kTilePixels), 0, s, p);
+        switch (variant) {
+        case 0: LSR_BWD(true, false, false); break;
+        case 1: LSR_BWD(true, true, false); break;
+        case 2: LSR_BWD(true, false, true); break;
+        default: LSR_BWD(true, true, true); break;
+        }
     } else {
-        hipLaunchKernelGGL((k_render_backward<false, false>), dim3(tiles), dim3(kTilePixels), 0, s, p);
+        switch (variant) {
+        case 0: LSR_BWD(false, false, false); break;
+        case 1: LSR_BWD(false, true, false); break;
+        case 2: LSR_BWD(false, false, true); break;
+        default: LSR_BWD(false, true, true); break;
+        }
     }
+#undef LSR_BWD
     return hipGetLastError();
 }
 

@@ -143,6 +143,26 @@ def test_forward_bit_exact_and_backward(case):
         check_backward(st, inp, run, out)
 
 
+@pytest.mark.parametrize("seed", [0, 5])
+def test_backward_without_colour_gradient(seed):
+    """LangSplat's language-feature step: the colour image does not reach the loss, autograd hands
+    the backward None, and the kernel specialised on a zero colour gradient must match the oracle
+    run with dL/dcolor = 0 (and give a zero colour gradient)."""
+    st, inp = scene(P=1500, W=96, H=80, seed=seed, sh_degree=3, scale_range=(0.03, 0.2))
+    run, std, ind, out = check_forward_exact(st, inp)
+    W, H = st.image_width, st.image_height
+    _, gl = grad_seed(H, W, seed=11)
+    ref = run.backward(torch.zeros_like(gl), gl)
+    nr, color, lang, radii, geom, binning, image = out
+    g = _native.rasterize_gaussians_backward(
+        std, ind["means3D"], ind["shs"], None, ind["language_feature_precomp"], ind["scales"], ind["rotations"],
+        None, radii, None, gl.to(DEV), nr, geom, binning, image)
+    torch.cuda.synchronize()
+    assert not g["colors_precomp"].any()
+    for n in ("means2D", "opacities", "means3D", "language_feature_precomp", "shs", "scales", "rotations"):
+        assert_grad_close(n, g[n].cpu().numpy(), ref[n])
+
+
 def test_colors_precomp_and_cov3d_precomp_paths():
     st, inp = scene(P=400, W=64, H=48, seed=11, sh_degree=3, scale_range=(0.03, 0.2))
     run0 = oracle.forward(st, **inp)

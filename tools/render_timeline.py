@@ -1,0 +1,114 @@
+"""Per-workgroup timeline of the render kernels at a BASELINE config (measurement aid).
+
+    python tools/render_timeline.py [C3]
+
+Runs one forward + backward with LSR_RENDER_STATS=1 and reads the {start, end, tile, CU} record
+every workgroup wrote (include/lsr.h lsr_debug_render_timeline).  Prints, per kernel, the span,
+the summed workgroup time over (span x CUs) (how full the CUs were), the concurrency profile
+(how much of the span ran below half / a quarter of the peak workgroup count: the tail), and the
+longest workgroups with their start times.
+"""
+import math
+import os
+import sys
+from collections import defaultdict
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+os.environ.setdefault("LSR_RENDER_STATS", "1")
+
+from langsplat_amd import _native  # noqa: E402
+from langsplat_amd.rasterizer import GaussianRasterizationSettings  # noqa: E402
+from langsplat_amd.synthetic import CONFIGS, activated_inputs, make_cameras, make_gaussians  # noqa: E402
+
+TICK_US = 0.01  # s_memrealtime: 100 MHz
+
+
+def analyse(name, recs, info=None):
+    recs = [r for r in recs if r[1] != 0 or r[0] != 0]
+    if not recs:
+        print(f"{name}: no records")
+        return
+    t0 = min(r[0] for r in recs)
+    ev = []
+    per_cu = defaultdict(float)
+    dur = []
+    for s, e, tile, slot in recs:
+        s, e = (s - t0) & 0xFFFFFFFF, (e - t0) & 0xFFFFFFFF
+        ev.append((s, 1))
+        ev.append((e, -1))
+        per_cu[slot] += e - s
+        dur.append((e - s, s, tile))
+    span = max(e for e, _ in ev if _ == -1)
+    ev.sort()
+    cur = peak = 0
+    prof = []
+    last = 0
+    for t, d in ev:
+        prof.append((last, t, cur))
+        cur += d
+        peak = max(peak, cur)
+        last = t
+    below = {f: sum(b - a for a, b, c in prof if c < f * peak) for f in (0.5, 0.25)}
+    busy = sum(d for d, _, _ in dur)
+    ncu = len(per_cu)
+    print(f"{name}: {len(recs)} workgroups on {ncu} CUs, span {span * TICK_US:.1f} us, "
+          f"peak concurrency {peak} ({peak / max(ncu, 1):.1f}/CU)")
+    print(f"  sum of workgroup time / (span x peak) = {busy / (span * peak):.3f}; "
+          f"span below 1/2 peak: {below[0.5] / span:.3f}, below 1/4 peak: {below[0.25] / span:.3f}")
+    dur.sort(reverse=True)
+    mean = busy / len(dur)
+    print(f"  workgroup time: mean {mean * TICK_US:.1f} us, max {dur[0][0] * TICK_US:.1f} us")
+    for d, s, tile in dur[:5]:
+        extra = info(tile) if info and tile >= 0 else ""
+        print(f"    tile {tile:6d}: {d * TICK_US:7.1f} us, starts at {s * TICK_US:6.1f} us {extra}")
+
+
+def main():
+    cfg = sys.argv[1] if len(sys.argv) > 1 else "C3"
+    c = CONFIGS[cfg]
+    dev = torch.device("cuda")
+    P, W, H = c["P"], c["width"], c["height"]
+    g = make_gaussians(P, seed=0).to(dev)
+    cam = make_cameras(1, W, H, device=dev)[0]
+    st = GaussianRasterizationSettings(H, W, math.tan(cam.FoVx * 0.5), math.tan(cam.FoVy * 0.5),
+                                       torch.zeros(3, device=dev), 1.0, cam.world_view_transform,
+                                       cam.full_proj_transform, 3, cam.camera_center, False, False, True)
+    with torch.no_grad():
+        inp = activated_inputs(g)
+    gc = torch.randn((3, H, W), device=dev) / (3 * H * W)
+    gl = torch.randn((3, H, W), device=dev) / (3 * H * W)
+    tiles = ((W + 15) // 16) * ((H + 15) // 16)
+    for it in range(3):  # the last iteration's records are read (warm caches)
+        nr, color, lang, radii, geom, binning, image = _native.rasterize_gaussians(
+            st, inp["means3D"], inp["shs"], None, inp["language_feature_precomp"], inp["opacities"],
+            inp["scales"], inp["rotations"], None)
+        torch.cuda.synchronize()
+        fwd = _native.debug_render_timeline(0, tiles)
+        _native.rasterize_gaussians_backward(st, inp["means3D"], inp["shs"], None, inp["language_feature_precomp"],
+                                             inp["scales"], inp["rotations"], None, radii, gc, gl, nr, geom,
+                                             binning, image)
+        torch.cuda.synchronize()
+        bwd = _native.debug_render_timeline(1, tiles)
+    _native.debug_render_stats()
+    lay = _native.state_layout(P, W, H, nr)
+    gx, gy = (W + 15) // 16, (H + 15) // 16
+    rng = image[lay["ranges"]:lay["ranges"] + 8 * tiles].view(torch.int32).view(tiles, 2).cpu().numpy()
+    nc = image[lay["n_contrib"]:lay["n_contrib"] + 4 * W * H].view(torch.int32).cpu().numpy().reshape(H, W)
+    fT = image[lay["final_T"]:lay["final_T"] + 4 * W * H].view(torch.float32).cpu().numpy().reshape(H, W)
+
+    def info(tile):
+        ty, tx = divmod(tile, gx)
+        blk = nc[ty * 16:(ty + 1) * 16, tx * 16:(tx + 1) * 16]
+        t = fT[ty * 16:(ty + 1) * 16, tx * 16:(tx + 1) * 16]
+        return (f"list {int(rng[tile, 1] - rng[tile, 0])}, max n_contrib {int(blk.max())}, "
+                f"saturated px {float((t < 1e-4).mean()):.2f}, mean final T {float(t.mean()):.2e}")
+    nb = sum(1 for r in bwd if r[2] >= 0 and r[1] != 0)
+    analyse(f"{cfg} render forward", fwd, info)
+    analyse(f"{cfg} render backward", [r for r in bwd[:nb]], info)
+
+
+if __name__ == "__main__":
+    main()
