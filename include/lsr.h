@@ -223,9 +223,10 @@ int32_t lsr_mark_visible(int32_t P, const float* means3D, const float* viewmatri
 int32_t lsr_debug_render_stats(uint64_t* out, int32_t n);
 
 /* Measurement hook, not part of the reference interface: with LSR_RENDER_STATS=1 the render
- * kernels (kernel 0 = forward, 1 = backward) record per workgroup b < n: {start, end} (100 MHz
- * wall clock, low 32 bits), the tile (-1: a workgroup that only filled empty tiles) and the
- * hardware slot (XCC_ID << 16 | CU/SH/SE bits of HW_ID) into out[4 b .. 4 b + 3] (synchronous). */
+ * kernels (kernel 0 = forward, 1 = backward) record per workgroup b < n into out[8 b .. 8 b + 7]:
+ * {start, end} (100 MHz wall clock, low 32 bits), the tile (-1: a workgroup that only filled empty
+ * tiles), the hardware slot (XCC_ID << 16 | CU/SH/SE bits of HW_ID), and (forward) the ticks spent
+ * loading, compacting and walking its batches and the batch count (synchronous). */
 int32_t lsr_debug_render_timeline(int32_t kernel, uint32_t* out, int32_t n);
 
 /* ---- the language-feature loss around the rasterizer ----------------

@@ -452,9 +452,15 @@ def debug_render_stats():
 
 def debug_render_timeline(kernel, n):
     """Per-workgroup timeline of the LSR_RENDER_STATS=1 render kernels (kernel 0 forward, 1 backward;
-    include/lsr.h lsr_debug_render_timeline): list of (start, end, tile, hw_slot) for workgroups < n."""
-    arr = (ctypes.c_uint32 * (4 * n))()
+    include/lsr.h lsr_debug_render_timeline): for workgroups < n, dicts with start, end, tile,
+    slot and (forward) the load / compact / walk ticks and the batch count."""
+    W = 8
+    arr = (ctypes.c_uint32 * (W * n))()
     _check(load().lsr_debug_render_timeline(kernel, arr, n), "lsr_debug_render_timeline")
     v = list(arr)
-    return [(v[4 * i], v[4 * i + 1], v[4 * i + 2] if v[4 * i + 2] < 2 ** 31 else v[4 * i + 2] - 2 ** 32, v[4 * i + 3])
-            for i in range(n)]
+    out = []
+    for i in range(n):
+        r = v[W * i:W * i + W]
+        out.append({"start": r[0], "end": r[1], "tile": r[2] if r[2] < 2 ** 31 else r[2] - 2 ** 32, "slot": r[3],
+                    "load": r[4], "compact": r[5], "walk": r[6], "batches": r[7]})
+    return out

@@ -64,21 +64,49 @@ __device__ __forceinline__ uint32_t wave_cover(const float4& E, float x0, float 
     return (xa && ya ? 1u : 0u) | (xb && ya ? 2u : 0u) | (xa && yb ? 4u : 0u) | (xb && yb ? 8u : 0u);
 }
 
-// Compacts the batch slots [0, cnt) whose reach box overlaps the wave's 8 x 8 pixel block at
-// (wx0, wy0) (and pass `keep`) into list[0, n); returns n.  An entry whose box misses the block
-// fails the cutoff test in every pixel of it, so skipping it is exact.
-template <typename Keep>
-__device__ __forceinline__ int wave_compact(const float4* sE, int cnt, float wx0, float wy0, int lane, uint8_t* list,
-                                            Keep keep)
+// Does the cutoff ellipse Q(p - mu) <= k (Q = [[a, b], [b, c]], the conic; k = -2 cutoff) meet the
+// rectangle of pixel centres [x0, x0 + 7] x [y0, y0 + 7]?  Exact minimum of the convex quadratic over
+// the rectangle: 0 if the centre is inside, else the smallest of its four edge minima (each the 1D
+// minimiser clamped to the edge).  A "no" is only returned with a margin (0.1 % of k + 1e-4 of the
+// largest term magnitude over the rectangle) far above the fp32 error of the kernels' power
+// evaluation, so an entry is dropped only where every pixel fails the cutoff test: exact, like the
+// box test.  Degenerate conics answer "yes".
+__device__ __forceinline__ bool ellipse_meets_block(float x, float y, float a, float b, float c, float k, float x0,
+                                                    float y0)
+{
+    const float u0 = x0 - x, u1 = x0 + 7.0f - x, w0 = y0 - y, w1 = y0 + 7.0f - y;
+    if (u0 <= 0.0f && u1 >= 0.0f && w0 <= 0.0f && w1 >= 0.0f) return true;
+    if (!(a > 0.0f && c > 0.0f && a * c - b * b > 0.0f)) return true;
+    const float ia = __builtin_amdgcn_rcpf(a), ic = __builtin_amdgcn_rcpf(c);
+    auto q = [&](float u, float w) { return fma_(a * u, u, fma_(2.0f * b * u, w, c * w * w)); };
+    auto on_u = [&](float u) { return q(u, fminf(fmaxf(-b * u * ic, w0), w1)); };
+    auto on_w = [&](float w) { return q(fminf(fmaxf(-b * w * ia, u0), u1), w); };
+    const float m = fminf(fminf(on_u(u0), on_u(u1)), fminf(on_w(w0), on_w(w1)));
+    const float U = fmaxf(fabsf(u0), fabsf(u1)), V = fmaxf(fabsf(w0), fabsf(w1));
+    const float S = fma_(a * U, U, fma_(c * V, V, 2.0f * fabsf(b) * U * V));
+    return m <= fma_(k, 1.001f, fma_(1e-4f, S, 1e-6f));
+}
+
+// 4-bit mask of the tile's wave blocks (wave_cover) an entry can reach: the box test, refined by the
+// exact ellipse test for the blocks the box meets.  conic = (a, b, c), cut = power_cutoff.
+__device__ __forceinline__ uint32_t entry_cover(float x, float y, float a, float b, float c, float cut, float x0,
+                                                float y0)
+{
+    uint32_t m = wave_cover(entry_box(x, y, a, b, c, cut), x0, y0);
+    const float k = -2.0f * cut;
+    for (uint32_t w = 0; w < 4; w++)
+        if (((m >> w) & 1u) && !ellipse_meets_block(x, y, a, b, c, k, x0 + 8.0f * (w & 1), y0 + 8.0f * (w >> 1)))
+            m &= ~(1u << w);
+    return m;
+}
+
+// Compacts the batch slots [0, cnt) whose cover mask includes this wave into list[0, n); returns n.
+__device__ __forceinline__ int wave_compact(const uint8_t* sM, int cnt, int wave, int lane, uint8_t* list)
 {
     int n = 0;
     for (int r = 0; r < cnt; r += 64) {
         const int e = r + lane;
-        bool ov = false;
-        if (e < cnt && keep(e)) {
-            const float4 E = sE[e];
-            ov = E.y >= wx0 && E.x <= wx0 + 7.0f && E.w >= wy0 && E.z <= wy0 + 7.0f;
-        }
+        const bool ov = e < cnt && ((sM[e] >> wave) & 1u);
         const uint64_t m = __ballot(ov);
         if (ov) list[n + __popcll(m & ((1ull << lane) - 1ull))] = (uint8_t)e;
         n += __popcll(m);
@@ -126,7 +154,8 @@ __device__ __forceinline__ int scheduled_tile(int b, const uint32_t* counts, con
 // kernels {start, end} (s_memrealtime, 100 MHz), the tile and the hardware slot (XCC_ID << 16 |
 // HW_ID bits 8..15: cu, sh, se).  Off by default.
 constexpr int kTimelineMax = 1 << 15;
-__device__ uint32_t g_render_timeline[2][kTimelineMax * 4];
+constexpr int kTimelineWords = 8;  // start, end, tile, slot, load, compact, walk (ticks), batches
+__device__ uint32_t g_render_timeline[2][kTimelineMax * kTimelineWords];
 
 __device__ __forceinline__ uint32_t hw_slot()
 {
@@ -135,15 +164,35 @@ __device__ __forceinline__ uint32_t hw_slot()
     return ((xcc & 0xFu) << 16) | ((hw >> 8) & 0xFFu);
 }
 
-__device__ __forceinline__ void timeline_put(int kernel, uint64_t t0, int tile)
+// Per-batch phase ticks of a workgroup as thread 0 sees them: load (global gather -> LDS, up to the
+// barrier), compact / cover (up to the next barrier), walk (up to the next batch's start, so it
+// includes the wait for the workgroup's slowest wave).
+struct PhaseTicks {
+    uint64_t load = 0, compact = 0, walk = 0, mark = 0;
+    uint32_t batches = 0;
+    bool stopped = false;  // left the batch loop at a batch start (its walk time already counted)
+    __device__ void begin() { mark = wall_clock64(); }
+    __device__ void lap(uint64_t& acc)
+    {
+        const uint64_t now = wall_clock64();
+        acc += now - mark;
+        mark = now;
+    }
+};
+
+__device__ __forceinline__ void timeline_put(int kernel, uint64_t t0, int tile, const PhaseTicks& ph = PhaseTicks())
 {
     const int b = (int)blockIdx.x;
     if (threadIdx.x != 0 || b >= kTimelineMax) return;
-    uint32_t* o = g_render_timeline[kernel] + 4 * b;
+    uint32_t* o = g_render_timeline[kernel] + kTimelineWords * b;
     o[0] = (uint32_t)t0;
     o[1] = (uint32_t)wall_clock64();
     o[2] = (uint32_t)tile;
     o[3] = hw_slot();
+    o[4] = (uint32_t)ph.load;
+    o[5] = (uint32_t)ph.compact;
+    o[6] = (uint32_t)ph.walk;
+    o[7] = ph.batches;
 }
 
 // Wave priority by launch position.  A tile's compositing is one serial chain per pixel, so the
@@ -224,7 +273,7 @@ __global__ __launch_bounds__(kTilePixels) void k_render_forward(RenderParams p)
     __shared__ float4 sB[kThreads];  // conic.y, opacity, power cutoff, f1
     __shared__ float4 sC[kThreads];  // r, g, b, f0
     __shared__ float sF[kThreads];   // f2
-    __shared__ float4 sE[kThreads];  // reach box (entry_box)
+    __shared__ uint8_t sM[kThreads];  // entry_cover mask
     __shared__ uint8_t sL[kThreads / 64][kThreads];  // per-wave culled slot lists
     __shared__ uint32_t s_last;
 
@@ -245,15 +294,23 @@ __global__ __launch_bounds__(kTilePixels) void k_render_forward(RenderParams p)
     int px, py;
     pixel_map(tx, ty, t, px, py);
     const float pfx = (float)px, pfy = (float)py;
-    const float wx0 = (float)(tx * kTile + 8 * (wave & 1)), wy0 = (float)(ty * kTile + 8 * (wave >> 1));
+    const float tx0 = (float)(tx * kTile), ty0 = (float)(ty * kTile);
     const uint2 range = p.ranges[tile];
     const uint32_t start = range.x, end = range.y;
     const bool inside = px < p.W && py < p.H;
     if (t == 0) s_last = 0;
 
     FwdPixel q{1.0f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0u, 0u, !inside};
+    PhaseTicks ph;
+    if (kStats) ph.begin();
     for (uint32_t base = start; base < end; base += kThreads) {
-        if (__syncthreads_count(q.done) == kThreads) break;
+        const bool all_done = __syncthreads_count(q.done) == kThreads;
+        if (kStats && base != start) ph.lap(ph.walk);
+        if (all_done) {
+            if (kStats) ph.stopped = true;
+            break;
+        }
+        if (kStats) ph.batches++;
         const uint32_t idx = base + t;
         if (idx < end) {
             const uint32_t g = p.point_list[idx];
@@ -265,13 +322,15 @@ __global__ __launch_bounds__(kTilePixels) void k_render_forward(RenderParams p)
             sB[t] = make_float4(a.w, b.y, cut, c.z);
             sC[t] = make_float4(b.z, b.w, c.x, c.y);
             sF[t] = c.w;
-            sE[t] = entry_box(a.x, a.y, a.z, a.w, b.x, cut);
+            sM[t] = (uint8_t)entry_cover(a.x, a.y, a.z, a.w, b.x, cut, tx0, ty0);
         }
         __syncthreads();
+        if (kStats) ph.lap(ph.load);
         const int cnt = (int)min((uint32_t)kThreads, end - base);
         const int n = __builtin_amdgcn_readfirstlane(
-            wave_compact(sE, cnt, wx0, wy0, lane, sL[wave], [](int) { return true; }));
+            wave_compact(sM, cnt, wave, lane, sL[wave]));
         __syncthreads();  // list visible to the wave's other lanes
+        if (kStats) ph.lap(ph.compact);
         const uint32_t list_base = base - start;  // list index of slot 0
         // two list entries per iteration: their power / exp / alpha do not depend on the pixel state,
         // so the two chains interleave; only the transmittance test and the blend are sequential.
@@ -308,7 +367,10 @@ __global__ __launch_bounds__(kTilePixels) void k_render_forward(RenderParams p)
     __syncthreads();
     if (t == 0 && p.sched_counts && s_last > 0)
         schedule_tile(p.sched_counts + kCntBwdClass, p.sched_lists + (size_t)kWorkClasses * T, T, tile, s_last);
-    if (kStats) timeline_put(0, t_start, tile);
+    if (kStats) {
+        if (!ph.stopped && ph.batches) ph.lap(ph.walk);  // the last batch's walk
+        timeline_put(0, t_start, tile, ph);
+    }
     if (!inside) return;
     const size_t HW = (size_t)p.W * p.H;
     const size_t pix = (size_t)py * p.W + px;
@@ -642,7 +704,7 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
             }
             const uint32_t k = (uint32_t)kload;
             const uint32_t live = (k < w0 ? 1u : 0u) | (k < w1 ? 2u : 0u) | (k < w2 ? 4u : 0u) | (k < w3 ? 8u : 0u);
-            cover = wave_cover(entry_box(a.x, a.y, a.z, a.w, b.x, cut), tx0, ty0) & live;
+            cover = entry_cover(a.x, a.y, a.z, a.w, b.x, cut, tx0, ty0) & live;
         }
         sM[t] = (uint8_t)cover;
         for (int i = t; i < kThreads * kGS; i += kThreads) sG[i] = 0.f;
@@ -747,8 +809,9 @@ hipError_t render_timeline_read(uint32_t* out, int kernel, int n)
 {
     if (kernel < 0 || kernel > 1) return hipErrorInvalidValue;
     if (n > kTimelineMax) n = kTimelineMax;
-    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_render_timeline), sizeof(uint32_t) * 4 * n,
-                                       sizeof(uint32_t) * 4 * kTimelineMax * kernel, hipMemcpyDeviceToHost);
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_render_timeline), sizeof(uint32_t) * kTimelineWords * n,
+                                       sizeof(uint32_t) * kTimelineWords * kTimelineMax * kernel,
+                                       hipMemcpyDeviceToHost);
     if (e != hipSuccess) return e;
     return hipSuccess;
 }

@@ -27,7 +27,7 @@ TICK_US = 0.01  # s_memrealtime: 100 MHz
 
 
 def analyse(name, recs, info=None):
-    recs = [r for r in recs if r[1] != 0 or r[0] != 0]
+    recs = [(r["start"], r["end"], r["tile"], r["slot"], r) for r in recs if r["end"] != 0 or r["start"] != 0]
     if not recs:
         print(f"{name}: no records")
         return
@@ -35,7 +35,10 @@ def analyse(name, recs, info=None):
     ev = []
     per_cu = defaultdict(float)
     dur = []
-    for s, e, tile, slot in recs:
+    phases = {}
+    for r in recs:
+        phases[r[2]] = r[4]
+    for s, e, tile, slot, _ in recs:
         s, e = (s - t0) & 0xFFFFFFFF, (e - t0) & 0xFFFFFFFF
         ev.append((s, 1))
         ev.append((e, -1))
@@ -63,6 +66,10 @@ def analyse(name, recs, info=None):
     print(f"  workgroup time: mean {mean * TICK_US:.1f} us, max {dur[0][0] * TICK_US:.1f} us")
     for d, s, tile in dur[:5]:
         extra = info(tile) if info and tile >= 0 else ""
+        ph = phases.get(tile)
+        if ph and ph["batches"]:
+            extra += (f"\n        {ph['batches']} batches: load {ph['load'] * TICK_US:.1f} us, compact "
+                      f"{ph['compact'] * TICK_US:.1f} us, walk {ph['walk'] * TICK_US:.1f} us")
         print(f"    tile {tile:6d}: {d * TICK_US:7.1f} us, starts at {s * TICK_US:6.1f} us {extra}")
 
 
@@ -105,7 +112,7 @@ def main():
         t = fT[ty * 16:(ty + 1) * 16, tx * 16:(tx + 1) * 16]
         return (f"list {int(rng[tile, 1] - rng[tile, 0])}, max n_contrib {int(blk.max())}, "
                 f"saturated px {float((t < 1e-4).mean()):.2f}, mean final T {float(t.mean()):.2e}")
-    nb = sum(1 for r in bwd if r[2] >= 0 and r[1] != 0)
+    nb = sum(1 for r in bwd if r["tile"] >= 0 and r["end"] != 0)
     analyse(f"{cfg} render forward", fwd, info)
     analyse(f"{cfg} render backward", [r for r in bwd[:nb]], info)
 
