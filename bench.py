@@ -259,6 +259,20 @@ def main():
     elapsed = time.perf_counter() - t0
     _native.profile_enable(False)
     dom = _native.profile_report()[DOMINANT_STAGE]
+    # the same step with every geometry gradient computed although no parameter needs one (what the
+    # reference extension does; LSR_ALL_GRADS=1): reported beside, never as `value`
+    _native.FORCE_GEOMETRY_GRADS = True
+    for _ in range(2):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    elapsed_all = time.perf_counter() - t1
+    _native.FORCE_GEOMETRY_GRADS = os.environ.get("LSR_ALL_GRADS", "0") == "1"
     # stage breakdown: a separate, untimed pass with every stage profiled
     prof_steps = min(args.steps, 10)
     _native.profile_enable(True)
@@ -317,7 +331,11 @@ def main():
                                f"include_feature train step, 1 view per GPU",
                    "gaussians": P, "width": W, "height": H, "views": world, "parallelism": f"dp{world} (views)",
                    "blends_per_step": blends_all, "num_rendered_rank0": nr, "visible_rank0": visible,
-                   "activation_and_loss": "fused" if fused else "torch"},
+                   "activation_and_loss": "fused" if fused else "torch",
+                   "gradients": "all geometry" if _native.FORCE_GEOMETRY_GRADS else
+                                "as needed: means2D + language feature (geometry frozen, "
+                                "scene/gaussian_model.py:203-217)"},
+        "ms_per_step_all_gradients": round(1000.0 * elapsed_all / args.steps, 4),
         "raster_ms_per_step": round(raster_ms, 4),
         "stages_ms_per_step": {k: round(v["total_ms"] / prof_steps, 4) for k, v in sorted(prof.items())},
         "roofline": roofline,

@@ -119,7 +119,12 @@ typedef struct lsr_forward_args {
 
 /* Inputs/outputs of _C.rasterize_gaussians_backward.  Every non-NULL output is fully written
  * (zeros for culled Gaussians).  dL_dsh may be NULL when shs is NULL; dL_dscales/dL_drotations
- * may be NULL when cov3D_precomp is given; dL_dcov3D may be NULL when scales are given. */
+ * may be NULL when cov3D_precomp is given; dL_dcov3D may be NULL when scales are given.
+ * Geometry gradients are all-or-nothing: when dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D,
+ * dL_dsh, dL_dsh_rest, dL_dscales and dL_drotations are ALL NULL (no geometry input needs a
+ * gradient: ctx.needs_input_grad, e.g. LangSplat's language step, scene/gaussian_model.py:203-217),
+ * only dL_dmeans2D and dL_dlanguage_feature (either may be NULL too) are computed and the
+ * preprocess backward is not run. */
 typedef struct lsr_backward_args {
     int32_t P;
     int32_t M;

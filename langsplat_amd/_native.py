@@ -320,12 +320,24 @@ def rasterize_gaussians(rs, means3D, shs, colors_precomp, language_feature, opac
             alloc.get(LSR_BUF_IMAGE))
 
 
+# LSR_ALL_GRADS=1 (or setting this to True) computes every geometry gradient even when no input
+# needs one -- the reference extension's behaviour; kept for comparisons and debugging.
+FORCE_GEOMETRY_GRADS = os.environ.get("LSR_ALL_GRADS", "0") == "1"
+
+
+def geometry_grads_needed(needs_input_grad, geometry_inputs):
+    """True if an autograd input among `geometry_inputs` (everything but means2D and the language
+    feature) needs a gradient -- torch's ctx.needs_input_grad, as any autograd.Function uses it."""
+    return FORCE_GEOMETRY_GRADS or any(needs_input_grad[i] for i in geometry_inputs)
+
+
 def rasterize_gaussians_backward(rs, means3D, shs, colors_precomp, language_feature, scales, rotations,
                                  cov3D_precomp, radii, grad_color, grad_language, num_rendered, geom, binning,
-                                 image, raw=0, shs_rest=None, opacities=None):
+                                 image, raw=0, shs_rest=None, opacities=None, geometry=True):
     """Native backward: returns the gradient tensors keyed like the reference's inputs (with raw
     flags: w.r.t. the raw parameters; "shs" is then dL/dfeatures_dc and "shs_rest"
-    dL/dfeatures_rest)."""
+    dL/dfeatures_rest).  geometry=False (no geometry input needs a gradient): only "means2D" and
+    "language_feature_precomp" are computed, the other entries are None (include/lsr.h)."""
     lib = load()
     device = means3D.device
     P = int(means3D.shape[0])
@@ -336,17 +348,18 @@ def rasterize_gaussians_backward(rs, means3D, shs, colors_precomp, language_feat
     keep: list = []
     s = make_settings(rs, keep)
     # every gradient output is a view of ONE allocation (one caching-allocator call per backward)
-    shapes = [("means2D", (P, 3)), ("colors_precomp", (P, 3)), ("language_feature_precomp", (P, 3)),
-              ("opacities", (P, 1)), ("means3D", (P, 3))]
-    if _ptr(cov3D_precomp) is not None:
+    shapes = [("means2D", (P, 3)), ("language_feature_precomp", (P, 3))]
+    if geometry:
+        shapes += [("colors_precomp", (P, 3)), ("opacities", (P, 1)), ("means3D", (P, 3))]
+    if geometry and _ptr(cov3D_precomp) is not None:
         shapes.append(("cov3D_precomp", (P, 6)))
-    if M_dc > 0:
+    if geometry and M_dc > 0:
         shapes.append(("shs", (P, M_dc, 3)))
-    if split:
+    if geometry and split:
         shapes.append(("shs_rest", (P, M_rest, 3)))
-    if _ptr(scales) is not None:
+    if geometry and _ptr(scales) is not None:
         shapes.append(("scales", (P, 3)))
-    if _ptr(rotations) is not None:
+    if geometry and _ptr(rotations) is not None:
         shapes.append(("rotations", (P, 4)))
     sizes = [math.prod(sh) for _, sh in shapes]
     aligned = [(n + 63) // 64 * 64 for n in sizes]  # 256-B aligned views (vector loads/stores)

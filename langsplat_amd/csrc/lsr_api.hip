@@ -328,13 +328,18 @@ int32_t lsr_backward(const lsr_settings* s, const lsr_backward_args* a, lsr_allo
     if (!s || !a || !alloc) return fail(LSR_ERR_INVALID, "lsr_backward: null argument");
     const int P = a->P, W = s->image_width, H = s->image_height;
     if (P < 0 || W <= 0 || H <= 0) return fail(LSR_ERR_INVALID, "lsr_backward: invalid P or image size");
-    if (!a->dL_dmeans2D || !a->dL_dcolors || !a->dL_dlanguage_feature || !a->dL_dopacity || !a->dL_dmeans3D)
-        return fail(LSR_ERR_INVALID, "lsr_backward: missing output pointer");
-    if ((a->shs && !a->dL_dsh) || (a->cov3D_precomp && !a->dL_dcov3D))
-        return fail(LSR_ERR_INVALID, "lsr_backward: missing dL_dsh / dL_dcov3D output");
+    // geometry outputs: all given (full backward) or all NULL (screen-space + language only)
+    const bool geometry = a->dL_dcolors || a->dL_dopacity || a->dL_dmeans3D || a->dL_dcov3D || a->dL_dsh ||
+                          a->dL_dsh_rest || a->dL_dscales || a->dL_drotations;
+    if (geometry) {
+        if (!a->dL_dmeans2D || !a->dL_dcolors || !a->dL_dlanguage_feature || !a->dL_dopacity || !a->dL_dmeans3D)
+            return fail(LSR_ERR_INVALID, "lsr_backward: missing output pointer");
+        if ((a->shs && !a->dL_dsh) || (a->cov3D_precomp && !a->dL_dcov3D))
+            return fail(LSR_ERR_INVALID, "lsr_backward: missing dL_dsh / dL_dcov3D output");
+    }
     if (a->raw & ~(LSR_RAW_OPACITY | LSR_RAW_SCALES | LSR_RAW_ROTATIONS | LSR_RAW_LANGUAGE))
         return fail(LSR_ERR_INVALID, "lsr_backward: unknown raw flag");
-    if (a->shs_rest && (!a->shs || a->M < 2 || !a->dL_dsh_rest))
+    if (geometry && a->shs_rest && (!a->shs || a->M < 2 || !a->dL_dsh_rest))
         return fail(LSR_ERR_INVALID, "lsr_backward: shs_rest needs shs, M >= 2 and dL_dsh_rest");
     if ((a->raw & LSR_RAW_OPACITY) && P > 0 && !a->opacities)
         return fail(LSR_ERR_INVALID, "lsr_backward: raw opacities missing");
@@ -369,6 +374,14 @@ int32_t lsr_backward(const lsr_settings* s, const lsr_backward_args* a, lsr_allo
     rp.dL_dlang = a->dL_dout_language_feature;
     rp.grad = grad;
     if (a->num_rendered > 0) LSR_TRY(launch_render_backward(rp, L.tiles, stream), "render backward");
+    if (!geometry) {
+        LSR_TRY(launch_grad_epilogue(P, a->radii, grad, a->language_feature, (a->raw & LSR_RAW_LANGUAGE) ? 1 : 0,
+                                     a->dL_dmeans2D, rp.include_feature ? a->dL_dlanguage_feature : nullptr, stream),
+                "gradient epilogue");
+        if (!rp.include_feature && a->dL_dlanguage_feature)
+            LSR_TRY(hipMemsetAsync(a->dL_dlanguage_feature, 0, (size_t)P * 3 * 4, stream), "memset dlang");
+        return LSR_OK;
+    }
 
     PreprocessBwdParams bp{};
     bp.P = P;

@@ -179,6 +179,8 @@ struct RenderParams {
 
 hipError_t launch_preprocess(const PreprocessParams& p, hipStream_t s);
 hipError_t launch_preprocess_backward(const PreprocessBwdParams& p, hipStream_t s);
+hipError_t launch_grad_epilogue(int P, const int* radii, const float* grad, const float* lang, int raw_lang,
+                                float* dmeans2D, float* dlang, hipStream_t s);
 hipError_t launch_mark_visible(int P, const float* means, const float* view, const float* proj,
                                uint8_t* visible, hipStream_t s);
 

@@ -98,16 +98,17 @@ class _RasterizeGaussians(torch.autograd.Function):
         gl = grad_out_language_feature if ctx.use_lang else None  # grad_out_color None: zero colour gradient
         args = (means3D, sh, colors_precomp, lang if ctx.use_lang else None, scales, rotations, cov3Ds_precomp,
                 radii, grad_out_color, gl, ctx.num_rendered, geom, binning, image)
+        geometry = _native.geometry_grads_needed(ctx.needs_input_grad, (0, 2, 3, 5, 6, 7, 8))
         if rs.debug:
             cpu_args = _cpu_deep_copy(args)
             try:
-                g = _native.rasterize_gaussians_backward(rs, *args)
+                g = _native.rasterize_gaussians_backward(rs, *args, geometry=geometry)
             except Exception as ex:
                 torch.save(cpu_args, "snapshot_bw.dump")
                 print("\nAn error occured in backward. Writing snapshot_bw.dump for debugging.\n")
                 raise ex
         else:
-            g = _native.rasterize_gaussians_backward(rs, *args)
+            g = _native.rasterize_gaussians_backward(rs, *args, geometry=geometry)
 
         def want(i, t):
             return t if ctx.needs_input_grad[i] else None
@@ -189,17 +190,18 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
         m3, dc, rest, ln, op, sc, ro, radii, geom, binning, image = ctx.saved_tensors
         rest = rest if rest.numel() > 0 else None  # grad_out_color None: zero colour gradient
         gl = grad_out_language_feature if ctx.use_lang else None
+        geometry = _native.geometry_grads_needed(ctx.needs_input_grad, (0, 2, 3, 4, 5, 6))
         g = _guarded(rs, "snapshot_bw.dump",
                      "\nAn error occured in backward. Writing snapshot_bw.dump for debugging.\n",
                      lambda *a: _native.rasterize_gaussians_backward(rs, *a[:14], raw=ctx.raw, shs_rest=a[14],
-                                                                     opacities=a[15]),
+                                                                     opacities=a[15], geometry=geometry),
                      (m3, dc, None, ln if ctx.use_lang else None, sc, ro, None, radii, grad_out_color, gl,
                       ctx.num_rendered, geom, binning, image, rest, op))
 
         def want(i, t):
             return t if ctx.needs_input_grad[i] else None
 
-        d_rest = g["shs_rest"]
+        d_rest = g.get("shs_rest")
         if d_rest is None and ctx.rest_shape is not None and ctx.needs_input_grad[3]:
             d_rest = torch.zeros(ctx.rest_shape, dtype=torch.float32, device=m3.device)
         return (want(0, g["means3D"]), want(1, g["means2D"]), want(2, g["shs"]), want(3, d_rest),

@@ -152,3 +152,28 @@ def test_render_fused_matches_unfused(monkeypatch):
     torch.testing.assert_close(l1, l0, rtol=1e-5, atol=1e-6)
     for k in g0:
         assert_grad_close(k, g1[k], g0[k])
+
+
+@pytest.mark.parametrize("fused", [False, True])
+def test_language_step_skips_geometry_gradients(fused, monkeypatch):
+    """LangSplat's language step freezes every geometry parameter (scene/gaussian_model.py:203-217):
+    the backward then computes only dL/dmeans2D and dL/dlanguage (include/lsr.h, geometry outputs
+    all NULL) and must give what the full backward gives for those two (up to the order of the
+    render backward's float atomics, which differs from run to run)."""
+    W, H = 96, 64
+    g = make_gaussians(1500, seed=9, scale_range=(0.03, 0.2))
+    cam = make_cameras(1, W, H, device=DEV)[0]
+    _, gl = (t.to(DEV) for t in grad_seed(H, W, seed=12))
+    monkeypatch.setenv("LANGSPLAT_AMD_FUSED", "1" if fused else "0")
+    out = {}
+    for force in (True, False):
+        monkeypatch.setattr(_native, "FORCE_GEOMETRY_GRADS", force)
+        m = _Model(g, DEV)
+        for n in ("xyz", "features_dc", "features_rest", "scaling", "rotation", "opacity"):
+            getattr(m, "_" + n).requires_grad_(False)
+        pkg = render(cam, m, _Pipe, torch.zeros(3, device=DEV), _Opt)
+        (pkg["language_feature_image"] * gl).sum().backward()
+        out[force] = (m._language_feature.grad.detach().clone(), pkg["viewspace_points"].grad.detach().clone())
+    for k in range(2):
+        assert_grad_close(f"out{k}", out[False][k].cpu().numpy(), out[True][k].cpu().numpy())
+    assert out[False][0].abs().sum() > 0
