@@ -373,6 +373,7 @@ int32_t lsr_backward(const lsr_settings* s, const lsr_backward_args* a, lsr_allo
     rp.dL_dcolor = a->dL_dout_color;
     rp.dL_dlang = a->dL_dout_language_feature;
     rp.grad = grad;
+    rp.geo = geometry ? 1 : 0;
     if (a->num_rendered > 0) LSR_TRY(launch_render_backward(rp, L.tiles, stream), "render backward");
     if (!geometry) {
         LSR_TRY(launch_grad_epilogue(P, a->radii, grad, a->language_feature, (a->raw & LSR_RAW_LANGUAGE) ? 1 : 0,

@@ -172,6 +172,7 @@ struct RenderParams {
     uint32_t* sched_counts;
     uint32_t* sched_lists;
     int prio;  // wave priority by launch position (longest tiles highest), 0: off
+    int geo;   // backward: the conic / opacity partials are needed (geometry gradients)
     // backward
     const float *dL_dcolor, *dL_dlang;
     float* grad;

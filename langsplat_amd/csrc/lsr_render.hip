@@ -554,7 +554,7 @@ __device__ __forceinline__ void bwd_pixel_init(BwdPixel& q, const RenderParams& 
 // Constant factors are applied once per (tile, Gaussian) at the flush instead of per pixel
 // (flush_scale): v[0] = dL/dmean2D.x / (2 ddelx_dx), v[1] likewise, v[2..4] = -2 dL/dconic.
 // A = {x, y, -conic.x / 2, -conic.z / 2}, B = {conic.y, opacity, .., ..}.
-template <bool kFeat, bool kColor>
+template <bool kFeat, bool kColor, bool kGeo>
 __device__ __forceinline__ void bwd_pixel_blend(BwdPixel& q, float G, float alpha, float dx, float dy,
                                                 const float4& A, const float4& B, const float3& C, const float3& F,
                                                 float (&v)[12])
@@ -606,17 +606,55 @@ __device__ __forceinline__ void bwd_pixel_blend(BwdPixel& q, float G, float alph
     // dG/ddelx dL/dG = -(ga conic.x + gb conic.y) = 2 (ga A.z - gb conic.y / 2), likewise y
     v[0] = fma_(-0.5f, gb * B.x, ga * A.z);
     v[1] = fma_(-0.5f, ga * B.x, gb * A.w);
-    v[2] = ga * dx;
-    v[3] = ga * dy;
-    v[4] = gb * dy;
-    v[5] = G * dL_dalpha;
+    if (kGeo) {  // conic and opacity partials: only the geometry gradients use them
+        v[2] = ga * dx;
+        v[3] = ga * dy;
+        v[4] = gb * dy;
+        v[5] = G * dL_dalpha;
+    } else {
+        v[2] = v[3] = v[4] = v[5] = 0.0f;
+    }
 }
 
-// LDS slot of gradient value c: without the colour gradient values 6..8 are not stored.
-template <bool kColor>
+// The language step's five values (no geometry, no colour gradient): v[0], v[1] (screen-space) and
+// v[9..11] (language).  Reduce-scatter: lane bit 5 picks v0 / f0, v1 / f1, f2 / - (permlane32),
+// bit 4 r0 / r1 (permlane16; r2 summed on both sides), bit 3 s0 / s1 (row_mirror), then bits 2..0.
+// Lane l then holds the wave total of value scatter_index5(l); scatter_writer5 picks one lane each.
+__device__ __forceinline__ float wave_reduce_scatter5(const float (&v)[12], int lane)
+{
+    const float r0 = swap32_add(v[0], v[9]), r1 = swap32_add(v[1], v[10]), r2 = swap32_add(v[11], 0.0f);
+    const float s0 = swap16_add(r0, r1), s1 = swap16_add(r2, r2);
+    float w = mirror_add<0x140>(s0, s1, (lane & 8) != 0);  // row_mirror
+    w += dpp<0x141>(w);                                   // row_half_mirror
+    w += dpp<0x4E>(w);                                    // quad_perm [2,3,0,1]
+    w += dpp<0xB1>(w);                                    // quad_perm [1,0,3,2]
+    return w;
+}
+
+__device__ __forceinline__ int scatter_index5(int lane)
+{
+    const bool b3 = lane & 8, b4 = lane & 16, b5 = lane & 32;
+    return b3 ? 11 : (b4 ? (b5 ? 10 : 1) : (b5 ? 9 : 0));
+}
+
+__device__ __forceinline__ bool scatter_writer5(int lane)
+{
+    return (lane & 7) == 0 && (!(lane & 8) || (lane & 48) == 0);
+}
+
+// LDS slot of gradient value c: without the colour gradient values 6..8 are not stored; in the
+// five-value form (no geometry, no colour) only 0, 1, 9, 10, 11.
+template <bool kColor, bool k5>
 __device__ __forceinline__ int gslot(int c)
 {
-    return kColor || c < 6 ? c : c - 3;
+    return k5 ? (c < 2 ? c : c - 7) : (kColor || c < 6 ? c : c - 3);
+}
+
+// Is gradient value c produced by this backward variant?
+template <bool kColor, bool kGeo>
+__device__ __forceinline__ bool gvalue(int c)
+{
+    return c < 2 || c >= 9 || (kGeo && c < 6) || (kColor && c >= 6);
 }
 
 // Factor of gradient slot c applied at the flush (see bwd_pixel_blend).
@@ -630,7 +668,7 @@ __device__ __forceinline__ float flush_scale(int c, int W, int H)
 // an alpha hit, [3] lanes hit, [8 + c] histogram of lanes hit (c = 0..64).  Off by default.
 __device__ unsigned long long g_render_stats[8 + 65];
 
-template <bool kStats, bool kFeat, bool kColor>
+template <bool kStats, bool kFeat, bool kColor, bool kGeo>
 __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
 {
     constexpr int kThreads = kTilePixels;
@@ -640,7 +678,8 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
     __shared__ float4 sB[kThreads];      // conic.y, opacity, power cutoff, f1
     // kColor: sC = {r, g, b, f0}, sF = {f2}; otherwise (the colour gradient is zero) only the language
     // feature is staged, sF = {f0, f2}, and the tile sums hold 9 slots per entry (no colour slots)
-    constexpr int kGS = kColor ? 12 : 9;
+    constexpr bool k5 = !kGeo && !kColor;  // the language step: five values per entry
+    constexpr int kGS = k5 ? 5 : (kColor ? 12 : 9);
     __shared__ float4 sC[kColor ? kThreads : 1];
     __shared__ float sF[kThreads * (kColor ? 1 : 2)];
     __shared__ float sG[kThreads * kGS];  // per-entry gradient sums of the tile
@@ -681,7 +720,7 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
     const uint32_t w0 = s_wmax[0], w1 = s_wmax[1], w2 = s_wmax[2], w3 = s_wmax[3];
     // entries at list index >= max over the tile of n_contrib can contribute to no pixel
     const int maxl = (int)max(max(w0, w1), max(w2, w3));
-    const int vidx = scatter_index(lane);
+    const int vidx = k5 ? scatter_index5(lane) : scatter_index(lane);
 
     for (int done_cnt = 0; done_cnt < maxl; done_cnt += kThreads) {
         __syncthreads();
@@ -761,10 +800,15 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
                     F = make_float3(f02.x, B.w, f02.y);
                 }
                 float v[12];
-                bwd_pixel_blend<kFeat, kColor>(q, G, al, dx, dy, A, B, C, F, v);
-                const float tot = wave_reduce_scatter12(v, lane);
-                if (scatter_writer(lane) && (kColor || vidx < 6 || vidx >= 9))
-                    atomicAdd(&sG[j * kGS + gslot<kColor>(vidx)], tot);
+                bwd_pixel_blend<kFeat, kColor, kGeo>(q, G, al, dx, dy, A, B, C, F, v);
+                if (k5) {
+                    const float tot = wave_reduce_scatter5(v, lane);
+                    if (scatter_writer5(lane)) atomicAdd(&sG[j * kGS + gslot<kColor, k5>(vidx)], tot);
+                } else {
+                    const float tot = wave_reduce_scatter12(v, lane);
+                    if (scatter_writer(lane) && gvalue<kColor, kGeo>(vidx))
+                        atomicAdd(&sG[j * kGS + gslot<kColor, k5>(vidx)], tot);
+                }
             }
         }
         if (kStats && lane == 0) atomicMax(&s_bmax, nw);
@@ -778,8 +822,8 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
         for (int slot = t; slot < cnt * 16; slot += kThreads) {
             const int e = slot >> 4, c = slot & 15;
             if (c < 12) {
-                if (!kColor && c >= 6 && c < 9) continue;  // zero colour gradient
-                const float val = sG[e * kGS + gslot<kColor>(c)] * fscale;
+                if (!gvalue<kColor, kGeo>(c)) continue;  // a value this variant does not produce
+                const float val = sG[e * kGS + gslot<kColor, k5>(c)] * fscale;
                 if (val != 0.0f) {  // the id again from point_list (an L2 hit; saves 1 KB of LDS)
                     const uint32_t g = p.point_list[start + (uint32_t)(maxl - 1 - (done_cnt + e))];
                     atomicAdd(&p.grad[(size_t)g * kGradStride + c], val);
@@ -824,24 +868,28 @@ hipError_t launch_render_backward(const RenderParams& pin, int tiles, hipStream_
     p.prio = p.sched_counts ? prio_levels() : 0;
     const bool feat = p.include_feature != 0;
     const bool color = p.dL_dcolor != nullptr;  // null: the colour image does not reach the loss
-    const int variant = (feat ? 1 : 0) | (color ? 2 : 0);
+    const int variant = (feat ? 1 : 0) | (color ? 2 : 0) | (p.geo ? 4 : 0);
     if (render_stats_on()) tiles = debug_grid(tiles);
-#define LSR_BWD(S, F, C) hipLaunchKernelGGL((k_render_backward<S, F, C>), dim3(tiles), dim3(kTilePixels), 0, s, p)
-    if (render_stats_on()) {
-        switch (variant) {
-        case 0: LSR_BWD(true, false, false); break;
-        case 1: LSR_BWD(true, true, false); break;
-        case 2: LSR_BWD(true, false, true); break;
-        default: LSR_BWD(true, true, true); break;
-        }
-    } else {
-        switch (variant) {
-        case 0: LSR_BWD(false, false, false); break;
-        case 1: LSR_BWD(false, true, false); break;
-        case 2: LSR_BWD(false, false, true); break;
-        default: LSR_BWD(false, true, true); break;
-        }
+#define LSR_BWD(S, V)                                                                                         \
+    hipLaunchKernelGGL((k_render_backward<S, (V & 1) != 0, (V & 2) != 0, (V & 4) != 0>), dim3(tiles), \
+                       dim3(kTilePixels), 0, s, p)
+#define LSR_BWD_ALL(S)            \
+    switch (variant) {            \
+    case 0: LSR_BWD(S, 0); break; \
+    case 1: LSR_BWD(S, 1); break; \
+    case 2: LSR_BWD(S, 2); break; \
+    case 3: LSR_BWD(S, 3); break; \
+    case 4: LSR_BWD(S, 4); break; \
+    case 5: LSR_BWD(S, 5); break; \
+    case 6: LSR_BWD(S, 6); break; \
+    default: LSR_BWD(S, 7); break; \
     }
+    if (render_stats_on()) {
+        LSR_BWD_ALL(true)
+    } else {
+        LSR_BWD_ALL(false)
+    }
+#undef LSR_BWD_ALL
 #undef LSR_BWD
     return hipGetLastError();
 }
