@@ -354,7 +354,10 @@ int32_t lsr_backward(const lsr_settings* s, const lsr_backward_args* a, lsr_allo
     char* binning = static_cast<char*>(a->binning_buffer);
     float* grad = static_cast<float*>(alloc(user, LSR_BUF_BACKWARD, lsr_backward_bytes(P)));
     if (!grad) return fail(LSR_ERR_ALLOC, "lsr_backward: gradient scratch allocation failed");
-    LSR_TRY(hipMemsetAsync(grad, 0, lsr_backward_bytes(P), stream), "memset grad");
+    // the render backward's 5-value form (no geometry, no colour gradient) keeps 32-B records
+    const bool compact = !geometry && !a->dL_dout_color;
+    const int stride = compact ? kGradStrideLang : kGradStride;
+    LSR_TRY(hipMemsetAsync(grad, 0, 4 * (size_t)stride * (size_t)P, stream), "memset grad");
 
     RenderParams rp{};
     rp.W = W;
@@ -376,8 +379,9 @@ int32_t lsr_backward(const lsr_settings* s, const lsr_backward_args* a, lsr_allo
     rp.geo = geometry ? 1 : 0;
     if (a->num_rendered > 0) LSR_TRY(launch_render_backward(rp, L.tiles, stream), "render backward");
     if (!geometry) {
-        LSR_TRY(launch_grad_epilogue(P, a->radii, grad, a->language_feature, (a->raw & LSR_RAW_LANGUAGE) ? 1 : 0,
-                                     a->dL_dmeans2D, rp.include_feature ? a->dL_dlanguage_feature : nullptr, stream),
+        LSR_TRY(launch_grad_epilogue(P, a->radii, grad, stride, a->language_feature,
+                                     (a->raw & LSR_RAW_LANGUAGE) ? 1 : 0, a->dL_dmeans2D,
+                                     rp.include_feature ? a->dL_dlanguage_feature : nullptr, stream),
                 "gradient epilogue");
         if (!rp.include_feature && a->dL_dlanguage_feature)
             LSR_TRY(hipMemsetAsync(a->dL_dlanguage_feature, 0, (size_t)P * 3 * 4, stream), "memset dlang");

@@ -273,6 +273,27 @@ hipError_t scan_exclusive_u32(const uint32_t* in, uint32_t* out, int n, uint32_t
 
 // ---------------------------------------------------------------- stable LSD radix sort
 
+// super-tile rectangle [sx0, sx1) x [sy0, sy1) of a packed tile rectangle
+__device__ __forceinline__ void super_rect(uint2 rc, int& sx0, int& sy0, int& sx1, int& sy1)
+{
+    const int x0 = rc.x & 0xFFFF, y0 = rc.x >> 16, x1 = rc.y & 0xFFFF, y1 = rc.y >> 16;
+    sx0 = x0 / kSuper;
+    sy0 = y0 / kSuper;
+    sx1 = (x1 + kSuper - 1) / kSuper;
+    sy1 = (y1 + kSuper - 1) / kSuper;
+}
+
+// Optional work of the depth sort's LAST scatter pass, per output rank r (= depth rank): the
+// Gaussian's tile rectangle copied into depth order (the binning's one random gather) and its
+// super-tile entry count (-> exclusive scan = entry offsets); the sorted keys are not stored.
+// rect == null: a plain pass.
+struct ScatterTail {
+    const uint2* rect;
+    uint2* rect_ranked;
+    uint32_t* ns;
+};
+
+
 // Both radix kernels use a BLOCKED arrangement: wave w of a block owns the contiguous keys
 // [w * 64 * kItems, (w + 1) * 64 * kItems) of the block's tile and walks them in rounds of 64
 // consecutive keys, counting digits in its own LDS row.  Rounds of one wave are ordered by the
@@ -335,7 +356,7 @@ template <int kItems>
 __global__ __launch_bounds__(kRadixThreads) void k_radix_scatter(
     const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in, int n, int shift, int nbits,
     const uint32_t* __restrict__ hist, int nblk, uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
-    const uint32_t* __restrict__ kxf)
+    const uint32_t* __restrict__ kxf, ScatterTail tail)
 {
     constexpr int kTile = kRadixThreads * kItems;
     constexpr int kWaves = kRadixThreads / 64;
@@ -406,12 +427,45 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_scatter(
     }
     __syncthreads();
     const int cnt = min(kTile, n - tile0);
-    for (int i = t; i < cnt; i += kRadixThreads) {
-        const uint32_t k = sk[i];
-        const uint32_t d = (k >> shift) & mask;
-        const uint32_t o = gbase[d] + (uint32_t)i - dstart[d];
-        keys_out[o] = k;
-        vals_out[o] = sv[i];
+    if (!tail.rect) {
+        for (int i = t; i < cnt; i += kRadixThreads) {
+            const uint32_t k = sk[i];
+            const uint32_t d = (k >> shift) & mask;
+            const uint32_t o = gbase[d] + (uint32_t)i - dstart[d];
+            keys_out[o] = k;
+            vals_out[o] = sv[i];
+        }
+        return;
+    }
+    // last depth pass: all of this thread's rectangle gathers in flight at once
+    uint32_t outp[kItems], vid[kItems];
+    uint2 rc[kItems];
+#pragma unroll
+    for (int it = 0; it < kItems; it++) {
+        const int i = t + it * kRadixThreads;
+        outp[it] = 0xFFFFFFFFu;
+        if (i < cnt) {
+            const uint32_t d = (sk[i] >> shift) & mask;
+            outp[it] = gbase[d] + (uint32_t)i - dstart[d];
+            vid[it] = sv[i];
+        }
+    }
+#pragma unroll
+    for (int it = 0; it < kItems; it++)
+        if (outp[it] != 0xFFFFFFFFu) rc[it] = tail.rect[vid[it]];
+#pragma unroll
+    for (int it = 0; it < kItems; it++) {
+        if (outp[it] == 0xFFFFFFFFu) continue;
+        const uint32_t o = outp[it];
+        vals_out[o] = vid[it];
+        tail.rect_ranked[o] = rc[it];
+        uint32_t c = 0;
+        if (rc[it].x != rc[it].y) {  // empty rectangle: culled
+            int sx0, sy0, sx1, sy1;
+            super_rect(rc[it], sx0, sy0, sx1, sy1);
+            c = (uint32_t)((sx1 - sx0) * (sy1 - sy0));
+        }
+        tail.ns[o] = c;
     }
 }
 
@@ -421,7 +475,7 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_scatter(
 static hipError_t radix_sort(const uint32_t* k0, const uint32_t* v0, int n, int total_bits, uint32_t* kA,
                              uint32_t* vA, uint32_t* kB, uint32_t* vB, uint32_t* hist, uint32_t* scan_regions,
                              size_t region_words, uint32_t* fault, hipStream_t s, bool debug, int* passes_out,
-                             const uint32_t* kxf = nullptr)
+                             const uint32_t* kxf = nullptr, ScatterTail last = ScatterTail{nullptr, nullptr, nullptr})
 {
     const bool small = n <= (1 << 21);
     const int tile = kRadixThreads * (small ? 4 : 16);
@@ -446,12 +500,13 @@ static hipError_t radix_sort(const uint32_t* k0, const uint32_t* v0, int n, int 
         if ((e = scan_exclusive(hist, hist, (1 << nbits) * nblk, scan_regions + pass * region_words, nullptr, fault,
                                 s, debug)) != hipSuccess)
             return e;
+        const ScatterTail tail = pass == passes - 1 ? last : ScatterTail{nullptr, nullptr, nullptr};
         if (small)
             hipLaunchKernelGGL(k_radix_scatter<4>, dim3(nblk), dim3(kRadixThreads), 0, s, kin, vin, n, shift, nbits,
-                               hist, nblk, kout, vout, pass == 0 ? kxf : nullptr);
+                               hist, nblk, kout, vout, pass == 0 ? kxf : nullptr, tail);
         else
             hipLaunchKernelGGL(k_radix_scatter<16>, dim3(nblk), dim3(kRadixThreads), 0, s, kin, vin, n, shift, nbits,
-                               hist, nblk, kout, vout, pass == 0 ? kxf : nullptr);
+                               hist, nblk, kout, vout, pass == 0 ? kxf : nullptr, tail);
         if ((e = post(debug, s)) != hipSuccess) return e;
         kin = kout;
         vin = vout;
@@ -465,16 +520,6 @@ size_t radix_hist_words(int64_t n) { return 256 * (size_t)((n + 4 * kRadixThread
 size_t scan_region_words(int64_t n) { return 2 * (size_t)((n + kScanChunk - 1) / kScanChunk) + 2; }
 
 // ---------------------------------------------------------------- super-tiles
-
-// super-tile rectangle [sx0, sx1) x [sy0, sy1) of a packed tile rectangle
-__device__ __forceinline__ void super_rect(uint2 rc, int& sx0, int& sy0, int& sx1, int& sy1)
-{
-    const int x0 = rc.x & 0xFFFF, y0 = rc.x >> 16, x1 = rc.y & 0xFFFF, y1 = rc.y >> 16;
-    sx0 = x0 / kSuper;
-    sy0 = y0 / kSuper;
-    sx1 = (x1 + kSuper - 1) / kSuper;
-    sy1 = (y1 + kSuper - 1) / kSuper;
-}
 
 // An entry key: super-tile id in the low 16 bits (the only bits sorted on), the Gaussian's tile
 // rectangle clipped to the super-tile in the high 16 (lx0, lx1, ly0, ly1: 4 bits each).
@@ -515,25 +560,6 @@ __device__ __forceinline__ uint64_t transpose64(uint64_t x)
 
 // ---------------------------------------------------------------- depth order + super-tile counts
 
-// Per depth rank r: the Gaussian's tile rectangle copied into depth order (the only random
-// gather of the binning) and its super-tile entry count (-> exclusive scan = entry offsets).
-__global__ __launch_bounds__(256) void k_super_counts(int P, const uint32_t* __restrict__ sorted_ids,
-                                                      const uint2* __restrict__ rect, uint2* __restrict__ rect_ranked,
-                                                      uint32_t* __restrict__ ns)
-{
-    const int r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= P) return;
-    const uint2 rc = rect[sorted_ids[r]];
-    rect_ranked[r] = rc;
-    uint32_t n = 0;
-    if (rc.x != rc.y) {  // empty rectangle: culled
-        int sx0, sy0, sx1, sy1;
-        super_rect(rc, sx0, sy0, sx1, sy1);
-        n = (uint32_t)((sx1 - sx0) * (sy1 - sy0));
-    }
-    ns[r] = n;
-}
-
 hipError_t launch_depth_order(int P, int passes, const Layout& L, char* geom, uint32_t* counters, hipStream_t s,
                               bool debug)
 {
@@ -549,17 +575,15 @@ hipError_t launch_depth_order(int P, int passes, const Layout& L, char* geom, ui
     // odd one: swap the roles so the ids always end in sorted_ids
     int done = 0;
     const uint32_t* keys = reinterpret_cast<const uint32_t*>(geom + L.depth_key);
+    uint32_t* off = reinterpret_cast<uint32_t*>(geom + L.super_offset);
+    const ScatterTail tail{reinterpret_cast<const uint2*>(geom + L.rect), reinterpret_cast<uint2*>(geom + L.rect_ranked),
+                           off};
     hipError_t e = (passes & 1)
         ? radix_sort(keys, nullptr, P, 8 * passes, kb, vb, ka, va, hist, regions, L.scan_region_geom, fault, s, debug,
-                     &done, counters + kCntKeyMin)
+                     &done, counters + kCntKeyMin, tail)
         : radix_sort(keys, nullptr, P, 8 * passes, ka, va, kb, vb, hist, regions, L.scan_region_geom, fault, s, debug,
-                     &done, counters + kCntKeyMin);
+                     &done, counters + kCntKeyMin, tail);
     if (e != hipSuccess) return e;
-    uint32_t* off = reinterpret_cast<uint32_t*>(geom + L.super_offset);
-    hipLaunchKernelGGL(k_super_counts, dim3((P + 255) / 256), dim3(256), 0, s, P, (const uint32_t*)va,
-                       reinterpret_cast<const uint2*>(geom + L.rect), reinterpret_cast<uint2*>(geom + L.rect_ranked),
-                       off);
-    if ((e = post(debug, s)) != hipSuccess) return e;
     return scan_exclusive(off, off, P, regions + passes * L.scan_region_geom, counters + kCntSuper, fault, s,
                           debug);
 }

@@ -34,6 +34,7 @@ constexpr int kPreThreads = 128;
 constexpr int kSuper = 8;          // super-tile = kSuper x kSuper tiles (64-bit tile masks)
 constexpr int kSegEntries = 512;   // super-tile list entries per binning workgroup
 constexpr int kGradStride = 16;                          // floats per Gaussian grad record
+constexpr int kGradStrideLang = 8;  // without geometry gradients: {dxy, dlang} in slots 0..4 (32 B)
 
 size_t radix_hist_words(int64_t n);   // per-block digit histograms for n keys
 size_t scan_region_words(int64_t n);  // look-back status + ticket of one scan of n words
@@ -180,8 +181,8 @@ struct RenderParams {
 
 hipError_t launch_preprocess(const PreprocessParams& p, hipStream_t s);
 hipError_t launch_preprocess_backward(const PreprocessBwdParams& p, hipStream_t s);
-hipError_t launch_grad_epilogue(int P, const int* radii, const float* grad, const float* lang, int raw_lang,
-                                float* dmeans2D, float* dlang, hipStream_t s);
+hipError_t launch_grad_epilogue(int P, const int* radii, const float* grad, int stride, const float* lang,
+                                int raw_lang, float* dmeans2D, float* dlang, hipStream_t s);
 hipError_t launch_mark_visible(int P, const float* means, const float* view, const float* proj,
                                uint8_t* visible, hipStream_t s);
 

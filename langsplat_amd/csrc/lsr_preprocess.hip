@@ -678,17 +678,18 @@ hipError_t launch_preprocess_backward(const PreprocessBwdParams& p, hipStream_t 
 // screen-space gradient (dmeans2D) and the language-feature gradient, straight from the render
 // backward's per-Gaussian record -- what preprocess_backward_one writes for these two outputs.
 __global__ __launch_bounds__(256) void k_grad_epilogue(int P, const int* __restrict__ radii,
-                                                       const float* __restrict__ grad, const float* __restrict__ lang,
-                                                       int raw_lang, float* __restrict__ dmeans2D,
-                                                       float* __restrict__ dlang)
+                                                       const float* __restrict__ grad, int stride,
+                                                       const float* __restrict__ lang, int raw_lang,
+                                                       float* __restrict__ dmeans2D, float* __restrict__ dlang)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P) return;
     const size_t i3 = 3 * (size_t)i;
     const bool live = radii[i] > 0;
-    const float4* g4 = reinterpret_cast<const float4*>(grad + (size_t)i * kGradStride);
+    // stride kGradStrideLang: {dx, dy, l0, l1}{l2, -, -, -}; kGradStride: the full record
+    const float4* g4 = reinterpret_cast<const float4*>(grad + (size_t)i * stride);
+    const float4 ga = live ? g4[0] : make_float4(0.f, 0.f, 0.f, 0.f);
     if (dmeans2D) {
-        const float4 ga = live ? g4[0] : make_float4(0.f, 0.f, 0.f, 0.f);
         dmeans2D[i3] = ga.x;
         dmeans2D[i3 + 1] = ga.y;
         dmeans2D[i3 + 2] = 0.f;
@@ -696,9 +697,14 @@ __global__ __launch_bounds__(256) void k_grad_epilogue(int P, const int* __restr
     if (dlang) {
         float3 d = make_float3(0.f, 0.f, 0.f);
         if (live) {
-            const float4 gc = g4[2];
-            d = (raw_lang && lang) ? act_lang_backward(lang[i3], lang[i3 + 1], lang[i3 + 2], gc.y, gc.z, gc.w)
-                                   : make_float3(gc.y, gc.z, gc.w);
+            float3 gl;
+            if (stride == kGradStrideLang) {
+                gl = make_float3(ga.z, ga.w, g4[1].x);
+            } else {
+                const float4 gc = g4[2];
+                gl = make_float3(gc.y, gc.z, gc.w);
+            }
+            d = (raw_lang && lang) ? act_lang_backward(lang[i3], lang[i3 + 1], lang[i3 + 2], gl.x, gl.y, gl.z) : gl;
         }
         dlang[i3] = d.x;
         dlang[i3 + 1] = d.y;
@@ -706,12 +712,12 @@ __global__ __launch_bounds__(256) void k_grad_epilogue(int P, const int* __restr
     }
 }
 
-hipError_t launch_grad_epilogue(int P, const int* radii, const float* grad, const float* lang, int raw_lang,
-                                float* dmeans2D, float* dlang, hipStream_t s)
+hipError_t launch_grad_epilogue(int P, const int* radii, const float* grad, int stride, const float* lang,
+                                int raw_lang, float* dmeans2D, float* dlang, hipStream_t s)
 {
     if (P == 0 || (!dmeans2D && !dlang)) return hipSuccess;
-    hipLaunchKernelGGL(k_grad_epilogue, dim3((P + 255) / 256), dim3(256), 0, s, P, radii, grad, lang, raw_lang,
-                       dmeans2D, dlang);
+    hipLaunchKernelGGL(k_grad_epilogue, dim3((P + 255) / 256), dim3(256), 0, s, P, radii, grad, stride, lang,
+                       raw_lang, dmeans2D, dlang);
     return hipGetLastError();
 }
 

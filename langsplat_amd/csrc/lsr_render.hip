@@ -100,13 +100,14 @@ __device__ __forceinline__ uint32_t entry_cover(float x, float y, float a, float
     return m;
 }
 
-// Compacts the batch slots [0, cnt) whose cover mask includes this wave into list[0, n); returns n.
-__device__ __forceinline__ int wave_compact(const uint8_t* sM, int cnt, int wave, int lane, uint8_t* list)
+// Compacts the batch slots [0, cnt) whose cover mask meets `bits` (the wave's blocks) into
+// list[0, n); returns n.
+__device__ __forceinline__ int wave_compact(const uint8_t* sM, int cnt, uint32_t bits, int lane, uint8_t* list)
 {
     int n = 0;
     for (int r = 0; r < cnt; r += 64) {
         const int e = r + lane;
-        const bool ov = e < cnt && ((sM[e] >> wave) & 1u);
+        const bool ov = e < cnt && (sM[e] & bits) != 0u;
         const uint64_t m = __ballot(ov);
         if (ov) list[n + __popcll(m & ((1ull << lane) - 1ull))] = (uint8_t)e;
         n += __popcll(m);
@@ -328,7 +329,7 @@ __global__ __launch_bounds__(kTilePixels) void k_render_forward(RenderParams p)
         if (kStats) ph.lap(ph.load);
         const int cnt = (int)min((uint32_t)kThreads, end - base);
         const int n = __builtin_amdgcn_readfirstlane(
-            wave_compact(sM, cnt, wave, lane, sL[wave]));
+            wave_compact(sM, cnt, 1u << wave, lane, sL[wave]));
         __syncthreads();  // list visible to the wave's other lanes
         if (kStats) ph.lap(ph.compact);
         const uint32_t list_base = base - start;  // list index of slot 0
@@ -826,7 +827,10 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
                 const float val = sG[e * kGS + gslot<kColor, k5>(c)] * fscale;
                 if (val != 0.0f) {  // the id again from point_list (an L2 hit; saves 1 KB of LDS)
                     const uint32_t g = p.point_list[start + (uint32_t)(maxl - 1 - (done_cnt + e))];
-                    atomicAdd(&p.grad[(size_t)g * kGradStride + c], val);
+                    if (k5)  // compact 32-B record: the five values in slots 0..4
+                        atomicAdd(&p.grad[(size_t)g * kGradStrideLang + gslot<kColor, k5>(c)], val);
+                    else
+                        atomicAdd(&p.grad[(size_t)g * kGradStride + c], val);
                 }
             }
         }
