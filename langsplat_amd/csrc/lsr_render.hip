@@ -4,22 +4,25 @@
 // (8 (w & 1), 8 (w >> 1)) and every lane one pixel.  Workgroups take tiles longest first
 // (scheduled_tile).  The tile's depth-ordered list is streamed through LDS in batches of 256
 // entries (one per thread: {x, y, -conic.x/2, -conic.z/2}{conic.y, opacity, power cutoff, f1}
-// {r, g, b, f0}{f2}); the loading thread also computes the screen box the entry can reach
-// (entry_box), and a wave skips the entries whose box misses its block:
-//   forward:  each wave compacts the batch into a slot list (wave_compact);
-//   backward: the loader stores a 4-bit mask of the wave blocks the box meets and each wave walks
-//             the set bits of a ballot over it -- no list, 26.9 KB of LDS, so 5 workgroups per CU.
-// (Measured both ways at C3: the list is faster in the forward, the mask in the backward.)
+// {r, g, b, f0}{f2}); the loading thread also computes a 4-bit mask of the wave blocks the entry
+// can reach (entry_cover: reach box, refined by the exact ellipse-vs-block test), and a wave skips
+// the entries that cannot reach its block:
+//   forward:  each wave compacts the batch into a slot list (wave_compact) and walks it two
+//             entries per step (their exps as one packed chain);
+//   backward: each wave walks the set bits of a ballot over the masks (no list).
 // Semantics: upstream FORWARD/BACKWARD::renderCUDA extended by the 3-channel language feature
 // (SURVEY.md §8a a10-a11, App. A.4-A.5); arithmetic order is that of oracle/lsr_oracle.c
-// render_pixel / backward_pixel.
+// render_pixel / backward_pixel (the forward bit-identically, the backward's gradient arithmetic
+// regrouped).
 //
 // Backward gradient scatter: every lane of a wave visits the same list entry at the same
-// iteration, so the 12 per-Gaussian partials of a wave are reduced in registers by a
-// reduce-scatter (permlane32/16 swaps + DPP mirrors, ~35 VALU ops), the 4 waves' results are summed
-// in LDS (ds_add_f32), and after each batch ONE 12-lane atomic instruction per (tile, Gaussian)
-// adds the tile's total into a 64-byte-aligned per-Gaussian record -- instead of the upstream 12
+// iteration, so the per-Gaussian partials of a wave are reduced in registers by a reduce-scatter
+// (permlane32/16 swaps + DPP mirrors: 27 operations for 12 values, 16 for the language step's 5),
+// the 4 waves' results are summed in LDS (ds_add_f32), and after each batch ONE atomic row per
+// (tile, Gaussian) adds the tile's total into a per-Gaussian record -- instead of the upstream 12
 // scattered atomics per pixel per blend.  Entries no lane contributes to are skipped by a ballot.
+// The backward is specialised (template) on the language feature, on a zero colour gradient and on
+// whether the geometry gradients are needed (k_render_backward<kStats, kFeat, kColor, kGeo>).
 #include <stdlib.h>
 
 #include "lsr_internal.h"
@@ -196,11 +199,12 @@ __device__ __forceinline__ void timeline_put(int kernel, uint64_t t0, int tile, 
     o[7] = ph.batches;
 }
 
-// Wave priority by launch position.  A tile's compositing is one serial chain per pixel, so the
-// kernel can end no earlier than its longest tile's chain -- and the longest tiles (launched first)
-// share their SIMDs with up to 7 other waves, which round-robin issue would give an equal share.
-// Raising the first-launched (longest) workgroups' priority lets their chains run at close to
-// their own latency while shorter tiles fill the issue gaps.  Changes no result.
+// Wave priority by launch position (LSR_PRIO=0: off).  A tile's compositing is one serial chain
+// per pixel, so the kernel can end no earlier than its longest tile's chain, and the longest tiles
+// (launched first) share their SIMDs with up to 7 other waves.  Raising the first-launched
+// workgroups' priority was meant to let those chains run closer to their own latency; measured at
+// C3 it changes neither their duration nor the kernel's (tools/render_timeline.py).  No result
+// depends on it.
 __device__ __forceinline__ void launch_priority(int b, int prio)
 {
     if (!prio) return;
