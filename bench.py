@@ -102,18 +102,23 @@ class Opt:
     include_feature = True
 
 
-def algorithmic_bytes(stage, P, V, R, HW, M):
-    """Compulsory HBM bytes per launch of each stage (SURVEY.md §8d per-unit model)."""
+def algorithmic_bytes(stage, P, V, R, HW, M, color_grad=True, geometry=True):
+    """Compulsory HBM bytes per launch of each stage (SURVEY.md §8d per-unit model).
+    The render backward's per-pixel and per-Gaussian terms follow its variant: dL/dcolor is read
+    only when the colour image reaches the loss, and the per-Gaussian record it accumulates holds
+    12 values with geometry gradients, 5 (dmean2D x/y + language) without."""
     sh = 12 * M
+    bwd_px = 4 + 4 + 12 + (12 if color_grad else 0)  # T, contributor count, dL/dlanguage, [dL/dcolor]
+    bwd_g = 4 * (12 if geometry else 5)
     return {
         # reads means 12, scale 12, rot 16, opacity 4, SH, lang 12; writes radii 4 + key 4 + tiles 4
         # + rect 8 + clamp 4 (all P) and the 48 B record for visible Gaussians
         "preprocess": P * (12 + 12 + 16 + 4 + sh + 12 + 24) + V * 48,
         # per instance: list id 4 + gathered record 48; per pixel: colour 12 + language 12 + T 4 + count 4
         "render forward": R * 52 + HW * 32,
-        # per instance: id 4 + record 48; per pixel: dL/dcolour 12 + dL/dlanguage 12 + T 4 + count 4;
-        # per visible Gaussian: the 12-float gradient record (48 B) accumulated once
-        "render backward": R * 52 + HW * 32 + V * 48,
+        # per instance: id 4 + record 48; per pixel: bwd_px; per visible Gaussian: its gradient
+        # record, accumulated once
+        "render backward": R * 52 + HW * bwd_px + V * bwd_g,
         # reads means/scale/rot/SH/radii/clamp + 48 B grad record; writes every gradient output
         "preprocess backward": P * (12 + 12 + 16 + sh + 4 + 4) + V * 48 + P * (12 + 12 + 12 + 4 + 12 + sh + 12 + 16),
     }.get(stage)
@@ -122,7 +127,10 @@ def algorithmic_bytes(stage, P, V, R, HW, M):
 # the stage that dominates the step (measured: profiles/r01_summary.json); timed live in the bench
 DOMINANT_STAGE = "render backward"
 
-STAGE_KERNEL = {"render backward": "lsr::k_render_backward", "render forward": "lsr::k_render_forward",
+# rocprofv3 names of the bench step's kernels (template arguments: k_render_forward<kStats, kFeat>,
+# k_render_backward<kStats, kFeat, kColor, kGeo>; the language step runs kColor = kGeo = false)
+STAGE_KERNEL = {"render backward": "lsr::k_render_backward<false, true, false, false>",
+                "render forward": "lsr::k_render_forward<false, true>",
                 "preprocess": "lsr::k_preprocess", "preprocess backward": "lsr::k_preprocess_backward"}
 
 
@@ -302,7 +310,9 @@ def main():
     raster_ms = sum(v["total_ms"] for k, v in prof.items()) / prof_steps
     dom_name = DOMINANT_STAGE
     M = (c["sh_degree"] + 1) ** 2
-    bytes_dom = algorithmic_bytes(dom_name, P, visible, nr, W * H, M)
+    # the language step: the colour image does not reach the loss; geometry gradients as needed
+    geometry = bool(_native.FORCE_GEOMETRY_GRADS)
+    bytes_dom = algorithmic_bytes(dom_name, P, visible, nr, W * H, M, color_grad=False, geometry=geometry)
     roofline = None
     if bytes_dom is not None:
         achieved = bytes_dom / (dom["avg_ms"] * 1e-3) / 1e9

@@ -16,7 +16,7 @@ from collections import defaultdict
 
 
 def short(name):
-    m = re.match(r"(?:void )?([\w:]+)", name)
+    m = re.match(r"(?:void )?([\w:]+(?:<[^>]*>)?)", name)
     return m.group(1) if m else name
 
 
