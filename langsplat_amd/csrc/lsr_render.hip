@@ -419,6 +419,17 @@ static int debug_grid(int tiles)
     return v > 0 && v < tiles ? v : tiles;
 }
 
+// LSR_FWD_PAD=bytes adds dynamic LDS to every forward workgroup, i.e. caps its workgroups per CU
+// (measurement aid: how the longest tiles' chains respond to sharing their CU)
+static size_t forward_pad()
+{
+    static const size_t v = [] {
+        const char* e = getenv("LSR_FWD_PAD");
+        return e ? (size_t)atoi(e) : (size_t)0;
+    }();
+    return v;
+}
+
 // LSR_ORDER=0 launches the tiles in tile order (measurement aid)
 static bool scheduled()
 {
@@ -439,13 +450,13 @@ hipError_t launch_render_forward(const RenderParams& pin, int tiles, hipStream_t
     if (render_stats_on()) {
         tiles = debug_grid(tiles);
         if (feat)
-            hipLaunchKernelGGL((k_render_forward<true, true>), dim3(tiles), dim3(kTilePixels), 0, s, p);
+            hipLaunchKernelGGL((k_render_forward<true, true>), dim3(tiles), dim3(kTilePixels), forward_pad(), s, p);
         else
-            hipLaunchKernelGGL((k_render_forward<true, false>), dim3(tiles), dim3(kTilePixels), 0, s, p);
+            hipLaunchKernelGGL((k_render_forward<true, false>), dim3(tiles), dim3(kTilePixels), forward_pad(), s, p);
     } else if (feat) {
-        hipLaunchKernelGGL((k_render_forward<false, true>), dim3(tiles), dim3(kTilePixels), 0, s, p);
+        hipLaunchKernelGGL((k_render_forward<false, true>), dim3(tiles), dim3(kTilePixels), forward_pad(), s, p);
     } else {
-        hipLaunchKernelGGL((k_render_forward<false, false>), dim3(tiles), dim3(kTilePixels), 0, s, p);
+        hipLaunchKernelGGL((k_render_forward<false, false>), dim3(tiles), dim3(kTilePixels), forward_pad(), s, p);
     }
     return hipGetLastError();
 }

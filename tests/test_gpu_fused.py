@@ -154,8 +154,8 @@ def test_render_fused_matches_unfused(monkeypatch):
         assert_grad_close(k, g1[k], g0[k])
 
 
-@pytest.mark.parametrize("fused", [False, True])
-def test_language_step_skips_geometry_gradients(fused, monkeypatch):
+@pytest.mark.parametrize("fused,colour", [(False, False), (True, False), (True, True)])
+def test_language_step_skips_geometry_gradients(fused, colour, monkeypatch):
     """LangSplat's language step freezes every geometry parameter (scene/gaussian_model.py:203-217):
     the backward then computes only dL/dmeans2D and dL/dlanguage (include/lsr.h, geometry outputs
     all NULL) and must give what the full backward gives for those two (up to the order of the
@@ -163,7 +163,7 @@ def test_language_step_skips_geometry_gradients(fused, monkeypatch):
     W, H = 96, 64
     g = make_gaussians(1500, seed=9, scale_range=(0.03, 0.2))
     cam = make_cameras(1, W, H, device=DEV)[0]
-    _, gl = (t.to(DEV) for t in grad_seed(H, W, seed=12))
+    gc, gl = (t.to(DEV) for t in grad_seed(H, W, seed=12))
     monkeypatch.setenv("LANGSPLAT_AMD_FUSED", "1" if fused else "0")
     out = {}
     for force in (True, False):
@@ -172,7 +172,10 @@ def test_language_step_skips_geometry_gradients(fused, monkeypatch):
         for n in ("xyz", "features_dc", "features_rest", "scaling", "rotation", "opacity"):
             getattr(m, "_" + n).requires_grad_(False)
         pkg = render(cam, m, _Pipe, torch.zeros(3, device=DEV), _Opt)
-        (pkg["language_feature_image"] * gl).sum().backward()
+        loss = (pkg["language_feature_image"] * gl).sum()
+        if colour:  # the colour image in the loss too: the 12-value backward without geometry
+            loss = loss + (pkg["render"] * gc).sum()
+        loss.backward()
         out[force] = (m._language_feature.grad.detach().clone(), pkg["viewspace_points"].grad.detach().clone())
     for k in range(2):
         assert_grad_close(f"out{k}", out[False][k].cpu().numpy(), out[True][k].cpu().numpy())
