@@ -308,6 +308,9 @@ __global__ __launch_bounds__(kTilePixels) void k_render_forward(RenderParams p)
     FwdPixel q{1.0f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0u, 0u, !inside};
     PhaseTicks ph;
     if (kStats) ph.begin();
+    // the point_list id of this thread's entry in the next batch is loaded before the current batch's
+    // walk, so a batch's load phase waits for one memory round trip (the record gather), not two
+    uint32_t g_next = start + t < end ? p.point_list[start + t] : 0u;
     for (uint32_t base = start; base < end; base += kThreads) {
         const bool all_done = __syncthreads_count(q.done) == kThreads;
         if (kStats && base != start) ph.lap(ph.walk);
@@ -318,7 +321,7 @@ __global__ __launch_bounds__(kTilePixels) void k_render_forward(RenderParams p)
         if (kStats) ph.batches++;
         const uint32_t idx = base + t;
         if (idx < end) {
-            const uint32_t g = p.point_list[idx];
+            const uint32_t g = g_next;
             const float4 a = p.record[3 * (size_t)g];
             const float4 b = p.record[3 * (size_t)g + 1];
             const float4 c = p.record[3 * (size_t)g + 2];
@@ -336,6 +339,7 @@ __global__ __launch_bounds__(kTilePixels) void k_render_forward(RenderParams p)
             wave_compact(sM, cnt, 1u << wave, lane, sL[wave]));
         __syncthreads();  // list visible to the wave's other lanes
         if (kStats) ph.lap(ph.compact);
+        if (idx + kThreads < end) g_next = p.point_list[idx + kThreads];
         const uint32_t list_base = base - start;  // list index of slot 0
         // two list entries per iteration: their power / exp / alpha do not depend on the pixel state,
         // so the two chains interleave; only the transmittance test and the blend are sequential.
