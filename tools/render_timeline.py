@@ -1,6 +1,9 @@
 """Per-workgroup timeline of the render kernels at a BASELINE config (measurement aid).
 
-    python tools/render_timeline.py [C3]
+    python tools/render_timeline.py [C3] [--full]
+
+The backward runs the bench's language-step variant (no colour gradient, no geometry gradients);
+--full runs the variant with every gradient.
 
 Runs one forward + backward with LSR_RENDER_STATS=1 and reads the {start, end, tile, CU} record
 every workgroup wrote (include/lsr.h lsr_debug_render_timeline).  Prints, per kernel, the span,
@@ -74,7 +77,9 @@ def analyse(name, recs, info=None):
 
 
 def main():
-    cfg = sys.argv[1] if len(sys.argv) > 1 else "C3"
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    full = "--full" in sys.argv
+    cfg = args[0] if args else "C3"
     c = CONFIGS[cfg]
     dev = torch.device("cuda")
     P, W, H = c["P"], c["width"], c["height"]
@@ -95,8 +100,8 @@ def main():
         torch.cuda.synchronize()
         fwd = _native.debug_render_timeline(0, tiles)
         _native.rasterize_gaussians_backward(st, inp["means3D"], inp["shs"], None, inp["language_feature_precomp"],
-                                             inp["scales"], inp["rotations"], None, radii, gc, gl, nr, geom,
-                                             binning, image)
+                                             inp["scales"], inp["rotations"], None, radii, gc if full else None, gl,
+                                             nr, geom, binning, image, geometry=full)
         torch.cuda.synchronize()
         bwd = _native.debug_render_timeline(1, tiles)
     _native.debug_render_stats()
