@@ -434,6 +434,16 @@ static size_t forward_pad()
     return v;
 }
 
+// LSR_BWD_PAD=bytes: the same for the backward
+static size_t backward_pad()
+{
+    static const size_t v = [] {
+        const char* e = getenv("LSR_BWD_PAD");
+        return e ? (size_t)atoi(e) : (size_t)0;
+    }();
+    return v;
+}
+
 // LSR_ORDER=0 launches the tiles in tile order (measurement aid)
 static bool scheduled()
 {
@@ -895,7 +905,7 @@ hipError_t launch_render_backward(const RenderParams& pin, int tiles, hipStream_
     if (render_stats_on()) tiles = debug_grid(tiles);
 #define LSR_BWD(S, V)                                                                                         \
     hipLaunchKernelGGL((k_render_backward<S, (V & 1) != 0, (V & 2) != 0, (V & 4) != 0>), dim3(tiles), \
-                       dim3(kTilePixels), 0, s, p)
+                       dim3(kTilePixels), backward_pad(), s, p)
 #define LSR_BWD_ALL(S)            \
     switch (variant) {            \
     case 0: LSR_BWD(S, 0); break; \
