@@ -82,8 +82,10 @@ __device__ __forceinline__ double block_sum_double(double v, double* wsum)
 // block (ticket) spins until every word carries this launch's epoch, then adds them in block
 // order.  No __threadfence (on gfx950 each one is an L2 writeback) and no scratch reset between
 // launches: the host passes a fresh nonzero epoch per launch.
-template <int V>
-__global__ __launch_bounds__(kFwdThreads) void k_masked_l1_forward(int C, int64_t HW, const float* __restrict__ pred,
+// kC: the channel count at compile time (LangSplat's 3: every load of a group in flight at once),
+// 0 = runtime C.
+template <int V, int kC>
+__global__ __launch_bounds__(kFwdThreads) void k_masked_l1_forward(int C_rt, int64_t HW, const float* __restrict__ pred,
                                                                     const float* __restrict__ gt, const void* mask,
                                                                     int mask_is_float, float* __restrict__ loss,
                                                                     uint32_t* __restrict__ ticket,
@@ -91,6 +93,7 @@ __global__ __launch_bounds__(kFwdThreads) void k_masked_l1_forward(int C, int64_
 {
     __shared__ double wsum[kFwdThreads / 64];
     __shared__ bool s_last;
+    const int C = kC > 0 ? kC : C_rt;
     const int64_t groups = HW / V;
     float acc = 0.0f;
     for (int64_t gi = (int64_t)blockIdx.x * kFwdThreads + threadIdx.x; gi < groups;
@@ -129,8 +132,8 @@ __global__ __launch_bounds__(kFwdThreads) void k_masked_l1_forward(int C, int64_
     }
 }
 
-template <int V>
-__global__ __launch_bounds__(kLossThreads) void k_masked_l1_backward(int C, int64_t HW, const float* __restrict__ pred,
+template <int V, int kC>
+__global__ __launch_bounds__(kLossThreads) void k_masked_l1_backward(int C_rt, int64_t HW, const float* __restrict__ pred,
                                                                      const float* __restrict__ gt, const void* mask,
                                                                      int mask_is_float,
                                                                      const float* __restrict__ grad_loss,
@@ -138,6 +141,7 @@ __global__ __launch_bounds__(kLossThreads) void k_masked_l1_backward(int C, int6
 {
     // autograd: mean backward grad.div(N) (torch's GPU div by a scalar multiplies by its
     // reciprocal), abs backward * sign, mul backward * m
+    const int C = kC > 0 ? kC : C_rt;
     const float gN = grad_loss[0] * (1.0f / (float)((int64_t)C * HW));
     const int64_t groups = HW / V;
     for (int64_t gi = (int64_t)blockIdx.x * kLossThreads + threadIdx.x; gi < groups;
@@ -200,24 +204,34 @@ hipError_t launch_masked_l1_forward(int C, int64_t HW, const float* pred, const 
         const int64_t b = (groups + kFwdThreads - 1) / kFwdThreads;
         return (int)(b < 1 ? 1 : (b > kFwdBlocks ? kFwdBlocks : b));
     };
-    if (vec4_ok(HW, pred, gt, nullptr, mask, mask_is_float))
-        hipLaunchKernelGGL(k_masked_l1_forward<4>, dim3(blocks(HW / 4)), dim3(kFwdThreads), 0, s, C, HW, pred, gt,
+    if (vec4_ok(HW, pred, gt, nullptr, mask, mask_is_float)) {
+        if (C == 3)
+            hipLaunchKernelGGL((k_masked_l1_forward<4, 3>), dim3(blocks(HW / 4)), dim3(kFwdThreads), 0, s, C, HW, pred,
+                               gt, mask, mask_is_float, loss, counter, partial, epoch);
+        else
+            hipLaunchKernelGGL((k_masked_l1_forward<4, 0>), dim3(blocks(HW / 4)), dim3(kFwdThreads), 0, s, C, HW, pred,
+                               gt, mask, mask_is_float, loss, counter, partial, epoch);
+    } else {
+        hipLaunchKernelGGL((k_masked_l1_forward<1, 0>), dim3(blocks(HW)), dim3(kFwdThreads), 0, s, C, HW, pred, gt,
                            mask, mask_is_float, loss, counter, partial, epoch);
-    else
-        hipLaunchKernelGGL(k_masked_l1_forward<1>, dim3(blocks(HW)), dim3(kFwdThreads), 0, s, C, HW, pred, gt, mask,
-                           mask_is_float, loss, counter, partial, epoch);
+    }
     return hipGetLastError();
 }
 
 hipError_t launch_masked_l1_backward(int C, int64_t HW, const float* pred, const float* gt, const void* mask,
                                      int mask_is_float, const float* grad_loss, float* grad_pred, hipStream_t s)
 {
-    if (vec4_ok(HW, pred, gt, grad_pred, mask, mask_is_float))
-        hipLaunchKernelGGL(k_masked_l1_backward<4>, dim3(loss_blocks(HW / 4)), dim3(kLossThreads), 0, s, C, HW, pred,
+    if (vec4_ok(HW, pred, gt, grad_pred, mask, mask_is_float)) {
+        if (C == 3)
+            hipLaunchKernelGGL((k_masked_l1_backward<4, 3>), dim3(loss_blocks(HW / 4)), dim3(kLossThreads), 0, s, C, HW,
+                               pred, gt, mask, mask_is_float, grad_loss, grad_pred);
+        else
+            hipLaunchKernelGGL((k_masked_l1_backward<4, 0>), dim3(loss_blocks(HW / 4)), dim3(kLossThreads), 0, s, C, HW,
+                               pred, gt, mask, mask_is_float, grad_loss, grad_pred);
+    } else {
+        hipLaunchKernelGGL((k_masked_l1_backward<1, 0>), dim3(loss_blocks(HW)), dim3(kLossThreads), 0, s, C, HW, pred,
                            gt, mask, mask_is_float, grad_loss, grad_pred);
-    else
-        hipLaunchKernelGGL(k_masked_l1_backward<1>, dim3(loss_blocks(HW)), dim3(kLossThreads), 0, s, C, HW, pred, gt,
-                           mask, mask_is_float, grad_loss, grad_pred);
+    }
     return hipGetLastError();
 }
 
