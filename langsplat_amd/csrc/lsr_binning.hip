@@ -771,6 +771,111 @@ __global__ __launch_bounds__(256) void k_bin_count(int S, int sgx, int gx, int g
 // with consecutive lanes on consecutive addresses (batches over kStage instances store directly).
 constexpr int kStage = 4096;
 
+// k_bin_count with the segment setup folded in, for a super-tile sort of ONE radix pass (S <= 256
+// super-tiles): the super-tile ranges are then the digit starts of the scanned [digit][block]
+// histogram (digit s starts at hist[s * nblk]; digits >= S are empty), so k_super_ranges and the
+// one-workgroup k_seg_setup are not launched.  Every workgroup rebuilds the segment map of the S
+// super-tiles in LDS (S loads + a block scan), finds its own segment in it, and workgroup 0 also
+// writes the map to global memory for k_bin_emit.  Same counts as k_seg_setup + k_bin_count.
+constexpr int kFusedSupers = 256;
+
+__global__ __launch_bounds__(256) void k_bin_count_fused(int S, int sgx, int sgy, int gx, int gy, int nblk, int ndig,
+                                                         int64_t E, const uint32_t* __restrict__ hist,
+                                                         uint2* __restrict__ g_sranges, uint32_t* __restrict__ g_seg_base,
+                                                         uint32_t* __restrict__ g_colpre, uint32_t* __restrict__ g_rowpre,
+                                                         const uint32_t* __restrict__ keys, uint32_t* __restrict__ table)
+{
+    __shared__ uint2 sr[kFusedSupers];
+    __shared__ uint32_t sbase[kFusedSupers + 1];
+    __shared__ uint32_t scol[kFusedSupers];
+    __shared__ uint32_t srow_tot[kFusedSupers];      // per super-row: segment-weighted count of one tile row
+    __shared__ uint32_t srow_pre[kFusedSupers + 1];  // whole tile rows above super-row sy
+    __shared__ uint32_t wsum[4];
+    __shared__ uint32_t cnt[64];
+    __shared__ int sh[2];
+    const int t = threadIdx.x;
+    uint32_t nseg = 0;
+    if (t < S) {
+        const uint32_t a = hist[(size_t)t * nblk];
+        const uint32_t b = t + 1 < ndig ? hist[(size_t)(t + 1) * nblk] : (uint32_t)E;
+        sr[t] = make_uint2(a, b);
+        nseg = super_segments(make_uint2(a, b));
+    }
+    uint32_t tot;
+    const uint32_t ex = block_exclusive_scan(nseg, wsum, &tot);
+    if (t < S) sbase[t] = ex;
+    if (t == 0) sbase[S] = tot;
+    __syncthreads();
+    if (t < S) {  // column prefix inside the super-row, and the row totals
+        const int sy = t / sgx, sx = t - sy * sgx;
+        uint32_t run = 0;
+        for (int x = 0; x < sx; x++)
+            run += super_segments(sr[sy * sgx + x]) * (uint32_t)min(kSuper, gx - x * kSuper);
+        scol[t] = run;
+        if (sx == sgx - 1) srow_tot[sy] = run + nseg * (uint32_t)min(kSuper, gx - sx * kSuper);
+    }
+    __syncthreads();
+    if (t == 0) {
+        uint32_t run = 0;
+        for (int sy = 0; sy < sgy; sy++) {
+            srow_pre[sy] = run;
+            run += srow_tot[sy] * (uint32_t)min(kSuper, gy - sy * kSuper);
+        }
+        srow_pre[sgy] = run;
+        // this workgroup's (super-tile, segment): last s with sbase[s] <= b
+        const uint32_t b = blockIdx.x;
+        int s = -1, seg = 0;
+        if (b < sbase[S]) {
+            int lo = 0, hi = S - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (sbase[mid] <= b) lo = mid;
+                else hi = mid - 1;
+            }
+            s = lo;
+            seg = (int)(b - sbase[lo]);
+        }
+        sh[0] = s;
+        sh[1] = seg;
+    }
+    __syncthreads();
+    auto row_prefix = [&](int y) { return srow_pre[y / kSuper] + (uint32_t)(y % kSuper) * srow_tot[y / kSuper]; };
+    if (blockIdx.x == 0) {  // the map for k_bin_emit
+        for (int i = t; i < S; i += blockDim.x) {
+            g_sranges[i] = sr[i];
+            g_seg_base[i] = sbase[i];
+            g_colpre[i] = scol[i];
+        }
+        if (t == 0) g_seg_base[S] = sbase[S];
+        for (int y = t; y <= gy; y += blockDim.x) g_rowpre[y] = y < gy ? row_prefix(y) : srow_pre[sgy];
+    }
+    const int s = sh[0], seg = sh[1];
+    if (s < 0) return;
+    SegmentCtx c;
+    c.s = s;
+    c.seg = seg;
+    c.ox = (s % sgx) * kSuper;
+    c.oy = (s / sgx) * kSuper;
+    c.e0 = sr[s].x + (uint32_t)seg * kSegEntries;
+    c.e1 = min(sr[s].y, c.e0 + (uint32_t)kSegEntries);
+    c.nseg = super_segments(sr[s]);
+    c.colpre = scol[s];
+    if (t < 64) cnt[t] = 0;
+    __syncthreads();
+    uint32_t mine = 0;  // lane l: entries of this wave covering local tile l
+    for (uint32_t b = c.e0 + (t & ~63u); b < c.e1; b += 256) {
+        const uint32_t e = b + (t & 63);
+        const uint64_t m = e < c.e1 ? entry_mask(keys[e]) : 0ull;
+        mine += (uint32_t)__popcll(transpose64(m));
+    }
+    atomicAdd(&cnt[t & 63], mine);
+    __syncthreads();
+    if (t < 64) {
+        const int x = c.ox + (t & 7), y = c.oy + (t >> 3);
+        if (x < gx && y < gy) table[(int64_t)row_prefix(y) + c.colpre + (uint32_t)(t & 7) * c.nseg + seg] = cnt[t];
+    }
+}
+
 __global__ __launch_bounds__(256) void k_bin_emit(int S, int sgx, int gx, int gy, const uint32_t* __restrict__ seg_base,
                                                   const uint2* __restrict__ sranges,
                                                   const uint32_t* __restrict__ col_prefix,
@@ -888,15 +993,27 @@ hipError_t launch_binning(int P, int64_t R, const Layout& L, char* geom, char* i
     if (e != hipSuccess) return e;
     const uint32_t* skeys = (passes & 1) ? kB : kA;
     const uint32_t* svals = (passes & 1) ? vB : vA;
-    hipLaunchKernelGGL(k_super_ranges, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, s, E, skeys, sranges);
-    if ((e = post(debug, s)) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_seg_setup, dim3(1), dim3(kScanThreads), 4 * (size_t)L.sgy, s, L.supers, L.sgx, L.sgy, L.gx,
-                       L.gy, (const uint2*)sranges, seg_base, colpre, rowpre);
-    if ((e = post(debug, s)) != hipSuccess) return e;
     const unsigned grid = (unsigned)L.seg_blocks;
-    hipLaunchKernelGGL(k_bin_count, dim3(grid), dim3(256), 0, s, L.supers, L.sgx, L.gx, L.gy, (const uint32_t*)seg_base,
-                       (const uint2*)sranges, (const uint32_t*)colpre, (const uint32_t*)rowpre, skeys, table);
-    if ((e = post(debug, s)) != hipSuccess) return e;
+    if (passes == 1 && L.supers <= kFusedSupers) {
+        // one pass: the scanned histogram of that pass holds the super-tile ranges (radix_sort's
+        // layout: [digit][block], nblk blocks of its tile size, 1 << super_bits digits)
+        const int tile = kRadixThreads * (E <= (1 << 21) ? 4 : 16);
+        const int nblk = (int)((E + tile - 1) / tile);
+        hipLaunchKernelGGL(k_bin_count_fused, dim3(grid), dim3(256), 0, s, L.supers, L.sgx, L.sgy, L.gx, L.gy, nblk,
+                           1 << L.super_bits, E, reinterpret_cast<const uint32_t*>(binning + L.bin_radix_hist), sranges,
+                           seg_base, colpre, rowpre, skeys, table);
+        if ((e = post(debug, s)) != hipSuccess) return e;
+    } else {
+        hipLaunchKernelGGL(k_super_ranges, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, s, E, skeys, sranges);
+        if ((e = post(debug, s)) != hipSuccess) return e;
+        hipLaunchKernelGGL(k_seg_setup, dim3(1), dim3(kScanThreads), 4 * (size_t)L.sgy, s, L.supers, L.sgx, L.sgy,
+                           L.gx, L.gy, (const uint2*)sranges, seg_base, colpre, rowpre);
+        if ((e = post(debug, s)) != hipSuccess) return e;
+        hipLaunchKernelGGL(k_bin_count, dim3(grid), dim3(256), 0, s, L.supers, L.sgx, L.gx, L.gy,
+                           (const uint32_t*)seg_base, (const uint2*)sranges, (const uint32_t*)colpre,
+                           (const uint32_t*)rowpre, skeys, table);
+        if ((e = post(debug, s)) != hipSuccess) return e;
+    }
     if ((e = scan_exclusive(table, table, (int)L.seg_table_words, regions + L.super_passes * L.scan_region_bin,
                             nullptr, fault, s, debug)) != hipSuccess)
         return e;

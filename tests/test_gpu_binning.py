@@ -1,0 +1,45 @@
+"""Binning paths at the edges of the super-tile scheme, HIP vs the oracle (bit-exact forward).
+
+The super-tile sort (lsr_binning.hip) is one 8-bit radix pass when the image has at most 256
+super-tiles of 8 x 8 tiles (1080p: 135), and then takes the fused count kernel
+(k_bin_count_fused: super-tile ranges straight from the scanned radix histogram); beyond 256
+super-tiles it takes two passes and the k_super_ranges / k_seg_setup kernels.  Both must give the
+oracle's per-tile lists, ranges and images bit for bit.
+"""
+import math
+
+import pytest
+import torch
+
+from tests.scenes import settings_for
+from tests.test_gpu_parity import check_backward, check_forward_exact
+from langsplat_amd.synthetic import make_cameras
+
+pytestmark = pytest.mark.gpu
+
+
+def strip_scene(P, W, H, seed):
+    """Gaussians spread over the whole field of view of a W x H camera at (0, 0, -4)."""
+    g = torch.Generator().manual_seed(seed)
+    cam = make_cameras(1, W, H)[0]
+    tx, ty = math.tan(cam.FoVx * 0.5), math.tan(cam.FoVy * 0.5)
+    d = 3.0 + torch.rand(P, generator=g) * 2.0
+    u, v = torch.rand(P, generator=g) * 2 - 1, torch.rand(P, generator=g) * 2 - 1
+    means = torch.stack([u * d * tx * 0.95, v * d * ty * 0.9, d - 4.0], 1)
+    s = 0.04 * d / 4.0
+    inp = dict(means3D=means, opacities=torch.rand((P, 1), generator=g) * 0.7 + 0.05,
+               colors_precomp=torch.rand((P, 3), generator=g),
+               language_feature_precomp=torch.nn.functional.normalize(torch.randn((P, 3), generator=g)),
+               scales=s[:, None] * (0.5 + torch.rand((P, 3), generator=g)),
+               rotations=torch.nn.functional.normalize(torch.randn((P, 4), generator=g)))
+    return settings_for(cam, sh_degree=0), inp
+
+
+@pytest.mark.parametrize("W,H,supers", [(2000, 250, 32), (8192, 72, 64), (33000, 64, 258)])
+def test_super_tile_counts(W, H, supers):
+    st, inp = strip_scene(3000, W, H, seed=W + H)
+    gx, gy = (W + 15) // 16, (H + 15) // 16
+    assert ((gx + 7) // 8) * ((gy + 7) // 8) == supers
+    run, std, ind, out = check_forward_exact(st, inp)
+    assert out[0] > 0
+    check_backward(st, inp, run, out)
