@@ -20,6 +20,8 @@
 //
 // Every step is deterministic, so point_list is bit-identical to the oracle's (tile, depth, id)
 // sort.  Scans are single-pass chained scans with decoupled look-back (one launch each).
+#include <stdlib.h>
+
 #include "lsr_internal.h"
 
 namespace lsr {
@@ -472,12 +474,23 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_scatter(
 // Sorts (keys, vals) by key bits [0, total_bits) in passes of <= 8 bits.  The input is read
 // from (k0, v0) (v0 == null: values are the input indices) and the result lands in
 // (kA, vA) after an even number of passes, or in (kB, vB) after an odd number; returns which.
+// Radix tile size: 4 keys per thread (>= ~1000 workgroups) up to kRadixSmallMax keys, else 16.
+// LSR_RADIX_SMALL_MAX=n moves the threshold (measurement aid).
+static bool radix_small(int64_t n)
+{
+    static const int64_t lim = [] {
+        const char* e = getenv("LSR_RADIX_SMALL_MAX");
+        return e ? (int64_t)atoll(e) : (int64_t)(1 << 21);
+    }();
+    return n <= lim;
+}
+
 static hipError_t radix_sort(const uint32_t* k0, const uint32_t* v0, int n, int total_bits, uint32_t* kA,
                              uint32_t* vA, uint32_t* kB, uint32_t* vB, uint32_t* hist, uint32_t* scan_regions,
                              size_t region_words, uint32_t* fault, hipStream_t s, bool debug, int* passes_out,
                              const uint32_t* kxf = nullptr, ScatterTail last = ScatterTail{nullptr, nullptr, nullptr})
 {
-    const bool small = n <= (1 << 21);
+    const bool small = radix_small(n);
     const int tile = kRadixThreads * (small ? 4 : 16);
     const int nblk = (n + tile - 1) / tile;
     const int passes = (total_bits + 7) / 8;
@@ -997,7 +1010,7 @@ hipError_t launch_binning(int P, int64_t R, const Layout& L, char* geom, char* i
     if (passes == 1 && L.supers <= kFusedSupers) {
         // one pass: the scanned histogram of that pass holds the super-tile ranges (radix_sort's
         // layout: [digit][block], nblk blocks of its tile size, 1 << super_bits digits)
-        const int tile = kRadixThreads * (E <= (1 << 21) ? 4 : 16);
+        const int tile = kRadixThreads * (radix_small(E) ? 4 : 16);
         const int nblk = (int)((E + tile - 1) / tile);
         hipLaunchKernelGGL(k_bin_count_fused, dim3(grid), dim3(256), 0, s, L.supers, L.sgx, L.sgy, L.gx, L.gy, nblk,
                            1 << L.super_bits, E, reinterpret_cast<const uint32_t*>(binning + L.bin_radix_hist), sranges,

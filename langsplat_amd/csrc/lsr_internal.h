@@ -30,7 +30,10 @@ constexpr int kCntWords = kCntSlots + 2 * kWorkClasses;
 constexpr int kRadixThreads = 256;
 // preprocess workgroups: the SH staging takes 4 (3M + 1) bytes of LDS per thread, so 128-thread
 // blocks let more of them share a CU and overlap one block's loads with another's arithmetic
-constexpr int kPreThreads = 128;
+#ifndef LSR_PRE_THREADS
+#define LSR_PRE_THREADS 128
+#endif
+constexpr int kPreThreads = LSR_PRE_THREADS;
 constexpr int kSuper = 8;          // super-tile = kSuper x kSuper tiles (64-bit tile masks)
 constexpr int kSegEntries = 512;   // super-tile list entries per binning workgroup
 constexpr int kGradStride = 16;                          // floats per Gaussian grad record

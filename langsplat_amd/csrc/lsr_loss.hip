@@ -96,8 +96,30 @@ __global__ __launch_bounds__(kFwdThreads) void k_masked_l1_forward(int C_rt, int
     const int C = kC > 0 ? kC : C_rt;
     const int64_t groups = HW / V;
     float acc = 0.0f;
-    for (int64_t gi = (int64_t)blockIdx.x * kFwdThreads + threadIdx.x; gi < groups;
-         gi += (int64_t)gridDim.x * kFwdThreads) {
+    const int64_t stride = (int64_t)gridDim.x * kFwdThreads;
+    int64_t gi = (int64_t)blockIdx.x * kFwdThreads + threadIdx.x;
+    if (kC > 0) {  // two groups per iteration: all 2 (2 kC + 1) loads in flight before the first use
+        for (; gi + stride < groups; gi += 2 * stride) {
+            float m[2][V], a[2][kC > 0 ? kC : 1][V], b[2][kC > 0 ? kC : 1][V];
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                const int64_t p = (gi + u * stride) * V;
+                load_mask<V>(mask, mask_is_float, p, m[u]);
+#pragma unroll
+                for (int c = 0; c < kC; c++) {
+                    load_px<V>(pred + (int64_t)c * HW, p, a[u][c]);
+                    load_px<V>(gt + (int64_t)c * HW, p, b[u][c]);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 2; u++)
+#pragma unroll
+                for (int c = 0; c < kC; c++)
+#pragma unroll
+                    for (int k = 0; k < V; k++) acc += fabsf(a[u][c][k] * m[u][k] - b[u][c][k] * m[u][k]);
+        }
+    }
+    for (; gi < groups; gi += stride) {
         const int64_t p = gi * V;
         float m[V];
         load_mask<V>(mask, mask_is_float, p, m);

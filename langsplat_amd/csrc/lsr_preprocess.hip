@@ -160,12 +160,8 @@ __global__ __launch_bounds__(kPreThreads) void k_preprocess(PreprocessParams p)
     }
     // per-thread contributions to the block partials: tile instances, super-tile entries, depth key
     uint32_t my_tiles = 0, my_supers = 0, my_key = 0xFFFFFFFFu, my_err = 0;
+    bool vis = false;  // reached the end of the block below (else culled: written after it)
     if (live) do {  // `break` = culled
-    p.radii[i] = 0;
-    if (p.visible) p.visible[i] = 0;
-    p.tiles[i] = 0;
-    p.depth_key[i] = 0xFFFFFFFFu;
-    *reinterpret_cast<uint2*>(p.rect + 2 * (size_t)i) = make_uint2(0u, 0u);  // empty: culled
     const float3 pv = xform4x3(p.view, px, py, pz);
     if (pv.z <= 0.2f) {
         if (p.prefiltered) my_err = 0x80000000u;
@@ -243,7 +239,15 @@ __global__ __launch_bounds__(kPreThreads) void k_preprocess(PreprocessParams p)
     my_supers = (uint32_t)(((r4[2] + kSuper - 1) / kSuper - r4[0] / kSuper) *
                            ((r4[3] + kSuper - 1) / kSuper - r4[1] / kSuper));
     my_key = __float_as_uint(pv.z);
+    vis = true;
     } while (0);
+    if (live && !vis) {  // culled: one store per output (the visible ones are written above)
+        p.radii[i] = 0;
+        if (p.visible) p.visible[i] = 0;
+        p.tiles[i] = 0;
+        p.depth_key[i] = 0xFFFFFFFFu;
+        *reinterpret_cast<uint2*>(p.rect + 2 * (size_t)i) = make_uint2(0u, 0u);  // empty: culled
+    }
     // block partials {R, E, min visible depth key, max visible depth key | error}: the host learns R, E and
     // the depth-key range before the depth sort (k_pre_reduce; the sort then needs only the bits
     // the visible keys actually span)
@@ -685,26 +689,26 @@ __global__ __launch_bounds__(256) void k_grad_epilogue(int P, const int* __restr
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P) return;
     const size_t i3 = 3 * (size_t)i;
-    const bool live = radii[i] > 0;
+    // every load is issued up front (one memory round trip): the records of culled Gaussians are
+    // zero (the backward zero-fills them and adds nothing), radii only selects the zero result
+    const int rad = radii[i];
     // stride kGradStrideLang: {dx, dy, l0, l1}{l2, -, -, -}; kGradStride: the full record
     const float4* g4 = reinterpret_cast<const float4*>(grad + (size_t)i * stride);
-    const float4 ga = live ? g4[0] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 ga = g4[0];
+    const float4 gb = stride == kGradStrideLang ? g4[1] : g4[2];
+    const bool raw = raw_lang && lang && dlang;
+    const float l0 = raw ? lang[i3] : 0.f, l1 = raw ? lang[i3 + 1] : 0.f, l2 = raw ? lang[i3 + 2] : 0.f;
+    const bool live = rad > 0;
     if (dmeans2D) {
-        dmeans2D[i3] = ga.x;
-        dmeans2D[i3 + 1] = ga.y;
+        dmeans2D[i3] = live ? ga.x : 0.f;
+        dmeans2D[i3 + 1] = live ? ga.y : 0.f;
         dmeans2D[i3 + 2] = 0.f;
     }
     if (dlang) {
         float3 d = make_float3(0.f, 0.f, 0.f);
         if (live) {
-            float3 gl;
-            if (stride == kGradStrideLang) {
-                gl = make_float3(ga.z, ga.w, g4[1].x);
-            } else {
-                const float4 gc = g4[2];
-                gl = make_float3(gc.y, gc.z, gc.w);
-            }
-            d = (raw_lang && lang) ? act_lang_backward(lang[i3], lang[i3 + 1], lang[i3 + 2], gl.x, gl.y, gl.z) : gl;
+            const float3 gl = stride == kGradStrideLang ? make_float3(ga.z, ga.w, gb.x) : make_float3(gb.y, gb.z, gb.w);
+            d = raw ? act_lang_backward(l0, l1, l2, gl.x, gl.y, gl.z) : gl;
         }
         dlang[i3] = d.x;
         dlang[i3 + 1] = d.y;
