@@ -71,6 +71,10 @@ class GradBucket:
         if not self.attached():
             raise RuntimeError("GradBucket: a parameter's .grad no longer aliases the bucket "
                                "(use zero_grad(set_to_none=False))")
+        if average and dist.get_backend(group) == "nccl":
+            # RCCL's ncclAvg: the division is part of the collective (no separate scaling kernel)
+            dist.all_reduce(self.flat, op=dist.ReduceOp.AVG, group=group)
+            return
         dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group)
         if average:
             self.flat.mul_(1.0 / dist.get_world_size(group))
