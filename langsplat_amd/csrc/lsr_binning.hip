@@ -818,38 +818,36 @@ __global__ __launch_bounds__(256) void k_bin_count_fused(int S, int sgx, int sgy
     const uint32_t ex = block_exclusive_scan(nseg, wsum, &tot);
     if (t < S) sbase[t] = ex;
     if (t == 0) sbase[S] = tot;
+    // column prefixes inside each super-row and the row totals from one scan of the
+    // tile-weighted segment counts (a row's prefix = scan - scan at the row start)
+    const int sy = t < S ? t / sgx : 0, sx = t - sy * sgx;
+    const uint32_t wv = t < S ? nseg * (uint32_t)min(kSuper, gx - sx * kSuper) : 0u;
+    uint32_t wtot;
+    const uint32_t wex = block_exclusive_scan(wv, wsum, &wtot);
+    scol[t] = wex;  // global exclusive scan for now
     __syncthreads();
-    if (t < S) {  // column prefix inside the super-row, and the row totals
-        const int sy = t / sgx, sx = t - sy * sgx;
-        uint32_t run = 0;
-        for (int x = 0; x < sx; x++)
-            run += super_segments(sr[sy * sgx + x]) * (uint32_t)min(kSuper, gx - x * kSuper);
-        scol[t] = run;
-        if (sx == sgx - 1) srow_tot[sy] = run + nseg * (uint32_t)min(kSuper, gx - sx * kSuper);
+    const uint32_t row0 = t < S ? scol[sy * sgx] : 0u;
+    if (t < S && sx == sgx - 1) srow_tot[sy] = wex + wv - row0;
+    __syncthreads();
+    if (t < S) scol[t] = wex - row0;
+    // whole tile rows above each super-row
+    const uint32_t rv = t < sgy ? srow_tot[t] * (uint32_t)min(kSuper, gy - t * kSuper) : 0u;
+    uint32_t rtot;
+    const uint32_t rex = block_exclusive_scan(rv, wsum, &rtot);
+    if (t < sgy) srow_pre[t] = rex;
+    if (t == 0) {
+        srow_pre[sgy] = rtot;
+        sh[0] = -1;
+        sh[1] = 0;
     }
     __syncthreads();
-    if (t == 0) {
-        uint32_t run = 0;
-        for (int sy = 0; sy < sgy; sy++) {
-            srow_pre[sy] = run;
-            run += srow_tot[sy] * (uint32_t)min(kSuper, gy - sy * kSuper);
-        }
-        srow_pre[sgy] = run;
-        // this workgroup's (super-tile, segment): last s with sbase[s] <= b
+    // this workgroup's (super-tile, segment): the s with sbase[s] <= b < sbase[s + 1]
+    {
         const uint32_t b = blockIdx.x;
-        int s = -1, seg = 0;
-        if (b < sbase[S]) {
-            int lo = 0, hi = S - 1;
-            while (lo < hi) {
-                const int mid = (lo + hi + 1) >> 1;
-                if (sbase[mid] <= b) lo = mid;
-                else hi = mid - 1;
-            }
-            s = lo;
-            seg = (int)(b - sbase[lo]);
+        if (t < S && sbase[t] <= b && b < sbase[t + 1]) {
+            sh[0] = t;
+            sh[1] = (int)(b - sbase[t]);
         }
-        sh[0] = s;
-        sh[1] = seg;
     }
     __syncthreads();
     auto row_prefix = [&](int y) { return srow_pre[y / kSuper] + (uint32_t)(y % kSuper) * srow_tot[y / kSuper]; };
