@@ -583,11 +583,11 @@ __device__ __forceinline__ void bwd_pixel_init(BwdPixel& q, const RenderParams& 
 // alpha or G) -- so the wave needs no exec-mask split and no zero-fill of v.
 // Constant factors are applied once per (tile, Gaussian) at the flush instead of per pixel
 // (flush_scale): v[0] = dL/dmean2D.x / (2 ddelx_dx), v[1] likewise, v[2..4] = -2 dL/dconic.
-// A = {x, y, -conic.x / 2, -conic.z / 2}, B = {conic.y, opacity, .., ..}.
+// A = {x, y, -conic.x / 2, -conic.z / 2}, B = {conic.y, opacity, .., ..}, hB = -conic.y / 2.
 template <bool kFeat, bool kColor, bool kGeo>
 __device__ __forceinline__ void bwd_pixel_blend(BwdPixel& q, float G, float alpha, float dx, float dy,
                                                 const float4& A, const float4& B, const float3& C, const float3& F,
-                                                float (&v)[12])
+                                                float hB, float (&v)[12])
 {
     const float one_m = 1.0f - alpha;
     // one v_rcp_f32 replaces the two IEEE divisions T / (1 - alpha) and T_final / (1 - alpha)
@@ -632,16 +632,21 @@ __device__ __forceinline__ void bwd_pixel_blend(BwdPixel& q, float G, float alph
     // dL/dalpha = T (sum) - T_final / (1 - alpha) (bg . dL/dpix); bg_term = -T_final (bg . dL/dpix)
     dL_dalpha = kColor ? fma_(q.bg_term, inv_one_m, dL_dalpha * q.T) : dL_dalpha * q.T;
     const float dL_dG = B.y * dL_dalpha;
-    const float ga = (G * dx) * dL_dG, gb = (G * dy) * dL_dG;
-    // dG/ddelx dL/dG = -(ga conic.x + gb conic.y) = 2 (ga A.z - gb conic.y / 2), likewise y
-    v[0] = fma_(-0.5f, gb * B.x, ga * A.z);
-    v[1] = fma_(-0.5f, ga * B.x, gb * A.w);
     if (kGeo) {  // conic and opacity partials: only the geometry gradients use them
+        const float ga = (G * dx) * dL_dG, gb = (G * dy) * dL_dG;
+        // dG/ddelx dL/dG = -(ga conic.x + gb conic.y) = 2 (ga A.z - gb conic.y / 2), likewise y
+        v[0] = fma_(-0.5f, gb * B.x, ga * A.z);
+        v[1] = fma_(-0.5f, ga * B.x, gb * A.w);
         v[2] = ga * dx;
         v[3] = ga * dy;
         v[4] = gb * dy;
         v[5] = G * dL_dalpha;
     } else {
+        // the same two values factored as G dL/dG (A.z dx - conic.y dy / 2) and likewise y:
+        // A.z dx, A.w dy and conic.y dx are the power's own products (shared by CSE)
+        const float sG = G * dL_dG;
+        v[0] = sG * fma_(hB, dy, A.z * dx);  // hB = -conic.y / 2
+        v[1] = sG * fma_(-0.5f, B.x * dx, A.w * dy);
         v[2] = v[3] = v[4] = v[5] = 0.0f;
     }
 }
@@ -700,12 +705,12 @@ __device__ unsigned long long g_render_stats[8 + 65];
 
 // One list entry's staged record as the backward walk reads it from LDS.
 struct BwdEntry {
-    float4 A, B;  // {x, y, -conic.x / 2, -conic.z / 2}, {conic.y, opacity, power cutoff, f1}
+    float4 A, B;  // {x, y, -conic.x / 2, -conic.z / 2}, {conic.y, opacity, power cutoff, f1 (kColor)}
     float4 C;     // kColor: {r, g, b, f0}
-    float2 F;     // kColor: {f2, -}; otherwise {f0, f2}
+    float4 F;     // kColor: {f2, -, -, -}; k5: {f0, f1, f2, -conic.y / 2}; otherwise {f0, f2, -, -}
 };
 
-template <bool kFeat, bool kColor>
+template <bool kFeat, bool kColor, bool kGeo>
 __device__ __forceinline__ BwdEntry load_entry(const float4* sA, const float4* sB, const float4* sC, const float* sF,
                                                int j)
 {
@@ -713,18 +718,22 @@ __device__ __forceinline__ BwdEntry load_entry(const float4* sA, const float4* s
     e.A = sA[j];
     e.B = sB[j];
     e.C = make_float4(0.f, 0.f, 0.f, 0.f);
-    e.F = make_float2(0.f, 0.f);
+    e.F = make_float4(0.f, 0.f, 0.f, 0.f);
     if (kColor) {
         e.C = sC[j];
         if (kFeat) e.F.x = sF[j];
+    } else if (!kGeo) {
+        e.F = *reinterpret_cast<const float4*>(&sF[4 * j]);
     } else if (kFeat) {
-        e.F = *reinterpret_cast<const float2*>(&sF[2 * j]);
+        const float2 f = *reinterpret_cast<const float2*>(&sF[2 * j]);
+        e.F = make_float4(f.x, f.y, 0.f, 0.f);
     }
     return e;
 }
 
 // One entry of a wave's back-to-front walk: the exact skip tests of the forward, the blend and the
-// wave reduce-scatter of its partials into the tile sums sG (slot j).  kk = the entry's list index.
+// wave reduce-scatter of its partials into the tile sums (sG = this lane's value slot of entry 0,
+// entry j at + j kGS).  kk = the entry's list index.
 template <bool kStats, bool kFeat, bool kColor, bool kGeo, bool k5>
 __device__ __forceinline__ void bwd_walk_entry(BwdPixel& q, const BwdEntry& E, int j, int kk, float pfx, float pfy,
                                                int lane, int vidx, float* sG, uint32_t* s_stat)
@@ -765,16 +774,16 @@ __device__ __forceinline__ void bwd_walk_entry(BwdPixel& q, const BwdEntry& E, i
         C = make_float3(E.C.x, E.C.y, E.C.z);
         if (kFeat) F = make_float3(E.C.w, B.w, E.F.x);
     } else if (kFeat) {
-        F = make_float3(E.F.x, B.w, E.F.y);
+        F = kGeo ? make_float3(E.F.x, B.w, E.F.y) : make_float3(E.F.x, E.F.y, E.F.z);
     }
     float v[12];
-    bwd_pixel_blend<kFeat, kColor, kGeo>(q, G, al, dx, dy, A, B, C, F, v);
+    bwd_pixel_blend<kFeat, kColor, kGeo>(q, G, al, dx, dy, A, B, C, F, (kColor || kGeo) ? -0.5f * B.x : E.F.w, v);
     if (k5) {
         const float tot = wave_reduce_scatter5(v, lane);
-        if (scatter_writer5(lane)) atomicAdd(&sG[j * kGS + gslot<kColor, k5>(vidx)], tot);
+        if (scatter_writer5(lane)) atomicAdd(sG + (uint32_t)(j * kGS), tot);  // sG: this lane's slot
     } else {
         const float tot = wave_reduce_scatter12(v, lane);
-        if (scatter_writer(lane) && gvalue<kColor, kGeo>(vidx)) atomicAdd(&sG[j * kGS + gslot<kColor, k5>(vidx)], tot);
+        if (scatter_writer(lane) && gvalue<kColor, kGeo>(vidx)) atomicAdd(sG + (uint32_t)(j * kGS), tot);
     }
 }
 
@@ -787,11 +796,15 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
     __shared__ float4 sA[kThreads];      // x, y, -0.5 conic.x, -0.5 conic.z
     __shared__ float4 sB[kThreads];      // conic.y, opacity, power cutoff, f1
     // kColor: sC = {r, g, b, f0}, sF = {f2}; otherwise (the colour gradient is zero) only the language
-    // feature is staged, sF = {f0, f2}, and the tile sums hold 9 slots per entry (no colour slots)
+    // feature is staged, sF = {f0, f2} (f1 in sB.w), and the tile sums hold 9 slots per entry (no colour
+    // slots); the language step (k5) stages sF = {f0, f1, f2, -conic.y / 2}: one 16-B read, f0 / f1
+    // adjacent for the packed subtract, the half conic.y of the screen-space gradient precomputed
     constexpr bool k5 = !kGeo && !kColor;  // the language step: five values per entry
     constexpr int kGS = k5 ? 5 : (kColor ? 12 : 9);
     __shared__ float4 sC[kColor ? kThreads : 1];
-    __shared__ float sF[kThreads * (kColor ? 1 : 2)];
+    __shared__ float4 sF4[k5 ? kThreads : 1];
+    __shared__ float sF1[k5 ? 1 : (kColor ? kThreads : 2 * kThreads)];
+    float* sF = k5 ? reinterpret_cast<float*>(sF4) : sF1;
     __shared__ float sG[kThreads * kGS];  // per-entry gradient sums of the tile
     __shared__ uint8_t sM[kThreads];     // wave_cover mask (& the waves' contributor bounds)
     __shared__ uint32_t s_wmax[kThreads / 64];
@@ -831,6 +844,7 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
     // entries at list index >= max over the tile of n_contrib can contribute to no pixel
     const int maxl = (int)max(max(w0, w1), max(w2, w3));
     const int vidx = k5 ? scatter_index5(lane) : scatter_index(lane);
+    float* const sGl = sG + gslot<kColor, k5>(vidx);  // this lane's value slot in the tile sums
 
     for (int done_cnt = 0; done_cnt < maxl; done_cnt += kThreads) {
         __syncthreads();
@@ -847,6 +861,8 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
             if (kColor) {
                 sC[t] = make_float4(b.z, b.w, c.x, c.y);
                 sF[t] = c.w;
+            } else if (k5) {
+                sF4[t] = make_float4(c.y, c.z, c.w, -0.5f * a.w);
             } else {
                 sF[2 * t] = c.y;
                 sF[2 * t + 1] = c.w;
@@ -871,9 +887,9 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
             while (m != 0ull) {
                 const int j = r + (int)__builtin_ctzll(m);
                 m &= m - 1ull;
-                const BwdEntry cur = load_entry<kFeat, kColor>(sA, sB, sC, sF, j);
+                const BwdEntry cur = load_entry<kFeat, kColor, kGeo>(sA, sB, sC, sF, j);
                 bwd_walk_entry<kStats, kFeat, kColor, kGeo, k5>(q, cur, j, maxl - 1 - (done_cnt + j), pfx, pfy, lane,
-                                                                vidx, sG, s_stat);
+                                                                vidx, sGl, s_stat);
             }
         }
         if (kStats && lane == 0) atomicMax(&s_bmax, nw);
