@@ -151,6 +151,23 @@ def pmc_traffic(stage):
     return None, None
 
 
+def pmc_valu(stage):
+    """VALU instructions issued per CU per cycle by the stage's kernel (at most 1: a CU issues one
+    wave64 VALU instruction per cycle) from the newest committed profiles/*_valu.json
+    (tools/valu_summary.py over tools/pmc_valu.sh), or (None, None)."""
+    import glob
+    kern = STAGE_KERNEL.get(stage)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_valu.json")), key=os.path.getmtime)
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))["kernels"].get(kern, {})
+        except (OSError, ValueError, KeyError):
+            continue
+        if "valu_per_cu_cycle" in d:
+            return float(d["valu_per_cu_cycle"]), os.path.relpath(f, ROOT)
+    return None, None
+
+
 def cpu_baseline(cfg, seconds_budget=25.0):
     """Oracle (oracle/lsr_oracle.c, 1 thread) fwd+bwd on a bounded sample of the same workload:
     the first P/2 Gaussians of the C3 scene, same camera and resolution (~15 s single-threaded)."""
@@ -182,8 +199,8 @@ def cpu_baseline(cfg, seconds_budget=25.0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=100)  # ~70 ms timed: averages out host jitter
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--json-out", default=None)
@@ -321,6 +338,11 @@ def main():
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                     "traffic": None if traffic is None else int(traffic), "traffic_source": src,
                     "avg_ms": round(dom["avg_ms"], 4), "bytes_per_launch": int(bytes_dom)}
+        # what actually bounds it: the render kernels are VALU-issue-bound
+        valu, vsrc = pmc_valu(dom_name)
+        if valu is not None:
+            roofline["valu_issue_frac"] = round(valu, 3)
+            roofline["valu_source"] = vsrc
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(cfg)
