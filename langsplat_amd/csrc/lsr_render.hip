@@ -526,6 +526,7 @@ __device__ __forceinline__ float wave_reduce_scatter12(const float (&v)[12], int
     float w = mirror_add<0x141>(t0, t1, u4);         // row_half_mirror
     w += dpp<0x4E>(w);                               // quad_perm [2,3,0,1]
     w += dpp<0xB1>(w);                               // quad_perm [1,0,3,2]
+    asm volatile("" : "+v"(w));                      // see wave_reduce_scatter5
     return w;
 }
 
@@ -663,6 +664,9 @@ __device__ __forceinline__ float wave_reduce_scatter5(const float (&v)[12], int 
     w += dpp<0x141>(w);                                   // row_half_mirror
     w += dpp<0x4E>(w);                                    // quad_perm [2,3,0,1]
     w += dpp<0xB1>(w);                                    // quad_perm [1,0,3,2]
+    // keep the last add next to its DPP move (one v_add_f32_dpp) instead of letting it sink into
+    // the writers' branch as a separate v_mov_dpp + v_add
+    asm volatile("" : "+v"(w));
     return w;
 }
 
