@@ -27,10 +27,20 @@ constexpr float SH_C3_0 = -0.5900435899266435f, SH_C3_1 = 2.890611442640554f,
                 SH_C3_6 = -0.5900435899266435f;
 
 // exp restatement (Cody-Waite by ln2 + degree-7 Taylor); identical op sequence to lso_expf.
+// n = x / ln2 rounded to nearest through the 1.5 * 2^23 shifter t (one fused rounding of the
+// exact product); bits(t) = 0x4B400000 + n, and since 0x4B400000 << 23 == 0 (mod 2^32) the scale
+// 2^n has the bits (bits(t) << 23) + (127 << 23): one shift-add, no rint / int conversion.
+constexpr float kExpShift = 12582912.0f;  // 1.5 * 2^23
+__device__ __forceinline__ float exp_scale(float t)
+{
+    return __uint_as_float((__float_as_uint(t) << 23) + (127u << 23));
+}
+
 __device__ __forceinline__ float expf_exact(float x)
 {
     if (x < -87.0f) return 0.0f;
-    float n = __builtin_rintf(x * 1.44269504088896341f);
+    const float t = __builtin_fmaf(x, 1.44269504088896341f, kExpShift);
+    const float n = t - kExpShift;
     float r = __builtin_fmaf(n, -0.693145751953125f, x);
     r = __builtin_fmaf(n, -1.42860682030941723212e-6f, r);
     float p = 1.98412698e-4f;
@@ -41,8 +51,7 @@ __device__ __forceinline__ float expf_exact(float x)
     p = __builtin_fmaf(p, r, 0.5f);
     p = __builtin_fmaf(p, r, 1.0f);
     p = __builtin_fmaf(p, r, 1.0f);
-    int e = (int)n;
-    return p * __uint_as_float((uint32_t)(e + 127) << 23);
+    return p * exp_scale(t);
 }
 
 // expf_exact without the underflow branch, for the render loops: every alpha they use comes from a
@@ -52,7 +61,8 @@ __device__ __forceinline__ float expf_exact(float x)
 __device__ __forceinline__ float expf_exact_render(float x)
 {
     x = __builtin_fmaxf(x, -87.0f);
-    float n = __builtin_rintf(x * 1.44269504088896341f);
+    const float t = __builtin_fmaf(x, 1.44269504088896341f, kExpShift);
+    const float n = t - kExpShift;
     float r = __builtin_fmaf(n, -0.693145751953125f, x);
     r = __builtin_fmaf(n, -1.42860682030941723212e-6f, r);
     float p = 1.98412698e-4f;
@@ -63,8 +73,7 @@ __device__ __forceinline__ float expf_exact_render(float x)
     p = __builtin_fmaf(p, r, 0.5f);
     p = __builtin_fmaf(p, r, 1.0f);
     p = __builtin_fmaf(p, r, 1.0f);
-    int e = (int)n;
-    return p * __uint_as_float((uint32_t)(e + 127) << 23);
+    return p * exp_scale(t);
 }
 
 // expf_exact_render of two values at once: the polynomial as packed fp32 (v_pk_fma_f32), i.e. the
@@ -73,7 +82,8 @@ typedef float lsr_f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ lsr_f2 expf_exact_render2(lsr_f2 x)
 {
     x = __builtin_elementwise_max(x, (lsr_f2)(-87.0f));
-    lsr_f2 n = __builtin_elementwise_rint(x * 1.44269504088896341f);
+    const lsr_f2 t = __builtin_elementwise_fma(x, (lsr_f2)(1.44269504088896341f), (lsr_f2)(kExpShift));
+    const lsr_f2 n = t - kExpShift;
     lsr_f2 r = __builtin_elementwise_fma(n, (lsr_f2)(-0.693145751953125f), x);
     r = __builtin_elementwise_fma(n, (lsr_f2)(-1.42860682030941723212e-6f), r);
     lsr_f2 p = (lsr_f2)(1.98412698e-4f);
@@ -84,10 +94,9 @@ __device__ __forceinline__ lsr_f2 expf_exact_render2(lsr_f2 x)
     p = __builtin_elementwise_fma(p, r, (lsr_f2)(0.5f));
     p = __builtin_elementwise_fma(p, r, (lsr_f2)(1.0f));
     p = __builtin_elementwise_fma(p, r, (lsr_f2)(1.0f));
-    const int e0 = (int)n.x, e1 = (int)n.y;
     lsr_f2 sc;
-    sc.x = __uint_as_float((uint32_t)(e0 + 127) << 23);
-    sc.y = __uint_as_float((uint32_t)(e1 + 127) << 23);
+    sc.x = exp_scale(t.x);
+    sc.y = exp_scale(t.y);
     return p * sc;
 }
 

@@ -107,7 +107,10 @@ static inline uint32_t f2bits(float f) { uint32_t u; memcpy(&u, &f, 4); return u
 float lso_expf(float x)
 {
     if (x < -87.0f) return 0.0f;
-    float n = rintf(x * 1.44269504088896341f);
+    /* n = x / ln2 rounded to nearest by the 1.5 * 2^23 shifter (one fused rounding of the exact
+       product); the shifted value's low mantissa bits are n, which also gives 2^n's exponent */
+    const float t = fmaf(x, 1.44269504088896341f, 12582912.0f);
+    const float n = t - 12582912.0f;
     float r = fmaf(n, -0.693145751953125f, x);
     r = fmaf(n, -1.42860682030941723212e-6f, r);
     float p = 1.98412698e-4f;
@@ -118,8 +121,8 @@ float lso_expf(float x)
     p = fmaf(p, r, 0.5f);
     p = fmaf(p, r, 1.0f);
     p = fmaf(p, r, 1.0f);
-    int e = (int)n;
-    return p * bits2f((uint32_t)(e + 127) << 23);
+    /* bits(t) = 0x4B400000 + n and 0x4B400000 << 23 == 0 (mod 2^32): (n + 127) << 23 */
+    return p * bits2f((f2bits(t) << 23) + (127u << 23));
 }
 
 /* ------------------------------------------------------------------------------------------ */
