@@ -79,6 +79,13 @@ __device__ __forceinline__ float expf_exact_render(float x)
 // expf_exact_render of two values at once: the polynomial as packed fp32 (v_pk_fma_f32), i.e. the
 // same IEEE operations per element in about half the instructions.
 typedef float lsr_f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ lsr_f2 make_f2(float x, float y)
+{
+    lsr_f2 v;
+    v.x = x;
+    v.y = y;
+    return v;
+}
 __device__ __forceinline__ lsr_f2 expf_exact_render2(lsr_f2 x)
 {
     x = __builtin_elementwise_max(x, (lsr_f2)(-87.0f));

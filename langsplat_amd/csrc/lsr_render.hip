@@ -214,10 +214,12 @@ __device__ __forceinline__ void launch_priority(int b, int prio)
 }
 
 // One pixel's front-to-back state (upstream FORWARD::renderCUDA locals).
+// T > 0 while the pixel composites; once it is done (the next entry would take T below 1e-4, or the
+// pixel is outside the image) T holds -T: one compare tests "active", and |T| is the final T.
 struct FwdPixel {
-    float T, C0, C1, C2, F0, F1, F2;
+    float T;
+    lsr_f2 C01, C2F0, F12;  // {C0, C1}, {C2, F0}, {F1, F2}: the colour / feature sums as packed pairs
     uint32_t contributor, last;
-    bool done;
 };
 
 // One front-to-back blend of list slot j with alpha al (upstream FORWARD::renderCUDA; the operation
@@ -228,18 +230,18 @@ __device__ __forceinline__ void fwd_pixel_blend(FwdPixel& q, float al, int j, ui
 {
     const float test_T = q.T * (1.0f - al);
     if (test_T < 0.0001f) {
-        q.done = true;
+        q.T = -q.T;  // done
         return;
     }
     const float4 Cc = sC[j];
     const float w = al * q.T;
-    q.C0 = fma_(Cc.x, w, q.C0);
-    q.C1 = fma_(Cc.y, w, q.C1);
-    q.C2 = fma_(Cc.z, w, q.C2);
+    const lsr_f2 w2 = make_f2(w, w);
+    q.C01 = __builtin_elementwise_fma(make_f2(Cc.x, Cc.y), w2, q.C01);
     if (kFeat) {
-        q.F0 = fma_(Cc.w, w, q.F0);
-        q.F1 = fma_(f1, w, q.F1);
-        q.F2 = fma_(sF[j], w, q.F2);
+        q.C2F0 = __builtin_elementwise_fma(make_f2(Cc.z, Cc.w), w2, q.C2F0);
+        q.F12 = __builtin_elementwise_fma(make_f2(f1, sF[j]), w2, q.F12);
+    } else {
+        q.C2F0.x = fma_(Cc.z, w, q.C2F0.x);
     }
     q.T = test_T;
     q.last = list_base + (uint32_t)j + 1u;  // upstream's 1-based contributor counter
@@ -299,20 +301,21 @@ __global__ __launch_bounds__(kTilePixels) void k_render_forward(RenderParams p)
     int px, py;
     pixel_map(tx, ty, t, px, py);
     const float pfx = (float)px, pfy = (float)py;
+    const lsr_f2 pxy = make_f2(pfx, pfy);
     const float tx0 = (float)(tx * kTile), ty0 = (float)(ty * kTile);
     const uint2 range = p.ranges[tile];
     const uint32_t start = range.x, end = range.y;
     const bool inside = px < p.W && py < p.H;
     if (t == 0) s_last = 0;
 
-    FwdPixel q{1.0f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0u, 0u, !inside};
+    FwdPixel q{inside ? 1.0f : -1.0f, make_f2(0.f, 0.f), make_f2(0.f, 0.f), make_f2(0.f, 0.f), 0u, 0u};
     PhaseTicks ph;
     if (kStats) ph.begin();
     // the point_list id of this thread's entry in the next batch is loaded before the current batch's
     // walk, so a batch's load phase waits for one memory round trip (the record gather), not two
     uint32_t g_next = start + t < end ? p.point_list[start + t] : 0u;
     for (uint32_t base = start; base < end; base += kThreads) {
-        const bool all_done = __syncthreads_count(q.done) == kThreads;
+        const bool all_done = __syncthreads_count(q.T < 0.0f) == kThreads;
         if (kStats && base != start) ph.lap(ph.walk);
         if (all_done) {
             if (kStats) ph.stopped = true;
@@ -345,16 +348,17 @@ __global__ __launch_bounds__(kTilePixels) void k_render_forward(RenderParams p)
         // so the two chains interleave; only the transmittance test and the blend are sequential.
         // Same operations per entry as one at a time (bit-identical results).
         for (int i = 0; i < n; i += 2) {
-            if (__ballot(!q.done) == 0ull) break;
+            if (__ballot(q.T > 0.0f) == 0ull) break;
             const int j0 = sL[wave][i];
             const bool has1 = i + 1 < n;
             const int j1 = has1 ? sL[wave][i + 1] : j0;
             const float4 A0 = sA[j0], B0 = sB[j0];
             const float4 A1 = sA[j1], B1 = sB[j1];
-            const float dx0 = A0.x - pfx, dy0 = A0.y - pfy;
-            const float dx1 = A1.x - pfx, dy1 = A1.y - pfy;
-            const float pw0 = fma_(A0.z * dx0, dx0, fma_(A0.w * dy0, dy0, -((B0.x * dx0) * dy0)));
-            const float pw1 = fma_(A1.z * dx1, dx1, fma_(A1.w * dy1, dy1, -((B1.x * dx1) * dy1)));
+            // per entry {dx, dy} and {A.z dx, A.w dy} as packed ops on the record's own register pairs
+            const lsr_f2 d0 = make_f2(A0.x, A0.y) - pxy, d1 = make_f2(A1.x, A1.y) - pxy;
+            const lsr_f2 m0 = make_f2(A0.z, A0.w) * d0, m1 = make_f2(A1.z, A1.w) * d1;
+            const float pw0 = fma_(m0.x, d0.x, fma_(m0.y, d0.y, -((B0.x * d0.x) * d0.y)));
+            const float pw1 = fma_(m1.x, d1.x, fma_(m1.y, d1.y, -((B1.x * d1.x) * d1.y)));
             lsr_f2 pw2;
             pw2.x = pw0;
             pw2.y = pw1;
@@ -363,8 +367,8 @@ __global__ __launch_bounds__(kTilePixels) void k_render_forward(RenderParams p)
             const float al1 = fminf(0.99f, B1.y * G2.y);
             const bool ok0 = !(pw0 > 0.0f || pw0 < B0.z) && !(al0 < 1.0f / 255.0f);
             const bool ok1 = has1 && !(pw1 > 0.0f || pw1 < B1.z) && !(al1 < 1.0f / 255.0f);
-            if (ok0 && !q.done) fwd_pixel_blend<kFeat>(q, al0, j0, list_base, sC, sF, B0.w);
-            if (ok1 && !q.done) fwd_pixel_blend<kFeat>(q, al1, j1, list_base, sC, sF, B1.w);
+            if (ok0 && q.T > 0.0f) fwd_pixel_blend<kFeat>(q, al0, j0, list_base, sC, sF, B0.w);
+            if (ok1 && q.T > 0.0f) fwd_pixel_blend<kFeat>(q, al1, j1, list_base, sC, sF, B1.w);
         }
     }
     // the tile's replay length, for the backward's launch order
@@ -383,14 +387,15 @@ __global__ __launch_bounds__(kTilePixels) void k_render_forward(RenderParams p)
     if (!inside) return;
     const size_t HW = (size_t)p.W * p.H;
     const size_t pix = (size_t)py * p.W + px;
-    p.final_T[pix] = q.T;
+    const float Tf = fabsf(q.T);
+    p.final_T[pix] = Tf;
     p.n_contrib[pix] = q.last;
-    p.out_color[pix] = fma_(q.T, p.bg[0], q.C0);
-    p.out_color[HW + pix] = fma_(q.T, p.bg[1], q.C1);
-    p.out_color[2 * HW + pix] = fma_(q.T, p.bg[2], q.C2);
-    p.out_lang[pix] = q.F0;
-    p.out_lang[HW + pix] = q.F1;
-    p.out_lang[2 * HW + pix] = q.F2;
+    p.out_color[pix] = fma_(Tf, p.bg[0], q.C01.x);
+    p.out_color[HW + pix] = fma_(Tf, p.bg[1], q.C01.y);
+    p.out_color[2 * HW + pix] = fma_(Tf, p.bg[2], q.C2F0.x);
+    p.out_lang[pix] = q.C2F0.y;
+    p.out_lang[HW + pix] = q.F12.x;
+    p.out_lang[2 * HW + pix] = q.F12.y;
 }
 
 static bool render_stats_on()
