@@ -104,15 +104,15 @@ __device__ __forceinline__ uint32_t entry_cover(float x, float y, float a, float
 }
 
 // Compacts the batch slots [0, cnt) whose cover mask meets `bits` (the wave's blocks) into
-// list[0, n); returns n.
-__device__ __forceinline__ int wave_compact(const uint8_t* sM, int cnt, uint32_t bits, int lane, uint8_t* list)
+// list[0, n) as LDS byte offsets 16 e of their 16-B records; returns n.
+__device__ __forceinline__ int wave_compact(const uint8_t* sM, int cnt, uint32_t bits, int lane, uint16_t* list)
 {
     int n = 0;
     for (int r = 0; r < cnt; r += 64) {
         const int e = r + lane;
         const bool ov = e < cnt && (sM[e] & bits) != 0u;
         const uint64_t m = __ballot(ov);
-        if (ov) list[n + __popcll(m & ((1ull << lane) - 1ull))] = (uint8_t)e;
+        if (ov) list[n + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)(16 * e);
         n += __popcll(m);
     }
     return n;
@@ -219,32 +219,33 @@ __device__ __forceinline__ void launch_priority(int b, int prio)
 struct FwdPixel {
     float T;
     lsr_f2 C01, C2F0, F12;  // {C0, C1}, {C2, F0}, {F1, F2}: the colour / feature sums as packed pairs
-    uint32_t contributor, last;
+    uint32_t contributor;
+    uint32_t last16;        // 16 x upstream's 1-based contributor counter (the walk's byte offsets)
 };
 
-// One front-to-back blend of list slot j with alpha al (upstream FORWARD::renderCUDA; the operation
-// order of oracle render_pixel): stop before the entry once T would fall below 1e-4.
+// One front-to-back blend of the entry at LDS byte offset o (slot o / 16) with alpha al (upstream
+// FORWARD::renderCUDA; the operation order of oracle render_pixel): stop before the entry once T
+// would fall below 1e-4 (then T -> -T: done).  lb16 = 16 (list index of slot 0 + 1).
 template <bool kFeat>
-__device__ __forceinline__ void fwd_pixel_blend(FwdPixel& q, float al, int j, uint32_t list_base, const float4* sC,
-                                                const float* sF, float f1)
+__device__ __forceinline__ void fwd_pixel_blend(FwdPixel& q, float al, uint32_t o, uint32_t lb16, const char* sC,
+                                                const char* sF)
 {
     const float test_T = q.T * (1.0f - al);
-    if (test_T < 0.0001f) {
-        q.T = -q.T;  // done
-        return;
+    const bool go = !(test_T < 0.0001f);
+    if (go) {
+        const float4 Cc = *reinterpret_cast<const float4*>(sC + o);
+        const float w = al * q.T;
+        const lsr_f2 w2 = make_f2(w, w);
+        q.C01 = __builtin_elementwise_fma(make_f2(Cc.x, Cc.y), w2, q.C01);
+        if (kFeat) {
+            q.C2F0 = __builtin_elementwise_fma(make_f2(Cc.z, Cc.w), w2, q.C2F0);
+            q.F12 = __builtin_elementwise_fma(*reinterpret_cast<const lsr_f2*>(sF + o), w2, q.F12);
+        } else {
+            q.C2F0.x = fma_(Cc.z, w, q.C2F0.x);
+        }
+        q.last16 = lb16 + o;
     }
-    const float4 Cc = sC[j];
-    const float w = al * q.T;
-    const lsr_f2 w2 = make_f2(w, w);
-    q.C01 = __builtin_elementwise_fma(make_f2(Cc.x, Cc.y), w2, q.C01);
-    if (kFeat) {
-        q.C2F0 = __builtin_elementwise_fma(make_f2(Cc.z, Cc.w), w2, q.C2F0);
-        q.F12 = __builtin_elementwise_fma(make_f2(f1, sF[j]), w2, q.F12);
-    } else {
-        q.C2F0.x = fma_(Cc.z, w, q.C2F0.x);
-    }
-    q.T = test_T;
-    q.last = list_base + (uint32_t)j + 1u;  // upstream's 1-based contributor counter
+    q.T = go ? test_T : -q.T;
 }
 
 // Output of the tiles without entries among u = j, j + M, ... (background colour, T = 1, no
@@ -277,11 +278,11 @@ __global__ __launch_bounds__(kTilePixels) void k_render_forward(RenderParams p)
     const uint64_t t_start = kStats ? wall_clock64() : 0;
     constexpr int kThreads = kTilePixels;
     __shared__ float4 sA[kThreads];  // x, y, -0.5 conic.x, -0.5 conic.z
-    __shared__ float4 sB[kThreads];  // conic.y, opacity, power cutoff, f1
+    __shared__ float4 sB[kThreads];  // conic.y, opacity, power cutoff, -
     __shared__ float4 sC[kThreads];  // r, g, b, f0
-    __shared__ float sF[kThreads];   // f2
+    __shared__ float4 sF[kThreads];  // f1, f2, -, -  (16-B slots: every record of slot s at byte 16 s)
     __shared__ uint8_t sM[kThreads];  // entry_cover mask
-    __shared__ uint8_t sL[kThreads / 64][kThreads];  // per-wave culled slot lists
+    __shared__ uint16_t sL[kThreads / 64][kThreads];  // per-wave culled slot lists, as byte offsets 16 s
     __shared__ uint32_t s_last;
 
     const int T = p.gx * p.gy;
@@ -330,9 +331,9 @@ __global__ __launch_bounds__(kTilePixels) void k_render_forward(RenderParams p)
             const float4 c = p.record[3 * (size_t)g + 2];
             const float cut = power_cutoff(b.y);
             sA[t] = make_float4(a.x, a.y, -0.5f * a.z, -0.5f * b.x);
-            sB[t] = make_float4(a.w, b.y, cut, c.z);
+            sB[t] = make_float4(a.w, b.y, cut, 0.0f);
             sC[t] = make_float4(b.z, b.w, c.x, c.y);
-            sF[t] = c.w;
+            sF[t] = make_float4(c.z, c.w, 0.0f, 0.0f);
             sM[t] = (uint8_t)entry_cover(a.x, a.y, a.z, a.w, b.x, cut, tx0, ty0);
         }
         __syncthreads();
@@ -343,36 +344,39 @@ __global__ __launch_bounds__(kTilePixels) void k_render_forward(RenderParams p)
         __syncthreads();  // list visible to the wave's other lanes
         if (kStats) ph.lap(ph.compact);
         if (idx + kThreads < end) g_next = p.point_list[idx + kThreads];
-        const uint32_t list_base = base - start;  // list index of slot 0
+        const uint32_t lb16 = 16u * (base - start + 1u);  // 16 x (list index of slot 0 + 1)
+        const char* const cA = reinterpret_cast<const char*>(sA);
+        const char* const cB = reinterpret_cast<const char*>(sB);
+        const char* const cC = reinterpret_cast<const char*>(sC);
+        const char* const cF = reinterpret_cast<const char*>(sF);
         // two list entries per iteration: their power / exp / alpha do not depend on the pixel state,
         // so the two chains interleave; only the transmittance test and the blend are sequential.
-        // Same operations per entry as one at a time (bit-identical results).
+        // Same operations per entry as one at a time (bit-identical results).  The list holds byte
+        // offsets, so every record read addresses LDS with the list value itself.
         for (int i = 0; i < n; i += 2) {
             if (__ballot(q.T > 0.0f) == 0ull) break;
-            const int j0 = sL[wave][i];
+            const uint32_t o0 = sL[wave][i];
             const bool has1 = i + 1 < n;
-            const int j1 = has1 ? sL[wave][i + 1] : j0;
-            const float4 A0 = sA[j0], B0 = sB[j0];
-            const float4 A1 = sA[j1], B1 = sB[j1];
+            const uint32_t o1 = has1 ? sL[wave][i + 1] : o0;
+            const float4 A0 = *reinterpret_cast<const float4*>(cA + o0), B0 = *reinterpret_cast<const float4*>(cB + o0);
+            const float4 A1 = *reinterpret_cast<const float4*>(cA + o1), B1 = *reinterpret_cast<const float4*>(cB + o1);
             // per entry {dx, dy} and {A.z dx, A.w dy} as packed ops on the record's own register pairs
             const lsr_f2 d0 = make_f2(A0.x, A0.y) - pxy, d1 = make_f2(A1.x, A1.y) - pxy;
             const lsr_f2 m0 = make_f2(A0.z, A0.w) * d0, m1 = make_f2(A1.z, A1.w) * d1;
             const float pw0 = fma_(m0.x, d0.x, fma_(m0.y, d0.y, -((B0.x * d0.x) * d0.y)));
             const float pw1 = fma_(m1.x, d1.x, fma_(m1.y, d1.y, -((B1.x * d1.x) * d1.y)));
-            lsr_f2 pw2;
-            pw2.x = pw0;
-            pw2.y = pw1;
-            const lsr_f2 G2 = expf_exact_render2(pw2);
+            const lsr_f2 G2 = expf_exact_render2(make_f2(pw0, pw1));
             const float al0 = fminf(0.99f, B0.y * G2.x);
             const float al1 = fminf(0.99f, B1.y * G2.y);
             const bool ok0 = !(pw0 > 0.0f || pw0 < B0.z) && !(al0 < 1.0f / 255.0f);
             const bool ok1 = has1 && !(pw1 > 0.0f || pw1 < B1.z) && !(al1 < 1.0f / 255.0f);
-            if (ok0 && q.T > 0.0f) fwd_pixel_blend<kFeat>(q, al0, j0, list_base, sC, sF, B0.w);
-            if (ok1 && q.T > 0.0f) fwd_pixel_blend<kFeat>(q, al1, j1, list_base, sC, sF, B1.w);
+            if (ok0 && q.T > 0.0f) fwd_pixel_blend<kFeat>(q, al0, o0, lb16, cC, cF);
+            if (ok1 && q.T > 0.0f) fwd_pixel_blend<kFeat>(q, al1, o1, lb16, cC, cF);
         }
     }
+    const uint32_t qlast = q.last16 >> 4;
     // the tile's replay length, for the backward's launch order
-    uint32_t wl = q.last;
+    uint32_t wl = qlast;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) wl = max(wl, (uint32_t)__shfl_xor((int)wl, o, 64));
     __syncthreads();
@@ -389,7 +393,7 @@ __global__ __launch_bounds__(kTilePixels) void k_render_forward(RenderParams p)
     const size_t pix = (size_t)py * p.W + px;
     const float Tf = fabsf(q.T);
     p.final_T[pix] = Tf;
-    p.n_contrib[pix] = q.last;
+    p.n_contrib[pix] = qlast;
     p.out_color[pix] = fma_(Tf, p.bg[0], q.C01.x);
     p.out_color[HW + pix] = fma_(Tf, p.bg[1], q.C01.y);
     p.out_color[2 * HW + pix] = fma_(Tf, p.bg[2], q.C2F0.x);
