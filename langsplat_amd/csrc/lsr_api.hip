@@ -95,9 +95,16 @@ struct Scope {
 // pageable device-to-host copy (which is synchronous) and no stream-synchronise wake-up latency.
 namespace {
 struct HostCounters {
-    uint32_t vals[8];
-    uint32_t seq;
+    uint64_t slot[8];  // {value, seq}: low word the counter, high word the sequence number
+    uint32_t seq;      // unused by the publish kernel (kept for the launch signature)
 };
+
+static bool counters_arrived(const HostCounters* hc, uint32_t seq)
+{
+    for (int i = 0; i < 8; i++)
+        if ((uint32_t)(__atomic_load_n(&hc->slot[i], __ATOMIC_ACQUIRE) >> 32) != seq) return false;
+    return true;
+}
 thread_local HostCounters* t_hc = nullptr;
 thread_local uint32_t t_seq = 0;
 }  // namespace
@@ -108,12 +115,12 @@ static int32_t fail(int32_t code, const char* what, hipError_t e = hipSuccess);
 static hipError_t wait_counters(HostCounters* hc, uint32_t seq, hipStream_t stream)
 {
     for (uint64_t spin = 0;; spin++) {
-        if (__atomic_load_n(&hc->seq, __ATOMIC_ACQUIRE) == seq) return hipSuccess;
+        if (counters_arrived(hc, seq)) return hipSuccess;
         if ((spin & 1023) == 1023) {
             const hipError_t q = hipStreamQuery(stream);
             if (q != hipSuccess && q != hipErrorNotReady) return q;
             if (q == hipSuccess) {  // stream idle: the store must be visible now
-                if (__atomic_load_n(&hc->seq, __ATOMIC_ACQUIRE) == seq) return hipSuccess;
+                if (counters_arrived(hc, seq)) return hipSuccess;
                 return hipErrorUnknown;
             }
         }
@@ -270,15 +277,16 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
         void* h = nullptr;
         LSR_TRY(hipHostMalloc(&h, sizeof(HostCounters), hipHostMallocCoherent), "pinned counters");
         t_hc = static_cast<HostCounters*>(h);
-        t_hc->seq = 0;
+        memset(t_hc, 0, sizeof(HostCounters));
     }
     const uint32_t seq = ++t_seq == 0 ? ++t_seq : t_seq;
-    LSR_TRY(launch_publish_counters((P + kPreThreads - 1) / kPreThreads, pp.partial, counters, t_hc->vals, &t_hc->seq,
+    LSR_TRY(launch_publish_counters((P + kPreThreads - 1) / kPreThreads, pp.partial, counters,
+                                    reinterpret_cast<uint32_t*>(t_hc->slot), &t_hc->seq,
                                     seq, stream),
             "publish counters");
     LSR_TRY(wait_counters(t_hc, seq, stream), "wait counters");
     uint32_t host_cnt[8];
-    for (int i = 0; i < 8; i++) host_cnt[i] = t_hc->vals[i];
+    for (int i = 0; i < 8; i++) host_cnt[i] = (uint32_t)t_hc->slot[i];
     if (host_cnt[kCntError] && s->prefiltered)
         return fail(LSR_ERR_PREFILTERED, "lsr_forward: prefiltered=True but a Gaussian is outside the frustum");
     const int64_t R = host_cnt[kCntRendered];

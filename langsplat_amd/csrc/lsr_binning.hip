@@ -206,7 +206,7 @@ static hipError_t scan_exclusive(const uint32_t* in, uint32_t* out, int n, uint3
 // min / max, the prefiltered error flag: bit 31 of the max key), clears the other counter words
 // (scan fault, the tile schedule's class counts) -- so the counters need no memset before the
 // forward -- then publishes counters[0..7] to pinned host memory (system scope) followed by the
-// sequence number the host spins on.
+// sequence number the host spins on (one {value, seq} 64-bit slot per counter).
 constexpr int kPublishThreads = 1024;
 
 __global__ __launch_bounds__(kPublishThreads) void k_publish_counters(int nb, const uint4* __restrict__ partial,
@@ -254,9 +254,12 @@ __global__ __launch_bounds__(kPublishThreads) void k_publish_counters(int nb, co
     counters[kCntKeyMin] = red[2][0];
     counters[kCntKeyMax] = red[3][0] & 0x7FFFFFFFu;
     counters[kCntError] = red[3][0] >> 31;
+    // each value travels with the sequence number in one 64-bit store (single-copy atomic): the
+    // host waits for all 8 slots to carry `seq`, so no release fence (L2 write-back) is needed
+    uint64_t* slot = reinterpret_cast<uint64_t*>(host_vals);
     for (int i = 0; i < 8; i++)
-        __hip_atomic_store(&host_vals[i], counters[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(host_seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&slot[i], (uint64_t)counters[i] | ((uint64_t)seq << 32), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 hipError_t launch_publish_counters(int nb, const uint4* partial, uint32_t* counters, uint32_t* host_vals,
