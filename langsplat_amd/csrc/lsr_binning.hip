@@ -217,12 +217,22 @@ __global__ __launch_bounds__(kPublishThreads) void k_publish_counters(int nb, co
     constexpr int kWaves = kPublishThreads / 64;
     __shared__ uint32_t red[4][kWaves];
     uint32_t t = 0, e = 0, kmin = 0xFFFFFFFFu, kmax = 0;
-    for (int b = threadIdx.x; b < nb; b += kPublishThreads) {
-        const uint4 v = partial[b];
-        t += v.x;
-        e += v.y;
-        kmin = min(kmin, v.z);
-        kmax = max(kmax, v.w);  // the error bit, if set anywhere, survives the max
+    // kPer loads in flight per thread before any is consumed (8k partials at 1M Gaussians: one round)
+    constexpr int kPer = 8;
+    for (int b0 = threadIdx.x; b0 < nb; b0 += kPublishThreads * kPer) {
+        uint4 v[kPer];
+#pragma unroll
+        for (int j = 0; j < kPer; j++) {
+            const int b = b0 + j * kPublishThreads;
+            v[j] = b < nb ? partial[b] : make_uint4(0u, 0u, 0xFFFFFFFFu, 0u);
+        }
+#pragma unroll
+        for (int j = 0; j < kPer; j++) {
+            t += v[j].x;
+            e += v[j].y;
+            kmin = min(kmin, v[j].z);
+            kmax = max(kmax, v[j].w);  // the error bit, if set anywhere, survives the max
+        }
     }
     for (int i = threadIdx.x; i < kCntWords; i += kPublishThreads)
         if (i != kCntRendered && i != kCntSuper && i != kCntKeyMin && i != kCntKeyMax && i != kCntError)
