@@ -325,19 +325,32 @@ __device__ __forceinline__ uint32_t key_xf(uint32_t k, const uint32_t* kxf)
     return k == 0xFFFFFFFFu ? kxf[1] - kxf[0] : k - kxf[0];
 }
 
+// XCD-aware tile order: workgroups are dispatched round-robin over the 8 XCDs (workgroup i on XCD
+// i % 8), so consecutive tiles would land on 8 different L2s and every output line (histogram
+// column, digit run) would be assembled from partial writes of several XCDs.  Tile of workgroup i:
+// XCD x = i % 8 takes the contiguous tile range [x q + min(x, r), ...) with q = nblk / 8, r = nblk % 8.
+__device__ __forceinline__ int xcd_tile(int nblk, int remap)
+{
+    const int i = blockIdx.x;
+    if (!remap) return i;
+    const int x = i & 7, q = nblk >> 3, r = nblk & 7;
+    return x * q + min(x, r) + (i >> 3);
+}
+
 template <int kItems>
 __global__ __launch_bounds__(kRadixThreads) void k_radix_hist(const uint32_t* __restrict__ keys, int n, int shift,
                                                               int nbits, uint32_t* __restrict__ hist, int nblk,
-                                                              const uint32_t* __restrict__ kxf)
+                                                              const uint32_t* __restrict__ kxf, int remap)
 {
     constexpr int kWaves = kRadixThreads / 64;
     __shared__ uint32_t wcnt[kWaves][256];
+    const int blk = xcd_tile(nblk, remap);
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
     const uint32_t mask = (1u << nbits) - 1u;
 #pragma unroll
     for (int w = 0; w < kWaves; w++) wcnt[w][t] = 0;
     __syncthreads();
-    const int base = blockIdx.x * kRadixThreads * kItems + wave * 64 * kItems;
+    const int base = blk * kRadixThreads * kItems + wave * 64 * kItems;
     uint32_t d[kItems];
     bool valid[kItems];
 #pragma unroll
@@ -358,7 +371,7 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_hist(const uint32_t* __
         uint32_t c = 0;
 #pragma unroll
         for (int w = 0; w < kWaves; w++) c += wcnt[w][t];
-        hist[t * nblk + blockIdx.x] = c;
+        hist[t * nblk + blk] = c;
     }
 }
 
@@ -371,8 +384,9 @@ template <int kItems>
 __global__ __launch_bounds__(kRadixThreads) void k_radix_scatter(
     const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in, int n, int shift, int nbits,
     const uint32_t* __restrict__ hist, int nblk, uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
-    const uint32_t* __restrict__ kxf, ScatterTail tail)
+    const uint32_t* __restrict__ kxf, ScatterTail tail, int remap)
 {
+    const int blk = xcd_tile(nblk, remap);
     constexpr int kTile = kRadixThreads * kItems;
     constexpr int kWaves = kRadixThreads / 64;
     __shared__ uint32_t sk[kTile];
@@ -385,8 +399,8 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_scatter(
     const uint32_t mask = (1u << nbits) - 1u;
 #pragma unroll
     for (int w = 0; w < kWaves; w++) wcnt[w][t] = 0;
-    gbase[t] = t <= (int)mask ? hist[t * nblk + blockIdx.x] : 0u;
-    const int tile0 = blockIdx.x * kTile;
+    gbase[t] = t <= (int)mask ? hist[t * nblk + blk] : 0u;
+    const int tile0 = blk * kTile;
     const int base = tile0 + wave * 64 * kItems;
     uint32_t key[kItems], val[kItems], rank[kItems];
 #pragma unroll
@@ -508,6 +522,10 @@ static hipError_t radix_sort(const uint32_t* k0, const uint32_t* v0, int n, int 
     const int nblk = (n + tile - 1) / tile;
     const int passes = (total_bits + 7) / 8;
     *passes_out = passes;
+    static const int remap = [] {  // LSR_XCD_REMAP=0: tiles in dispatch order (measurement knob)
+        const char* v = getenv("LSR_XCD_REMAP");
+        return v && v[0] == '0' ? 0 : 1;
+    }();
     const uint32_t* kin = k0;
     const uint32_t* vin = v0;
     hipError_t e;
@@ -518,10 +536,10 @@ static hipError_t radix_sort(const uint32_t* k0, const uint32_t* v0, int n, int 
         uint32_t* vout = (pass & 1) ? vA : vB;
         if (small)
             hipLaunchKernelGGL(k_radix_hist<4>, dim3(nblk), dim3(kRadixThreads), 0, s, kin, n, shift, nbits, hist, nblk,
-                               pass == 0 ? kxf : nullptr);
+                               pass == 0 ? kxf : nullptr, remap);
         else
             hipLaunchKernelGGL(k_radix_hist<16>, dim3(nblk), dim3(kRadixThreads), 0, s, kin, n, shift, nbits, hist,
-                               nblk, pass == 0 ? kxf : nullptr);
+                               nblk, pass == 0 ? kxf : nullptr, remap);
         if ((e = post(debug, s)) != hipSuccess) return e;
         if ((e = scan_exclusive(hist, hist, (1 << nbits) * nblk, scan_regions + pass * region_words, nullptr, fault,
                                 s, debug)) != hipSuccess)
@@ -529,10 +547,10 @@ static hipError_t radix_sort(const uint32_t* k0, const uint32_t* v0, int n, int 
         const ScatterTail tail = pass == passes - 1 ? last : ScatterTail{nullptr, nullptr, nullptr};
         if (small)
             hipLaunchKernelGGL(k_radix_scatter<4>, dim3(nblk), dim3(kRadixThreads), 0, s, kin, vin, n, shift, nbits,
-                               hist, nblk, kout, vout, pass == 0 ? kxf : nullptr, tail);
+                               hist, nblk, kout, vout, pass == 0 ? kxf : nullptr, tail, remap);
         else
             hipLaunchKernelGGL(k_radix_scatter<16>, dim3(nblk), dim3(kRadixThreads), 0, s, kin, vin, n, shift, nbits,
-                               hist, nblk, kout, vout, pass == 0 ? kxf : nullptr, tail);
+                               hist, nblk, kout, vout, pass == 0 ? kxf : nullptr, tail, remap);
         if ((e = post(debug, s)) != hipSuccess) return e;
         kin = kout;
         vin = vout;
