@@ -6,8 +6,12 @@ BASELINE.json metric: "train-step ms & Gaussian-pixel blends/sec (fwd+bwd) @1M G
 1/2/4/8 GPU".  One step mirrors train.py:76-138 in LangSplat's language-feature mode
 (include_feature=True, the default of arguments/__init__.py:84): render() of one view (activations
 + the rasterizer forward, gaussian_renderer/__init__.py:19-115), masked L1 on the language image
-(train.py:96-99), loss.backward() (the full rasterizer backward into means/cov/opacity/SH/language),
-[N>1: one RCCL all-reduce of the trainable gradient bucket], Adam step, zero_grad.
+(train.py:96-99), loss.backward(), [N>1: one RCCL all-reduce of the trainable gradient bucket],
+Adam step, zero_grad.  The timed backward computes the gradients autograd asks for: in the
+language step every geometry parameter is frozen (scene/gaussian_model.py:203-217), so the
+rasterizer backward replays every blend but produces only dL/dmeans2D and dL/dlanguage_feature.
+The same step with every geometry gradient computed as well (what the reference extension does)
+is timed separately and reported beside it as `ms_per_step_all_gradients`, never as `value`.
 
 N = 1 runs BASELINE configs[2] (C3: 1M Gaussians, one 1920x1080 camera); N > 1 runs configs[3]
 (C4: the same scene, camera `rank % 8` of 8 on a circle, one per GPU: weak scaling).  Data is

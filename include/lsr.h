@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define LSR_ABI_VERSION 3
+#define LSR_ABI_VERSION 4
 
 enum lsr_status {
     LSR_OK = 0,
@@ -170,7 +170,7 @@ typedef struct lsr_state_layout {
     size_t sorted_ids;     /* uint32[P]  Gaussians by (depth, id); culled ones tie with the farthest */
     size_t super_offset;   /* uint32[P]  first super-tile entry of the Gaussian of depth rank r */
     /* image buffer */
-    size_t counters;       /* uint32[16] {reserved, num_rendered, error, scan fault, super entries, ...} */
+    size_t counters;       /* uint32[16] {reserved, num_rendered, error, reserved, super entries, ...} */
     size_t ranges;         /* uint32[2T] [start, end) of each tile in point_list */
     size_t final_T;        /* float[H*W] */
     size_t n_contrib;      /* uint32[H*W] */
@@ -234,6 +234,18 @@ int32_t lsr_debug_render_stats(uint64_t* out, int32_t n);
  * loading, compacting and walking its batches and the batch count (synchronous). */
 int32_t lsr_debug_render_timeline(int32_t kernel, uint32_t* out, int32_t n);
 
+/* Look-back stalls, not part of the reference interface.  The single-pass scans of the forward
+ * (depth order, binning), of lsr_dist_cuda2 and the block-sum hand-off of lsr_masked_l1_forward wait
+ * for values published by other workgroups.  A wait is bounded: after `limit` polls (default
+ * 1 << 24) the waiting workgroup computes the value itself from the inputs -- the results are the
+ * same, only slower -- and flags the event.  lsr_debug_scan_stalls returns 1 if a launch made by
+ * the calling thread on the current device took that path since the last call (read it after the
+ * work finished, e.g. after a stream synchronise), and clears the flag; negative on error.
+ * lsr_debug_set_spin_limit sets the poll bound for launches made after it and returns the old one;
+ * 0 makes every wait take the fallback at once (fault injection for tests). */
+int32_t lsr_debug_scan_stalls(void);
+uint32_t lsr_debug_set_spin_limit(uint32_t limit);
+
 /* ---- the language-feature loss around the rasterizer ----------------
  *
  * lsr_masked_l1_forward replaces, in LangSplat's include_feature step (train.py:97-98),
@@ -252,7 +264,9 @@ int32_t lsr_debug_render_timeline(int32_t kernel, uint32_t* out, int32_t n);
  * the GPU: seg = seg_map[level] (L x H x W int64), mask = (seg != -1), feature = feature_map[seg]
  * (N x D fp32; index -1 reads the last row, as torch indexing does) written as D x H x W, and
  * mask as H x W bytes -- so a training loop can decode each view's map once and keep it in HBM
- * instead of np.load + CPU gather + H2D every step. */
+ * instead of np.load + CPU gather + H2D every step.  A segment id outside [-N, N) (the reference's
+ * feature_map[seg] raises IndexError) returns LSR_ERR_INVALID; the call waits for its kernel to
+ * find that out (once per view). */
 /* ---- optimiser step --------------------------------------------------
  * One Adam step of torch.optim.Adam (amsgrad=False, weight_decay=0), the optimiser of
  * scene/gaussian_model.py:229 stepped at train.py:134-137, over one fp32 parameter tensor of n

@@ -21,7 +21,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "liblsr.so")
 
 LSR_BUF_GEOM, LSR_BUF_BINNING, LSR_BUF_IMAGE, LSR_BUF_BACKWARD = 0, 1, 2, 3
-ABI_VERSION = 3
+ABI_VERSION = 4
 # lsr_raw_flags (include/lsr.h): inputs are GaussianModel's raw parameters
 RAW_OPACITY, RAW_SCALES, RAW_ROTATIONS, RAW_LANGUAGE = 1, 2, 4, 8
 _vp = ctypes.c_void_p
@@ -101,6 +101,8 @@ SIGNATURES = {
     "lsr_decode_language_feature": (ctypes.c_int32, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _vp,
                                                      ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _vp, _vp, _vp,
                                                      _vp]),
+    "lsr_debug_scan_stalls": (ctypes.c_int32, []),
+    "lsr_debug_set_spin_limit": (ctypes.c_uint32, [ctypes.c_uint32]),
     "lsr_debug_render_stats": (ctypes.c_int32, [ctypes.POINTER(ctypes.c_uint64), ctypes.c_int32]),
     "lsr_debug_render_timeline": (ctypes.c_int32, [ctypes.c_int32, ctypes.POINTER(ctypes.c_uint32), ctypes.c_int32]),
     "lsr_profile_enable": (ctypes.c_int32, [ctypes.c_int32]),

@@ -89,46 +89,71 @@ struct Scope {
 };
 }  // namespace
 
-// ------------------------------------------------------------------ counter hand-off to the host
-// The forward's one host wait: a one-thread kernel publishes the counters into pinned host memory
-// (system-scope stores, then a sequence number) and the host spins on the sequence number -- no
-// pageable device-to-host copy (which is synchronous) and no stream-synchronise wake-up latency.
+// ------------------------------------------------------------------ pinned host block
+// Per (thread, device) pinned host memory the kernels write with system-scope stores:
+//   slot[8]: the forward's one host wait -- a one-workgroup kernel publishes the counters, each with
+//            the call's sequence number in one 64-bit store, and the host spins until all 8 slots
+//            carry it (no pageable device-to-host copy, which is synchronous, and no
+//            stream-synchronise wake-up latency);
+//   stall:   set by a look-back that stopped waiting and took its fallback (lsr_debug_scan_stalls).
+// Per thread, because a sequence number belongs to one caller; per device, because the block is
+// written by that device's kernels.  Freed when the thread exits.
 namespace {
-struct HostCounters {
+struct HostBlock {
     uint64_t slot[8];  // {value, seq}: low word the counter, high word the sequence number
-    uint32_t seq;      // unused by the publish kernel (kept for the launch signature)
+    uint32_t stall;
+    uint32_t seq;      // the last sequence number used (host side)
+    uint32_t bad_segment;  // lsr_decode_language_feature: a segment id outside [-N, N)
 };
 
-static bool counters_arrived(const HostCounters* hc, uint32_t seq)
+struct HostBlocks {
+    std::vector<std::pair<int, HostBlock*>> blocks;
+    ~HostBlocks()
+    {
+        for (auto& b : blocks) (void)hipHostFree(b.second);
+    }
+    // the calling thread's block for the current device (allocated on first use); null on failure
+    HostBlock* get(hipError_t* err)
+    {
+        int dev = 0;
+        if ((*err = hipGetDevice(&dev)) != hipSuccess) return nullptr;
+        for (auto& b : blocks)
+            if (b.first == dev) return b.second;
+        void* h = nullptr;
+        if ((*err = hipHostMalloc(&h, sizeof(HostBlock), hipHostMallocCoherent)) != hipSuccess) return nullptr;
+        memset(h, 0, sizeof(HostBlock));
+        blocks.emplace_back(dev, static_cast<HostBlock*>(h));
+        return static_cast<HostBlock*>(h);
+    }
+};
+thread_local HostBlocks t_host;
+
+bool counters_arrived(const HostBlock* hb, uint32_t seq)
 {
     for (int i = 0; i < 8; i++)
-        if ((uint32_t)(__atomic_load_n(&hc->slot[i], __ATOMIC_ACQUIRE) >> 32) != seq) return false;
+        if ((uint32_t)(__atomic_load_n(&hb->slot[i], __ATOMIC_ACQUIRE) >> 32) != seq) return false;
     return true;
 }
-thread_local HostCounters* t_hc = nullptr;
-thread_local uint32_t t_seq = 0;
-}  // namespace
 
-static int32_t fail(int32_t code, const char* what, hipError_t e = hipSuccess);
-
-// Waits until the counters published with `seq` arrived; false (and a HIP error) on failure.
-static hipError_t wait_counters(HostCounters* hc, uint32_t seq, hipStream_t stream)
+// Waits until the counters published with `seq` arrived; a HIP error on failure.
+hipError_t wait_counters(const HostBlock* hb, uint32_t seq, hipStream_t stream)
 {
     for (uint64_t spin = 0;; spin++) {
-        if (counters_arrived(hc, seq)) return hipSuccess;
+        if (counters_arrived(hb, seq)) return hipSuccess;
         if ((spin & 1023) == 1023) {
             const hipError_t q = hipStreamQuery(stream);
             if (q != hipSuccess && q != hipErrorNotReady) return q;
-            if (q == hipSuccess) {  // stream idle: the store must be visible now
-                if (counters_arrived(hc, seq)) return hipSuccess;
+            if (q == hipSuccess) {  // stream idle: the stores must be visible now
+                if (counters_arrived(hb, seq)) return hipSuccess;
                 return hipErrorUnknown;
             }
         }
         __builtin_ia32_pause();
     }
 }
+}  // namespace
 
-static int32_t fail(int32_t code, const char* what, hipError_t e)
+static int32_t fail(int32_t code, const char* what, hipError_t e = hipSuccess)
 {
     char buf[512];
     if (e != hipSuccess)
@@ -224,6 +249,9 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
 
     Layout L = make_layout(P, W, H, 0, 0);
     if (L.supers > 65536) return fail(LSR_ERR_INVALID, "lsr_forward: image larger than 65536 super-tiles");
+    hipError_t herr = hipSuccess;
+    HostBlock* hb = t_host.get(&herr);
+    if (!hb) return fail(LSR_ERR_HIP, "lsr_forward: pinned host block", herr);
     char* geom = static_cast<char*>(alloc(user, LSR_BUF_GEOM, L.geom_bytes));
     char* image = static_cast<char*>(alloc(user, LSR_BUF_IMAGE, L.image_bytes));
     if (!geom || !image) return fail(LSR_ERR_ALLOC, "lsr_forward: geometry/image buffer allocation failed");
@@ -273,20 +301,12 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
 
     // The one host wait, right after preprocess: num_rendered R and the super-tile entries E size
     // the binning buffer, and the visible depth-key range fixes the number of sort passes.
-    if (!t_hc) {
-        void* h = nullptr;
-        LSR_TRY(hipHostMalloc(&h, sizeof(HostCounters), hipHostMallocCoherent), "pinned counters");
-        t_hc = static_cast<HostCounters*>(h);
-        memset(t_hc, 0, sizeof(HostCounters));
-    }
-    const uint32_t seq = ++t_seq == 0 ? ++t_seq : t_seq;
-    LSR_TRY(launch_publish_counters((P + kPreThreads - 1) / kPreThreads, pp.partial, counters,
-                                    reinterpret_cast<uint32_t*>(t_hc->slot), &t_hc->seq,
-                                    seq, stream),
+    const uint32_t seq = ++hb->seq == 0 ? ++hb->seq : hb->seq;
+    LSR_TRY(launch_publish_counters((P + kPreThreads - 1) / kPreThreads, pp.partial, counters, hb->slot, seq, stream),
             "publish counters");
-    LSR_TRY(wait_counters(t_hc, seq, stream), "wait counters");
+    LSR_TRY(wait_counters(hb, seq, stream), "wait counters");
     uint32_t host_cnt[8];
-    for (int i = 0; i < 8; i++) host_cnt[i] = (uint32_t)t_hc->slot[i];
+    for (int i = 0; i < 8; i++) host_cnt[i] = (uint32_t)hb->slot[i];
     if (host_cnt[kCntError] && s->prefiltered)
         return fail(LSR_ERR_PREFILTERED, "lsr_forward: prefiltered=True but a Gaussian is outside the frustum");
     const int64_t R = host_cnt[kCntRendered];
@@ -297,19 +317,13 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
         int bits = 0;
         while (bits < 32 && (span >> bits) != 0) bits++;
         const int passes = bits <= 8 ? 1 : (bits + 7) / 8;
-        LSR_TRY(launch_depth_order(P, passes, L, geom, counters, stream, debug), "depth order");
+        LSR_TRY(launch_depth_order(P, passes, L, geom, counters, &hb->stall, stream, debug), "depth order");
     }
 
     L = make_layout(P, W, H, R, (int64_t)host_cnt[kCntSuper]);
     char* binning = static_cast<char*>(alloc(user, LSR_BUF_BINNING, L.binning_bytes));
     if (!binning) return fail(LSR_ERR_ALLOC, "lsr_forward: binning buffer allocation failed");
-    LSR_TRY(launch_binning(P, R, L, geom, image, binning, stream, debug), "binning");
-    if (debug) {  // the look-back scans' safety bound (kMaxSpins) flags a stall here
-        uint32_t fault = 0;
-        LSR_TRY(hipMemcpyAsync(&fault, counters + kCntScanFault, 4, hipMemcpyDeviceToHost, stream), "read fault");
-        LSR_TRY(hipStreamSynchronize(stream), "sync");
-        if (fault) return fail(LSR_ERR_HIP, "lsr_forward: scan look-back stalled");
-    }
+    LSR_TRY(launch_binning(P, R, L, geom, image, binning, &hb->stall, stream, debug), "binning");
     RenderParams rp{};
     rp.W = W;
     rp.H = H;
@@ -511,6 +525,16 @@ int32_t lsr_debug_render_timeline(int32_t kernel, uint32_t* out, int32_t n)
     return LSR_OK;
 }
 
+int32_t lsr_debug_scan_stalls(void)
+{
+    hipError_t herr = hipSuccess;
+    HostBlock* hb = t_host.get(&herr);
+    if (!hb) return -fail(LSR_ERR_HIP, "lsr_debug_scan_stalls: pinned host block", herr);
+    return (int32_t)__atomic_exchange_n(&hb->stall, 0u, __ATOMIC_ACQ_REL);
+}
+
+uint32_t lsr_debug_set_spin_limit(uint32_t limit) { return set_stall_spin_limit(limit); }
+
 int32_t lsr_mark_visible(int32_t P, const float* means3D, const float* viewmatrix, const float* projmatrix,
                          uint8_t* visible, void* stream_ptr)
 {
@@ -536,6 +560,9 @@ int32_t lsr_masked_l1_forward(int32_t C, int64_t HW, const float* pred, const fl
         return fail(LSR_ERR_INVALID, "lsr_masked_l1_forward: invalid argument");
     hipStream_t stream = reinterpret_cast<hipStream_t>(stream_ptr);
     const bool debug = false;
+    hipError_t herr = hipSuccess;
+    HostBlock* hb = t_host.get(&herr);
+    if (!hb) return fail(LSR_ERR_HIP, "lsr_masked_l1_forward: pinned host block", herr);
     // per-scratch launch epoch (never 0, the value of freshly zeroed scratch)
     uint32_t epoch = 0;
     {
@@ -546,7 +573,7 @@ int32_t lsr_masked_l1_forward(int32_t C, int64_t HW, const float* pred, const fl
         e = e + 1 == 0 ? 1 : e + 1;
         epoch = e;
     }
-    LSR_TRY(launch_masked_l1_forward(C, HW, pred, gt, mask, mask_is_float, loss, scratch, epoch, stream),
+    LSR_TRY(launch_masked_l1_forward(C, HW, pred, gt, mask, mask_is_float, loss, scratch, epoch, &hb->stall, stream),
             "masked l1");
     return LSR_OK;
 }
@@ -594,7 +621,10 @@ int32_t lsr_dist_cuda2(int64_t N, const float* points, float* out_mean_dist, lsr
     const bool debug = false;
     void* scratch = alloc(user, LSR_BUF_BACKWARD, knn_scratch_bytes(N));
     if (!scratch) return fail(LSR_ERR_ALLOC, "lsr_dist_cuda2: scratch allocation failed");
-    LSR_TRY(launch_knn_mean_dist3(N, points, out_mean_dist, scratch, stream), "dist_cuda2");
+    hipError_t herr = hipSuccess;
+    HostBlock* hb = t_host.get(&herr);
+    if (!hb) return fail(LSR_ERR_HIP, "lsr_dist_cuda2: pinned host block", herr);
+    LSR_TRY(launch_knn_mean_dist3(N, points, out_mean_dist, scratch, &hb->stall, stream), "dist_cuda2");
     return LSR_OK;
 }
 
@@ -607,9 +637,17 @@ int32_t lsr_decode_language_feature(int32_t L, int32_t H, int32_t W, const int64
         return fail(LSR_ERR_INVALID, "lsr_decode_language_feature: invalid argument");
     hipStream_t stream = reinterpret_cast<hipStream_t>(stream_ptr);
     const bool debug = false;
+    hipError_t herr = hipSuccess;
+    HostBlock* hb = t_host.get(&herr);
+    if (!hb) return fail(LSR_ERR_HIP, "lsr_decode_language_feature: pinned host block", herr);
+    __atomic_store_n(&hb->bad_segment, 0u, __ATOMIC_RELEASE);
     LSR_TRY(launch_decode_language_feature(H, W, seg_map + (int64_t)level * H * W, N, D, feature_map, out_feature,
-                                           out_mask, stream),
+                                           out_mask, &hb->bad_segment, stream),
             "decode language feature");
+    // once per view: wait, so that an id the reference's feature_map[seg] would reject is reported
+    LSR_TRY(hipStreamSynchronize(stream), "decode language feature (sync)");
+    if (__atomic_exchange_n(&hb->bad_segment, 0u, __ATOMIC_ACQ_REL))
+        return fail(LSR_ERR_INVALID, "lsr_decode_language_feature: segment id outside [-N, N) of the feature map");
     return LSR_OK;
 }
 

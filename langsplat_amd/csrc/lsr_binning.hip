@@ -22,6 +22,8 @@
 // sort.  Scans are single-pass chained scans with decoupled look-back (one launch each).
 #include <stdlib.h>
 
+#include <atomic>
+
 #include "lsr_internal.h"
 
 namespace lsr {
@@ -89,7 +91,15 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* w
 // at launch; launch_preprocess / k_emit clear them (no memset launches).
 constexpr uint64_t kFlagAgg = 1ull << 62;
 constexpr uint64_t kFlagInc = 2ull << 62;
-constexpr uint32_t kMaxSpins = 1u << 24;  // a safety bound only; a stalled look-back flags kCntScanFault
+// Stall bound (stall_spin_limit(), lsr_internal.h): a look-back that has polled that many times
+// without its predecessors becoming ready stops waiting and computes its exclusive prefix itself,
+// straight from the input (scans are out-of-place, so in[] is never overwritten): the result is the
+// same, only slower.  It notes the event in the calling thread's pinned stall word
+// (lsr_debug_scan_stalls).  Limit 0 takes that path in every chunk (tests).  With chunk ids from a
+// ticket the predecessors are always resident, so only a GPU that stops scheduling them gets here.
+static std::atomic<uint32_t> g_spin_limit{1u << 24};
+uint32_t stall_spin_limit() { return g_spin_limit.load(std::memory_order_relaxed); }
+uint32_t set_stall_spin_limit(uint32_t v) { return g_spin_limit.exchange(v); }
 
 __host__ __device__ inline int scan_blocks(int n) { return (n + kScanChunk - 1) / kScanChunk; }
 
@@ -100,9 +110,11 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v)
     return v;
 }
 
+// in != out: the stall fallback re-reads predecessors' inputs.
 __global__ __launch_bounds__(kScanThreads) void k_scan(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
                                                        int n, uint64_t* __restrict__ status,
-                                                       uint32_t* __restrict__ total, uint32_t* __restrict__ fault)
+                                                       uint32_t* __restrict__ total, uint32_t* stall,
+                                                       uint32_t spin_limit)
 {
     __shared__ uint32_t wsum[kScanThreads / 64];
     __shared__ uint32_t s_chunk, s_prefix;
@@ -149,9 +161,12 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const uint32_t* __restric
                 const uint64_t inc = __ballot(flag == 2u);
                 const int k = inc ? __ffsll((unsigned long long)inc) - 1 : 63;  // nearest inclusive
                 const uint64_t upto = k == 63 ? ~0ull : ((2ull << k) - 1ull);
-                if (__ballot(flag == 0u) & upto) {                             // a predecessor is not ready
-                    if (++spins > kMaxSpins) {
-                        if (lane == 0) atomicOr(fault, 1u);
+                if (spin_limit == 0u || (__ballot(flag == 0u) & upto)) {      // a predecessor is not ready
+                    if (++spins > spin_limit) {  // stop waiting: the exclusive prefix from the input
+                        uint32_t part = 0;
+                        for (int i = lane; i < c * kScanChunk; i += 64) part += in[i];
+                        prefix = wave_sum(part);
+                        if (lane == 0) note_stall(stall);
                         break;
                     }
                     continue;
@@ -191,14 +206,15 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const uint32_t* __restric
     }
 }
 
-// out[i] = sum(in[0..i)); if total != null it receives the grand total.  `in` may equal `out`.
+// out[i] = sum(in[0..i)); if total != null it receives the grand total.  `in` must not alias `out`.
 // region: scan_region_words(n) zeroed words (status per chunk + ticket).
 static hipError_t scan_exclusive(const uint32_t* in, uint32_t* out, int n, uint32_t* region, uint32_t* total,
-                                 uint32_t* fault, hipStream_t s, bool debug)
+                                 uint32_t* stall, hipStream_t s, bool debug)
 {
     if (n <= 0) return hipSuccess;
+    if (in == out) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_scan, dim3(scan_blocks(n)), dim3(kScanThreads), 0, s, in, out, n,
-                       reinterpret_cast<uint64_t*>(region), total, fault);
+                       reinterpret_cast<uint64_t*>(region), total, stall, stall_spin_limit());
     return post(debug, s);
 }
 
@@ -211,8 +227,7 @@ constexpr int kPublishThreads = 1024;
 
 __global__ __launch_bounds__(kPublishThreads) void k_publish_counters(int nb, const uint4* __restrict__ partial,
                                                                       uint32_t* __restrict__ counters,
-                                                                      uint32_t* host_vals, uint32_t* host_seq,
-                                                                      uint32_t seq)
+                                                                      uint64_t* host_slots, uint32_t seq)
 {
     constexpr int kWaves = kPublishThreads / 64;
     __shared__ uint32_t red[4][kWaves];
@@ -266,24 +281,23 @@ __global__ __launch_bounds__(kPublishThreads) void k_publish_counters(int nb, co
     counters[kCntError] = red[3][0] >> 31;
     // each value travels with the sequence number in one 64-bit store (single-copy atomic): the
     // host waits for all 8 slots to carry `seq`, so no release fence (L2 write-back) is needed
-    uint64_t* slot = reinterpret_cast<uint64_t*>(host_vals);
     for (int i = 0; i < 8; i++)
-        __hip_atomic_store(&slot[i], (uint64_t)counters[i] | ((uint64_t)seq << 32), __ATOMIC_RELAXED,
+        __hip_atomic_store(&host_slots[i], (uint64_t)counters[i] | ((uint64_t)seq << 32), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-hipError_t launch_publish_counters(int nb, const uint4* partial, uint32_t* counters, uint32_t* host_vals,
-                                   uint32_t* host_seq, uint32_t seq, hipStream_t s)
+hipError_t launch_publish_counters(int nb, const uint4* partial, uint32_t* counters, uint64_t* host_slots,
+                                   uint32_t seq, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_publish_counters, dim3(1), dim3(kPublishThreads), 0, s, nb, partial, counters, host_vals,
-                       host_seq, seq);
+    hipLaunchKernelGGL(k_publish_counters, dim3(1), dim3(kPublishThreads), 0, s, nb, partial, counters, host_slots,
+                       seq);
     return hipGetLastError();
 }
 
-hipError_t scan_exclusive_u32(const uint32_t* in, uint32_t* out, int n, uint32_t* region, uint32_t* fault,
+hipError_t scan_exclusive_u32(const uint32_t* in, uint32_t* out, int n, uint32_t* region, uint32_t* stall,
                               hipStream_t s)
 {
-    return scan_exclusive(in, out, n, region, nullptr, fault, s, false);
+    return scan_exclusive(in, out, n, region, nullptr, stall, s, false);
 }
 
 // ---------------------------------------------------------------- stable LSD radix sort
@@ -513,8 +527,9 @@ static bool radix_small(int64_t n)
 }
 
 static hipError_t radix_sort(const uint32_t* k0, const uint32_t* v0, int n, int total_bits, uint32_t* kA,
-                             uint32_t* vA, uint32_t* kB, uint32_t* vB, uint32_t* hist, uint32_t* scan_regions,
-                             size_t region_words, uint32_t* fault, hipStream_t s, bool debug, int* passes_out,
+                             uint32_t* vA, uint32_t* kB, uint32_t* vB, uint32_t* hist, uint32_t* hist_scan,
+                             uint32_t* scan_regions, size_t region_words, uint32_t* stall, hipStream_t s, bool debug,
+                             int* passes_out,
                              const uint32_t* kxf = nullptr, ScatterTail last = ScatterTail{nullptr, nullptr, nullptr})
 {
     const bool small = radix_small(n);
@@ -541,16 +556,16 @@ static hipError_t radix_sort(const uint32_t* k0, const uint32_t* v0, int n, int 
             hipLaunchKernelGGL(k_radix_hist<16>, dim3(nblk), dim3(kRadixThreads), 0, s, kin, n, shift, nbits, hist,
                                nblk, pass == 0 ? kxf : nullptr, remap);
         if ((e = post(debug, s)) != hipSuccess) return e;
-        if ((e = scan_exclusive(hist, hist, (1 << nbits) * nblk, scan_regions + pass * region_words, nullptr, fault,
-                                s, debug)) != hipSuccess)
+        if ((e = scan_exclusive(hist, hist_scan, (1 << nbits) * nblk, scan_regions + pass * region_words, nullptr,
+                                stall, s, debug)) != hipSuccess)
             return e;
         const ScatterTail tail = pass == passes - 1 ? last : ScatterTail{nullptr, nullptr, nullptr};
         if (small)
             hipLaunchKernelGGL(k_radix_scatter<4>, dim3(nblk), dim3(kRadixThreads), 0, s, kin, vin, n, shift, nbits,
-                               hist, nblk, kout, vout, pass == 0 ? kxf : nullptr, tail, remap);
+                               hist_scan, nblk, kout, vout, pass == 0 ? kxf : nullptr, tail, remap);
         else
             hipLaunchKernelGGL(k_radix_scatter<16>, dim3(nblk), dim3(kRadixThreads), 0, s, kin, vin, n, shift, nbits,
-                               hist, nblk, kout, vout, pass == 0 ? kxf : nullptr, tail, remap);
+                               hist_scan, nblk, kout, vout, pass == 0 ? kxf : nullptr, tail, remap);
         if ((e = post(debug, s)) != hipSuccess) return e;
         kin = kout;
         vin = vout;
@@ -604,13 +619,13 @@ __device__ __forceinline__ uint64_t transpose64(uint64_t x)
 
 // ---------------------------------------------------------------- depth order + super-tile counts
 
-hipError_t launch_depth_order(int P, int passes, const Layout& L, char* geom, uint32_t* counters, hipStream_t s,
-                              bool debug)
+hipError_t launch_depth_order(int P, int passes, const Layout& L, char* geom, uint32_t* counters, uint32_t* stall,
+                              hipStream_t s, bool debug)
 {
     if (P == 0) return hipSuccess;
     uint32_t* hist = reinterpret_cast<uint32_t*>(geom + L.radix_hist);
+    uint32_t* hist_scan = reinterpret_cast<uint32_t*>(geom + L.radix_hist_scan);
     uint32_t* regions = reinterpret_cast<uint32_t*>(geom + L.scan_regions);
-    uint32_t* fault = counters + kCntScanFault;
     uint32_t* ka = reinterpret_cast<uint32_t*>(geom + L.keys_a);
     uint32_t* kb = reinterpret_cast<uint32_t*>(geom + L.keys_b);
     uint32_t* va = reinterpret_cast<uint32_t*>(geom + L.sorted_ids);
@@ -620,16 +635,17 @@ hipError_t launch_depth_order(int P, int passes, const Layout& L, char* geom, ui
     int done = 0;
     const uint32_t* keys = reinterpret_cast<const uint32_t*>(geom + L.depth_key);
     uint32_t* off = reinterpret_cast<uint32_t*>(geom + L.super_offset);
+    // the last pass stores no keys, so its key output buffer (keys_a in both role assignments) is
+    // free: the per-rank super-tile entry counts go there and are scanned into super_offset
     const ScatterTail tail{reinterpret_cast<const uint2*>(geom + L.rect), reinterpret_cast<uint2*>(geom + L.rect_ranked),
-                           off};
+                           ka};
     hipError_t e = (passes & 1)
-        ? radix_sort(keys, nullptr, P, 8 * passes, kb, vb, ka, va, hist, regions, L.scan_region_geom, fault, s, debug,
-                     &done, counters + kCntKeyMin, tail)
-        : radix_sort(keys, nullptr, P, 8 * passes, ka, va, kb, vb, hist, regions, L.scan_region_geom, fault, s, debug,
-                     &done, counters + kCntKeyMin, tail);
+        ? radix_sort(keys, nullptr, P, 8 * passes, kb, vb, ka, va, hist, hist_scan, regions, L.scan_region_geom, stall,
+                     s, debug, &done, counters + kCntKeyMin, tail)
+        : radix_sort(keys, nullptr, P, 8 * passes, ka, va, kb, vb, hist, hist_scan, regions, L.scan_region_geom, stall,
+                     s, debug, &done, counters + kCntKeyMin, tail);
     if (e != hipSuccess) return e;
-    return scan_exclusive(off, off, P, regions + passes * L.scan_region_geom, counters + kCntSuper, fault, s,
-                          debug);
+    return scan_exclusive(ka, off, P, regions + passes * L.scan_region_geom, counters + kCntSuper, stall, s, debug);
 }
 
 // ---------------------------------------------------------------- binning
@@ -1002,14 +1018,13 @@ __global__ __launch_bounds__(256) void k_bin_emit(int S, int sgx, int gx, int gy
     }
 }
 
-hipError_t launch_binning(int P, int64_t R, const Layout& L, char* geom, char* image, char* binning, hipStream_t s,
-                          bool debug)
+hipError_t launch_binning(int P, int64_t R, const Layout& L, char* geom, char* image, char* binning, uint32_t* stall,
+                          hipStream_t s, bool debug)
 {
     uint2* ranges = reinterpret_cast<uint2*>(image + L.ranges);
     if (R == 0) return hipMemsetAsync(ranges, 0, 8 * (size_t)L.tiles, s);
     const int64_t E = L.super_entries;
     uint32_t* regions = reinterpret_cast<uint32_t*>(binning + L.bin_scan_regions);
-    uint32_t* fault = reinterpret_cast<uint32_t*>(image + L.counters) + kCntScanFault;
     uint32_t* kA = reinterpret_cast<uint32_t*>(binning + L.super_keys);
     uint32_t* vA = reinterpret_cast<uint32_t*>(binning + L.super_vals);
     uint32_t* kB = reinterpret_cast<uint32_t*>(binning + L.alt_keys);
@@ -1030,8 +1045,9 @@ hipError_t launch_binning(int P, int64_t R, const Layout& L, char* geom, char* i
                        (int)((L.super_passes + 1) * L.scan_region_bin));
     if ((e = post(debug, s)) != hipSuccess) return e;
     int passes = 0;
+    uint32_t* bin_hist_scan = reinterpret_cast<uint32_t*>(binning + L.bin_radix_hist_scan);
     e = radix_sort(kA, vA, (int)E, L.super_bits, kA, vA, kB, vB, reinterpret_cast<uint32_t*>(binning + L.bin_radix_hist),
-                   regions, L.scan_region_bin, fault, s, debug, &passes);
+                   bin_hist_scan, regions, L.scan_region_bin, stall, s, debug, &passes);
     if (e != hipSuccess) return e;
     const uint32_t* skeys = (passes & 1) ? kB : kA;
     const uint32_t* svals = (passes & 1) ? vB : vA;
@@ -1042,7 +1058,7 @@ hipError_t launch_binning(int P, int64_t R, const Layout& L, char* geom, char* i
         const int tile = kRadixThreads * (radix_small(E) ? 4 : 16);
         const int nblk = (int)((E + tile - 1) / tile);
         hipLaunchKernelGGL(k_bin_count_fused, dim3(grid), dim3(256), 0, s, L.supers, L.sgx, L.sgy, L.gx, L.gy, nblk,
-                           1 << L.super_bits, E, reinterpret_cast<const uint32_t*>(binning + L.bin_radix_hist), sranges,
+                           1 << L.super_bits, E, (const uint32_t*)bin_hist_scan, sranges,
                            seg_base, colpre, rowpre, skeys, table);
         if ((e = post(debug, s)) != hipSuccess) return e;
     } else {
@@ -1056,12 +1072,13 @@ hipError_t launch_binning(int P, int64_t R, const Layout& L, char* geom, char* i
                            (const uint32_t*)rowpre, skeys, table);
         if ((e = post(debug, s)) != hipSuccess) return e;
     }
-    if ((e = scan_exclusive(table, table, (int)L.seg_table_words, regions + L.super_passes * L.scan_region_bin,
-                            nullptr, fault, s, debug)) != hipSuccess)
+    uint32_t* table_scan = reinterpret_cast<uint32_t*>(binning + L.seg_table_scan);
+    if ((e = scan_exclusive(table, table_scan, (int)L.seg_table_words, regions + L.super_passes * L.scan_region_bin,
+                            nullptr, stall, s, debug)) != hipSuccess)
         return e;
     hipLaunchKernelGGL(k_bin_emit, dim3(grid), dim3(256), 0, s, L.supers, L.sgx, L.gx, L.gy, (const uint32_t*)seg_base,
                        (const uint2*)sranges, (const uint32_t*)colpre, (const uint32_t*)rowpre, skeys, svals,
-                       (const uint32_t*)table, pl, ranges,
+                       (const uint32_t*)table_scan, pl, ranges,
                        reinterpret_cast<uint32_t*>(image + L.counters) + kCntFwdClass,
                        reinterpret_cast<uint32_t*>(image + L.tile_lists));
     return post(debug, s);

@@ -14,7 +14,6 @@ namespace lsr {
 enum Counter : int {
     kCntRendered = 1,
     kCntError = 2,
-    kCntScanFault = 3,
     kCntSuper = 4,       // super-tile entries E (binning)
     kCntKeyMin = 5,      // smallest visible depth key (float bits)
     kCntKeyMax = 6,      // largest visible depth key
@@ -46,15 +45,15 @@ constexpr int kDepthScans = 5;         // 4 depth-sort passes + the instance-off
 struct Layout {
     // geometry (per Gaussian)
     size_t depth_key, tiles_touched, rect, record, clamped, sorted_ids, super_offset;
-    size_t keys_a, keys_b, vals_b, radix_hist, scan_regions, rect_ranked, pre_partial;
+    size_t keys_a, keys_b, vals_b, radix_hist, radix_hist_scan, scan_regions, rect_ranked, pre_partial;
     size_t scan_region_geom;  // u32 words per depth-order scan region
     size_t geom_bytes;
     // image (per pixel / tile)
     size_t counters, ranges, final_T, n_contrib, tile_lists;
     size_t image_bytes;
     // binning (point_list per tile instance, the rest per super-tile entry / segment)
-    size_t point_list, super_keys, super_vals, alt_keys, alt_vals, bin_radix_hist, bin_scan_regions;
-    size_t super_ranges, seg_base, col_prefix, row_prefix, seg_table;
+    size_t point_list, super_keys, super_vals, alt_keys, alt_vals, bin_radix_hist, bin_radix_hist_scan;
+    size_t bin_scan_regions, super_ranges, seg_base, col_prefix, row_prefix, seg_table, seg_table_scan;
     size_t scan_region_bin;   // u32 words per binning scan region
     size_t seg_table_words;   // (tile, segment) count table incl. one trailing slot
     int64_t super_entries;    // E
@@ -83,6 +82,7 @@ inline Layout make_layout(int P, int W, int H, int64_t R, int64_t E)
     L.vals_b = take(4 * p);
     const size_t hw_p = radix_hist_words((int64_t)p);
     L.radix_hist = take(4 * hw_p);
+    L.radix_hist_scan = take(4 * hw_p);  // scans are out-of-place (k_scan's stall fallback)
     L.scan_region_geom = scan_region_words((int64_t)(hw_p > p ? hw_p : p));
     L.scan_regions = take(4 * kDepthScans * L.scan_region_geom);
     L.rect_ranked = take(8 * p);
@@ -121,6 +121,7 @@ inline Layout make_layout(int P, int W, int H, int64_t R, int64_t E)
     L.alt_vals = take(4 * e);
     const size_t hw_e = radix_hist_words((int64_t)e);
     L.bin_radix_hist = take(4 * hw_e);
+    L.bin_radix_hist_scan = take(4 * hw_e);
     L.scan_region_bin = scan_region_words((int64_t)(hw_e > L.seg_table_words ? hw_e : L.seg_table_words));
     L.bin_scan_regions = take(4 * (L.super_passes + 1) * L.scan_region_bin);
     L.super_ranges = take(8 * (size_t)L.supers);
@@ -128,6 +129,7 @@ inline Layout make_layout(int P, int W, int H, int64_t R, int64_t E)
     L.col_prefix = take(4 * (size_t)L.supers);
     L.row_prefix = take(4 * ((size_t)L.gy + 1));
     L.seg_table = take(4 * L.seg_table_words);
+    L.seg_table_scan = take(4 * L.seg_table_words);
     L.binning_bytes = o;
     return L;
 }
@@ -192,11 +194,23 @@ hipError_t launch_mark_visible(int P, const float* means, const float* view, con
 // depth sort of all P Gaussians by (depth key, id) on `passes` 8-bit digits of the key minus the
 // smallest visible key (counters[kCntKeyMin/Max], from launch_preprocess) -> sorted_ids; per-Gaussian
 // super-tile entry offsets in that order
-hipError_t launch_depth_order(int P, int passes, const Layout& L, char* geom, uint32_t* counters, hipStream_t s,
-                              bool debug);
+hipError_t launch_depth_order(int P, int passes, const Layout& L, char* geom, uint32_t* counters, uint32_t* stall,
+                              hipStream_t s, bool debug);
 // super-tile lists, per-(tile, segment) counts, scanned bases -> point_list and tile ranges
-hipError_t launch_binning(int P, int64_t R, const Layout& L, char* geom, char* image, char* binning,
+hipError_t launch_binning(int P, int64_t R, const Layout& L, char* geom, char* image, char* binning, uint32_t* stall,
                           hipStream_t s, bool debug);
+
+// Look-back stall handling (k_scan, k_masked_l1_forward).  A single-pass look-back polls at most
+// stall_spin_limit() times for a predecessor's value; past that it computes the value itself from
+// the inputs (same result) and stores 1 into `stall`, a word of the calling thread's pinned host
+// block (lsr_api.hip), which lsr_debug_scan_stalls reads.  set_stall_spin_limit returns the old
+// limit; 0 = never wait (every look-back takes the fallback: tests).
+uint32_t stall_spin_limit();
+uint32_t set_stall_spin_limit(uint32_t v);
+__device__ __forceinline__ void note_stall(uint32_t* stall)
+{
+    if (stall) __hip_atomic_store(stall, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 // work class of a tile with w >= 1 units of work: quarter-octaves, monotone in w, 0..63 (w >= 2^16
 // shares the top class)
@@ -228,19 +242,23 @@ hipError_t launch_adam(int64_t n, float* param, const float* grad, float* exp_av
 // out[i] = sum(in[0..i)); region: scan_region_words(n) zeroed words (single-pass look-back scan)
 hipError_t scan_exclusive_u32(const uint32_t* in, uint32_t* out, int n, uint32_t* region, uint32_t* fault,
                               hipStream_t s);
-// reduces the preprocess block partials into counters and publishes counters[0..7] + seq to the host
-hipError_t launch_publish_counters(int nb, const uint4* partial, uint32_t* counters, uint32_t* host_vals,
-                                   uint32_t* host_seq, uint32_t seq, hipStream_t s);
+// reduces the preprocess block partials into counters and publishes counters[0..7], each with seq,
+// to the host slots (8 x u64 pinned)
+hipError_t launch_publish_counters(int nb, const uint4* partial, uint32_t* counters, uint64_t* host_slots,
+                                   uint32_t seq, hipStream_t s);
 size_t knn_scratch_bytes(int64_t N);
-hipError_t launch_knn_mean_dist3(int64_t N, const float* pts, float* out, void* scratch, hipStream_t s);
+hipError_t launch_knn_mean_dist3(int64_t N, const float* pts, float* out, void* scratch, uint32_t* stall,
+                                 hipStream_t s);
 
 size_t masked_l1_scratch_bytes();
 hipError_t launch_masked_l1_forward(int C, int64_t HW, const float* pred, const float* gt, const void* mask,
-                                    int mask_is_float, float* loss, void* scratch, uint32_t epoch, hipStream_t s);
+                                    int mask_is_float, float* loss, void* scratch, uint32_t epoch, uint32_t* stall,
+                                    hipStream_t s);
 hipError_t launch_masked_l1_backward(int C, int64_t HW, const float* pred, const float* gt, const void* mask,
                                      int mask_is_float, const float* grad_loss, float* grad_pred, hipStream_t s);
 hipError_t launch_decode_language_feature(int H, int W, const int64_t* seg_level, int N, int D,
-                                          const float* feature_map, float* out, uint8_t* mask, hipStream_t s);
+                                          const float* feature_map, float* out, uint8_t* mask, uint32_t* bad,
+                                          hipStream_t s);
 
 hipError_t launch_render_forward(const RenderParams& p, int tiles, hipStream_t s);
 hipError_t launch_render_backward(const RenderParams& p, int tiles, hipStream_t s);

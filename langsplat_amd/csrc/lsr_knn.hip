@@ -218,11 +218,11 @@ size_t knn_scratch_bytes(int64_t N)
     const size_t nb = (n + kKnnThreads - 1) / kKnnThreads;
     const size_t pb = nb < 1024 ? nb : 1024;
     return align_up(sizeof(KnnGrid)) + align_up(4 * 6 * pb) + align_up(4 * n) + align_up(4 * (cells + 1)) +
-           align_up(4 * (cells + 1)) + align_up(16 * n) + align_up(4 * scan_region_words((int64_t)cells + 1)) +
-           align_up(4);
+           align_up(4 * (cells + 1)) + align_up(16 * n) + align_up(4 * scan_region_words((int64_t)cells + 1));
 }
 
-hipError_t launch_knn_mean_dist3(int64_t N, const float* pts, float* out, void* scratch, hipStream_t s)
+hipError_t launch_knn_mean_dist3(int64_t N, const float* pts, float* out, void* scratch, uint32_t* stall,
+                                 hipStream_t s)
 {
     if (N <= 0) return hipSuccess;
     const size_t n = (size_t)N;
@@ -239,17 +239,13 @@ hipError_t launch_knn_mean_dist3(int64_t N, const float* pts, float* out, void* 
     uint32_t* start = reinterpret_cast<uint32_t*>(take(4 * ((size_t)cells + 1)));
     float4* sorted = reinterpret_cast<float4*>(take(16 * n));
     uint32_t* region = reinterpret_cast<uint32_t*>(take(4 * scan_region_words(cells + 1)));
-    uint32_t* fault = reinterpret_cast<uint32_t*>(take(4));
     hipError_t e;
     if ((e = hipMemsetAsync(count, 0, 4 * ((size_t)cells + 1), s)) != hipSuccess) return e;
-    // the scan status region and the fault word are contiguous
-    if ((e = hipMemsetAsync(region, 0, (size_t)(reinterpret_cast<char*>(fault) - reinterpret_cast<char*>(region)) + 4,
-                            s)) != hipSuccess)
-        return e;
+    if ((e = hipMemsetAsync(region, 0, 4 * scan_region_words(cells + 1), s)) != hipSuccess) return e;
     hipLaunchKernelGGL(k_knn_bbox_partial, dim3(pb), dim3(kKnnThreads), 0, s, N, pts, partial);
     hipLaunchKernelGGL(k_knn_grid, dim3(1), dim3(64), 0, s, pb, (const float*)partial, N, cells, grid);
     hipLaunchKernelGGL(k_knn_cell, dim3(nb), dim3(kKnnThreads), 0, s, N, pts, (const KnnGrid*)grid, cell, count);
-    if ((e = scan_exclusive_u32(count, start, (int)(cells + 1), region, fault, s)) != hipSuccess) return e;
+    if ((e = scan_exclusive_u32(count, start, (int)(cells + 1), region, stall, s)) != hipSuccess) return e;
     // the scatter advances a copy of the cell starts as per-cell cursors
     if ((e = hipMemcpyAsync(count, start, 4 * ((size_t)cells + 1), hipMemcpyDeviceToDevice, s)) != hipSuccess)
         return e;

@@ -22,6 +22,7 @@ constexpr int kLossMaxBlocks = 1024;
 // runs on one 512-thread block per CU
 constexpr int kFwdThreads = 512;
 constexpr int kFwdBlocks = 256;
+static_assert(kFwdBlocks <= kFwdThreads, "the last block's threads take one block sum each");
 
 // mask value of pixel p (bool bytes or fp32)
 __device__ __forceinline__ float mask_at(const void* mask, int is_float, int64_t p)
@@ -78,26 +79,20 @@ __device__ __forceinline__ double block_sum_double(double v, double* wsum)
     return t;  // valid in thread 0
 }
 
-// Block sums are published as ONE 64-bit word {epoch, float bits} with an sc1 store; the last
-// block (ticket) spins until every word carries this launch's epoch, then adds them in block
-// order.  No __threadfence (on gfx950 each one is an L2 writeback) and no scratch reset between
-// launches: the host passes a fresh nonzero epoch per launch.
+// Thread t's partial sum of block `bid` of the forward's grid (grid-stride over V-pixel groups).
 // kC: the channel count at compile time (LangSplat's 3: every load of a group in flight at once),
-// 0 = runtime C.
+// 0 = runtime C.  One function for the block's own pass and the last block's stall fallback, so
+// a recomputed block sum is bit-identical to the one the block would have published.
 template <int V, int kC>
-__global__ __launch_bounds__(kFwdThreads) void k_masked_l1_forward(int C_rt, int64_t HW, const float* __restrict__ pred,
-                                                                    const float* __restrict__ gt, const void* mask,
-                                                                    int mask_is_float, float* __restrict__ loss,
-                                                                    uint32_t* __restrict__ ticket,
-                                                                    uint64_t* __restrict__ partial, uint32_t epoch)
+__device__ __forceinline__ float l1_thread_partial(int bid, int nblocks, int C_rt, int64_t HW,
+                                                   const float* __restrict__ pred, const float* __restrict__ gt,
+                                                   const void* mask, int mask_is_float)
 {
-    __shared__ double wsum[kFwdThreads / 64];
-    __shared__ bool s_last;
     const int C = kC > 0 ? kC : C_rt;
     const int64_t groups = HW / V;
     float acc = 0.0f;
-    const int64_t stride = (int64_t)gridDim.x * kFwdThreads;
-    int64_t gi = (int64_t)blockIdx.x * kFwdThreads + threadIdx.x;
+    const int64_t stride = (int64_t)nblocks * kFwdThreads;
+    int64_t gi = (int64_t)bid * kFwdThreads + threadIdx.x;
     if (kC > 0) {  // two groups per iteration: all 2 (2 kC + 1) loads in flight before the first use
         for (; gi + stride < groups; gi += 2 * stride) {
             float m[2][V], a[2][kC > 0 ? kC : 1][V], b[2][kC > 0 ? kC : 1][V];
@@ -131,23 +126,84 @@ __global__ __launch_bounds__(kFwdThreads) void k_masked_l1_forward(int C_rt, int
             for (int k = 0; k < V; k++) acc += fabsf(a[k] * m[k] - b[k] * m[k]);
         }
     }
-    const double bs = block_sum_double<kFwdThreads>((double)acc, wsum);
-    if (threadIdx.x == 0) {
-        const uint64_t word = ((uint64_t)epoch << 32) | __float_as_uint((float)bs);
-        __hip_atomic_store(&partial[blockIdx.x], word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+    return acc;
+}
+
+// First set bit of the kFwdBlocks-bit LDS mask at index > after, or -1.
+__device__ __forceinline__ int next_flagged(const uint32_t* mask, int after)
+{
+    for (int w = (after + 1) >> 5; w < kFwdBlocks / 32; w++) {
+        uint32_t m = mask[w];
+        if (w == (after + 1) >> 5) m &= ~0u << ((after + 1) & 31);
+        if (m) return 32 * w + __builtin_ctz(m);
     }
-    __syncthreads();
-    if (!s_last) return;
-    double v = 0.0;
-    for (int i = threadIdx.x; i < (int)gridDim.x; i += kFwdThreads) {
-        uint64_t w = __hip_atomic_load(&partial[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        for (uint32_t spins = 0; (uint32_t)(w >> 32) != epoch && spins < (1u << 24); spins++)
-            w = __hip_atomic_load(&partial[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        v += (double)__uint_as_float((uint32_t)w);
+    return -1;
+}
+
+// Block sums are published as ONE 64-bit word {epoch, float bits} with an sc1 store; the last
+// block (ticket) waits until every word carries this launch's epoch, then adds them in block
+// order.  No __threadfence (on gfx950 each one is an L2 writeback) and no scratch reset between
+// launches: the host passes a fresh nonzero epoch per launch.  A word still missing after
+// spin_limit polls (stall_spin_limit(), lsr_internal.h) is recomputed by the last block from the
+// inputs and the event is noted in *stall.  The recomputation runs the SAME loop body as the
+// block's own pass (one inlined copy: the loop below iterates over block ids), so the value is
+// bit-identical to the one the block would have published.
+template <int V, int kC>
+__global__ __launch_bounds__(kFwdThreads) void k_masked_l1_forward(int C_rt, int64_t HW, const float* __restrict__ pred,
+                                                                    const float* __restrict__ gt, const void* mask,
+                                                                    int mask_is_float, float* __restrict__ loss,
+                                                                    uint32_t* __restrict__ ticket,
+                                                                    uint64_t* __restrict__ partial, uint32_t epoch,
+                                                                    uint32_t* stall, uint32_t spin_limit)
+{
+    __shared__ double wsum[kFwdThreads / 64];
+    __shared__ bool s_last;
+    __shared__ uint32_t s_missing[kFwdBlocks / 32];
+    __shared__ float s_redo[kFwdBlocks];
+    const int C = kC > 0 ? kC : C_rt;
+    const int nb = (int)gridDim.x;
+    const int i = (int)threadIdx.x;  // in the last block: thread i takes block i's sum (nb <= kFwdThreads)
+    float mine = 0.0f;
+    bool any = false;
+    for (int bid = (int)blockIdx.x;;) {
+        const float acc = l1_thread_partial<V, kC>(bid, nb, C_rt, HW, pred, gt, mask, mask_is_float);
+        const double bs = block_sum_double<kFwdThreads>((double)acc, wsum);
+        if (bid == (int)blockIdx.x && !any) {  // the block's own pass
+            if (threadIdx.x == 0) {
+                const uint64_t word = ((uint64_t)epoch << 32) | __float_as_uint((float)bs);
+                __hip_atomic_store(&partial[blockIdx.x], word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                s_last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+            }
+            if (threadIdx.x < kFwdBlocks / 32) s_missing[threadIdx.x] = 0u;
+            __syncthreads();
+            if (!s_last) return;
+            if (i < nb) {
+                uint64_t w = __hip_atomic_load(&partial[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                uint32_t spins = 0;
+                while ((uint32_t)(w >> 32) != epoch || spin_limit == 0u) {
+                    if (++spins > spin_limit) {
+                        atomicOr(&s_missing[i >> 5], 1u << (i & 31));
+                        break;
+                    }
+                    w = __hip_atomic_load(&partial[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                mine = __uint_as_float((uint32_t)w);
+            }
+            __syncthreads();
+            bid = -1;
+        } else {  // stall fallback: a missing block's sum
+            if (threadIdx.x == 0) s_redo[bid] = (float)bs;
+            __syncthreads();
+        }
+        bid = next_flagged(s_missing, bid);
+        if (bid < 0) break;
+        any = true;
     }
-    __syncthreads();
-    const double total = block_sum_double<kFwdThreads>(v, wsum);
+    if (any) {
+        if (i < nb && ((s_missing[i >> 5] >> (i & 31)) & 1u)) mine = s_redo[i];
+        if (threadIdx.x == 0) note_stall(stall);
+    }
+    const double total = block_sum_double<kFwdThreads>((double)mine, wsum);
     if (threadIdx.x == 0) {
         *loss = (float)(total / (double)((int64_t)C * HW));
         *ticket = 0u;  // the next launch on this scratch is stream-ordered after this one
@@ -189,9 +245,12 @@ __global__ __launch_bounds__(kLossThreads) void k_masked_l1_backward(int C_rt, i
     }
 }
 
+// Segment ids outside [-N, N) -- an IndexError in the reference's feature_map[seg] -- write zeros
+// and set *bad (pinned host memory; the API syncs and reports it).
 __global__ __launch_bounds__(256) void k_decode_language_feature(int H, int W, const int64_t* __restrict__ seg_level,
                                                                  int N, int D, const float* __restrict__ feature_map,
-                                                                 float* __restrict__ out, uint8_t* __restrict__ mask)
+                                                                 float* __restrict__ out, uint8_t* __restrict__ mask,
+                                                                 uint32_t* bad)
 {
     const int64_t HW = (int64_t)H * W;
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -200,6 +259,7 @@ __global__ __launch_bounds__(256) void k_decode_language_feature(int H, int W, c
     mask[p] = s != -1 ? 1 : 0;
     if (s < 0) s += N;  // torch indexing: -1 is the last row
     const bool ok = s >= 0 && s < N;
+    if (!ok) __hip_atomic_store(bad, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     for (int d = 0; d < D; d++) out[(int64_t)d * HW + p] = ok ? feature_map[s * D + d] : 0.0f;
 }
 
@@ -218,8 +278,10 @@ static int loss_blocks(int64_t groups)
 size_t masked_l1_scratch_bytes() { return 256 + 8 * (size_t)kLossMaxBlocks; }
 
 hipError_t launch_masked_l1_forward(int C, int64_t HW, const float* pred, const float* gt, const void* mask,
-                                    int mask_is_float, float* loss, void* scratch, uint32_t epoch, hipStream_t s)
+                                    int mask_is_float, float* loss, void* scratch, uint32_t epoch, uint32_t* stall,
+                                    hipStream_t s)
 {
+    const uint32_t spin = stall_spin_limit();
     uint32_t* counter = static_cast<uint32_t*>(scratch);
     uint64_t* partial = reinterpret_cast<uint64_t*>(static_cast<char*>(scratch) + 256);
     auto blocks = [](int64_t groups) {
@@ -229,13 +291,13 @@ hipError_t launch_masked_l1_forward(int C, int64_t HW, const float* pred, const 
     if (vec4_ok(HW, pred, gt, nullptr, mask, mask_is_float)) {
         if (C == 3)
             hipLaunchKernelGGL((k_masked_l1_forward<4, 3>), dim3(blocks(HW / 4)), dim3(kFwdThreads), 0, s, C, HW, pred,
-                               gt, mask, mask_is_float, loss, counter, partial, epoch);
+                               gt, mask, mask_is_float, loss, counter, partial, epoch, stall, spin);
         else
             hipLaunchKernelGGL((k_masked_l1_forward<4, 0>), dim3(blocks(HW / 4)), dim3(kFwdThreads), 0, s, C, HW, pred,
-                               gt, mask, mask_is_float, loss, counter, partial, epoch);
+                               gt, mask, mask_is_float, loss, counter, partial, epoch, stall, spin);
     } else {
         hipLaunchKernelGGL((k_masked_l1_forward<1, 0>), dim3(blocks(HW)), dim3(kFwdThreads), 0, s, C, HW, pred, gt,
-                           mask, mask_is_float, loss, counter, partial, epoch);
+                           mask, mask_is_float, loss, counter, partial, epoch, stall, spin);
     }
     return hipGetLastError();
 }
@@ -258,11 +320,12 @@ hipError_t launch_masked_l1_backward(int C, int64_t HW, const float* pred, const
 }
 
 hipError_t launch_decode_language_feature(int H, int W, const int64_t* seg_level, int N, int D,
-                                          const float* feature_map, float* out, uint8_t* mask, hipStream_t s)
+                                          const float* feature_map, float* out, uint8_t* mask, uint32_t* bad,
+                                          hipStream_t s)
 {
     const int64_t HW = (int64_t)H * W;
     hipLaunchKernelGGL(k_decode_language_feature, dim3((unsigned)((HW + 255) / 256)), dim3(256), 0, s, H, W, seg_level,
-                       N, D, feature_map, out, mask);
+                       N, D, feature_map, out, mask, bad);
     return hipGetLastError();
 }
 

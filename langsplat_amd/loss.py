@@ -105,7 +105,8 @@ def decode_language_feature(seg_map: torch.Tensor, feature_map: torch.Tensor, fe
 
     seg_map: (L,H,W) segment ids (-1 = no segment), feature_map: (N,D).  Returns
     (feature (D,H,W) fp32, mask (1,H,W) bool) exactly as the reference builds them, including
-    torch's reading of index -1 as the last feature row."""
+    torch's reading of index -1 as the last feature row.  A segment id outside [-N, N) raises
+    IndexError, as the reference's feature_map[seg] does."""
     if seg_map.dim() != 3:
         raise ValueError("seg_map must be (L,H,W)")
     L, H, W = seg_map.shape
@@ -119,10 +120,12 @@ def decode_language_feature(seg_map: torch.Tensor, feature_map: torch.Tensor, fe
     mask = torch.empty((1, H, W), dtype=torch.bool, device=device)
     lib = _native.load()
     with _native._on_device(device):
-        _native._check(lib.lsr_decode_language_feature(L, H, W, _native._ptr(seg), int(feature_level), N, D,
-                                                       _native._ptr(fm), _native._ptr(out),
-                                                       ctypes.c_void_p(mask.data_ptr()), _stream_ptr(device)),
-                       "lsr_decode_language_feature")
+        status = lib.lsr_decode_language_feature(L, H, W, _native._ptr(seg), int(feature_level), N, D,
+                                                 _native._ptr(fm), _native._ptr(out),
+                                                 ctypes.c_void_p(mask.data_ptr()), _stream_ptr(device))
+    if status == 1:  # LSR_ERR_INVALID: a segment id outside the feature map
+        raise IndexError(f"decode_language_feature: {_native.last_error()}")
+    _native._check(status, "lsr_decode_language_feature")
     return out, mask
 
 
@@ -143,8 +146,11 @@ class LanguageFeatureCache:
             seg = torch.from_numpy(np.load(base + "_s.npy"))           # allow_pickle=False (default)
             feat = torch.from_numpy(np.load(base + "_f.npy"))
             H, W = int(camera.image_height), int(camera.image_width)
-            if tuple(seg.shape[1:]) != (H, W):
-                raise ValueError(f"{base}_s.npy is {tuple(seg.shape)}, camera is {H}x{W}")
+            # scene/cameras.py:69-73 reads seg_map[:, y, x] for y < H, x < W: a larger map is cropped
+            # to its top-left H x W, a smaller one raises IndexError there
+            if seg.dim() != 3 or seg.shape[1] < H or seg.shape[2] < W:
+                raise IndexError(f"{base}_s.npy is {tuple(seg.shape)}, smaller than the camera's {H}x{W}")
+            seg = seg[:, :H, :W]
             hit = decode_language_feature(seg.to(self.device), feat.to(self.device), feature_level)
             self._maps[key] = hit
         return hit

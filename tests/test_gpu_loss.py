@@ -9,6 +9,7 @@ import numpy as np
 import pytest
 import torch
 
+from langsplat_amd import _native
 from langsplat_amd.loss import LanguageFeatureCache, decode_language_feature, masked_l1_loss
 
 pytestmark = pytest.mark.gpu
@@ -83,3 +84,63 @@ def test_decode_language_feature_matches_reference(tmp_path):
     assert f1 is f2 and len(cache) == 1
     rf, rm = _reference_decode(seg_map, feature_map, 2, H, W)
     assert torch.equal(f1.cpu(), rf.contiguous()) and torch.equal(m1.cpu(), rm)
+
+
+def test_masked_l1_stall_fallback_is_exact():
+    """Spin limit 0: the last block recomputes every other block's sum from the inputs instead of
+    waiting for it; the loss is bit-identical and the event is reported."""
+    lib = _native.load()
+    g = torch.Generator().manual_seed(4)
+    pred = torch.randn((3, 720, 1280), generator=g).to(DEV)
+    gt = torch.randn((3, 720, 1280), generator=g).to(DEV)
+    mask = (torch.rand((1, 720, 1280), generator=g) < 0.9).to(DEV)
+    a = masked_l1_loss(pred, gt, mask)
+    torch.cuda.synchronize()
+    lib.lsr_debug_scan_stalls()
+    old = lib.lsr_debug_set_spin_limit(0)
+    try:
+        b = masked_l1_loss(pred, gt, mask)
+        torch.cuda.synchronize()
+        assert lib.lsr_debug_scan_stalls() == 1
+    finally:
+        lib.lsr_debug_set_spin_limit(old)
+    assert torch.equal(a, b)
+
+
+def test_decode_rejects_out_of_range_segment_ids():
+    """feature_map[seg] in scene/cameras.py:75-84 raises IndexError for ids outside [-N, N)."""
+    N, D = 10, 3
+    feature_map = torch.randn((N, D)).to(DEV)
+    for bad in (N, -N - 1):
+        seg_map = torch.zeros((4, 8, 9), dtype=torch.int64)
+        seg_map[1, 3, 4] = bad
+        with pytest.raises(IndexError, match="outside"):
+            decode_language_feature(seg_map.to(DEV), feature_map, 1)
+    # other levels than the bad one decode (the reference only indexes the requested level)
+    seg_map = torch.zeros((4, 8, 9), dtype=torch.int64)
+    seg_map[1, 3, 4] = N
+    f, m = decode_language_feature(seg_map.to(DEV), feature_map, 0)
+    assert m.all() and torch.equal(f[:, 0, 0], feature_map[0])
+
+
+def test_cache_crops_a_larger_segment_map_and_rejects_a_smaller_one(tmp_path):
+    """scene/cameras.py:69-73 gathers seg_map[:, y, x] for y < H, x < W."""
+    g = torch.Generator().manual_seed(6)
+    L, N, D, H, W = 4, 50, 3, 20, 30
+    big = torch.randint(-1, N, (L, H + 5, W + 7), generator=g)
+    feature_map = torch.randn((N, D), generator=g)
+    np.save(tmp_path / "v_s.npy", big.numpy())
+    np.save(tmp_path / "v_f.npy", feature_map.numpy())
+
+    class Cam:
+        image_name, image_height, image_width = "v", H, W
+
+    f, m = LanguageFeatureCache(DEV).get(Cam, str(tmp_path), 1)
+    rf, rm = _reference_decode(big, feature_map, 1, H, W)
+    assert torch.equal(f.cpu(), rf.contiguous()) and torch.equal(m.cpu(), rm)
+
+    class Big:
+        image_name, image_height, image_width = "v", H + 6, W
+
+    with pytest.raises(IndexError):
+        LanguageFeatureCache(DEV).get(Big, str(tmp_path), 1)

@@ -358,3 +358,25 @@ def test_depth_sort_pass_counts(kind):
     run, std, ind, out = check_forward_exact(st, inp)
     assert out[0] > 0
     check_backward(st, inp, run, out)
+
+
+def test_lookback_stall_fallback_is_exact():
+    """Every single-pass look-back (depth-sort histogram scans, super-tile offset scan, binning
+    table scan) forced onto its stall path (spin limit 0: no chunk waits for its predecessors; each
+    computes its prefix from the input instead) gives the same bit-exact forward, and the event is
+    reported by lsr_debug_scan_stalls."""
+    lib = _native.load()
+    st, inp = scene(P=40000, W=320, H=240, seed=8, sh_degree=1, scale_range=(0.01, 0.06))
+    run = oracle.forward(st, **inp)
+    torch.cuda.synchronize()
+    lib.lsr_debug_scan_stalls()  # clear
+    old = lib.lsr_debug_set_spin_limit(0)
+    try:
+        run, std, ind, out = check_forward_exact(st, inp, run)
+        torch.cuda.synchronize()
+        assert lib.lsr_debug_scan_stalls() == 1
+    finally:
+        lib.lsr_debug_set_spin_limit(old)
+    check_forward_exact(st, inp, run)
+    torch.cuda.synchronize()
+    assert lib.lsr_debug_scan_stalls() == 0

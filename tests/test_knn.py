@@ -79,3 +79,21 @@ def test_gpu_knn_large_and_simple_knn_import_path():
     idx = g.choice(len(p), 300, replace=False)
     np.testing.assert_allclose(got[idx].astype(np.float64), _numpy_knn(p, idx), rtol=2e-6)
     assert got.shape == (len(p),) and np.all(got > 0)
+
+
+@pytest.mark.gpu
+def test_gpu_knn_scan_stall_fallback_is_exact():
+    """The cell-count scan forced onto its stall path (spin limit 0) gives the same distances."""
+    from langsplat_amd import _native
+    from langsplat_amd.knn import dist_cuda2
+    lib = _native.load()
+    p = np.random.default_rng(3).uniform(-1, 1, (20000, 3)).astype(np.float32)
+    ref = dist_cuda2(torch.from_numpy(p).cuda()).cpu().numpy()
+    lib.lsr_debug_scan_stalls()
+    old = lib.lsr_debug_set_spin_limit(0)
+    try:
+        got = dist_cuda2(torch.from_numpy(p).cuda()).cpu().numpy()
+        assert lib.lsr_debug_scan_stalls() == 1
+    finally:
+        lib.lsr_debug_set_spin_limit(old)
+    np.testing.assert_array_equal(got, ref)

@@ -31,7 +31,7 @@ def test_library_loads_and_exports_every_declared_symbol():
     for name in _declared_functions():
         assert hasattr(lib, name), name
         assert name in _native.SIGNATURES, f"ctypes binding misses {name}"
-    assert lib.lsr_abi_version() == _native.ABI_VERSION == 3
+    assert lib.lsr_abi_version() == _native.ABI_VERSION == 4
 
 
 def test_sizes_and_layout_are_consistent():
@@ -50,6 +50,13 @@ def test_invalid_arguments_report_errors_without_gpu():
     assert lib.lsr_state_layout_of(-1, 10, 10, 0, None) != 0
     assert "invalid" in _native.last_error()
     assert lib.lsr_mark_visible(-5, None, None, None, None, None) != 0
+
+
+def test_spin_limit_knob_round_trips_without_gpu():
+    lib = _native.load()
+    old = lib.lsr_debug_set_spin_limit(7)
+    assert lib.lsr_debug_set_spin_limit(old) == 7
+    assert old == 1 << 24
 
 
 def _settings(device="cpu", include_feature=True):
