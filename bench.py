@@ -37,7 +37,6 @@ sys.path.insert(0, ROOT)
 
 from langsplat_amd import _native  # noqa: E402
 from langsplat_amd.distributed import GradBucket, init_from_env  # noqa: E402
-from langsplat_amd.loss import masked_l1_loss  # noqa: E402
 from langsplat_amd.optim import Adam as AmdAdam  # noqa: E402
 from langsplat_amd.render import render  # noqa: E402
 from langsplat_amd.synthetic import CONFIGS, activated_inputs, make_cameras, make_gaussians  # noqa: E402
@@ -106,20 +105,23 @@ class Opt:
     include_feature = True
 
 
-def algorithmic_bytes(stage, P, V, R, HW, M, color_grad=True, geometry=True):
+def algorithmic_bytes(stage, P, V, R, HW, M, color_grad=True, geometry=True, fused_loss=False):
     """Compulsory HBM bytes per launch of each stage (SURVEY.md §8d per-unit model).
     The render backward's per-pixel and per-Gaussian terms follow its variant: dL/dcolor is read
     only when the colour image reaches the loss, and the per-Gaussian record it accumulates holds
-    12 values with geometry gradients, 5 (dmean2D x/y + language) without."""
+    12 values with geometry gradients, 5 (dmean2D x/y + language) without.  fused_loss: the forward
+    also reads the target (12 B/px) and mask (1) and writes a 1-B sign code, which the backward
+    reads instead of dL/dlanguage (12 B/px)."""
     sh = 12 * M
-    bwd_px = 4 + 4 + 12 + (12 if color_grad else 0)  # T, contributor count, dL/dlanguage, [dL/dcolor]
+    bwd_px = 4 + 4 + (1 if fused_loss else 12) + (12 if color_grad else 0)  # T, count, dL/dlang | code, [dL/dcolor]
+    fwd_px = 32 + (14 if fused_loss else 0)
     bwd_g = 4 * (12 if geometry else 5)
     return {
         # reads means 12, scale 12, rot 16, opacity 4, SH, lang 12; writes radii 4 + key 4 + tiles 4
         # + rect 8 + clamp 4 (all P) and the 48 B record for visible Gaussians
         "preprocess": P * (12 + 12 + 16 + 4 + sh + 12 + 24) + V * 48,
         # per instance: list id 4 + gathered record 48; per pixel: colour 12 + language 12 + T 4 + count 4
-        "render forward": R * 52 + HW * 32,
+        "render forward": R * 52 + HW * fwd_px,
         # per instance: id 4 + record 48; per pixel: bwd_px; per visible Gaussian: its gradient
         # record, accumulated once
         "render backward": R * 52 + HW * bwd_px + V * bwd_g,
@@ -131,10 +133,10 @@ def algorithmic_bytes(stage, P, V, R, HW, M, color_grad=True, geometry=True):
 # the stage that dominates the step (measured: profiles/r01_summary.json); timed live in the bench
 DOMINANT_STAGE = "render backward"
 
-# rocprofv3 names of the bench step's kernels (template arguments: k_render_forward<kStats, kFeat>,
+# rocprofv3 names of the bench step's kernels (template arguments: k_render_forward<kStats, kFeat, kLoss>,
 # k_render_backward<kStats, kFeat, kColor, kGeo>; the language step runs kColor = kGeo = false)
 STAGE_KERNEL = {"render backward": "lsr::k_render_backward<false, true, false, false>",
-                "render forward": "lsr::k_render_forward<false, true>",
+                "render forward": "lsr::k_render_forward<false, true, true>",
                 "preprocess": "lsr::k_preprocess", "preprocess backward": "lsr::k_preprocess_backward"}
 
 
@@ -240,11 +242,10 @@ def main():
     bucket = GradBucket(model.trainable()) if world > 1 else None
 
     def step():
-        pkg = render(cam, model, Pipe, bg, Opt)
-        lang = pkg["language_feature_image"]
-        if fused:  # one kernel each way
-            loss = masked_l1_loss(lang, gt, mask)
+        if fused:  # the loss inside the compositing kernel, its backward in the replay
+            loss = render(cam, model, Pipe, bg, Opt, language_target=(gt, mask))["language_l1"]
         else:      # train.py:98 + utils/loss_utils.py:17-18 as torch ops
+            lang = render(cam, model, Pipe, bg, Opt)["language_feature_image"]
             loss = torch.abs(lang * mask - gt * mask).mean()
         loss.backward()
         if bucket is not None:
@@ -333,7 +334,8 @@ def main():
     M = (c["sh_degree"] + 1) ** 2
     # the language step: the colour image does not reach the loss; geometry gradients as needed
     geometry = bool(_native.FORCE_GEOMETRY_GRADS)
-    bytes_dom = algorithmic_bytes(dom_name, P, visible, nr, W * H, M, color_grad=False, geometry=geometry)
+    bytes_dom = algorithmic_bytes(dom_name, P, visible, nr, W * H, M, color_grad=False, geometry=geometry,
+                                  fused_loss=fused)
     roofline = None
     if bytes_dom is not None:
         achieved = bytes_dom / (dom["avg_ms"] * 1e-3) / 1e9

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define LSR_ABI_VERSION 4
+#define LSR_ABI_VERSION 5
 
 enum lsr_status {
     LSR_OK = 0,
@@ -115,6 +115,14 @@ typedef struct lsr_forward_args {
                                         (scene/gaussian_model.py:146-150) */
     uint8_t* visible;                /* NULL, or P bytes: radii > 0 (render()'s visibility_filter,
                                         gaussian_renderer/__init__.py:99), written by preprocess */
+    /* Fused language-feature loss (train.py:96-99):
+     *     *out_loss = l1_loss(language_feature_image * mask, loss_target * mask)
+     *               = sum |f m - gt m| / (3 H W)          (utils/loss_utils.py:17-18)
+     * computed by the compositing kernel from the pixels it just produced (deterministic order).
+     * out_loss NULL: off.  Needs include_feature and language_feature. */
+    const float* loss_target;        /* 3 x H x W, or NULL */
+    const uint8_t* loss_mask;        /* H x W bool bytes (scene/cameras.py:72 seg != -1), or NULL */
+    float* out_loss;                 /* one float (device), or NULL */
 } lsr_forward_args;
 
 /* Inputs/outputs of _C.rasterize_gaussians_backward.  Every non-NULL output is fully written
@@ -156,6 +164,9 @@ typedef struct lsr_backward_args {
     int32_t reserved;
     const float* shs_rest;           /* as in the forward */
     float* dL_dsh_rest;              /* P x (M-1) x 3 when shs_rest is set (dL_dsh is then P x 1 x 3) */
+    const float* dL_dloss;           /* NULL, or the device scalar dL/d(out_loss) of a forward that fused
+                                        the loss: its gradient dL/dloss * sign(f m - gt m) * m / (3 H W)
+                                        (autograd's) is added to dL_dout_language_feature (NULL = 0) */
 } lsr_backward_args;
 
 /* Byte offsets of the internal state inside the forward buffers, for inspection by tests and

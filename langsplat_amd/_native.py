@@ -21,7 +21,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "liblsr.so")
 
 LSR_BUF_GEOM, LSR_BUF_BINNING, LSR_BUF_IMAGE, LSR_BUF_BACKWARD = 0, 1, 2, 3
-ABI_VERSION = 4
+ABI_VERSION = 5
 # lsr_raw_flags (include/lsr.h): inputs are GaussianModel's raw parameters
 RAW_OPACITY, RAW_SCALES, RAW_ROTATIONS, RAW_LANGUAGE = 1, 2, 4, 8
 _vp = ctypes.c_void_p
@@ -50,7 +50,8 @@ class LsrForwardArgs(ctypes.Structure):
     _fields_ = [("P", ctypes.c_int32), ("M", ctypes.c_int32)] + [
         (n, _vp) for n in ("means3D", "shs", "colors_precomp", "language_feature", "opacities", "scales",
                            "rotations", "cov3D_precomp", "out_color", "out_language_feature", "radii")
-    ] + [("raw", ctypes.c_int32), ("reserved", ctypes.c_int32), ("shs_rest", _vp), ("visible", _vp)]
+    ] + [("raw", ctypes.c_int32), ("reserved", ctypes.c_int32), ("shs_rest", _vp), ("visible", _vp),
+         ("loss_target", _vp), ("loss_mask", _vp), ("out_loss", _vp)]
 
 
 class LsrBackwardArgs(ctypes.Structure):
@@ -60,7 +61,8 @@ class LsrBackwardArgs(ctypes.Structure):
                            "geom_buffer", "binning_buffer", "image_buffer", "dL_dmeans2D", "dL_dcolors",
                            "dL_dlanguage_feature", "dL_dopacity", "dL_dmeans3D", "dL_dcov3D", "dL_dsh",
                            "dL_dscales", "dL_drotations")
-    ] + [("raw", ctypes.c_int32), ("reserved", ctypes.c_int32), ("shs_rest", _vp), ("dL_dsh_rest", _vp)]
+    ] + [("raw", ctypes.c_int32), ("reserved", ctypes.c_int32), ("shs_rest", _vp), ("dL_dsh_rest", _vp),
+         ("dL_dloss", _vp)]
 
 
 class LsrStateLayout(ctypes.Structure):
@@ -276,12 +278,14 @@ def _f32c_cached(src: torch.Tensor) -> torch.Tensor:
 
 
 def rasterize_gaussians(rs, means3D, shs, colors_precomp, language_feature, opacities, scales, rotations,
-                        cov3D_precomp, raw=0, shs_rest=None, visible=None):
+                        cov3D_precomp, raw=0, shs_rest=None, visible=None, loss_target=None, loss_mask=None,
+                        out_loss=None):
     """Native forward: returns (num_rendered, color, language_feature_image, radii, geom, binning, image).
 
     raw / shs_rest: the fused-activation form (include/lsr.h lsr_raw_flags); shs is then
     features_dc (P,1,3) and shs_rest features_rest (P,M-1,3).  visible: optional (P,) bool tensor
-    that receives radii > 0."""
+    that receives radii > 0.  out_loss: optional () fp32 tensor that receives the fused
+    l1_loss(lang * mask, loss_target * mask) (loss_target (3,H,W) fp32, loss_mask H*W bool)."""
     lib = load()
     device = means3D.device
     P = int(means3D.shape[0])
@@ -313,6 +317,16 @@ def rasterize_gaussians(rs, means3D, shs, colors_precomp, language_feature, opac
         if visible.dtype != torch.bool or visible.numel() != P or not visible.is_contiguous():
             raise ValueError("visible must be a contiguous (P,) bool tensor")
         a.visible = _ptr(visible)
+    if out_loss is not None:
+        if loss_target is None or tuple(loss_target.shape) != (3, H, W) or loss_target.dtype != torch.float32 \
+                or not loss_target.is_contiguous():
+            raise ValueError("loss_target must be a contiguous (3,H,W) fp32 tensor")
+        if loss_mask is None or loss_mask.dtype != torch.bool or loss_mask.numel() != H * W \
+                or not loss_mask.is_contiguous():
+            raise ValueError("loss_mask must be a contiguous bool tensor of H*W elements")
+        a.loss_target = _ptr(loss_target)
+        a.loss_mask = _ptr(loss_mask)
+        a.out_loss = _ptr(out_loss)
     alloc = _Allocator(device)
     nr = ctypes.c_int64(0)
     with _on_device(device), alloc:
@@ -335,11 +349,12 @@ def geometry_grads_needed(needs_input_grad, geometry_inputs):
 
 def rasterize_gaussians_backward(rs, means3D, shs, colors_precomp, language_feature, scales, rotations,
                                  cov3D_precomp, radii, grad_color, grad_language, num_rendered, geom, binning,
-                                 image, raw=0, shs_rest=None, opacities=None, geometry=True):
+                                 image, raw=0, shs_rest=None, opacities=None, geometry=True, grad_loss=None):
     """Native backward: returns the gradient tensors keyed like the reference's inputs (with raw
     flags: w.r.t. the raw parameters; "shs" is then dL/dfeatures_dc and "shs_rest"
     dL/dfeatures_rest).  geometry=False (no geometry input needs a gradient): only "means2D" and
-    "language_feature_precomp" are computed, the other entries are None (include/lsr.h)."""
+    "language_feature_precomp" are computed, the other entries are None (include/lsr.h).
+    grad_loss: dL/d(the fused loss of the forward), a () device tensor, or None."""
     lib = load()
     device = means3D.device
     P = int(means3D.shape[0])
@@ -397,6 +412,10 @@ def rasterize_gaussians_backward(rs, means3D, shs, colors_precomp, language_feat
     if grad_language is not None:
         gl = _f32c(grad_language.detach())
         a.dL_dout_language_feature = _ptr(gl)
+    gls = None
+    if grad_loss is not None:
+        gls = _f32c(grad_loss.detach().reshape(1))
+        a.dL_dloss = _ptr(gls)
     a.geom_buffer = _ptr(geom)
     a.binning_buffer = _ptr(binning)
     a.image_buffer = _ptr(image)

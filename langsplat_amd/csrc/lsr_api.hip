@@ -236,6 +236,9 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
         return fail(LSR_ERR_INVALID, "lsr_forward: unknown raw flag");
     if (a->shs_rest && (!a->shs || a->M < 2))
         return fail(LSR_ERR_INVALID, "lsr_forward: shs_rest needs shs (features_dc) and M >= 2");
+    if (a->out_loss && (!s->include_feature || (P > 0 && !a->language_feature) || !a->loss_target || !a->loss_mask))
+        return fail(LSR_ERR_INVALID, "lsr_forward: the fused loss needs include_feature, language_feature, "
+                                     "loss_target and loss_mask");
     hipStream_t stream = reinterpret_cast<hipStream_t>(stream_ptr);
     const bool debug = s->debug != 0;
     *num_rendered = 0;
@@ -244,6 +247,20 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
         // upstream leaves the images at their zero initialisation when there is nothing to draw
         LSR_TRY(hipMemsetAsync(a->out_color, 0, 3 * HW * 4, stream), "memset color");
         LSR_TRY(hipMemsetAsync(a->out_language_feature, 0, 3 * HW * 4, stream), "memset language");
+        if (a->out_loss) {
+            const Layout L0 = make_layout(0, W, H, 0, 0);
+            char* image = static_cast<char*>(alloc(user, LSR_BUF_IMAGE, L0.image_bytes));
+            if (!image) return fail(LSR_ERR_ALLOC, "lsr_forward: image buffer allocation failed");
+            RenderParams rp{};
+            rp.W = W;
+            rp.H = H;
+            rp.loss_gt = a->loss_target;
+            rp.loss_mask = a->loss_mask;
+            rp.loss_code = reinterpret_cast<uint8_t*>(image + L0.loss_code);
+            rp.loss_partial = reinterpret_cast<double*>(image + L0.loss_partial);
+            rp.out_loss = a->out_loss;
+            LSR_TRY(launch_loss(rp, 0, true, stream), "loss");
+        }
         return LSR_OK;
     }
 
@@ -340,7 +357,15 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
     rp.sched_lists = reinterpret_cast<uint32_t*>(image + L.tile_lists);
     rp.out_color = a->out_color;
     rp.out_lang = a->out_language_feature;
+    if (a->out_loss && rp.include_feature) {
+        rp.loss_gt = a->loss_target;
+        rp.loss_mask = a->loss_mask;
+        rp.loss_code = reinterpret_cast<uint8_t*>(image + L.loss_code);
+        rp.loss_partial = reinterpret_cast<double*>(image + L.loss_partial);
+        rp.out_loss = a->out_loss;
+    }
     LSR_TRY(launch_render_forward(rp, L.tiles, stream), "render forward");
+    if (rp.out_loss) LSR_TRY(launch_loss(rp, L.tiles, false, stream), "loss");
     return LSR_OK;
 }
 
@@ -397,6 +422,8 @@ int32_t lsr_backward(const lsr_settings* s, const lsr_backward_args* a, lsr_allo
     rp.sched_lists = reinterpret_cast<uint32_t*>(image + L.tile_lists);
     rp.dL_dcolor = a->dL_dout_color;
     rp.dL_dlang = a->dL_dout_language_feature;
+    rp.dL_dloss = a->dL_dloss;
+    rp.loss_code = reinterpret_cast<uint8_t*>(image + L.loss_code);
     rp.grad = grad;
     rp.geo = geometry ? 1 : 0;
     if (a->num_rendered > 0) LSR_TRY(launch_render_backward(rp, L.tiles, stream), "render backward");

@@ -49,7 +49,7 @@ struct Layout {
     size_t scan_region_geom;  // u32 words per depth-order scan region
     size_t geom_bytes;
     // image (per pixel / tile)
-    size_t counters, ranges, final_T, n_contrib, tile_lists;
+    size_t counters, ranges, final_T, n_contrib, tile_lists, loss_partial, loss_code;
     size_t image_bytes;
     // binning (point_list per tile instance, the rest per super-tile entry / segment)
     size_t point_list, super_keys, super_vals, alt_keys, alt_vals, bin_radix_hist, bin_radix_hist_scan;
@@ -106,6 +106,8 @@ inline Layout make_layout(int P, int W, int H, int64_t R, int64_t E)
     L.final_T = take(4 * (HW > 0 ? HW : 1));
     L.n_contrib = take(4 * (HW > 0 ? HW : 1));
     L.tile_lists = take(4 * 2 * kWorkClasses * T);  // [fwd | bwd][class][T]
+    L.loss_partial = take(8 * T);                    // fused loss: one double per forward workgroup
+    L.loss_code = take(HW > 0 ? HW : 1);             // fused loss: per-pixel sign / mask code
     L.image_bytes = o;
 
     o = 0;
@@ -182,6 +184,14 @@ struct RenderParams {
     // backward
     const float *dL_dcolor, *dL_dlang;
     float* grad;
+    // fused language-feature loss (null: off).  forward: gt (3 x HW), mask (HW bool bytes) -> codes,
+    // per-workgroup partials, out_loss; backward: dL_dloss (device scalar) with the forward's codes
+    const float* loss_gt;
+    const uint8_t* loss_mask;
+    uint8_t* loss_code;
+    double* loss_partial;
+    float* out_loss;
+    const float* dL_dloss;
 };
 
 hipError_t launch_preprocess(const PreprocessParams& p, hipStream_t s);
@@ -262,6 +272,9 @@ hipError_t launch_decode_language_feature(int H, int W, const int64_t* seg_level
 
 hipError_t launch_render_forward(const RenderParams& p, int tiles, hipStream_t s);
 hipError_t launch_render_backward(const RenderParams& p, int tiles, hipStream_t s);
+// the fused loss's final sum into p.out_loss over the render forward's `tiles` partials; background:
+// first the partials of an empty scene (P == 0: no render forward ran)
+hipError_t launch_loss(const RenderParams& p, int tiles, bool background, hipStream_t s);
 hipError_t render_stats_read(unsigned long long* out, int n);  // reads and clears
 hipError_t render_timeline_read(uint32_t* out, int kernel, int n);
 

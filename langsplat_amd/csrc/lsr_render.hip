@@ -248,10 +248,47 @@ __device__ __forceinline__ void fwd_pixel_blend(FwdPixel& q, float al, uint32_t 
     q.T = go ? test_T : -q.T;
 }
 
-// Output of the tiles without entries among u = j, j + M, ... (background colour, T = 1, no
-// contributors); tiles with entries are skipped (their own workgroups render them).
-__device__ void render_empty_tiles(const RenderParams& p, int j, int M)
+// ---- fused language-feature loss (train.py:96-99: Ll1 = l1_loss(lang * mask, gt * mask)) ----
+// Per pixel: d_c = f_c m - gt_c m (the operations of torch's lang * mask - gt * mask), the pixel's
+// share sum_c |d_c| of the L1 sum, and a code byte for the backward -- bits 2c..2c+1 the sign of d_c
+// (1: +, 2: -, 0: zero), bit 6 the mask -- from which the backward forms autograd's gradient
+// grad * (1 / (3 HW)) * sign(d_c) * m without reading the images again.
+__device__ __forceinline__ uint32_t sign_code(float d) { return d > 0.0f ? 1u : (d < 0.0f ? 2u : 0u); }
+
+__device__ __forceinline__ float loss_pixel(const RenderParams& p, size_t pix, size_t HW, float f0, float f1, float f2)
 {
+    const float m = p.loss_mask[pix] ? 1.0f : 0.0f;
+    const float d0 = f0 * m - p.loss_gt[pix] * m;
+    const float d1 = f1 * m - p.loss_gt[HW + pix] * m;
+    const float d2 = f2 * m - p.loss_gt[2 * HW + pix] * m;
+    p.loss_code[pix] = (uint8_t)(sign_code(d0) | (sign_code(d1) << 2) | (sign_code(d2) << 4) | (m != 0.0f ? 64u : 0u));
+    return fabsf(d0) + fabsf(d1) + fabsf(d2);
+}
+
+// The workgroup's L1 partial (every thread calls it): per-thread floats summed in double in a fixed
+// order into loss_partial[blockIdx.x]; lsr_loss.hip k_loss_finalize adds the partials in block order.
+__device__ __forceinline__ void loss_block_partial(const RenderParams& p, float part)
+{
+    __shared__ double s_lw[kTilePixels / 64];
+    double v = (double)part;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if ((threadIdx.x & 63) == 0) s_lw[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+        for (int w = 0; w < kTilePixels / 64; w++) t += s_lw[w];
+        p.loss_partial[blockIdx.x] = t;
+    }
+}
+
+// Output of the tiles without entries among u = j, j + M, ... (background colour, T = 1, no
+// contributors); tiles with entries are skipped (their own workgroups render them).  kLoss: returns
+// the thread's loss share of those pixels (language image 0 there).
+template <bool kLoss>
+__device__ float render_empty_tiles(const RenderParams& p, int j, int M)
+{
+    float part = 0.0f;
     const int T = p.gx * p.gy;
     const size_t HW = (size_t)p.W * p.H;
     for (int u = j; u < T; u += M) {
@@ -269,10 +306,12 @@ __device__ void render_empty_tiles(const RenderParams& p, int j, int M)
         p.out_lang[pix] = 0.0f;
         p.out_lang[HW + pix] = 0.0f;
         p.out_lang[2 * HW + pix] = 0.0f;
+        if (kLoss) part += loss_pixel(p, pix, HW, 0.0f, 0.0f, 0.0f);
     }
+    return part;
 }
 
-template <bool kStats, bool kFeat>
+template <bool kStats, bool kFeat, bool kLoss>
 __global__ __launch_bounds__(kTilePixels) void k_render_forward(RenderParams p)
 {
     const uint64_t t_start = kStats ? wall_clock64() : 0;
@@ -291,7 +330,8 @@ __global__ __launch_bounds__(kTilePixels) void k_render_forward(RenderParams p)
         tile = scheduled_tile((int)blockIdx.x, p.sched_counts + kCntFwdClass, p.sched_lists, T);
         if (tile < 0) {  // past the tiles with entries: fill the empty ones, strided
             const int listed = -1 - tile;
-            render_empty_tiles(p, (int)blockIdx.x - listed, T - listed);
+            const float part = render_empty_tiles<kLoss>(p, (int)blockIdx.x - listed, T - listed);
+            if (kLoss) loss_block_partial(p, part);
             if (kStats) timeline_put(0, t_start, -1);
             return;
         }
@@ -388,9 +428,10 @@ __global__ __launch_bounds__(kTilePixels) void k_render_forward(RenderParams p)
         if (!ph.stopped && ph.batches) ph.lap(ph.walk);  // the last batch's walk
         timeline_put(0, t_start, tile, ph);
     }
-    if (!inside) return;
     const size_t HW = (size_t)p.W * p.H;
     const size_t pix = (size_t)py * p.W + px;
+    if (kLoss) loss_block_partial(p, inside ? loss_pixel(p, pix, HW, q.C2F0.y, q.F12.x, q.F12.y) : 0.0f);
+    if (!inside) return;
     const float Tf = fabsf(q.T);
     p.final_T[pix] = Tf;
     p.n_contrib[pix] = qlast;
@@ -400,6 +441,60 @@ __global__ __launch_bounds__(kTilePixels) void k_render_forward(RenderParams p)
     p.out_lang[pix] = q.C2F0.y;
     p.out_lang[HW + pix] = q.F12.x;
     p.out_lang[2 * HW + pix] = q.F12.y;
+}
+
+// P == 0: the language image is 0 everywhere; its loss terms, one workgroup per 256 pixels.
+__global__ __launch_bounds__(kTilePixels) void k_loss_background(RenderParams p)
+{
+    const size_t HW = (size_t)p.W * p.H;
+    const size_t pix = (size_t)blockIdx.x * kTilePixels + threadIdx.x;
+    loss_block_partial(p, pix < HW ? loss_pixel(p, pix, HW, 0.0f, 0.0f, 0.0f) : 0.0f);
+}
+
+// Ll1 = (sum of the n workgroup partials, in workgroup order) / (3 HW): one workgroup.
+constexpr int kFinalizeThreads = 1024;
+__global__ __launch_bounds__(kFinalizeThreads) void k_loss_finalize(int n, const double* __restrict__ partial,
+                                                                    int64_t HW, float* __restrict__ loss)
+{
+    __shared__ double s_w[kFinalizeThreads / 64];
+    // thread t sums the contiguous run [t * per, (t + 1) * per): threads in order = partials in order;
+    // kBatch loads in flight before the first add (one memory round trip for n <= 8k partials)
+    constexpr int kBatch = 8;
+    const int per = (n + kFinalizeThreads - 1) / kFinalizeThreads;
+    const int i0 = threadIdx.x * per, e = min(n, (int)(threadIdx.x + 1) * per);
+    double v = 0.0;
+    for (int i = i0; i < e; i += kBatch) {
+        double x[kBatch];
+#pragma unroll
+        for (int k = 0; k < kBatch; k++) x[k] = i + k < e ? partial[i + k] : 0.0;
+#pragma unroll
+        for (int k = 0; k < kBatch; k++) v += x[k];
+    }
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {  // inclusive scan order within the wave: lane 63 = lanes 0..63 in order
+        const double y = __shfl_up(v, o, 64);
+        if ((threadIdx.x & 63) >= o) v += y;
+    }
+    if ((threadIdx.x & 63) == 63) s_w[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+        for (int w = 0; w < kFinalizeThreads / 64; w++) t += s_w[w];
+        *loss = (float)(t / (double)(3 * HW));
+    }
+}
+
+hipError_t launch_loss(const RenderParams& p, int tiles, bool background, hipStream_t s)
+{
+    const int64_t HW = (int64_t)p.W * p.H;
+    int n = tiles;
+    if (background) {
+        n = (int)((HW + kTilePixels - 1) / kTilePixels);
+        hipLaunchKernelGGL(k_loss_background, dim3(n), dim3(kTilePixels), 0, s, p);
+    }
+    hipLaunchKernelGGL(k_loss_finalize, dim3(1), dim3(kFinalizeThreads), 0, s, n, (const double*)p.loss_partial, HW,
+                       p.out_loss);
+    return hipGetLastError();
 }
 
 static bool render_stats_on()
@@ -470,16 +565,21 @@ hipError_t launch_render_forward(const RenderParams& pin, int tiles, hipStream_t
     if (!scheduled()) p.sched_counts = p.sched_lists = nullptr;
     p.prio = p.sched_counts ? prio_levels() : 0;
     const bool feat = p.include_feature != 0;
-    if (render_stats_on()) {
+    const bool loss = feat && p.loss_partial != nullptr;  // one partial per workgroup: the full grid
+    if (render_stats_on() && !loss) {
         tiles = debug_grid(tiles);
         if (feat)
-            hipLaunchKernelGGL((k_render_forward<true, true>), dim3(tiles), dim3(kTilePixels), forward_pad(), s, p);
+            hipLaunchKernelGGL((k_render_forward<true, true, false>), dim3(tiles), dim3(kTilePixels), forward_pad(), s,
+                               p);
         else
-            hipLaunchKernelGGL((k_render_forward<true, false>), dim3(tiles), dim3(kTilePixels), forward_pad(), s, p);
+            hipLaunchKernelGGL((k_render_forward<true, false, false>), dim3(tiles), dim3(kTilePixels), forward_pad(), s,
+                               p);
+    } else if (loss) {
+        hipLaunchKernelGGL((k_render_forward<false, true, true>), dim3(tiles), dim3(kTilePixels), forward_pad(), s, p);
     } else if (feat) {
-        hipLaunchKernelGGL((k_render_forward<false, true>), dim3(tiles), dim3(kTilePixels), forward_pad(), s, p);
+        hipLaunchKernelGGL((k_render_forward<false, true, false>), dim3(tiles), dim3(kTilePixels), forward_pad(), s, p);
     } else {
-        hipLaunchKernelGGL((k_render_forward<false, false>), dim3(tiles), dim3(kTilePixels), forward_pad(), s, p);
+        hipLaunchKernelGGL((k_render_forward<false, false, false>), dim3(tiles), dim3(kTilePixels), forward_pad(), s, p);
     }
     return hipGetLastError();
 }
@@ -579,6 +679,17 @@ __device__ __forceinline__ void bwd_pixel_init(BwdPixel& q, const RenderParams& 
             q.dq0 = p.dL_dlang[pix];
             q.dq1 = p.dL_dlang[HW + pix];
             q.dq2 = p.dL_dlang[2 * HW + pix];
+        }
+        if (kFeat && p.dL_dloss) {  // the fused loss: autograd's mean -> abs -> sub -> mul backward
+            const uint32_t code = p.loss_code[pix];
+            const float gN = p.dL_dloss[0] * (1.0f / (float)(3 * (int64_t)HW));
+            const float m = (code & 64u) ? 1.0f : 0.0f;
+            auto sg = [](uint32_t c) { return c == 1u ? 1.0f : (c == 2u ? -1.0f : 0.0f); };
+            const float t0 = gN * sg(code & 3u) * m, t1 = gN * sg((code >> 2) & 3u) * m;
+            const float t2 = gN * sg((code >> 4) & 3u) * m;
+            q.dq0 = p.dL_dlang ? q.dq0 + t0 : t0;
+            q.dq1 = p.dL_dlang ? q.dq1 + t1 : t1;
+            q.dq2 = p.dL_dlang ? q.dq2 + t2 : t2;
         }
     }
     q.bg_term = kColor ? -q.T_final * fma_(p.bg[2], q.dp2, fma_(p.bg[1], q.dp1, p.bg[0] * q.dp0)) : 0.0f;

@@ -119,7 +119,7 @@ class _RasterizeGaussians(torch.autograd.Function):
 
 
 def rasterize_gaussians_fused(means3D, means2D, features_dc, features_rest, opacity_raw, scaling_raw, rotation_raw,
-                              language_feature_raw, raster_settings, with_visibility=False):
+                              language_feature_raw, raster_settings, with_visibility=False, language_target=None):
     """Fused-activation form of the rasterizer call.
 
     Takes GaussianModel's RAW parameters -- _features_dc (P,1,3), _features_rest (P,M-1,3),
@@ -130,11 +130,25 @@ def rasterize_gaussians_fused(means3D, means2D, features_dc, features_rest, opac
     themselves (include/lsr.h lsr_raw_flags), so those torch passes and their backward kernels
     disappear; gradients come back w.r.t. the raw parameters.  with_visibility=True appends
     render()'s visibility_filter (radii > 0, written by the preprocess kernel).
+
+    language_target=(gt (3,H,W), mask (1,H,W) or (H,W) bool): also returns, last, LangSplat's
+    language loss Ll1 = l1_loss(language_feature_image * mask, gt * mask) (train.py:96-99), computed
+    by the compositing kernel from the pixels it produces; its backward is folded into the render
+    backward's per-pixel seed (no separate loss kernels).
     """
-    color, lang, radii, visible = _RasterizeGaussiansFused.apply(
+    gt = mask = None
+    if language_target is not None:
+        gt, mask = language_target
+        gt = _f32(gt.detach())
+        mask = mask.detach()
+        if mask.dtype != torch.bool:
+            mask = mask != 0
+        mask = mask.contiguous()
+    color, lang, radii, visible, loss = _RasterizeGaussiansFused.apply(
         means3D, means2D, features_dc, features_rest, opacity_raw, scaling_raw, rotation_raw, language_feature_raw,
-        raster_settings)
-    return (color, lang, radii, visible) if with_visibility else (color, lang, radii)
+        raster_settings, gt, mask)
+    out = (color, lang, radii, visible) if with_visibility else (color, lang, radii)
+    return out + (loss,) if language_target is not None else out
 
 
 def _guarded(rs, dump, msg, fn, args):
@@ -153,7 +167,7 @@ def _guarded(rs, dump, msg, fn, args):
 class _RasterizeGaussiansFused(torch.autograd.Function):
     @staticmethod
     def forward(ctx, means3D, means2D, features_dc, features_rest, opacity_raw, scaling_raw, rotation_raw,
-                language_feature_raw, raster_settings):
+                language_feature_raw, raster_settings, loss_target=None, loss_mask=None):
         if means3D.device.type != "cuda":
             raise RuntimeError("langsplat_amd rasterizer: inputs must be on a ROCm GPU device "
                                f"(got {means3D.device}); there is no CPU implementation")
@@ -166,11 +180,18 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
         m3, dc, ln, op, sc, ro = (_f32(means3D), _f32(features_dc), _f32(lang) if use_lang else None,
                                   _f32(opacity_raw), _f32(scaling_raw), _f32(rotation_raw))
         visible = torch.empty((P,), dtype=torch.bool, device=m3.device)  # radii > 0, written by preprocess
+        fuse_loss = loss_target is not None
+        if fuse_loss and not raster_settings.include_feature:
+            raise ValueError("the fused language loss needs include_feature=True")
+        # without the fused loss this output is never handed to the caller (no fill kernel)
+        loss = torch.empty((), dtype=torch.float32, device=m3.device)
         out = _guarded(raster_settings, "snapshot_fw.dump",
                        "\nAn error occured in forward. Please forward snapshot_fw.dump for debugging.",
                        lambda *a: _native.rasterize_gaussians(raster_settings, *a[:8], raw=raw, shs_rest=a[8],
-                                                              visible=a[9]),
-                       (m3, dc, None, ln, op, sc, ro, None, rest, visible))
+                                                              visible=a[9], loss_target=a[10], loss_mask=a[11],
+                                                              out_loss=a[12]),
+                       (m3, dc, None, ln, op, sc, ro, None, rest, visible, loss_target, loss_mask,
+                        loss if fuse_loss else None))
         num_rendered, color, language_feature, radii, geom, binning, image = out
         ctx.raster_settings = raster_settings
         ctx.num_rendered = num_rendered
@@ -180,12 +201,15 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
         empty = torch.empty(0)
         ctx.save_for_backward(m3, dc, rest if rest is not None else empty, ln if ln is not None else empty, op, sc,
                               ro, radii, geom, binning, image)
+        ctx.fuse_loss = fuse_loss
         ctx.mark_non_differentiable(radii, visible)
+        if not fuse_loss:
+            ctx.mark_non_differentiable(loss)
         ctx.set_materialize_grads(False)  # an output off the loss path arrives as None (= zeros)
-        return color, language_feature, radii, visible
+        return color, language_feature, radii, visible, loss
 
     @staticmethod
-    def backward(ctx, grad_out_color, grad_out_language_feature, _grad_radii, _grad_visible):
+    def backward(ctx, grad_out_color, grad_out_language_feature, _grad_radii, _grad_visible, grad_loss=None):
         rs = ctx.raster_settings
         m3, dc, rest, ln, op, sc, ro, radii, geom, binning, image = ctx.saved_tensors
         rest = rest if rest.numel() > 0 else None  # grad_out_color None: zero colour gradient
@@ -194,9 +218,11 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
         g = _guarded(rs, "snapshot_bw.dump",
                      "\nAn error occured in backward. Writing snapshot_bw.dump for debugging.\n",
                      lambda *a: _native.rasterize_gaussians_backward(rs, *a[:14], raw=ctx.raw, shs_rest=a[14],
-                                                                     opacities=a[15], geometry=geometry),
+                                                                     opacities=a[15], geometry=geometry,
+                                                                     grad_loss=a[16]),
                      (m3, dc, None, ln if ctx.use_lang else None, sc, ro, None, radii, grad_out_color, gl,
-                      ctx.num_rendered, geom, binning, image, rest, op))
+                      ctx.num_rendered, geom, binning, image, rest, op,
+                      grad_loss if ctx.fuse_loss and ctx.use_lang else None))
 
         def want(i, t):
             return t if ctx.needs_input_grad[i] else None
@@ -206,7 +232,7 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
             d_rest = torch.zeros(ctx.rest_shape, dtype=torch.float32, device=m3.device)
         return (want(0, g["means3D"]), want(1, g["means2D"]), want(2, g["shs"]), want(3, d_rest),
                 want(4, g["opacities"]), want(5, g["scales"]), want(6, g["rotations"]),
-                want(7, g["language_feature_precomp"] if ctx.use_lang else None), None)
+                want(7, g["language_feature_precomp"] if ctx.use_lang else None), None, None, None)
 
 
 class GaussianRasterizer(nn.Module):

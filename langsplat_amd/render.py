@@ -77,7 +77,12 @@ def _screenspace_points(xyz: torch.Tensor) -> torch.Tensor:
     return z.detach().requires_grad_(True)
 
 
-def render(viewpoint_camera, pc, pipe, bg_color: torch.Tensor, opt, scaling_modifier=1.0, override_color=None):
+def render(viewpoint_camera, pc, pipe, bg_color: torch.Tensor, opt, scaling_modifier=1.0, override_color=None,
+           language_target=None):
+    """gaussian_renderer/__init__.py:19-115.  language_target=(gt, mask) -- what
+    Camera.get_language_feature returns (scene/cameras.py:58-92), e.g. from loss.LanguageFeatureCache
+    -- additionally returns "language_l1" = l1_loss(language_feature_image * mask, gt * mask), the
+    language loss of train.py:96-99, computed inside the rasterizer kernels."""
     screenspace_points = _screenspace_points(pc.get_xyz)
 
     tanfovx = math.tan(viewpoint_camera.FoVx * 0.5)
@@ -101,14 +106,19 @@ def render(viewpoint_camera, pc, pipe, bg_color: torch.Tensor, opt, scaling_modi
 
     if _fusable(pc, pipe, override_color, screenspace_points.device):
         lang_raw = pc.get_language_feature if opt.include_feature else None
-        rendered_image, language_feature_image, radii, visible = rasterize_gaussians_fused(
+        fused = rasterize_gaussians_fused(
             pc.get_xyz, screenspace_points, pc._features_dc, pc._features_rest, pc._opacity, pc._scaling,
-            pc._rotation, lang_raw, raster_settings, with_visibility=True)
-        return {"render": rendered_image,
-                "language_feature_image": language_feature_image,
-                "viewspace_points": screenspace_points,
-                "visibility_filter": visible,  # radii > 0, from the preprocess kernel
-                "radii": radii}
+            pc._rotation, lang_raw, raster_settings, with_visibility=True,
+            language_target=language_target if opt.include_feature else None)
+        rendered_image, language_feature_image, radii, visible = fused[:4]
+        pkg = {"render": rendered_image,
+               "language_feature_image": language_feature_image,
+               "viewspace_points": screenspace_points,
+               "visibility_filter": visible,  # radii > 0, from the preprocess kernel
+               "radii": radii}
+        if language_target is not None:
+            pkg["language_l1"] = fused[4] if opt.include_feature else _l1(language_feature_image, *language_target)
+        return pkg
 
     means3D = pc.get_xyz
     means2D = screenspace_points
@@ -142,8 +152,16 @@ def render(viewpoint_camera, pc, pipe, bg_color: torch.Tensor, opt, scaling_modi
         means3D=means3D, means2D=means2D, shs=shs, colors_precomp=colors_precomp,
         language_feature_precomp=language_feature_precomp, opacities=opacity, scales=scales,
         rotations=rotations, cov3D_precomp=cov3D_precomp)
-    return {"render": rendered_image,
-            "language_feature_image": language_feature_image,
-            "viewspace_points": screenspace_points,
-            "visibility_filter": radii > 0,
-            "radii": radii}
+    pkg = {"render": rendered_image,
+           "language_feature_image": language_feature_image,
+           "viewspace_points": screenspace_points,
+           "visibility_filter": radii > 0,
+           "radii": radii}
+    if language_target is not None:
+        pkg["language_l1"] = _l1(language_feature_image, *language_target)
+    return pkg
+
+
+def _l1(language_feature_image, gt, mask):
+    """train.py:98 with utils/loss_utils.py:17-18, for the paths that do not fuse the loss."""
+    return torch.abs(language_feature_image * mask - gt * mask).mean()

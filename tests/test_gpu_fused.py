@@ -180,3 +180,63 @@ def test_language_step_skips_geometry_gradients(fused, colour, monkeypatch):
     for k in range(2):
         assert_grad_close(f"out{k}", out[False][k].cpu().numpy(), out[True][k].cpu().numpy())
     assert out[False][0].abs().sum() > 0
+
+
+def _language_step(g, cam, gt, mask, fused_loss, monkeypatch, extra=None, geometry_frozen=True):
+    """One language-feature train step (train.py:76-104): render, Ll1, backward."""
+    monkeypatch.setenv("LANGSPLAT_AMD_FUSED", "1")
+    m = _Model(g, DEV)
+    if geometry_frozen:
+        for n in ("xyz", "features_dc", "features_rest", "scaling", "rotation", "opacity"):
+            getattr(m, "_" + n).requires_grad_(False)
+    if fused_loss:
+        pkg = render(cam, m, _Pipe, torch.zeros(3, device=DEV), _Opt, language_target=(gt, mask))
+        loss = pkg["language_l1"]
+    else:
+        pkg = render(cam, m, _Pipe, torch.zeros(3, device=DEV), _Opt)
+        loss = torch.abs(pkg["language_feature_image"] * mask - gt * mask).mean()
+    total = loss if extra is None else loss + (pkg["language_feature_image"] * extra).sum()
+    total.backward()
+    grads = {"language_feature": m._language_feature.grad.detach().cpu().numpy(),
+             "viewspace": pkg["viewspace_points"].grad.detach().cpu().numpy()}
+    if not geometry_frozen:
+        for n in ("xyz", "opacity", "scaling", "rotation", "features_dc"):
+            grads[n] = getattr(m, "_" + n).grad.detach().cpu().numpy()
+    return loss.detach(), pkg["language_feature_image"].detach(), grads
+
+
+@pytest.mark.parametrize("W,H,extra,frozen", [(96, 64, False, True), (67, 45, True, True), (80, 48, False, False)])
+def test_fused_language_loss_matches_torch_loss(W, H, extra, frozen, monkeypatch):
+    """render(..., language_target=(gt, mask))["language_l1"] (loss inside the compositing kernel,
+    its gradient folded into the replay's per-pixel seed) vs the same step with the loss as torch
+    ops on the returned image (train.py:98): same image, loss within summation-order rounding,
+    gradients within the parity tolerance (the render backward's float atomics differ run to run).
+    extra: the language image also feeds a second loss term (the two gradients add)."""
+    g = make_gaussians(1500, seed=10, scale_range=(0.03, 0.2))
+    cam = make_cameras(1, W, H, device=DEV)[0]
+    gen = torch.Generator().manual_seed(W)
+    gt = torch.nn.functional.normalize(torch.randn((3, H, W), generator=gen), dim=0).to(DEV)
+    mask = (torch.rand((1, H, W), generator=gen) < 0.8).to(DEV)
+    ex = (torch.randn((3, H, W), generator=gen) / (3 * H * W)).to(DEV) if extra else None
+    l0, img0, g0 = _language_step(g, cam, gt, mask, False, monkeypatch, ex, frozen)
+    l1, img1, g1 = _language_step(g, cam, gt, mask, True, monkeypatch, ex, frozen)
+    assert torch.equal(img0, img1)
+    torch.testing.assert_close(l1, l0, rtol=2e-6, atol=0)
+    for k in g0:
+        assert_grad_close(k, g1[k], g0[k])
+    assert np.abs(g1["language_feature"]).sum() > 0
+
+
+def test_fused_language_loss_empty_scene(monkeypatch):
+    """P = 0: the language image is all zeros; the loss is mean |0 - gt m|."""
+    W, H = 40, 24
+    g = make_gaussians(0, seed=0)
+    cam = make_cameras(1, W, H, device=DEV)[0]
+    gen = torch.Generator().manual_seed(1)
+    gt = torch.randn((3, H, W), generator=gen).to(DEV)
+    mask = (torch.rand((1, H, W), generator=gen) < 0.5).to(DEV)
+    monkeypatch.setenv("LANGSPLAT_AMD_FUSED", "1")
+    m = _Model(g, DEV)
+    loss = render(cam, m, _Pipe, torch.zeros(3, device=DEV), _Opt, language_target=(gt, mask))["language_l1"]
+    ref = torch.abs(torch.zeros_like(gt) * mask - gt * mask).mean()
+    torch.testing.assert_close(loss, ref, rtol=2e-6, atol=0)
