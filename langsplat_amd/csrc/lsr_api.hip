@@ -104,6 +104,7 @@ struct HostBlock {
     uint32_t stall;
     uint32_t seq;      // the last sequence number used (host side)
     uint32_t bad_segment;  // lsr_decode_language_feature: a segment id outside [-N, N)
+    int32_t depth_passes;  // depth-sort passes the last forward needed (0: none yet)
 };
 
 struct HostBlocks {
@@ -259,7 +260,7 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
             rp.loss_code = reinterpret_cast<uint8_t*>(image + L0.loss_code);
             rp.loss_partial = reinterpret_cast<double*>(image + L0.loss_partial);
             rp.out_loss = a->out_loss;
-            LSR_TRY(launch_loss(rp, 0, true, stream), "loss");
+            LSR_TRY(launch_loss_background(rp, stream), "loss");
         }
         return LSR_OK;
     }
@@ -310,17 +311,23 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
     pp.record = reinterpret_cast<float4*>(geom + L.record);
     pp.counters = counters;
     pp.zero = reinterpret_cast<uint32_t*>(geom + L.scan_regions);
-    pp.zero_words = (int)(kDepthScans * L.scan_region_geom);
+    pp.zero_words = (int)L.zero_words;  // depth-sort scan status and the fused loss's words
     pp.raw = a->raw;
     pp.shs_rest = a->shs_rest;
     pp.partial = reinterpret_cast<uint4*>(geom + L.pre_partial);
     LSR_TRY(launch_preprocess(pp, stream), "preprocess");
 
-    // The one host wait, right after preprocess: num_rendered R and the super-tile entries E size
-    // the binning buffer, and the visible depth-key range fixes the number of sort passes.
+    // The one host wait: num_rendered R and the super-tile entries E size the binning buffer, and
+    // the visible depth-key range fixes the number of depth-sort passes.  The depth sort is enqueued
+    // BEFORE the wait, with this thread's last pass count: it reads the key range on the device, and
+    // any pass count >= the needed one gives the same order (the extra digits are all 0), so the GPU
+    // sorts while the host waits, instead of idling until the host has enqueued the next launch.
+    // Should the range need more passes than guessed, the sort is run again below.
     const uint32_t seq = ++hb->seq == 0 ? ++hb->seq : hb->seq;
     LSR_TRY(launch_publish_counters((P + kPreThreads - 1) / kPreThreads, pp.partial, counters, hb->slot, seq, stream),
             "publish counters");
+    const int guess = hb->depth_passes > 0 ? hb->depth_passes : 4;
+    LSR_TRY(launch_depth_order(P, guess, L, geom, counters, &hb->stall, stream, debug), "depth order");
     LSR_TRY(wait_counters(hb, seq, stream), "wait counters");
     uint32_t host_cnt[8];
     for (int i = 0; i < 8; i++) host_cnt[i] = (uint32_t)hb->slot[i];
@@ -334,7 +341,12 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
         int bits = 0;
         while (bits < 32 && (span >> bits) != 0) bits++;
         const int passes = bits <= 8 ? 1 : (bits + 7) / 8;
-        LSR_TRY(launch_depth_order(P, passes, L, geom, counters, &hb->stall, stream, debug), "depth order");
+        hb->depth_passes = passes;
+        if (passes > guess) {  // the guess was short: clear the sort's scan status and sort again
+            LSR_TRY(hipMemsetAsync(geom + L.scan_regions, 0, 4 * kDepthScans * L.scan_region_geom, stream),
+                    "clear scan status");
+            LSR_TRY(launch_depth_order(P, passes, L, geom, counters, &hb->stall, stream, debug), "depth order");
+        }
     }
 
     L = make_layout(P, W, H, R, (int64_t)host_cnt[kCntSuper]);
@@ -361,11 +373,10 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
         rp.loss_gt = a->loss_target;
         rp.loss_mask = a->loss_mask;
         rp.loss_code = reinterpret_cast<uint8_t*>(image + L.loss_code);
-        rp.loss_partial = reinterpret_cast<double*>(image + L.loss_partial);
+        rp.loss_words = reinterpret_cast<uint64_t*>(geom + L.loss_words);
         rp.out_loss = a->out_loss;
     }
     LSR_TRY(launch_render_forward(rp, L.tiles, stream), "render forward");
-    if (rp.out_loss) LSR_TRY(launch_loss(rp, L.tiles, false, stream), "loss");
     return LSR_OK;
 }
 

@@ -47,6 +47,8 @@ struct Layout {
     size_t depth_key, tiles_touched, rect, record, clamped, sorted_ids, super_offset;
     size_t keys_a, keys_b, vals_b, radix_hist, radix_hist_scan, scan_regions, rect_ranked, pre_partial;
     size_t scan_region_geom;  // u32 words per depth-order scan region
+    size_t loss_words;        // fused loss: per-workgroup / per-group words and tickets, after the scan regions
+    size_t zero_words;        // u32 words preprocess clears from scan_regions (scan status + loss words)
     size_t geom_bytes;
     // image (per pixel / tile)
     size_t counters, ranges, final_T, n_contrib, tile_lists, loss_partial, loss_code;
@@ -85,6 +87,12 @@ inline Layout make_layout(int P, int W, int H, int64_t R, int64_t E)
     L.radix_hist_scan = take(4 * hw_p);  // scans are out-of-place (k_scan's stall fallback)
     L.scan_region_geom = scan_region_words((int64_t)(hw_p > p ? hw_p : p));
     L.scan_regions = take(4 * kDepthScans * L.scan_region_geom);
+    {
+        const size_t gx = (size_t)(W + kTile - 1) / kTile, gy = (size_t)(H + kTile - 1) / kTile;
+        const size_t loss_bytes = 8 * gx * gy;  // one word per render forward workgroup
+        L.loss_words = take(loss_bytes);
+        L.zero_words = (L.loss_words + loss_bytes - L.scan_regions + 3) / 4;
+    }
     L.rect_ranked = take(8 * p);
     L.pre_partial = take(16 * ((p + kPreThreads - 1) / kPreThreads));
     L.geom_bytes = o;
@@ -106,7 +114,7 @@ inline Layout make_layout(int P, int W, int H, int64_t R, int64_t E)
     L.final_T = take(4 * (HW > 0 ? HW : 1));
     L.n_contrib = take(4 * (HW > 0 ? HW : 1));
     L.tile_lists = take(4 * 2 * kWorkClasses * T);  // [fwd | bwd][class][T]
-    L.loss_partial = take(8 * T);                    // fused loss: one double per forward workgroup
+    L.loss_partial = take(8 * T);                    // fused loss, P == 0: one double per workgroup
     L.loss_code = take(HW > 0 ? HW : 1);             // fused loss: per-pixel sign / mask code
     L.image_bytes = o;
 
@@ -189,7 +197,8 @@ struct RenderParams {
     const float* loss_gt;
     const uint8_t* loss_mask;
     uint8_t* loss_code;
-    double* loss_partial;
+    double* loss_partial;     // P == 0 (k_loss_background): one double per workgroup
+    uint64_t* loss_words;     // render forward: words and tickets of loss_block_publish (zeroed)
     float* out_loss;
     const float* dL_dloss;
 };
@@ -272,9 +281,8 @@ hipError_t launch_decode_language_feature(int H, int W, const int64_t* seg_level
 
 hipError_t launch_render_forward(const RenderParams& p, int tiles, hipStream_t s);
 hipError_t launch_render_backward(const RenderParams& p, int tiles, hipStream_t s);
-// the fused loss's final sum into p.out_loss over the render forward's `tiles` partials; background:
-// first the partials of an empty scene (P == 0: no render forward ran)
-hipError_t launch_loss(const RenderParams& p, int tiles, bool background, hipStream_t s);
+// the fused loss of an empty scene (P == 0: no render forward runs) into p.out_loss
+hipError_t launch_loss_background(const RenderParams& p, hipStream_t s);
 hipError_t render_stats_read(unsigned long long* out, int n);  // reads and clears
 hipError_t render_timeline_read(uint32_t* out, int kernel, int n);
 

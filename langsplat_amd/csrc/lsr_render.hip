@@ -265,9 +265,9 @@ __device__ __forceinline__ float loss_pixel(const RenderParams& p, size_t pix, s
     return fabsf(d0) + fabsf(d1) + fabsf(d2);
 }
 
-// The workgroup's L1 partial (every thread calls it): per-thread floats summed in double in a fixed
-// order into loss_partial[blockIdx.x]; lsr_loss.hip k_loss_finalize adds the partials in block order.
-__device__ __forceinline__ void loss_block_partial(const RenderParams& p, float part)
+// The workgroup's L1 share (every thread calls it): per-thread floats summed in double in a fixed
+// order; thread 0 gets it.
+__device__ __forceinline__ double loss_block_sum(float part)
 {
     __shared__ double s_lw[kTilePixels / 64];
     double v = (double)part;
@@ -275,10 +275,64 @@ __device__ __forceinline__ void loss_block_partial(const RenderParams& p, float 
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     if ((threadIdx.x & 63) == 0) s_lw[threadIdx.x >> 6] = v;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        double t = 0.0;
+    double t = 0.0;
+    if (threadIdx.x == 0)
         for (int w = 0; w < kTilePixels / 64; w++) t += s_lw[w];
-        p.loss_partial[blockIdx.x] = t;
+    return t;
+}
+
+// P == 0 path: the partial into loss_partial[blockIdx.x] (k_loss_finalize adds them).
+__device__ __forceinline__ void loss_block_partial(const RenderParams& p, float part)
+{
+    const double t = loss_block_sum(part);
+    if (threadIdx.x == 0) p.loss_partial[blockIdx.x] = t;
+}
+
+// Render forward: each workgroup publishes its share as ONE 64-bit word {1, float} (agent-scope
+// store, coherent across the XCDs' L2s; no atomic, so no workgroup waits for a round trip before it
+// retires).  The LAST workgroup of the grid -- dispatched after every other one, so all of them are
+// resident or done and none depends on it -- waits for every word and adds them in workgroup order
+// (deterministic) into Ll1: no second launch.  The words start at 0 (cleared by preprocess).
+__device__ __forceinline__ void loss_block_publish(const RenderParams& p, float part)
+{
+    __shared__ double s_fw[kTilePixels / 64];
+    const double t = loss_block_sum(part);
+    const int nb = (int)gridDim.x;
+    if (threadIdx.x == 0)
+        __hip_atomic_store(&p.loss_words[blockIdx.x], (1ull << 32) | __float_as_uint((float)t), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    if ((int)blockIdx.x != nb - 1) return;
+    // thread i adds the run [i per, (i + 1) per) in order (threads in order = workgroups in order)
+    const int per = (nb + kTilePixels - 1) / kTilePixels;
+    const int i0 = (int)threadIdx.x * per, e = min(nb, i0 + per);
+    double v = 0.0;
+    constexpr int kBatch = 16;  // loads in flight per round trip
+    for (int i = i0; i < e; i += kBatch) {
+        uint64_t w[kBatch];
+#pragma unroll
+        for (int k = 0; k < kBatch; k++)
+            w[k] = i + k < e ? __hip_atomic_load(&p.loss_words[i + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                             : (1ull << 32);
+#pragma unroll
+        for (int k = 0; k < kBatch; k++) {
+            while ((w[k] >> 32) == 0ull) {
+                __builtin_amdgcn_s_sleep(2);
+                w[k] = __hip_atomic_load(&p.loss_words[i + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            v += (double)__uint_as_float((uint32_t)w[k]);  // padding words add +0
+        }
+    }
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {  // in-order prefix within the wave: lane 63 holds lanes 0..63 in order
+        const double y = __shfl_up(v, o, 64);
+        if ((threadIdx.x & 63) >= o) v += y;
+    }
+    if ((threadIdx.x & 63) == 63) s_fw[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double tot = 0.0;
+        for (int w = 0; w < kTilePixels / 64; w++) tot += s_fw[w];
+        *p.out_loss = (float)(tot / (double)(3 * (int64_t)p.W * p.H));
     }
 }
 
@@ -331,7 +385,7 @@ __global__ __launch_bounds__(kTilePixels) void k_render_forward(RenderParams p)
         if (tile < 0) {  // past the tiles with entries: fill the empty ones, strided
             const int listed = -1 - tile;
             const float part = render_empty_tiles<kLoss>(p, (int)blockIdx.x - listed, T - listed);
-            if (kLoss) loss_block_partial(p, part);
+            if (kLoss) loss_block_publish(p, part);
             if (kStats) timeline_put(0, t_start, -1);
             return;
         }
@@ -430,7 +484,7 @@ __global__ __launch_bounds__(kTilePixels) void k_render_forward(RenderParams p)
     }
     const size_t HW = (size_t)p.W * p.H;
     const size_t pix = (size_t)py * p.W + px;
-    if (kLoss) loss_block_partial(p, inside ? loss_pixel(p, pix, HW, q.C2F0.y, q.F12.x, q.F12.y) : 0.0f);
+    if (kLoss) loss_block_publish(p, inside ? loss_pixel(p, pix, HW, q.C2F0.y, q.F12.x, q.F12.y) : 0.0f);
     if (!inside) return;
     const float Tf = fabsf(q.T);
     p.final_T[pix] = Tf;
@@ -484,14 +538,11 @@ __global__ __launch_bounds__(kFinalizeThreads) void k_loss_finalize(int n, const
     }
 }
 
-hipError_t launch_loss(const RenderParams& p, int tiles, bool background, hipStream_t s)
+hipError_t launch_loss_background(const RenderParams& p, hipStream_t s)
 {
     const int64_t HW = (int64_t)p.W * p.H;
-    int n = tiles;
-    if (background) {
-        n = (int)((HW + kTilePixels - 1) / kTilePixels);
-        hipLaunchKernelGGL(k_loss_background, dim3(n), dim3(kTilePixels), 0, s, p);
-    }
+    const int n = (int)((HW + kTilePixels - 1) / kTilePixels);
+    hipLaunchKernelGGL(k_loss_background, dim3(n), dim3(kTilePixels), 0, s, p);
     hipLaunchKernelGGL(k_loss_finalize, dim3(1), dim3(kFinalizeThreads), 0, s, n, (const double*)p.loss_partial, HW,
                        p.out_loss);
     return hipGetLastError();
@@ -565,7 +616,7 @@ hipError_t launch_render_forward(const RenderParams& pin, int tiles, hipStream_t
     if (!scheduled()) p.sched_counts = p.sched_lists = nullptr;
     p.prio = p.sched_counts ? prio_levels() : 0;
     const bool feat = p.include_feature != 0;
-    const bool loss = feat && p.loss_partial != nullptr;  // one partial per workgroup: the full grid
+    const bool loss = feat && p.loss_words != nullptr;  // one word per workgroup: the full grid
     if (render_stats_on() && !loss) {
         tiles = debug_grid(tiles);
         if (feat)
