@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define LSR_ABI_VERSION 5
+#define LSR_ABI_VERSION 6
 
 enum lsr_status {
     LSR_OK = 0,
@@ -73,6 +73,14 @@ enum lsr_raw_flags {
     LSR_RAW_ROTATIONS = 4,  /* rotations = _rotation:           x / max(||x||, 1e-12) (F.normalize) */
     LSR_RAW_LANGUAGE = 8    /* language_feature = _language_feature: x / (||x|| + 1e-9)             */
 };
+
+/* The language step's backward (no geometry gradient, no colour gradient) accumulates 32-byte
+ * per-Gaussian gradient records that must start at zero.  With LSR_FWD_ZERO_GRAD_RECORDS the
+ * forward clears them inside its compositing kernel (stores beside a VALU-bound loop: no separate
+ * memset launch) in the geometry buffer; the FIRST backward of that forward then passes
+ * LSR_BWD_RECORDS_ZEROED and uses them as they are.  Any other backward clears its own records. */
+enum lsr_forward_flags { LSR_FWD_ZERO_GRAD_RECORDS = 1 };
+enum lsr_backward_flags { LSR_BWD_RECORDS_ZEROED = 1 };
 
 /* GaussianRasterizationSettings (gaussian_renderer/__init__.py:37-51), device-pointer form. */
 typedef struct lsr_settings {
@@ -109,7 +117,7 @@ typedef struct lsr_forward_args {
     float* out_language_feature;     /* 3 x H x W */
     int32_t* radii;                  /* P */
     int32_t raw;                     /* lsr_raw_flags; 0 = activated inputs (reference API) */
-    int32_t reserved;
+    int32_t flags;                   /* lsr_forward_flags */
     const float* shs_rest;           /* NULL, or P x (M-1) x 3 (_features_rest) with shs = P x 1 x 3
                                         (_features_dc): the SH rows without torch.cat
                                         (scene/gaussian_model.py:146-150) */
@@ -161,7 +169,7 @@ typedef struct lsr_backward_args {
     float* dL_dscales;               /* P x 3 or NULL */
     float* dL_drotations;            /* P x 4 or NULL */
     int32_t raw;                     /* as in the forward; gradients are then w.r.t. the raw inputs */
-    int32_t reserved;
+    int32_t flags;                   /* lsr_backward_flags */
     const float* shs_rest;           /* as in the forward */
     float* dL_dsh_rest;              /* P x (M-1) x 3 when shs_rest is set (dL_dsh is then P x 1 x 3) */
     const float* dL_dloss;           /* NULL, or the device scalar dL/d(out_loss) of a forward that fused

@@ -21,9 +21,11 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "liblsr.so")
 
 LSR_BUF_GEOM, LSR_BUF_BINNING, LSR_BUF_IMAGE, LSR_BUF_BACKWARD = 0, 1, 2, 3
-ABI_VERSION = 5
+ABI_VERSION = 6
 # lsr_raw_flags (include/lsr.h): inputs are GaussianModel's raw parameters
 RAW_OPACITY, RAW_SCALES, RAW_ROTATIONS, RAW_LANGUAGE = 1, 2, 4, 8
+FWD_ZERO_GRAD_RECORDS = 1  # lsr_forward_flags
+BWD_RECORDS_ZEROED = 1     # lsr_backward_flags
 _vp = ctypes.c_void_p
 
 
@@ -50,7 +52,7 @@ class LsrForwardArgs(ctypes.Structure):
     _fields_ = [("P", ctypes.c_int32), ("M", ctypes.c_int32)] + [
         (n, _vp) for n in ("means3D", "shs", "colors_precomp", "language_feature", "opacities", "scales",
                            "rotations", "cov3D_precomp", "out_color", "out_language_feature", "radii")
-    ] + [("raw", ctypes.c_int32), ("reserved", ctypes.c_int32), ("shs_rest", _vp), ("visible", _vp),
+    ] + [("raw", ctypes.c_int32), ("flags", ctypes.c_int32), ("shs_rest", _vp), ("visible", _vp),
          ("loss_target", _vp), ("loss_mask", _vp), ("out_loss", _vp)]
 
 
@@ -61,7 +63,7 @@ class LsrBackwardArgs(ctypes.Structure):
                            "geom_buffer", "binning_buffer", "image_buffer", "dL_dmeans2D", "dL_dcolors",
                            "dL_dlanguage_feature", "dL_dopacity", "dL_dmeans3D", "dL_dcov3D", "dL_dsh",
                            "dL_dscales", "dL_drotations")
-    ] + [("raw", ctypes.c_int32), ("reserved", ctypes.c_int32), ("shs_rest", _vp), ("dL_dsh_rest", _vp),
+    ] + [("raw", ctypes.c_int32), ("flags", ctypes.c_int32), ("shs_rest", _vp), ("dL_dsh_rest", _vp),
          ("dL_dloss", _vp)]
 
 
@@ -279,7 +281,7 @@ def _f32c_cached(src: torch.Tensor) -> torch.Tensor:
 
 def rasterize_gaussians(rs, means3D, shs, colors_precomp, language_feature, opacities, scales, rotations,
                         cov3D_precomp, raw=0, shs_rest=None, visible=None, loss_target=None, loss_mask=None,
-                        out_loss=None):
+                        out_loss=None, flags=0):
     """Native forward: returns (num_rendered, color, language_feature_image, radii, geom, binning, image).
 
     raw / shs_rest: the fused-activation form (include/lsr.h lsr_raw_flags); shs is then
@@ -302,6 +304,7 @@ def rasterize_gaussians(rs, means3D, shs, colors_precomp, language_feature, opac
         a.M += int(shs_rest.shape[1])
         a.shs_rest = _ptr(shs_rest)
     a.raw = int(raw)
+    a.flags = int(flags)
     a.means3D = _ptr(means3D)
     a.shs = _ptr(shs)
     a.colors_precomp = _ptr(colors_precomp)
@@ -349,7 +352,8 @@ def geometry_grads_needed(needs_input_grad, geometry_inputs):
 
 def rasterize_gaussians_backward(rs, means3D, shs, colors_precomp, language_feature, scales, rotations,
                                  cov3D_precomp, radii, grad_color, grad_language, num_rendered, geom, binning,
-                                 image, raw=0, shs_rest=None, opacities=None, geometry=True, grad_loss=None):
+                                 image, raw=0, shs_rest=None, opacities=None, geometry=True, grad_loss=None,
+                                 flags=0):
     """Native backward: returns the gradient tensors keyed like the reference's inputs (with raw
     flags: w.r.t. the raw parameters; "shs" is then dL/dfeatures_dc and "shs_rest"
     dL/dfeatures_rest).  geometry=False (no geometry input needs a gradient): only "means2D" and
@@ -399,6 +403,7 @@ def rasterize_gaussians_backward(rs, means3D, shs, colors_precomp, language_feat
     a.language_feature = _ptr(language_feature)
     a.opacities = _ptr(opacities)
     a.raw = int(raw)
+    a.flags = int(flags)
     if split:
         a.shs_rest = _ptr(shs_rest)
         a.dL_dsh_rest = _ptr(g["shs_rest"])

@@ -235,6 +235,7 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
         return fail(LSR_ERR_INVALID, "lsr_forward: settings tensors missing");
     if (a->raw & ~(LSR_RAW_OPACITY | LSR_RAW_SCALES | LSR_RAW_ROTATIONS | LSR_RAW_LANGUAGE))
         return fail(LSR_ERR_INVALID, "lsr_forward: unknown raw flag");
+    if (a->flags & ~LSR_FWD_ZERO_GRAD_RECORDS) return fail(LSR_ERR_INVALID, "lsr_forward: unknown flag");
     if (a->shs_rest && (!a->shs || a->M < 2))
         return fail(LSR_ERR_INVALID, "lsr_forward: shs_rest needs shs (features_dc) and M >= 2");
     if (a->out_loss && (!s->include_feature || (P > 0 && !a->language_feature) || !a->loss_target || !a->loss_mask))
@@ -369,6 +370,10 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
     rp.sched_lists = reinterpret_cast<uint32_t*>(image + L.tile_lists);
     rp.out_color = a->out_color;
     rp.out_lang = a->out_language_feature;
+    if (a->flags & LSR_FWD_ZERO_GRAD_RECORDS) {
+        rp.zero_records = reinterpret_cast<float4*>(geom + L.grad_records);
+        rp.zero_records_n4 = (int64_t)P * kGradStrideLang / 4;
+    }
     if (a->out_loss && rp.include_feature) {
         rp.loss_gt = a->loss_target;
         rp.loss_mask = a->loss_mask;
@@ -397,6 +402,7 @@ int32_t lsr_backward(const lsr_settings* s, const lsr_backward_args* a, lsr_allo
     }
     if (a->raw & ~(LSR_RAW_OPACITY | LSR_RAW_SCALES | LSR_RAW_ROTATIONS | LSR_RAW_LANGUAGE))
         return fail(LSR_ERR_INVALID, "lsr_backward: unknown raw flag");
+    if (a->flags & ~LSR_BWD_RECORDS_ZEROED) return fail(LSR_ERR_INVALID, "lsr_backward: unknown flag");
     if (geometry && a->shs_rest && (!a->shs || a->M < 2 || !a->dL_dsh_rest))
         return fail(LSR_ERR_INVALID, "lsr_backward: shs_rest needs shs, M >= 2 and dL_dsh_rest");
     if ((a->raw & LSR_RAW_OPACITY) && P > 0 && !a->opacities)
@@ -410,12 +416,18 @@ int32_t lsr_backward(const lsr_settings* s, const lsr_backward_args* a, lsr_allo
     char* geom = static_cast<char*>(a->geom_buffer);
     char* image = static_cast<char*>(a->image_buffer);
     char* binning = static_cast<char*>(a->binning_buffer);
-    float* grad = static_cast<float*>(alloc(user, LSR_BUF_BACKWARD, lsr_backward_bytes(P)));
-    if (!grad) return fail(LSR_ERR_ALLOC, "lsr_backward: gradient scratch allocation failed");
-    // the render backward's 5-value form (no geometry, no colour gradient) keeps 32-B records
+    // the render backward's 5-value form (no geometry, no colour gradient) keeps 32-B records; the
+    // first backward of a forward that cleared them (LSR_FWD_ZERO_GRAD_RECORDS) uses them directly
     const bool compact = !geometry && !a->dL_dout_color;
     const int stride = compact ? kGradStrideLang : kGradStride;
-    LSR_TRY(hipMemsetAsync(grad, 0, 4 * (size_t)stride * (size_t)P, stream), "memset grad");
+    float* grad = nullptr;
+    if (compact && (a->flags & LSR_BWD_RECORDS_ZEROED)) {
+        grad = reinterpret_cast<float*>(geom + L.grad_records);
+    } else {
+        grad = static_cast<float*>(alloc(user, LSR_BUF_BACKWARD, lsr_backward_bytes(P)));
+        if (!grad) return fail(LSR_ERR_ALLOC, "lsr_backward: gradient scratch allocation failed");
+        LSR_TRY(hipMemsetAsync(grad, 0, 4 * (size_t)stride * (size_t)P, stream), "memset grad");
+    }
 
     RenderParams rp{};
     rp.W = W;

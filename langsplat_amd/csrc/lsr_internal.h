@@ -49,6 +49,8 @@ struct Layout {
     size_t scan_region_geom;  // u32 words per depth-order scan region
     size_t loss_words;        // fused loss: per-workgroup / per-group words and tickets, after the scan regions
     size_t zero_words;        // u32 words preprocess clears from scan_regions (scan status + loss words)
+    size_t grad_records;      // P x kGradStrideLang floats: the language step's gradient records (cleared
+                              // by the render forward under LSR_FWD_ZERO_GRAD_RECORDS)
     size_t geom_bytes;
     // image (per pixel / tile)
     size_t counters, ranges, final_T, n_contrib, tile_lists, loss_partial, loss_code;
@@ -94,6 +96,7 @@ inline Layout make_layout(int P, int W, int H, int64_t R, int64_t E)
         L.zero_words = (L.loss_words + loss_bytes - L.scan_regions + 3) / 4;
     }
     L.rect_ranked = take(8 * p);
+    L.grad_records = take(4 * kGradStrideLang * p);
     L.pre_partial = take(16 * ((p + kPreThreads - 1) / kPreThreads));
     L.geom_bytes = o;
 
@@ -189,6 +192,8 @@ struct RenderParams {
     uint32_t* sched_lists;
     int prio;  // wave priority by launch position (longest tiles highest), 0: off
     int geo;   // backward: the conic / opacity partials are needed (geometry gradients)
+    float4* zero_records;  // forward: clear these zero_records_n4 float4s (grid-stride), or null
+    int64_t zero_records_n4;
     // backward
     const float *dL_dcolor, *dL_dlang;
     float* grad;

@@ -379,6 +379,12 @@ __global__ __launch_bounds__(kTilePixels) void k_render_forward(RenderParams p)
     __shared__ uint32_t s_last;
 
     const int T = p.gx * p.gy;
+    if (p.zero_records) {  // the backward's gradient records: stores beside the VALU-bound walk
+        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int64_t k = (int64_t)blockIdx.x * kThreads + threadIdx.x; k < p.zero_records_n4;
+             k += (int64_t)gridDim.x * kThreads)
+            p.zero_records[k] = z;
+    }
     int tile = (int)blockIdx.x;
     if (p.sched_counts) {
         tile = scheduled_tile((int)blockIdx.x, p.sched_counts + kCntFwdClass, p.sched_lists, T);

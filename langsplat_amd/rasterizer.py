@@ -69,16 +69,19 @@ class _RasterizeGaussians(torch.autograd.Function):
         lang_in = _f32(lang) if use_lang else None
         args = (_f32(means3D), _f32(sh), _f32(colors_precomp), lang_in, _f32(opacities), _f32(scales),
                 _f32(rotations), _f32(cov3Ds_precomp))
+        # a backward will follow: let the compositing kernel clear its gradient records
+        flags = _native.FWD_ZERO_GRAD_RECORDS if any(ctx.needs_input_grad) else 0
+        ctx.records_zeroed = flags != 0
         if raster_settings.debug:
             cpu_args = _cpu_deep_copy(args)
             try:
-                out = _native.rasterize_gaussians(raster_settings, *args)
+                out = _native.rasterize_gaussians(raster_settings, *args, flags=flags)
             except Exception as ex:
                 torch.save(cpu_args, "snapshot_fw.dump")
                 print("\nAn error occured in forward. Please forward snapshot_fw.dump for debugging.")
                 raise ex
         else:
-            out = _native.rasterize_gaussians(raster_settings, *args)
+            out = _native.rasterize_gaussians(raster_settings, *args, flags=flags)
         num_rendered, color, language_feature, radii, geom, binning, image = out
         ctx.raster_settings = raster_settings
         ctx.num_rendered = num_rendered
@@ -99,16 +102,18 @@ class _RasterizeGaussians(torch.autograd.Function):
         args = (means3D, sh, colors_precomp, lang if ctx.use_lang else None, scales, rotations, cov3Ds_precomp,
                 radii, grad_out_color, gl, ctx.num_rendered, geom, binning, image)
         geometry = _native.geometry_grads_needed(ctx.needs_input_grad, (0, 2, 3, 5, 6, 7, 8))
+        flags = _native.BWD_RECORDS_ZEROED if ctx.records_zeroed else 0
+        ctx.records_zeroed = False  # a second backward (retain_graph) clears its own records
         if rs.debug:
             cpu_args = _cpu_deep_copy(args)
             try:
-                g = _native.rasterize_gaussians_backward(rs, *args, geometry=geometry)
+                g = _native.rasterize_gaussians_backward(rs, *args, geometry=geometry, flags=flags)
             except Exception as ex:
                 torch.save(cpu_args, "snapshot_bw.dump")
                 print("\nAn error occured in backward. Writing snapshot_bw.dump for debugging.\n")
                 raise ex
         else:
-            g = _native.rasterize_gaussians_backward(rs, *args, geometry=geometry)
+            g = _native.rasterize_gaussians_backward(rs, *args, geometry=geometry, flags=flags)
 
         def want(i, t):
             return t if ctx.needs_input_grad[i] else None
@@ -185,11 +190,14 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
             raise ValueError("the fused language loss needs include_feature=True")
         # without the fused loss this output is never handed to the caller (no fill kernel)
         loss = torch.empty((), dtype=torch.float32, device=m3.device)
+        # a backward will follow: let the compositing kernel clear its gradient records
+        flags = _native.FWD_ZERO_GRAD_RECORDS if any(ctx.needs_input_grad) else 0
+        ctx.records_zeroed = flags != 0
         out = _guarded(raster_settings, "snapshot_fw.dump",
                        "\nAn error occured in forward. Please forward snapshot_fw.dump for debugging.",
                        lambda *a: _native.rasterize_gaussians(raster_settings, *a[:8], raw=raw, shs_rest=a[8],
                                                               visible=a[9], loss_target=a[10], loss_mask=a[11],
-                                                              out_loss=a[12]),
+                                                              out_loss=a[12], flags=flags),
                        (m3, dc, None, ln, op, sc, ro, None, rest, visible, loss_target, loss_mask,
                         loss if fuse_loss else None))
         num_rendered, color, language_feature, radii, geom, binning, image = out
@@ -215,11 +223,13 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
         rest = rest if rest.numel() > 0 else None  # grad_out_color None: zero colour gradient
         gl = grad_out_language_feature if ctx.use_lang else None
         geometry = _native.geometry_grads_needed(ctx.needs_input_grad, (0, 2, 3, 4, 5, 6))
+        flags = _native.BWD_RECORDS_ZEROED if ctx.records_zeroed else 0
+        ctx.records_zeroed = False  # a second backward (retain_graph) clears its own records
         g = _guarded(rs, "snapshot_bw.dump",
                      "\nAn error occured in backward. Writing snapshot_bw.dump for debugging.\n",
                      lambda *a: _native.rasterize_gaussians_backward(rs, *a[:14], raw=ctx.raw, shs_rest=a[14],
                                                                      opacities=a[15], geometry=geometry,
-                                                                     grad_loss=a[16]),
+                                                                     grad_loss=a[16], flags=flags),
                      (m3, dc, None, ln if ctx.use_lang else None, sc, ro, None, radii, grad_out_color, gl,
                       ctx.num_rendered, geom, binning, image, rest, op,
                       grad_loss if ctx.fuse_loss and ctx.use_lang else None))

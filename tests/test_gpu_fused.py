@@ -240,3 +240,32 @@ def test_fused_language_loss_empty_scene(monkeypatch):
     loss = render(cam, m, _Pipe, torch.zeros(3, device=DEV), _Opt, language_target=(gt, mask))["language_l1"]
     ref = torch.abs(torch.zeros_like(gt) * mask - gt * mask).mean()
     torch.testing.assert_close(loss, ref, rtol=2e-6, atol=0)
+
+
+@pytest.mark.parametrize("fused_loss", [False, True])
+def test_second_backward_clears_its_own_records(fused_loss, monkeypatch):
+    """The forward clears the language step's gradient records inside its compositing kernel and
+    the first backward uses them as they are (include/lsr.h LSR_FWD_ZERO_GRAD_RECORDS); a second
+    backward over the same graph (retain_graph) must clear its own: same gradients both times."""
+    W, H = 96, 64
+    g = make_gaussians(1500, seed=13, scale_range=(0.03, 0.2))
+    cam = make_cameras(1, W, H, device=DEV)[0]
+    gen = torch.Generator().manual_seed(2)
+    gt = torch.nn.functional.normalize(torch.randn((3, H, W), generator=gen), dim=0).to(DEV)
+    mask = (torch.rand((1, H, W), generator=gen) < 0.8).to(DEV)
+    monkeypatch.setenv("LANGSPLAT_AMD_FUSED", "1")
+    m = _Model(g, DEV)
+    for n in ("xyz", "features_dc", "features_rest", "scaling", "rotation", "opacity"):
+        getattr(m, "_" + n).requires_grad_(False)
+    if fused_loss:
+        loss = render(cam, m, _Pipe, torch.zeros(3, device=DEV), _Opt, language_target=(gt, mask))["language_l1"]
+    else:
+        img = render(cam, m, _Pipe, torch.zeros(3, device=DEV), _Opt)["language_feature_image"]
+        loss = torch.abs(img * mask - gt * mask).mean()
+    loss.backward(retain_graph=True)
+    g1 = m._language_feature.grad.detach().clone()
+    m._language_feature.grad = None
+    loss.backward()
+    g2 = m._language_feature.grad.detach().clone()
+    assert g1.abs().sum() > 0
+    assert_grad_close("second backward", g2.cpu().numpy(), g1.cpu().numpy())
