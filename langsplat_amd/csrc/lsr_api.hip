@@ -342,8 +342,8 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
         int bits = 0;
         while (bits < 32 && (span >> bits) != 0) bits++;
         const int passes = bits <= 8 ? 1 : (bits + 7) / 8;
-        hb->depth_passes = passes;
-        if (passes > guess) {  // the guess was short: clear the sort's scan status and sort again
+        if (depth_order_uses_pass_count(P)) hb->depth_passes = passes;
+        if (depth_order_uses_pass_count(P) && passes > guess) {  // short guess: clear the scan status, sort again
             LSR_TRY(hipMemsetAsync(geom + L.scan_regions, 0, 4 * kDepthScans * L.scan_region_geom, stream),
                     "clear scan status");
             LSR_TRY(launch_depth_order(P, passes, L, geom, counters, &hb->stall, stream, debug), "depth order");

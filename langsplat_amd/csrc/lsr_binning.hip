@@ -312,6 +312,15 @@ __device__ __forceinline__ void super_rect(uint2 rc, int& sx0, int& sy0, int& sx
     sy1 = (y1 + kSuper - 1) / kSuper;
 }
 
+// super-tile entries of a tile rectangle (0 for the empty rectangle of a culled Gaussian)
+__device__ __forceinline__ uint32_t super_count(uint2 rc)
+{
+    if (rc.x == rc.y) return 0u;
+    int sx0, sy0, sx1, sy1;
+    super_rect(rc, sx0, sy0, sx1, sy1);
+    return (uint32_t)((sx1 - sx0) * (sy1 - sy0));
+}
+
 // Optional work of the depth sort's LAST scatter pass, per output rank r (= depth rank): the
 // Gaussian's tile rectangle copied into depth order (the binning's one random gather) and its
 // super-tile entry count (-> exclusive scan = entry offsets); the sorted keys are not stored.
@@ -351,13 +360,25 @@ __device__ __forceinline__ int xcd_tile(int nblk, int remap)
     return x * q + min(x, r) + (i >> 3);
 }
 
+// MSD depth sort (launch_depth_order, P <= kMsdMaxKeys): the pass sorts on the TOP <= 8 bits the
+// visible keys span -- read on the device from kxf (min / max visible key) -- so no host value is
+// needed: bits = bit length of (max - min), digit = (key_xf >> max(bits - 8, 0)) & 0xFF.
+__device__ __forceinline__ void msd_digit(const uint32_t* kxf, int& shift, int& nbits)
+{
+    const uint32_t span = kxf[1] - kxf[0];
+    const int bits = span ? 32 - __clz(span) : 0;
+    shift = bits > 8 ? bits - 8 : 0;
+    nbits = bits - shift;
+}
+
 template <int kItems>
 __global__ __launch_bounds__(kRadixThreads) void k_radix_hist(const uint32_t* __restrict__ keys, int n, int shift,
                                                               int nbits, uint32_t* __restrict__ hist, int nblk,
-                                                              const uint32_t* __restrict__ kxf, int remap)
+                                                              const uint32_t* __restrict__ kxf, int remap, int msd)
 {
     constexpr int kWaves = kRadixThreads / 64;
     __shared__ uint32_t wcnt[kWaves][256];
+    if (msd) msd_digit(kxf, shift, nbits);
     const int blk = xcd_tile(nblk, remap);
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
     const uint32_t mask = (1u << nbits) - 1u;
@@ -398,8 +419,9 @@ template <int kItems>
 __global__ __launch_bounds__(kRadixThreads) void k_radix_scatter(
     const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in, int n, int shift, int nbits,
     const uint32_t* __restrict__ hist, int nblk, uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
-    const uint32_t* __restrict__ kxf, ScatterTail tail, int remap)
+    const uint32_t* __restrict__ kxf, ScatterTail tail, int remap, int msd)
 {
+    if (msd) msd_digit(kxf, shift, nbits);
     const int blk = xcd_tile(nblk, remap);
     constexpr int kTile = kRadixThreads * kItems;
     constexpr int kWaves = kRadixThreads / 64;
@@ -502,13 +524,7 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_scatter(
         const uint32_t o = outp[it];
         vals_out[o] = vid[it];
         tail.rect_ranked[o] = rc[it];
-        uint32_t c = 0;
-        if (rc[it].x != rc[it].y) {  // empty rectangle: culled
-            int sx0, sy0, sx1, sy1;
-            super_rect(rc[it], sx0, sy0, sx1, sy1);
-            c = (uint32_t)((sx1 - sx0) * (sy1 - sy0));
-        }
-        tail.ns[o] = c;
+        tail.ns[o] = super_count(rc[it]);
     }
 }
 
@@ -551,10 +567,10 @@ static hipError_t radix_sort(const uint32_t* k0, const uint32_t* v0, int n, int 
         uint32_t* vout = (pass & 1) ? vA : vB;
         if (small)
             hipLaunchKernelGGL(k_radix_hist<4>, dim3(nblk), dim3(kRadixThreads), 0, s, kin, n, shift, nbits, hist, nblk,
-                               pass == 0 ? kxf : nullptr, remap);
+                               pass == 0 ? kxf : nullptr, remap, 0);
         else
             hipLaunchKernelGGL(k_radix_hist<16>, dim3(nblk), dim3(kRadixThreads), 0, s, kin, n, shift, nbits, hist,
-                               nblk, pass == 0 ? kxf : nullptr, remap);
+                               nblk, pass == 0 ? kxf : nullptr, remap, 0);
         if ((e = post(debug, s)) != hipSuccess) return e;
         if ((e = scan_exclusive(hist, hist_scan, (1 << nbits) * nblk, scan_regions + pass * region_words, nullptr,
                                 stall, s, debug)) != hipSuccess)
@@ -562,10 +578,10 @@ static hipError_t radix_sort(const uint32_t* k0, const uint32_t* v0, int n, int 
         const ScatterTail tail = pass == passes - 1 ? last : ScatterTail{nullptr, nullptr, nullptr};
         if (small)
             hipLaunchKernelGGL(k_radix_scatter<4>, dim3(nblk), dim3(kRadixThreads), 0, s, kin, vin, n, shift, nbits,
-                               hist_scan, nblk, kout, vout, pass == 0 ? kxf : nullptr, tail, remap);
+                               hist_scan, nblk, kout, vout, pass == 0 ? kxf : nullptr, tail, remap, 0);
         else
             hipLaunchKernelGGL(k_radix_scatter<16>, dim3(nblk), dim3(kRadixThreads), 0, s, kin, vin, n, shift, nbits,
-                               hist_scan, nblk, kout, vout, pass == 0 ? kxf : nullptr, tail, remap);
+                               hist_scan, nblk, kout, vout, pass == 0 ? kxf : nullptr, tail, remap, 0);
         if ((e = post(debug, s)) != hipSuccess) return e;
         kin = kout;
         vin = vout;
@@ -617,6 +633,249 @@ __device__ __forceinline__ uint64_t transpose64(uint64_t x)
     return x;
 }
 
+// ---------------------------------------------------------------- MSD depth sort: bucket pass
+//
+// Depth order for P <= kMsdMaxKeys: ONE stable radix pass on the top <= 8 bits of the key range
+// (k_radix_hist / scan / k_radix_scatter with msd = 1) puts every key in its bucket in id order;
+// then one workgroup per bucket sorts the bucket on the remaining low bits in LDS (stable LSD
+// passes of 8 bits, wave64 ballot ranking) and writes the depth-order outputs (sorted ids, the
+// rectangle in depth order, super-tile entry counts).  Same (key, id) order as the LSD sort: four
+// kernels instead of up to twelve.  A bucket larger than LDS (kBucketCap keys: a depth range
+// dense far beyond the average) is sorted by its workgroup in global memory, 1024 keys at a time.
+constexpr int kBucketThreads = 1024;
+constexpr int kBucketWaves = kBucketThreads / 64;
+constexpr int kBucketCap = 8192;
+constexpr int kBucketRounds = kBucketCap / kBucketThreads;  // rounds of 64 keys per wave
+constexpr int64_t kMsdMaxKeys = 2000000;                    // above: expected buckets exceed LDS
+
+struct BucketLds {
+    uint32_t k[2][kBucketCap];
+    uint32_t v[2][kBucketCap];
+    uint32_t wcnt[kBucketWaves][256];  // per wave: running digit counts, then the wave's offset in the digit
+    uint32_t dstart[256];              // digit starts (LDS passes) / running digit bases (global passes)
+    uint32_t ctot[256];                // global passes: the chunk's digit totals
+    uint32_t wsum[kBucketWaves];
+};
+constexpr size_t kBucketLdsBytes = sizeof(BucketLds);
+
+// exclusive scan of v over the first 256 threads (4 waves); every thread of the block must call it
+__device__ __forceinline__ uint32_t scan256(uint32_t v, uint32_t* wsum)
+{
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (t < 256 && lane == 63) wsum[w] = x;
+    __syncthreads();
+    uint32_t before = 0;
+    for (int i = 0; i < w && i < 4; i++) before += wsum[i];
+    __syncthreads();
+    return before + x - v;
+}
+
+// One stable pass of the LDS sort: (k, v)[src] -> [dst] by digit (k >> sh) & mask.  Wave w owns
+// keys [w R 64, (w + 1) R 64) and ranks them round by round (ballot match + the wave's running
+// digit counts), then the per-digit wave offsets and digit starts place every key.
+__device__ void bucket_lds_pass(BucketLds& L, int src, int nb, int sh, int nbits)
+{
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+    const uint32_t mask = (1u << nbits) - 1u;
+    for (int i = t; i < kBucketWaves * 256; i += kBucketThreads) (&L.wcnt[0][0])[i] = 0u;
+    __syncthreads();
+    uint32_t key[kBucketRounds], val[kBucketRounds], rank[kBucketRounds];
+#pragma unroll
+    for (int r = 0; r < kBucketRounds; r++) {
+        const int idx = (w * kBucketRounds + r) * 64 + lane;
+        const bool valid = idx < nb;
+        key[r] = valid ? L.k[src][idx] : 0u;
+        val[r] = valid ? L.v[src][idx] : 0u;
+        const uint32_t d = (key[r] >> sh) & mask;
+        const uint64_t peers = match_digit(d, valid, nbits);
+        const uint32_t rr = (uint32_t)__popcll(peers & lanemask_lt());
+        const uint32_t c = L.wcnt[w][d];
+        rank[r] = c + rr;
+        if (valid && rr == 0) L.wcnt[w][d] = c + (uint32_t)__popcll(peers);
+    }
+    __syncthreads();
+    uint32_t tot = 0;
+    if (t < 256) {
+        for (int i = 0; i < kBucketWaves; i++) {
+            const uint32_t c = L.wcnt[i][t];
+            L.wcnt[i][t] = tot;
+            tot += c;
+        }
+    }
+    const uint32_t ex = scan256(tot, L.wsum);
+    if (t < 256) L.dstart[t] = ex;
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kBucketRounds; r++) {
+        const int idx = (w * kBucketRounds + r) * 64 + lane;
+        if (idx < nb) {
+            const uint32_t d = (key[r] >> sh) & mask;
+            const uint32_t pos = L.dstart[d] + L.wcnt[w][d] + rank[r];
+            L.k[src ^ 1][pos] = key[r];
+            L.v[src ^ 1][pos] = val[r];
+        }
+    }
+    __syncthreads();
+}
+
+// Bucket too large for LDS: the same stable passes through global memory, 1024 keys at a time
+// (digit bases from a histogram of the whole bucket, advanced chunk by chunk).  (k0, v0) holds the
+// bucket; (k1, v1) is scratch of the same size.  Returns the buffer index holding the result.
+__device__ int bucket_global_sort(BucketLds& L, uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, int nb,
+                                  int lowbits)
+{
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+    uint32_t* K[2] = {k0, k1};
+    uint32_t* V[2] = {v0, v1};
+    int src = 0;
+    for (int sh = 0; sh < lowbits; sh += 8) {
+        const int nbits = min(8, lowbits - sh);
+        const uint32_t mask = (1u << nbits) - 1u;
+        if (t < 256) L.ctot[t] = 0u;
+        __syncthreads();
+        for (int i = t; i < nb; i += kBucketThreads) atomicAdd(&L.ctot[(K[src][i] >> sh) & mask], 1u);
+        __syncthreads();
+        const uint32_t ex = scan256(t < 256 ? L.ctot[t] : 0u, L.wsum);
+        if (t < 256) L.dstart[t] = ex;
+        __syncthreads();
+        for (int c0 = 0; c0 < nb; c0 += kBucketThreads) {
+            const int idx = c0 + t;
+            const bool valid = idx < nb;
+            const uint32_t key = valid ? K[src][idx] : 0u, val = valid ? V[src][idx] : 0u;
+            const uint32_t d = (key >> sh) & mask;
+            const uint64_t peers = match_digit(d, valid, nbits);
+            const uint32_t rr = (uint32_t)__popcll(peers & lanemask_lt());
+            for (int i = t; i < kBucketWaves * 256; i += kBucketThreads) (&L.wcnt[0][0])[i] = 0u;
+            __syncthreads();
+            if (valid && rr == 0) L.wcnt[w][d] = (uint32_t)__popcll(peers);
+            __syncthreads();
+            if (t < 256) {
+                uint32_t run = 0;
+                for (int i = 0; i < kBucketWaves; i++) {
+                    const uint32_t c = L.wcnt[i][t];
+                    L.wcnt[i][t] = run;
+                    run += c;
+                }
+                L.ctot[t] = run;
+            }
+            __syncthreads();
+            if (valid) {
+                const uint32_t pos = L.dstart[d] + L.wcnt[w][d] + rr;
+                K[src ^ 1][pos] = key;
+                V[src ^ 1][pos] = val;
+            }
+            __syncthreads();
+            if (t < 256) L.dstart[t] += L.ctot[t];
+            __syncthreads();
+        }
+        src ^= 1;
+        (void)lane;
+    }
+    return src;
+}
+
+// One workgroup per bucket (top-digit value).  keys / ids: the MSD pass's output (transformed keys,
+// bucket-contiguous, id order inside a bucket); hist_scan: its scanned [digit][block] histogram,
+// whose digit starts are the bucket ranges.  Writes sorted_ids, rect_ranked and the super-tile
+// entry counts ns for every position of the bucket.  scratch_k is P words of scratch for the
+// global fallback (its ids go through sorted_ids itself).
+__global__ __launch_bounds__(kBucketThreads) void k_depth_bucket_sort(
+    int n, uint32_t* __restrict__ keys, uint32_t* __restrict__ ids, const uint32_t* __restrict__ hist_scan, int nblk,
+    const uint32_t* __restrict__ kxf, const uint2* __restrict__ rect, uint32_t* __restrict__ sorted_ids,
+    uint2* __restrict__ rect_ranked, uint32_t* __restrict__ ns, uint32_t* __restrict__ scratch_k)
+{
+    extern __shared__ uint4 s_bucket_raw[];
+    BucketLds& L = *reinterpret_cast<BucketLds*>(s_bucket_raw);
+    int shift, nbits;
+    msd_digit(kxf, shift, nbits);
+    const int d = (int)blockIdx.x;
+    if (d >= (1 << nbits)) return;  // no such top digit
+    const uint32_t start = hist_scan[(size_t)d * nblk];
+    const uint32_t end = d + 1 < (1 << nbits) ? hist_scan[(size_t)(d + 1) * nblk] : (uint32_t)n;
+    const int nb = (int)(end - start);
+    if (nb <= 0) return;
+    const int t = threadIdx.x;
+    const int lowbits = shift;  // the bits below the top digit (equal top digits inside a bucket)
+    auto emit = [&](int i, uint32_t id) {
+        const uint32_t o = start + (uint32_t)i;
+        const uint2 rc = rect[id];
+        sorted_ids[o] = id;
+        rect_ranked[o] = rc;
+        ns[o] = super_count(rc);
+    };
+    if (nb <= kBucketCap) {
+        {  // every load in flight before the first LDS store (one memory round trip)
+            uint32_t k[kBucketRounds], v[kBucketRounds];
+#pragma unroll
+            for (int r = 0; r < kBucketRounds; r++) {
+                const int i = t + r * kBucketThreads;
+                k[r] = i < nb ? keys[start + i] : 0u;
+                v[r] = i < nb ? ids[start + i] : 0u;
+            }
+#pragma unroll
+            for (int r = 0; r < kBucketRounds; r++) {
+                const int i = t + r * kBucketThreads;
+                if (i < nb) {
+                    L.k[0][i] = k[r];
+                    L.v[0][i] = v[r];
+                }
+            }
+        }
+        __syncthreads();
+        int src = 0;
+        for (int sh = 0; sh < lowbits; sh += 8) {
+            bucket_lds_pass(L, src, nb, sh, min(8, lowbits - sh));
+            src ^= 1;
+        }
+        // outputs: all rectangle gathers in flight at once
+        uint32_t id[kBucketRounds];
+        uint2 rc[kBucketRounds];
+#pragma unroll
+        for (int r = 0; r < kBucketRounds; r++) {
+            const int i = t + r * kBucketThreads;
+            id[r] = i < nb ? L.v[src][i] : 0u;
+        }
+#pragma unroll
+        for (int r = 0; r < kBucketRounds; r++) rc[r] = t + r * kBucketThreads < nb ? rect[id[r]] : make_uint2(0u, 0u);
+#pragma unroll
+        for (int r = 0; r < kBucketRounds; r++) {
+            const int i = t + r * kBucketThreads;
+            if (i < nb) {
+                const uint32_t o = start + (uint32_t)i;
+                sorted_ids[o] = id[r];
+                rect_ranked[o] = rc[r];
+                ns[o] = super_count(rc[r]);
+            }
+        }
+        return;
+    }
+    // beyond LDS: global passes between (keys, ids) and (scratch_k, sorted_ids) over the bucket
+    const int res = bucket_global_sort(L, keys + start, ids + start, scratch_k + start, sorted_ids + start, nb,
+                                       lowbits);
+    const uint32_t* rid = res ? sorted_ids + start : ids + start;
+    for (int i = t; i < nb; i += kBucketThreads) emit(i, rid[i]);  // same position: in place when rid aliases
+}
+
+static hipError_t allow_bucket_lds()
+{
+    static const hipError_t e = hipFuncSetAttribute((const void*)k_depth_bucket_sort,
+                                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)kBucketLdsBytes);
+    return e;
+}
+
+// LSR_DEPTH_LSD=1 forces the LSD passes at any P (measurement / test knob, read per call)
+bool depth_order_uses_pass_count(int P)
+{
+    const char* e = getenv("LSR_DEPTH_LSD");
+    return P > kMsdMaxKeys || (e && e[0] == '1');
+}
+
 // ---------------------------------------------------------------- depth order + super-tile counts
 
 hipError_t launch_depth_order(int P, int passes, const Layout& L, char* geom, uint32_t* counters, uint32_t* stall,
@@ -639,6 +898,38 @@ hipError_t launch_depth_order(int P, int passes, const Layout& L, char* geom, ui
     // free: the per-rank super-tile entry counts go there and are scanned into super_offset
     const ScatterTail tail{reinterpret_cast<const uint2*>(geom + L.rect), reinterpret_cast<uint2*>(geom + L.rect_ranked),
                            ka};
+    const uint32_t* kxf = counters + kCntKeyMin;
+    if (!depth_order_uses_pass_count(P)) {  // MSD pass + per-bucket LDS sort; `passes` is not used
+        hipError_t e = allow_bucket_lds();
+        if (e != hipSuccess) return e;
+        static const int remap = [] {
+            const char* v = getenv("LSR_XCD_REMAP");
+            return v && v[0] == '0' ? 0 : 1;
+        }();
+        const bool small = radix_small(P);
+        const int nblk = (P + kRadixThreads * (small ? 4 : 16) - 1) / (kRadixThreads * (small ? 4 : 16));
+        if (small)
+            hipLaunchKernelGGL(k_radix_hist<4>, dim3(nblk), dim3(kRadixThreads), 0, s, keys, P, 0, 8, hist, nblk, kxf,
+                               remap, 1);
+        else
+            hipLaunchKernelGGL(k_radix_hist<16>, dim3(nblk), dim3(kRadixThreads), 0, s, keys, P, 0, 8, hist, nblk, kxf,
+                               remap, 1);
+        if ((e = post(debug, s)) != hipSuccess) return e;
+        if ((e = scan_exclusive(hist, hist_scan, 256 * nblk, regions, nullptr, stall, s, debug)) != hipSuccess)
+            return e;
+        const ScatterTail none{nullptr, nullptr, nullptr};
+        if (small)
+            hipLaunchKernelGGL(k_radix_scatter<4>, dim3(nblk), dim3(kRadixThreads), 0, s, keys, (const uint32_t*)nullptr,
+                               P, 0, 8, hist_scan, nblk, kb, vb, kxf, none, remap, 1);
+        else
+            hipLaunchKernelGGL(k_radix_scatter<16>, dim3(nblk), dim3(kRadixThreads), 0, s, keys,
+                               (const uint32_t*)nullptr, P, 0, 8, hist_scan, nblk, kb, vb, kxf, none, remap, 1);
+        if ((e = post(debug, s)) != hipSuccess) return e;
+        hipLaunchKernelGGL(k_depth_bucket_sort, dim3(256), dim3(kBucketThreads), kBucketLdsBytes, s, P, kb, vb,
+                           (const uint32_t*)hist_scan, nblk, kxf, tail.rect, va, tail.rect_ranked, ka, ka);
+        if ((e = post(debug, s)) != hipSuccess) return e;
+        return scan_exclusive(ka, off, P, regions + L.scan_region_geom, counters + kCntSuper, stall, s, debug);
+    }
     hipError_t e = (passes & 1)
         ? radix_sort(keys, nullptr, P, 8 * passes, kb, vb, ka, va, hist, hist_scan, regions, L.scan_region_geom, stall,
                      s, debug, &done, counters + kCntKeyMin, tail)

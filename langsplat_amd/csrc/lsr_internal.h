@@ -220,6 +220,9 @@ hipError_t launch_mark_visible(int P, const float* means, const float* view, con
 // super-tile entry offsets in that order
 hipError_t launch_depth_order(int P, int passes, const Layout& L, char* geom, uint32_t* counters, uint32_t* stall,
                               hipStream_t s, bool debug);
+// false: the depth order reads its pass count on the device (MSD pass + per-bucket LDS sort) and
+// ignores `passes`; true (large P): LSD passes, `passes` must cover the visible key range
+bool depth_order_uses_pass_count(int P);
 // super-tile lists, per-(tile, segment) counts, scanned bases -> point_list and tile ranges
 hipError_t launch_binning(int P, int64_t R, const Layout& L, char* geom, char* image, char* binning, uint32_t* stall,
                           hipStream_t s, bool debug);

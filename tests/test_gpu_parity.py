@@ -331,18 +331,27 @@ def test_full_size_properties(cfg):
         assert (lhs - rhs).abs().max().item() <= 1e-3 * scale, k
 
 
-@pytest.mark.parametrize("kind", ["wide", "narrow", "ties"])
-def test_depth_sort_pass_counts(kind):
-    """The depth sort radix-sorts only the bits the visible keys span (key - min): a depth range
-    of 0.3..80 needs 4 passes, a sliver 1 pass, exact ties 1 pass and fall back to id order.  The
-    per-tile order (and everything downstream) must stay bit-identical to the oracle's."""
-    g = torch.Generator().manual_seed({"wide": 31, "narrow": 32, "ties": 33}[kind])
-    P, W, H = 3000, 96, 64
+@pytest.mark.parametrize("lsd", [False, True])
+@pytest.mark.parametrize("kind", ["wide", "narrow", "ties", "cluster"])
+def test_depth_sort_pass_counts(kind, lsd, monkeypatch):
+    """The depth sort orders only the bits the visible keys span (key - min): a depth range of
+    0.3..80 spans 27 bits, a sliver 12, exact ties none (id order).  cluster: 20k of 30k Gaussians
+    within 1e-3 of one depth, the rest over 0.5..50 -- one top-digit bucket far larger than the
+    MSD sort's LDS capacity (its global fallback).  The per-tile order (and everything downstream)
+    must stay bit-identical to the oracle's.  lsd: the LSD passes large P uses (LSR_DEPTH_LSD=1),
+    with the host's pass count: 4 passes, 2, none."""
+    if lsd:
+        monkeypatch.setenv("LSR_DEPTH_LSD", "1")
+    g = torch.Generator().manual_seed({"wide": 31, "narrow": 32, "ties": 33, "cluster": 34}[kind])
+    P, W, H = (30000, 160, 120) if kind == "cluster" else (3000, 96, 64)
     cam = make_cameras(1, W, H)[0]  # at (0, 0, -4) looking along +z: view depth = z + 4
     if kind == "wide":
         d = torch.exp(torch.rand(P, generator=g) * (math.log(80.0) - math.log(0.3)) + math.log(0.3))
     elif kind == "narrow":
         d = 4.0 + torch.rand(P, generator=g) * 1e-3
+    elif kind == "cluster":
+        d = torch.exp(torch.rand(P, generator=g) * (math.log(50.0) - math.log(0.5)) + math.log(0.5))
+        d[torch.randperm(P, generator=g)[:20000]] = 4.0 + torch.rand(20000, generator=g) * 1e-3
     else:
         d = torch.full((P,), 4.0)
     u, v = torch.rand(P, generator=g) * 2 - 1, torch.rand(P, generator=g) * 2 - 1

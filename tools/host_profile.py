@@ -16,7 +16,6 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 import bench  # noqa: E402
-from langsplat_amd.loss import masked_l1_loss  # noqa: E402
 from langsplat_amd.optim import Adam as AmdAdam  # noqa: E402
 from langsplat_amd.render import render  # noqa: E402
 from langsplat_amd.synthetic import CONFIGS, make_cameras, make_gaussians  # noqa: E402
@@ -37,8 +36,7 @@ def main():
                     eps=1e-15)
 
     def step():
-        pkg = render(cam, model, bench.Pipe, bg, bench.Opt)
-        loss = masked_l1_loss(pkg["language_feature_image"], gt, mask)
+        loss = render(cam, model, bench.Pipe, bg, bench.Opt, language_target=(gt, mask))["language_l1"]
         loss.backward()
         optim.step()
         optim.zero_grad(set_to_none=True)
