@@ -780,35 +780,61 @@ __device__ int bucket_global_sort(BucketLds& L, uint32_t* k0, uint32_t* v0, uint
     return src;
 }
 
+// Exclusive scan of one value per thread over a kBucketThreads workgroup (every thread calls it);
+// *total receives the sum.
+__device__ __forceinline__ uint32_t scan1024(uint32_t v, uint32_t* wsum, uint32_t* total)
+{
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    uint32_t before = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < kBucketWaves; i++) {
+        const uint32_t c = wsum[i];
+        before += i < w ? c : 0u;
+        tot += c;
+    }
+    __syncthreads();
+    *total = tot;
+    return before + x - v;
+}
+
 // One workgroup per bucket (top-digit value).  keys / ids: the MSD pass's output (transformed keys,
 // bucket-contiguous, id order inside a bucket); hist_scan: its scanned [digit][block] histogram,
-// whose digit starts are the bucket ranges.  Writes sorted_ids, rect_ranked and the super-tile
-// entry counts ns for every position of the bucket.  scratch_k is P words of scratch for the
-// global fallback (its ids go through sorted_ids itself).
+// whose digit starts are the bucket ranges.  Writes, for every position of the bucket, the sorted
+// id, the depth-ordered rectangle and the BUCKET-LOCAL exclusive prefix of the super-tile entry
+// counts (local_off), and the bucket's total entry count (totals[d], 0 for empty buckets):
+// k_emit_super adds the scanned bucket totals, so no separate P-long scan is launched.  scratch_k
+// is P words of scratch for the global fallback (whose ids go through sorted_ids itself).
 __global__ __launch_bounds__(kBucketThreads) void k_depth_bucket_sort(
     int n, uint32_t* __restrict__ keys, uint32_t* __restrict__ ids, const uint32_t* __restrict__ hist_scan, int nblk,
     const uint32_t* __restrict__ kxf, const uint2* __restrict__ rect, uint32_t* __restrict__ sorted_ids,
-    uint2* __restrict__ rect_ranked, uint32_t* __restrict__ ns, uint32_t* __restrict__ scratch_k)
+    uint2* __restrict__ rect_ranked, uint32_t* __restrict__ local_off, uint32_t* __restrict__ totals,
+    uint32_t* __restrict__ scratch_k)
 {
     extern __shared__ uint4 s_bucket_raw[];
     BucketLds& L = *reinterpret_cast<BucketLds*>(s_bucket_raw);
     int shift, nbits;
     msd_digit(kxf, shift, nbits);
     const int d = (int)blockIdx.x;
-    if (d >= (1 << nbits)) return;  // no such top digit
-    const uint32_t start = hist_scan[(size_t)d * nblk];
-    const uint32_t end = d + 1 < (1 << nbits) ? hist_scan[(size_t)(d + 1) * nblk] : (uint32_t)n;
-    const int nb = (int)(end - start);
-    if (nb <= 0) return;
     const int t = threadIdx.x;
+    uint32_t start = 0, end = 0;
+    if (d < (1 << nbits)) {
+        start = hist_scan[(size_t)d * nblk];
+        end = d + 1 < (1 << nbits) ? hist_scan[(size_t)(d + 1) * nblk] : (uint32_t)n;
+    }
+    const int nb = (int)(end - start);
+    if (nb <= 0) {  // no such top digit, or no key in it
+        if (t == 0) totals[d] = 0u;
+        return;
+    }
     const int lowbits = shift;  // the bits below the top digit (equal top digits inside a bucket)
-    auto emit = [&](int i, uint32_t id) {
-        const uint32_t o = start + (uint32_t)i;
-        const uint2 rc = rect[id];
-        sorted_ids[o] = id;
-        rect_ranked[o] = rc;
-        ns[o] = super_count(rc);
-    };
     if (nb <= kBucketCap) {
         {  // every load in flight before the first LDS store (one memory round trip)
             uint32_t k[kBucketRounds], v[kBucketRounds];
@@ -833,7 +859,9 @@ __global__ __launch_bounds__(kBucketThreads) void k_depth_bucket_sort(
             bucket_lds_pass(L, src, nb, sh, min(8, lowbits - sh));
             src ^= 1;
         }
-        // outputs: all rectangle gathers in flight at once
+        // outputs: all rectangle gathers in flight at once; the entry counts go through LDS (the
+        // free key buffer) so that each thread scans a contiguous run of kBucketRounds of them
+        uint32_t* X = L.k[src ^ 1];
         uint32_t id[kBucketRounds];
         uint2 rc[kBucketRounds];
 #pragma unroll
@@ -850,8 +878,31 @@ __global__ __launch_bounds__(kBucketThreads) void k_depth_bucket_sort(
                 const uint32_t o = start + (uint32_t)i;
                 sorted_ids[o] = id[r];
                 rect_ranked[o] = rc[r];
-                ns[o] = super_count(rc[r]);
+                X[i] = super_count(rc[r]);
             }
+        }
+        __syncthreads();
+        uint32_t c[kBucketRounds], run = 0;
+#pragma unroll
+        for (int k = 0; k < kBucketRounds; k++) {
+            const int j = kBucketRounds * t + k;
+            c[k] = j < nb ? X[j] : 0u;
+            run += c[k];
+        }
+        uint32_t tot;
+        uint32_t acc = scan1024(run, L.wsum, &tot);
+#pragma unroll
+        for (int k = 0; k < kBucketRounds; k++) {
+            const int j = kBucketRounds * t + k;
+            if (j < nb) X[j] = acc;
+            acc += c[k];
+        }
+        if (t == 0) totals[d] = tot;
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < kBucketRounds; r++) {
+            const int i = t + r * kBucketThreads;
+            if (i < nb) local_off[start + i] = X[i];
         }
         return;
     }
@@ -859,7 +910,23 @@ __global__ __launch_bounds__(kBucketThreads) void k_depth_bucket_sort(
     const int res = bucket_global_sort(L, keys + start, ids + start, scratch_k + start, sorted_ids + start, nb,
                                        lowbits);
     const uint32_t* rid = res ? sorted_ids + start : ids + start;
-    for (int i = t; i < nb; i += kBucketThreads) emit(i, rid[i]);  // same position: in place when rid aliases
+    uint32_t carry = 0;
+    for (int c0 = 0; c0 < nb; c0 += kBucketThreads) {  // in order, 1024 positions at a time
+        const int i = c0 + t;
+        uint32_t cnt = 0;
+        if (i < nb) {
+            const uint32_t g = rid[i];
+            const uint2 rc = rect[g];
+            sorted_ids[start + i] = g;  // in place when rid aliases sorted_ids
+            rect_ranked[start + i] = rc;
+            cnt = super_count(rc);
+        }
+        uint32_t tot;
+        const uint32_t ex = scan1024(cnt, L.wsum, &tot);
+        if (i < nb) local_off[start + i] = carry + ex;
+        carry += tot;
+    }
+    if (t == 0) totals[d] = carry;
 }
 
 static hipError_t allow_bucket_lds()
@@ -925,10 +992,11 @@ hipError_t launch_depth_order(int P, int passes, const Layout& L, char* geom, ui
             hipLaunchKernelGGL(k_radix_scatter<16>, dim3(nblk), dim3(kRadixThreads), 0, s, keys,
                                (const uint32_t*)nullptr, P, 0, 8, hist_scan, nblk, kb, vb, kxf, none, remap, 1);
         if ((e = post(debug, s)) != hipSuccess) return e;
+        // bucket-local offsets into super_offset, bucket totals for k_emit_super (no P-long scan)
         hipLaunchKernelGGL(k_depth_bucket_sort, dim3(256), dim3(kBucketThreads), kBucketLdsBytes, s, P, kb, vb,
-                           (const uint32_t*)hist_scan, nblk, kxf, tail.rect, va, tail.rect_ranked, ka, ka);
-        if ((e = post(debug, s)) != hipSuccess) return e;
-        return scan_exclusive(ka, off, P, regions + L.scan_region_geom, counters + kCntSuper, stall, s, debug);
+                           (const uint32_t*)hist_scan, nblk, kxf, tail.rect, va, tail.rect_ranked, off,
+                           reinterpret_cast<uint32_t*>(geom + L.bucket_totals), ka);
+        return post(debug, s);
     }
     hipError_t e = (passes & 1)
         ? radix_sort(keys, nullptr, P, 8 * passes, kb, vb, ka, va, hist, hist_scan, regions, L.scan_region_geom, stall,
@@ -943,27 +1011,68 @@ hipError_t launch_depth_order(int P, int passes, const Layout& L, char* geom, ui
 
 // Super-tile entries in depth order (keys = entry_key, vals = Gaussian id); also clears what the
 // later kernels need cleared (tile and super-tile ranges, the segment count table, scan status).
+// offset[r]: the entry offset of depth rank r; with the MSD depth order (msd.totals != null) only
+// bucket-local, the bucket bases being the exclusive scan of msd.totals over the buckets.
+struct MsdOffsets {
+    const uint32_t* totals;     // per top-digit bucket: super-tile entries (k_depth_bucket_sort), or null
+    const uint32_t* hist_scan;  // the MSD pass's scanned [digit][block] histogram: bucket starts
+    int nblk;
+    const uint32_t* kxf;        // visible depth-key min / max: the number of buckets
+};
+
 __global__ __launch_bounds__(256) void k_emit_super(int P, int sgx, const uint32_t* __restrict__ sorted_ids,
                                                     const uint32_t* __restrict__ offset,
                                                     const uint2* __restrict__ rect_ranked,
                                                     uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
                                                     uint32_t* __restrict__ z0, int n0, uint32_t* __restrict__ z1,
                                                     int n1, uint32_t* __restrict__ z2, int n2,
-                                                    uint32_t* __restrict__ z3, int n3)
+                                                    uint32_t* __restrict__ z3, int n3, MsdOffsets msd)
 {
+    __shared__ uint32_t s_start[256], s_base[256], s_wsum[4];
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
     const int stride = gridDim.x * blockDim.x;
+    // this rank's inputs first: their round trip overlaps the bucket bases' below
+    uint2 rc = make_uint2(0u, 0u);
+    uint32_t g = 0, o = 0;
+    if (r < P) {
+        rc = rect_ranked[r];
+        g = sorted_ids[r];
+        o = offset[r];
+    }
+    if (msd.totals) {  // bucket starts and bases (every workgroup, 256 threads = 256 buckets)
+        int shift, nbits;
+        msd_digit(msd.kxf, shift, nbits);
+        const int t = threadIdx.x, ndig = 1 << nbits;
+        s_start[t] = t < ndig ? msd.hist_scan[(size_t)t * msd.nblk] : (uint32_t)P;
+        uint32_t x = msd.totals[t], v = x;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if ((t & 63) >= o) x += y;
+        }
+        if ((t & 63) == 63) s_wsum[t >> 6] = x;
+        __syncthreads();
+        uint32_t before = 0;
+        for (int i = 0; i < (t >> 6); i++) before += s_wsum[i];
+        s_base[t] = before + x - v;
+        __syncthreads();
+    }
     for (int w = r; w < n0; w += stride) z0[w] = 0u;
     for (int w = r; w < n1; w += stride) z1[w] = 0u;
     for (int w = r; w < n2; w += stride) z2[w] = 0u;
     for (int w = r; w < n3; w += stride) z3[w] = 0u;
-    if (r >= P) return;
-    const uint2 rc = rect_ranked[r];
-    if (rc.x == rc.y) return;  // culled (empty rectangle)
-    const uint32_t g = sorted_ids[r];
+    if (r >= P || rc.x == rc.y) return;  // past the ranks, or culled (empty rectangle)
     int sx0, sy0, sx1, sy1;
     super_rect(rc, sx0, sy0, sx1, sy1);
-    uint32_t o = offset[r];
+    if (msd.totals) {  // + the base of the bucket holding rank r: the last bucket starting at or before r
+        int lo = 0, hi = 255;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (s_start[mid] <= (uint32_t)r) lo = mid;
+            else hi = mid - 1;
+        }
+        o += s_base[lo];
+    }
     for (int y = sy0; y < sy1; y++)
         for (int x = sx0; x < sx1; x++) {
             keys[o] = entry_key(rc, x, y, sgx);
@@ -1309,6 +1418,19 @@ __global__ __launch_bounds__(256) void k_bin_emit(int S, int sgx, int gx, int gy
     }
 }
 
+// the MSD depth order's offset parts for k_emit_super (null totals: LSD order, global offsets)
+static MsdOffsets msd_offsets(int P, const Layout& L, char* geom, char* image)
+{
+    MsdOffsets m{nullptr, nullptr, 0, nullptr};
+    if (depth_order_uses_pass_count(P)) return m;
+    const int tile = kRadixThreads * (radix_small(P) ? 4 : 16);
+    m.totals = reinterpret_cast<const uint32_t*>(geom + L.bucket_totals);
+    m.hist_scan = reinterpret_cast<const uint32_t*>(geom + L.radix_hist_scan);
+    m.nblk = (P + tile - 1) / tile;
+    m.kxf = reinterpret_cast<const uint32_t*>(image + L.counters) + kCntKeyMin;
+    return m;
+}
+
 hipError_t launch_binning(int P, int64_t R, const Layout& L, char* geom, char* image, char* binning, uint32_t* stall,
                           hipStream_t s, bool debug)
 {
@@ -1333,7 +1455,7 @@ hipError_t launch_binning(int P, int64_t R, const Layout& L, char* geom, char* i
                        reinterpret_cast<const uint2*>(geom + L.rect_ranked), kA, vA,
                        reinterpret_cast<uint32_t*>(ranges), 2 * L.tiles, reinterpret_cast<uint32_t*>(sranges),
                        2 * L.supers, table, (int)L.seg_table_words, regions,
-                       (int)((L.super_passes + 1) * L.scan_region_bin));
+                       (int)((L.super_passes + 1) * L.scan_region_bin), msd_offsets(P, L, geom, image));
     if ((e = post(debug, s)) != hipSuccess) return e;
     int passes = 0;
     uint32_t* bin_hist_scan = reinterpret_cast<uint32_t*>(binning + L.bin_radix_hist_scan);

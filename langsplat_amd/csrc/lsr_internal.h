@@ -49,6 +49,7 @@ struct Layout {
     size_t scan_region_geom;  // u32 words per depth-order scan region
     size_t loss_words;        // fused loss: per-workgroup / per-group words and tickets, after the scan regions
     size_t zero_words;        // u32 words preprocess clears from scan_regions (scan status + loss words)
+    size_t bucket_totals;     // MSD depth order: super-tile entries per top-digit bucket (256 u32)
     size_t grad_records;      // P x kGradStrideLang floats: the language step's gradient records (cleared
                               // by the render forward under LSR_FWD_ZERO_GRAD_RECORDS)
     size_t geom_bytes;
@@ -97,6 +98,7 @@ inline Layout make_layout(int P, int W, int H, int64_t R, int64_t E)
     }
     L.rect_ranked = take(8 * p);
     L.grad_records = take(4 * kGradStrideLang * p);
+    L.bucket_totals = take(4 * 256);
     L.pre_partial = take(16 * ((p + kPreThreads - 1) / kPreThreads));
     L.geom_bytes = o;
 
