@@ -21,6 +21,10 @@ static thread_local std::string g_last_error;
 
 // ------------------------------------------------------------------ opt-in event profiler
 namespace {
+// timing-only events: no system-scope fence (cache writeback + invalidate) when they are recorded,
+// which would otherwise stall the stream around the measured launches (~6 us per step measured
+// at C3 with the default flags)
+constexpr unsigned kEventFlags = hipEventDisableSystemFence;
 struct Pending {
     const char* name;
     hipEvent_t a, b;
@@ -41,7 +45,7 @@ struct Profiler {
             return e;
         }
         hipEvent_t e = nullptr;
-        if (hipEventCreate(&e) != hipSuccess) return nullptr;
+        if (hipEventCreateWithFlags(&e, kEventFlags) != hipSuccess) return nullptr;
         return e;
     }
     void drain()
@@ -105,6 +109,10 @@ struct HostBlock {
     uint32_t seq;      // the last sequence number used (host side)
     uint32_t bad_segment;  // lsr_decode_language_feature: a segment id outside [-N, N)
     int32_t depth_passes;  // depth-sort passes the last forward needed (0: none yet)
+    // binning buffer size to request before the host wait (the last forward's, with headroom), for
+    // the same P and image size; the exact size is requested after the wait if it is larger
+    int32_t hint_P, hint_W, hint_H;
+    size_t binning_hint;
 };
 
 struct HostBlocks {
@@ -329,6 +337,14 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
             "publish counters");
     const int guess = hb->depth_passes > 0 ? hb->depth_passes : 4;
     LSR_TRY(launch_depth_order(P, guess, L, geom, counters, &hb->stall, stream, debug), "depth order");
+    // the binning buffer from the last forward's size while the GPU works (the allocator callback
+    // is host work that would otherwise sit between the wait and the binning launches)
+    char* binning = nullptr;
+    size_t binning_have = 0;
+    if (hb->binning_hint && hb->hint_P == P && hb->hint_W == W && hb->hint_H == H) {
+        binning = static_cast<char*>(alloc(user, LSR_BUF_BINNING, hb->binning_hint));
+        binning_have = binning ? hb->binning_hint : 0;
+    }
     LSR_TRY(wait_counters(hb, seq, stream), "wait counters");
     uint32_t host_cnt[8];
     for (int i = 0; i < 8; i++) host_cnt[i] = (uint32_t)hb->slot[i];
@@ -351,8 +367,14 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
     }
 
     L = make_layout(P, W, H, R, (int64_t)host_cnt[kCntSuper]);
-    char* binning = static_cast<char*>(alloc(user, LSR_BUF_BINNING, L.binning_bytes));
-    if (!binning) return fail(LSR_ERR_ALLOC, "lsr_forward: binning buffer allocation failed");
+    if (!binning || L.binning_bytes > binning_have) {
+        binning = static_cast<char*>(alloc(user, LSR_BUF_BINNING, L.binning_bytes));
+        if (!binning) return fail(LSR_ERR_ALLOC, "lsr_forward: binning buffer allocation failed");
+    }
+    hb->hint_P = P;
+    hb->hint_W = W;
+    hb->hint_H = H;
+    hb->binning_hint = L.binning_bytes + L.binning_bytes / 8;  // 12.5 % headroom for the next view
     LSR_TRY(launch_binning(P, R, L, geom, image, binning, &hb->stall, stream, debug), "binning");
     RenderParams rp{};
     rp.W = W;
@@ -511,7 +533,7 @@ int32_t lsr_profile_enable(int32_t on)
         // events come from a pool filled here, not created inside the measured launches
         while (g_prof.pool.size() < 512) {
             hipEvent_t e = nullptr;
-            if (hipEventCreate(&e) != hipSuccess) break;
+            if (hipEventCreateWithFlags(&e, kEventFlags) != hipSuccess) break;
             g_prof.pool.push_back(e);
         }
     }

@@ -389,3 +389,21 @@ def test_lookback_stall_fallback_is_exact():
     check_forward_exact(st, inp, run)
     torch.cuda.synchronize()
     assert lib.lsr_debug_scan_stalls() == 0
+
+
+def test_binning_buffer_grows_between_views():
+    """The forward requests its binning buffer before the host wait, sized from the thread's last
+    forward of the same P and image size; a view with many more tile instances must get a larger
+    buffer after the wait.  Far camera first (few instances), then a close one: both bit-exact."""
+    P, W, H = 4000, 128, 96
+    g = make_gaussians(P, seed=12, scale_range=(0.01, 0.05))
+    with torch.no_grad():
+        inp = {k: v.contiguous() for k, v in activated_inputs(g).items()}
+    far = make_cameras(1, W, H, radius=12.0)[0]
+    near = make_cameras(1, W, H, radius=2.5)[0]
+    runs = []
+    for cam in (far, near, far):
+        st = settings_for(cam, sh_degree=3)
+        run, std, ind, out = check_forward_exact(st, inp)
+        runs.append(run.num_rendered)
+    assert runs[1] > 1.2 * runs[0]  # beyond the 12.5 % headroom of the first view's size
