@@ -18,7 +18,8 @@ from typing import Dict, Optional
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "liblsr.so")
+# LSR_LIB: a measurement variant built by tools/build_variant.py (same-box A/B); default the product
+LIB_PATH = os.environ.get("LSR_LIB") or os.path.join(_HERE, "liblsr.so")
 
 LSR_BUF_GEOM, LSR_BUF_BINNING, LSR_BUF_IMAGE, LSR_BUF_BACKWARD = 0, 1, 2, 3
 ABI_VERSION = 6
