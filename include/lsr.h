@@ -265,6 +265,13 @@ int32_t lsr_debug_render_timeline(int32_t kernel, uint32_t* out, int32_t n);
 int32_t lsr_debug_scan_stalls(void);
 uint32_t lsr_debug_set_spin_limit(uint32_t limit);
 
+/* Measurement hook, not part of the reference interface: with LSR_BUCKET_TIMELINE=1 the MSD depth
+ * sort's bucket kernel records per workgroup b < min(n, 256) into out[8 b .. 8 b + 7]: {start, end}
+ * (100 MHz wall clock, low 32 bits), the hardware slot (XCC_ID << 16 | CU/SH/SE bits of HW_ID),
+ * the bucket's key count, the end times of the first pass, of all passes and of the output gathers,
+ * and the time the bucket's keys had arrived (synchronous). */
+int32_t lsr_debug_bucket_timeline(uint32_t* out, int32_t n);
+
 /* ---- the language-feature loss around the rasterizer ----------------
  *
  * lsr_masked_l1_forward replaces, in LangSplat's include_feature step (train.py:97-98),

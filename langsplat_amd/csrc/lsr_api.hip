@@ -607,6 +607,16 @@ int32_t lsr_debug_scan_stalls(void)
 
 uint32_t lsr_debug_set_spin_limit(uint32_t limit) { return set_stall_spin_limit(limit); }
 
+int32_t lsr_debug_bucket_timeline(uint32_t* out, int32_t n)
+{
+    if (!out || n <= 0) return fail(LSR_ERR_INVALID, "lsr_debug_bucket_timeline: invalid argument");
+    const bool debug = false;
+    hipStream_t stream = nullptr;
+    (void)stream;
+    LSR_TRY(bucket_timeline_read(out, n), "bucket timeline");
+    return LSR_OK;
+}
+
 int32_t lsr_mark_visible(int32_t P, const float* means3D, const float* viewmatrix, const float* projmatrix,
                          uint8_t* visible, void* stream_ptr)
 {

@@ -415,7 +415,10 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_hist(const uint32_t* __
 // exclusive offset (sum over lower waves).  The tile is reordered by digit in LDS and written
 // from LDS in digit-contiguous runs, so global stores coalesce (a direct scatter would send the
 // 64 lanes of a store to up to 64 different buckets).
-template <int kItems>
+// kCarry (MSD depth pass, vals_in == null): the Gaussian's rectangle tail.rect[idx] rides along
+// with its key into tail.rect_ranked, so the bucket sort permutes rectangles inside its bucket
+// instead of gathering them across all of rect (tail.ns is not used).
+template <int kItems, bool kCarry = false>
 __global__ __launch_bounds__(kRadixThreads) void k_radix_scatter(
     const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in, int n, int shift, int nbits,
     const uint32_t* __restrict__ hist, int nblk, uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
@@ -431,6 +434,7 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_scatter(
     __shared__ uint32_t gbase[256];         // global output position of this block's first key per digit
     __shared__ uint32_t dstart[256];        // block-local start of each digit in the reordered tile
     __shared__ uint32_t wsum[kWaves];
+    __shared__ uint2 sr[kCarry ? kTile : 1];
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
     const uint32_t mask = (1u << nbits) - 1u;
 #pragma unroll
@@ -439,6 +443,7 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_scatter(
     const int tile0 = blk * kTile;
     const int base = tile0 + wave * 64 * kItems;
     uint32_t key[kItems], val[kItems], rank[kItems];
+    uint2 rcv[kCarry ? kItems : 1];
 #pragma unroll
     for (int it = 0; it < kItems; it++) {
         const int idx = base + it * 64 + lane;
@@ -446,6 +451,7 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_scatter(
         key[it] = valid ? keys_in[idx] : 0u;
         if (kxf) key[it] = key_xf(key[it], kxf);
         val[it] = valid ? (vals_in ? vals_in[idx] : (uint32_t)idx) : 0u;
+        if (kCarry) rcv[kCarry ? it : 0] = valid ? tail.rect[idx] : make_uint2(0u, 0u);
     }
     __syncthreads();
 #pragma unroll
@@ -488,17 +494,19 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_scatter(
             const uint32_t pos = dstart[d] + wcnt[wave][d] + rank[it];
             sk[pos] = key[it];
             sv[pos] = val[it];
+            if (kCarry) sr[pos] = rcv[kCarry ? it : 0];
         }
     }
     __syncthreads();
     const int cnt = min(kTile, n - tile0);
-    if (!tail.rect) {
+    if (kCarry || !tail.rect) {
         for (int i = t; i < cnt; i += kRadixThreads) {
             const uint32_t k = sk[i];
             const uint32_t d = (k >> shift) & mask;
             const uint32_t o = gbase[d] + (uint32_t)i - dstart[d];
             keys_out[o] = k;
             vals_out[o] = sv[i];
+            if (kCarry) tail.rect_ranked[o] = sr[i];
         }
         return;
     }
@@ -648,10 +656,14 @@ constexpr int kBucketCap = 8192;
 constexpr int kBucketRounds = kBucketCap / kBucketThreads;  // rounds of 64 keys per wave
 constexpr int64_t kMsdMaxKeys = 2000000;                    // above: expected buckets exceed LDS
 
+// A bucket in LDS is kBucketCap packed words {key bits not yet ranked, local index (13 bits)}:
+// pass 0 ranks on the low 8 key bits held in registers and packs the rest (<= 16 bits) above the
+// index, so the two ping-pong buffers take 64 KB and two workgroups share a CU.
+constexpr int kIdxBits = 13;  // local index within a bucket (kBucketCap = 1 << kIdxBits)
+static_assert((1 << kIdxBits) == kBucketCap, "local index width");
 struct BucketLds {
-    uint32_t k[2][kBucketCap];
-    uint32_t v[2][kBucketCap];
-    uint32_t wcnt[kBucketWaves][256];  // per wave: running digit counts, then the wave's offset in the digit
+    uint32_t w[2][kBucketCap];
+    uint16_t wcnt[kBucketWaves][256];  // per wave: running digit counts, then the wave's offset in the digit
     uint32_t dstart[256];              // digit starts (LDS passes) / running digit bases (global passes)
     uint32_t ctot[256];                // global passes: the chunk's digit totals
     uint32_t wsum[kBucketWaves];
@@ -676,35 +688,32 @@ __device__ __forceinline__ uint32_t scan256(uint32_t v, uint32_t* wsum)
     return before + x - v;
 }
 
-// One stable pass of the LDS sort: (k, v)[src] -> [dst] by digit (k >> sh) & mask.  Wave w owns
-// keys [w R 64, (w + 1) R 64) and ranks them round by round (ballot match + the wave's running
-// digit counts), then the per-digit wave offsets and digit starts place every key.
-__device__ void bucket_lds_pass(BucketLds& L, int src, int nb, int sh, int nbits)
+// One stable pass of the LDS sort: the values val[] (kBucketRounds per thread, wave w holding
+// positions [w R 64, (w + 1) R 64) round by round) are placed by digit dig[] into out.  Ranks: per
+// wave, round by round (ballot match + the wave's running digit counts); then per digit the wave
+// offsets and the digit starts.
+__device__ void bucket_rank_scatter(BucketLds& L, const uint32_t (&dig)[kBucketRounds],
+                                    const uint32_t (&val)[kBucketRounds], int nb, int nbits, uint32_t* out)
 {
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
-    const uint32_t mask = (1u << nbits) - 1u;
-    for (int i = t; i < kBucketWaves * 256; i += kBucketThreads) (&L.wcnt[0][0])[i] = 0u;
+    for (int i = t; i < kBucketWaves * 256; i += kBucketThreads) (&L.wcnt[0][0])[i] = 0;
     __syncthreads();
-    uint32_t key[kBucketRounds], val[kBucketRounds], rank[kBucketRounds];
+    uint32_t rank[kBucketRounds];
 #pragma unroll
     for (int r = 0; r < kBucketRounds; r++) {
-        const int idx = (w * kBucketRounds + r) * 64 + lane;
-        const bool valid = idx < nb;
-        key[r] = valid ? L.k[src][idx] : 0u;
-        val[r] = valid ? L.v[src][idx] : 0u;
-        const uint32_t d = (key[r] >> sh) & mask;
-        const uint64_t peers = match_digit(d, valid, nbits);
+        const bool valid = (w * kBucketRounds + r) * 64 + lane < nb;
+        const uint64_t peers = match_digit(dig[r], valid, nbits);
         const uint32_t rr = (uint32_t)__popcll(peers & lanemask_lt());
-        const uint32_t c = L.wcnt[w][d];
+        const uint32_t c = L.wcnt[w][dig[r]];
         rank[r] = c + rr;
-        if (valid && rr == 0) L.wcnt[w][d] = c + (uint32_t)__popcll(peers);
+        if (valid && rr == 0) L.wcnt[w][dig[r]] = (uint16_t)(c + (uint32_t)__popcll(peers));
     }
     __syncthreads();
     uint32_t tot = 0;
     if (t < 256) {
         for (int i = 0; i < kBucketWaves; i++) {
             const uint32_t c = L.wcnt[i][t];
-            L.wcnt[i][t] = tot;
+            L.wcnt[i][t] = (uint16_t)tot;
             tot += c;
         }
     }
@@ -712,15 +721,8 @@ __device__ void bucket_lds_pass(BucketLds& L, int src, int nb, int sh, int nbits
     if (t < 256) L.dstart[t] = ex;
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < kBucketRounds; r++) {
-        const int idx = (w * kBucketRounds + r) * 64 + lane;
-        if (idx < nb) {
-            const uint32_t d = (key[r] >> sh) & mask;
-            const uint32_t pos = L.dstart[d] + L.wcnt[w][d] + rank[r];
-            L.k[src ^ 1][pos] = key[r];
-            L.v[src ^ 1][pos] = val[r];
-        }
-    }
+    for (int r = 0; r < kBucketRounds; r++)
+        if ((w * kBucketRounds + r) * 64 + lane < nb) out[L.dstart[dig[r]] + L.wcnt[w][dig[r]] + rank[r]] = val[r];
     __syncthreads();
 }
 
@@ -806,71 +808,160 @@ __device__ __forceinline__ uint32_t scan1024(uint32_t v, uint32_t* wsum, uint32_
 }
 
 // One workgroup per bucket (top-digit value).  keys / ids: the MSD pass's output (transformed keys,
-// bucket-contiguous, id order inside a bucket); hist_scan: its scanned [digit][block] histogram,
-// whose digit starts are the bucket ranges.  Writes, for every position of the bucket, the sorted
+// bucket-contiguous, id order inside a bucket; rect_ranked holds the rectangles in the same
+// layout); hist_scan: its scanned [digit][block] histogram, whose digit starts are the bucket
+// ranges.  rect: the rectangles by id (global fallback only).  Writes, for every position of the bucket, the sorted
 // id, the depth-ordered rectangle and the BUCKET-LOCAL exclusive prefix of the super-tile entry
 // counts (local_off), and the bucket's total entry count (totals[d], 0 for empty buckets):
 // k_emit_super adds the scanned bucket totals, so no separate P-long scan is launched.  scratch_k
 // is P words of scratch for the global fallback (whose ids go through sorted_ids itself).
-__global__ __launch_bounds__(kBucketThreads) void k_depth_bucket_sort(
+// Measurement hook (LSR_BUCKET_TIMELINE=1): per bucket workgroup {start, end} (s_memrealtime,
+// 100 MHz), its hardware slot (XCC_ID << 16 | HW_ID bits 8..15), its key count and the times at
+// which the first pass, all passes and the output gathers ended.
+__device__ uint32_t g_bucket_timeline[256 * 8];
+
+#ifndef LSR_BUCKET_WAVES  // one bucket workgroup per CU: no need to squeeze registers for two
+#define LSR_BUCKET_WAVES 4
+#endif
+__global__ __launch_bounds__(kBucketThreads) __attribute__((amdgpu_waves_per_eu(LSR_BUCKET_WAVES, 8)))
+void k_depth_bucket_sort(
     int n, uint32_t* __restrict__ keys, uint32_t* __restrict__ ids, const uint32_t* __restrict__ hist_scan, int nblk,
     const uint32_t* __restrict__ kxf, const uint2* __restrict__ rect, uint32_t* __restrict__ sorted_ids,
     uint2* __restrict__ rect_ranked, uint32_t* __restrict__ local_off, uint32_t* __restrict__ totals,
-    uint32_t* __restrict__ scratch_k)
+    uint32_t* __restrict__ scratch_k, int timeline)
 {
+    const uint64_t t_start = timeline ? wall_clock64() : 0;
+    struct TimelineGuard {  // written when the workgroup leaves, on every path
+        int on;
+        uint64_t t0;
+        int nb;
+        uint32_t ph[4];
+        __device__ void mark(int i)
+        {
+            if (on) ph[i] = (uint32_t)wall_clock64();
+        }
+        __device__ ~TimelineGuard()
+        {
+            if (!on || threadIdx.x != 0) return;
+            const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+            const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);
+            uint32_t* o = g_bucket_timeline + 8 * blockIdx.x;
+            o[0] = (uint32_t)t0;
+            o[1] = (uint32_t)wall_clock64();
+            o[2] = ((xcc & 0xFu) << 16) | ((hw >> 8) & 0xFFu);
+            o[3] = (uint32_t)nb;
+            o[4] = ph[0];
+            o[5] = ph[1];
+            o[6] = ph[2];
+            o[7] = ph[3];
+        }
+    } guard{timeline, t_start, 0, {0u, 0u, 0u, 0u}};
     extern __shared__ uint4 s_bucket_raw[];
     BucketLds& L = *reinterpret_cast<BucketLds*>(s_bucket_raw);
-    int shift, nbits;
-    msd_digit(kxf, shift, nbits);
     const int d = (int)blockIdx.x;
     const int t = threadIdx.x;
+    // bucket range: both scanned starts are loaded (in bounds: the histogram has 256 digit rows)
+    // together with the width (kxf), then discarded for digits beyond the width, whose histogram
+    // rows the MSD pass did not write
+    const uint32_t s0 = hist_scan[(size_t)d * nblk];
+    const uint32_t s1 = d < 255 ? hist_scan[(size_t)(d + 1) * nblk] : 0u;
+    int shift, nbits;
+    msd_digit(kxf, shift, nbits);
     uint32_t start = 0, end = 0;
     if (d < (1 << nbits)) {
-        start = hist_scan[(size_t)d * nblk];
-        end = d + 1 < (1 << nbits) ? hist_scan[(size_t)(d + 1) * nblk] : (uint32_t)n;
+        start = s0;
+        end = d + 1 < (1 << nbits) ? s1 : (uint32_t)n;
     }
     const int nb = (int)(end - start);
+    guard.nb = nb;
     if (nb <= 0) {  // no such top digit, or no key in it
         if (t == 0) totals[d] = 0u;
         return;
     }
     const int lowbits = shift;  // the bits below the top digit (equal top digits inside a bucket)
     if (nb <= kBucketCap) {
-        {  // every load in flight before the first LDS store (one memory round trip)
-            uint32_t k[kBucketRounds], v[kBucketRounds];
+        const int w = t >> 6, lane = t & 63;
+        const uint32_t lowmask = lowbits >= 32 ? 0xFFFFFFFFu : ((1u << lowbits) - 1u);
+        uint32_t dig[kBucketRounds], val[kBucketRounds];
+        // pass 0 from registers: the keys in wave-blocked order, digit = key bits 0..7, and the
+        // packed word {key bits 8.., local index} as the value
 #pragma unroll
-            for (int r = 0; r < kBucketRounds; r++) {
-                const int i = t + r * kBucketThreads;
-                k[r] = i < nb ? keys[start + i] : 0u;
-                v[r] = i < nb ? ids[start + i] : 0u;
-            }
-#pragma unroll
-            for (int r = 0; r < kBucketRounds; r++) {
-                const int i = t + r * kBucketThreads;
-                if (i < nb) {
-                    L.k[0][i] = k[r];
-                    L.v[0][i] = v[r];
-                }
-            }
+        for (int r = 0; r < kBucketRounds; r++) {
+            const int idx = (w * kBucketRounds + r) * 64 + lane;
+            const uint32_t k = idx < nb ? keys[start + idx] & lowmask : 0u;
+            dig[r] = k & 0xFFu;
+            val[r] = ((k >> 8) << kIdxBits) | (uint32_t)idx;
         }
-        __syncthreads();
+        if (timeline) {  // measurement only: the keys' arrival
+            __builtin_amdgcn_s_waitcnt(0);
+            guard.mark(3);
+        }
         int src = 0;
-        for (int sh = 0; sh < lowbits; sh += 8) {
-            bucket_lds_pass(L, src, nb, sh, min(8, lowbits - sh));
+        if (lowbits > 0) {
+            bucket_rank_scatter(L, dig, val, nb, min(8, lowbits), L.w[0]);
+            guard.mark(0);
+        } else {
+#pragma unroll
+            for (int r = 0; r < kBucketRounds; r++) {
+                const int idx = (w * kBucketRounds + r) * 64 + lane;
+                if (idx < nb) L.w[0][idx] = val[r];
+            }
+            __syncthreads();
+        }
+        for (int sh = 8; sh < lowbits; sh += 8) {  // later passes: the digit from the packed word
+#pragma unroll
+            for (int r = 0; r < kBucketRounds; r++) {
+                const int idx = (w * kBucketRounds + r) * 64 + lane;
+                val[r] = idx < nb ? L.w[src][idx] : 0u;
+                dig[r] = (val[r] >> (kIdxBits + sh - 8)) & 0xFFu;
+            }
+            bucket_rank_scatter(L, dig, val, nb, min(8, lowbits - sh), L.w[src ^ 1]);
             src ^= 1;
         }
-        // outputs: all rectangle gathers in flight at once; the entry counts go through LDS (the
-        // free key buffer) so that each thread scans a contiguous run of kBucketRounds of them
-        uint32_t* X = L.k[src ^ 1];
-        uint32_t id[kBucketRounds];
+        guard.mark(1);
+        // outputs: ids and rectangles (carried into rect_ranked by the MSD pass) permuted inside the
+        // bucket.  Global reads and writes stay coalesced: each array is loaded in bucket order,
+        // staged in the two free 32 KB LDS buffers and gathered there through the local indices
+        // (lidx).  rect_ranked is permuted in place: all of its loads have landed in LDS before the
+        // barriers that precede the stores.  The entry counts then go through LDS so that each thread
+        // scans a contiguous run of kBucketRounds of them.
+        uint32_t* S = L.w[src];
+        uint32_t* X = L.w[src ^ 1];
+        uint32_t lidx[kBucketRounds], id[kBucketRounds], ry[kBucketRounds];
         uint2 rc[kBucketRounds];
 #pragma unroll
         for (int r = 0; r < kBucketRounds; r++) {
             const int i = t + r * kBucketThreads;
-            id[r] = i < nb ? L.v[src][i] : 0u;
+            lidx[r] = i < nb ? S[i] & (kBucketCap - 1u) : 0u;
+            id[r] = i < nb ? ids[start + i] : 0u;
+            rc[r] = i < nb ? rect_ranked[start + i] : make_uint2(0u, 0u);
         }
+        __syncthreads();  // S read by everyone
 #pragma unroll
-        for (int r = 0; r < kBucketRounds; r++) rc[r] = t + r * kBucketThreads < nb ? rect[id[r]] : make_uint2(0u, 0u);
+        for (int r = 0; r < kBucketRounds; r++) {
+            const int i = t + r * kBucketThreads;
+            if (i < nb) {
+                X[i] = id[r];
+                S[i] = rc[r].x;
+            }
+            ry[r] = rc[r].y;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < kBucketRounds; r++) {
+            id[r] = X[lidx[r]];
+            rc[r].x = S[lidx[r]];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < kBucketRounds; r++) {
+            const int i = t + r * kBucketThreads;
+            if (i < nb) X[i] = ry[r];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < kBucketRounds; r++) rc[r].y = X[lidx[r]];
+        __syncthreads();
 #pragma unroll
         for (int r = 0; r < kBucketRounds; r++) {
             const int i = t + r * kBucketThreads;
@@ -882,6 +973,7 @@ __global__ __launch_bounds__(kBucketThreads) void k_depth_bucket_sort(
             }
         }
         __syncthreads();
+        guard.mark(2);
         uint32_t c[kBucketRounds], run = 0;
 #pragma unroll
         for (int k = 0; k < kBucketRounds; k++) {
@@ -927,6 +1019,22 @@ __global__ __launch_bounds__(kBucketThreads) void k_depth_bucket_sort(
         carry += tot;
     }
     if (t == 0) totals[d] = carry;
+}
+
+static int bucket_timeline_on()
+{
+    static const int v = [] {
+        const char* e = getenv("LSR_BUCKET_TIMELINE");
+        return e && e[0] == '1' ? 1 : 0;
+    }();
+    return v;
+}
+
+hipError_t bucket_timeline_read(uint32_t* out, int n)
+{
+    if (n > 256) n = 256;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bucket_timeline), sizeof(uint32_t) * 8 * n, 0,
+                               hipMemcpyDeviceToHost);
 }
 
 static hipError_t allow_bucket_lds()
@@ -984,18 +1092,19 @@ hipError_t launch_depth_order(int P, int passes, const Layout& L, char* geom, ui
         if ((e = post(debug, s)) != hipSuccess) return e;
         if ((e = scan_exclusive(hist, hist_scan, 256 * nblk, regions, nullptr, stall, s, debug)) != hipSuccess)
             return e;
-        const ScatterTail none{nullptr, nullptr, nullptr};
+        // the rectangles ride along into rect_ranked (bucket layout); the bucket sort permutes them
+        const ScatterTail carry{tail.rect, tail.rect_ranked, nullptr};
         if (small)
-            hipLaunchKernelGGL(k_radix_scatter<4>, dim3(nblk), dim3(kRadixThreads), 0, s, keys, (const uint32_t*)nullptr,
-                               P, 0, 8, hist_scan, nblk, kb, vb, kxf, none, remap, 1);
+            hipLaunchKernelGGL((k_radix_scatter<4, true>), dim3(nblk), dim3(kRadixThreads), 0, s, keys,
+                               (const uint32_t*)nullptr, P, 0, 8, hist_scan, nblk, kb, vb, kxf, carry, remap, 1);
         else
-            hipLaunchKernelGGL(k_radix_scatter<16>, dim3(nblk), dim3(kRadixThreads), 0, s, keys,
-                               (const uint32_t*)nullptr, P, 0, 8, hist_scan, nblk, kb, vb, kxf, none, remap, 1);
+            hipLaunchKernelGGL((k_radix_scatter<16, true>), dim3(nblk), dim3(kRadixThreads), 0, s, keys,
+                               (const uint32_t*)nullptr, P, 0, 8, hist_scan, nblk, kb, vb, kxf, carry, remap, 1);
         if ((e = post(debug, s)) != hipSuccess) return e;
         // bucket-local offsets into super_offset, bucket totals for k_emit_super (no P-long scan)
         hipLaunchKernelGGL(k_depth_bucket_sort, dim3(256), dim3(kBucketThreads), kBucketLdsBytes, s, P, kb, vb,
                            (const uint32_t*)hist_scan, nblk, kxf, tail.rect, va, tail.rect_ranked, off,
-                           reinterpret_cast<uint32_t*>(geom + L.bucket_totals), ka);
+                           reinterpret_cast<uint32_t*>(geom + L.bucket_totals), ka, bucket_timeline_on());
         return post(debug, s);
     }
     hipError_t e = (passes & 1)
