@@ -22,6 +22,7 @@ max-over-ranks wall time of the timed steps.
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import math
 import os
@@ -278,6 +279,10 @@ def main():
     # roofline), so event bookkeeping does not sit on the host's critical path of every stage
     live = os.environ.get("LSR_BENCH_LIVE_EVENTS", "1") != "0"  # 0: measurement of the events' own cost
     _native.profile_enable(live, stages=[DOMINANT_STAGE])
+    # the collector stays off inside the timed loops (as timeit does): a collection of the steps'
+    # autograd garbage would land on the host's critical path of one step
+    gc.collect()
+    gc.disable()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -303,6 +308,7 @@ def main():
         step()
     torch.cuda.synchronize()
     elapsed_all = time.perf_counter() - t1
+    gc.enable()
     _native.FORCE_GEOMETRY_GRADS = os.environ.get("LSR_ALL_GRADS", "0") == "1"
     # stage breakdown: a separate, untimed pass with every stage profiled
     prof_steps = min(args.steps, 10)

@@ -1458,6 +1458,7 @@ __global__ __launch_bounds__(256) void k_bin_emit(int S, int sgx, int gx, int gy
     __shared__ uint32_t toff[65];      // batch staging offset of tile l (exclusive scan), total
     __shared__ uint32_t stage_g[kStage];
     __shared__ uint8_t stage_t[kStage];
+    __shared__ uint32_t sg[4][64];     // the batch's Gaussian ids, entry order
     int s, seg;
     if (!block_segment(S, seg_base, &s, &seg)) return;
     const SegmentCtx c = segment_ctx(s, seg, sgx, sranges, col_prefix);
@@ -1473,7 +1474,6 @@ __global__ __launch_bounds__(256) void k_bin_emit(int S, int sgx, int gx, int gy
             if (r.y > r.x) schedule_tile(sched_counts, sched_lists, gx * gy, gt, r.y - r.x);
         }
     }
-    const uint64_t below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     for (uint32_t b = c.e0; b < c.e1; b += 256) {
         const uint32_t e = b + t;
         uint32_t g = 0;
@@ -1483,6 +1483,7 @@ __global__ __launch_bounds__(256) void k_bin_emit(int S, int sgx, int gx, int gy
             m = entry_mask(keys[e]);
         }
         colw[wave][lane] = transpose64(m);
+        sg[wave][lane] = g;
         __syncthreads();
         if (t < 64) {  // wave 0, lane l = tile l: per-wave bases and the tile-major staging scan
             uint32_t run = 0;
@@ -1502,13 +1503,19 @@ __global__ __launch_bounds__(256) void k_bin_emit(int S, int sgx, int gx, int gy
         }
         __syncthreads();
         const uint32_t total = toff[64];
+        // thread (wave, lane = local tile l) places the wave's entries covering tile l, in entry
+        // order: a loop over one column of the transposed masks, so the trip count is a tile's
+        // share of the batch rather than the widest entry's tile count
+        uint64_t col = colw[wave][lane];
+        const uint32_t* gw = sg[wave];
         if (total <= (uint32_t)kStage) {
-            while (m) {
-                const int l = __ffsll((unsigned long long)m) - 1;
-                m &= m - 1ull;
-                const uint32_t i = toff[l] + pre[wave][l] + (uint32_t)__popcll(colw[wave][l] & below);
-                stage_g[i] = g;
-                stage_t[i] = (uint8_t)l;
+            uint32_t i = toff[lane] + pre[wave][lane];
+            while (col) {
+                const int j = __ffsll((unsigned long long)col) - 1;
+                col &= col - 1ull;
+                stage_g[i] = gw[j];
+                stage_t[i] = (uint8_t)lane;
+                i++;
             }
             __syncthreads();
             for (uint32_t i = t; i < total; i += 256) {
@@ -1516,10 +1523,11 @@ __global__ __launch_bounds__(256) void k_bin_emit(int S, int sgx, int gx, int gy
                 point_list[cursor[l] + (i - toff[l])] = stage_g[i];
             }
         } else {
-            while (m) {
-                const int l = __ffsll((unsigned long long)m) - 1;
-                m &= m - 1ull;
-                point_list[cursor[l] + pre[wave][l] + (uint32_t)__popcll(colw[wave][l] & below)] = g;
+            uint32_t o = cursor[lane] + pre[wave][lane];
+            while (col) {
+                const int j = __ffsll((unsigned long long)col) - 1;
+                col &= col - 1ull;
+                point_list[o++] = gw[j];
             }
         }
         __syncthreads();
