@@ -131,7 +131,7 @@ def algorithmic_bytes(stage, P, V, R, HW, M, color_grad=True, geometry=True, fus
     }.get(stage)
 
 
-# the stage that dominates the step (measured: profiles/r01_summary.json); timed live in the bench
+# the stage that dominates the step (measured: profiles/r02_summary.json); timed live in the bench
 DOMINANT_STAGE = "render backward"
 
 # rocprofv3 names of the bench step's kernels (template arguments: k_render_forward<kStats, kFeat, kLoss>,
@@ -147,7 +147,7 @@ def pmc_traffic(stage):
     or (None, None) when no profile covers it."""
     import glob
     kern = STAGE_KERNEL.get(stage)
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_summary.json")), key=os.path.getmtime)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9]*_summary.json")))  # by round tag
     for f in reversed(files):
         try:
             d = json.load(open(f))["kernels"].get(kern, {})
@@ -164,7 +164,7 @@ def pmc_valu(stage):
     (tools/valu_summary.py over tools/pmc_valu.sh), or (None, None)."""
     import glob
     kern = STAGE_KERNEL.get(stage)
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_valu.json")), key=os.path.getmtime)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9]*_valu.json")))  # by round tag
     for f in reversed(files):
         try:
             d = json.load(open(f))["kernels"].get(kern, {})
