@@ -131,6 +131,9 @@ def algorithmic_bytes(stage, P, V, R, HW, M, color_grad=True, geometry=True, fus
     }.get(stage)
 
 
+# the timed loop records the dominant kernel's events on every LIVE_EVENT_EVERY-th step
+LIVE_EVENT_EVERY = 5
+
 # the stage that dominates the step (measured: profiles/r02_summary.json); timed live in the bench
 DOMINANT_STAGE = "render backward"
 
@@ -276,9 +279,10 @@ def main():
     torch.cuda.synchronize()
 
     # timed region: HIP events around the dominant kernel only (its live average feeds the
-    # roofline), so event bookkeeping does not sit on the host's critical path of every stage
+    # roofline), so event bookkeeping does not sit on the host's critical path of every stage; and
+    # only on every 5th step (each event pair stalls the stream for ~2 x 4 us: DESIGN.md section 5)
     live = os.environ.get("LSR_BENCH_LIVE_EVENTS", "1") != "0"  # 0: measurement of the events' own cost
-    _native.profile_enable(live, stages=[DOMINANT_STAGE])
+    _native.profile_enable(live, stages=[DOMINANT_STAGE], every=LIVE_EVENT_EVERY)
     # the collector stays off inside the timed loops (as timeit does): a collection of the steps'
     # autograd garbage would land on the host's critical path of one step
     gc.collect()

@@ -234,6 +234,9 @@ int32_t lsr_profile_report(lsr_kernel_stat* out, int32_t capacity);
 /* Restricts profiling to the comma-separated stage names (NULL or "" = every stage), so a timed
  * run can time its dominant kernel live without event overhead around the other stages. */
 int32_t lsr_profile_select(const char* stages);
+/* Records the events on every `every`-th launch of a selected stage only (default 1; reset by each
+ * call): a timed run samples its dominant kernel's duration at a fraction of the events' cost. */
+int32_t lsr_profile_sample(int32_t every);
 
 /* _C.mark_visible: visible[i] = 1 iff Gaussian i passes the near-plane frustum test. */
 int32_t lsr_mark_visible(int32_t P, const float* means3D, const float* viewmatrix,

@@ -114,6 +114,7 @@ SIGNATURES = {
     "lsr_profile_enable": (ctypes.c_int32, [ctypes.c_int32]),
     "lsr_profile_report": (ctypes.c_int32, [ctypes.POINTER(LsrKernelStat), ctypes.c_int32]),
     "lsr_profile_select": (ctypes.c_int32, [ctypes.c_char_p]),
+    "lsr_profile_sample": (ctypes.c_int32, [ctypes.c_int32]),
 }
 
 _lib: Optional[ctypes.CDLL] = None
@@ -460,11 +461,13 @@ def state_layout(P: int, W: int, H: int, num_rendered: int) -> Dict[str, int]:
     return {name: int(getattr(lay, name)) for name, _ in LsrStateLayout._fields_}
 
 
-def profile_enable(on: bool = True, stages=None):
+def profile_enable(on: bool = True, stages=None, every: int = 1):
     """Start (clearing) / stop the per-stage HIP-event profiler; `stages` restricts it to those
-    stage names (lsr_profile_select)."""
+    stage names (lsr_profile_select), `every` > 1 records only every every-th selected launch
+    (lsr_profile_sample)."""
     lib = load()
     lib.lsr_profile_select(",".join(stages).encode() if stages else None)
+    _check(lib.lsr_profile_sample(int(every)), "lsr_profile_sample")
     lib.lsr_profile_enable(1 if on else 0)
 
 

@@ -33,6 +33,7 @@ struct Profiler {
     std::mutex mu;
     bool on = false;
     std::vector<std::string> select;  // empty: every stage
+    int64_t every = 1, seen = 0;      // lsr_profile_sample: events on every `every`-th selected launch
     std::vector<Pending> pending;
     std::vector<hipEvent_t> pool;
     std::map<std::string, std::pair<int64_t, double>> stats;
@@ -79,6 +80,7 @@ struct Scope {
             for (const auto& x : g_prof.select) hit = hit || x == n;
             if (!hit) return;
         }
+        if (g_prof.seen++ % g_prof.every != 0) return;
         a = g_prof.get();
         b = g_prof.get();
         if (a && b) (void)hipEventRecord(a, s);
@@ -538,6 +540,15 @@ int32_t lsr_profile_enable(int32_t on)
         }
     }
     g_prof.on = on != 0;
+    return LSR_OK;
+}
+
+int32_t lsr_profile_sample(int32_t every)
+{
+    if (every < 1) return fail(LSR_ERR_INVALID, "lsr_profile_sample: every must be >= 1");
+    std::lock_guard<std::mutex> g(g_prof.mu);
+    g_prof.every = every;
+    g_prof.seen = 0;
     return LSR_OK;
 }
 

@@ -249,31 +249,32 @@ __device__ __forceinline__ Cov2D cov2d(float px, float py, float pz, float fx, f
     return o;
 }
 
-// SH -> RGB for one channel (utils/sh_utils.py:57-112).  sh points at coefficient 0 of the
-// channel, coefficients strided by 3 (P x M x 3 layout of GaussianModel.get_features).
-__device__ __forceinline__ float sh_eval_channel(int deg, const float* sh, float x, float y, float z)
+// SH -> RGB for one channel (utils/sh_utils.py:57-112).  c0 is coefficient 0 of the channel; rest
+// points at the channel's coefficient 1, coefficients strided by 3 (the P x M x 3 layout of
+// GaussianModel.get_features from column 3, or a _features_rest row).
+__device__ __forceinline__ float sh_eval_channel(int deg, float c0, const float* rest, float x, float y, float z)
 {
-    float res = SH_C0 * sh[0];
+    float res = SH_C0 * c0;
     if (deg > 0) {
-        res = res - (SH_C1 * y) * sh[1 * 3];
-        res = res + (SH_C1 * z) * sh[2 * 3];
-        res = res - (SH_C1 * x) * sh[3 * 3];
+        res = res - (SH_C1 * y) * rest[0 * 3];
+        res = res + (SH_C1 * z) * rest[1 * 3];
+        res = res - (SH_C1 * x) * rest[2 * 3];
         if (deg > 1) {
             float xx = x * x, yy = y * y, zz = z * z;
             float xy = x * y, yz = y * z, xz = x * z;
-            res = res + (SH_C2_0 * xy) * sh[4 * 3];
-            res = res + (SH_C2_1 * yz) * sh[5 * 3];
-            res = res + (SH_C2_2 * (2.0f * zz - xx - yy)) * sh[6 * 3];
-            res = res + (SH_C2_3 * xz) * sh[7 * 3];
-            res = res + (SH_C2_4 * (xx - yy)) * sh[8 * 3];
+            res = res + (SH_C2_0 * xy) * rest[3 * 3];
+            res = res + (SH_C2_1 * yz) * rest[4 * 3];
+            res = res + (SH_C2_2 * (2.0f * zz - xx - yy)) * rest[5 * 3];
+            res = res + (SH_C2_3 * xz) * rest[6 * 3];
+            res = res + (SH_C2_4 * (xx - yy)) * rest[7 * 3];
             if (deg > 2) {
-                res = res + (SH_C3_0 * y * (3.0f * xx - yy)) * sh[9 * 3];
-                res = res + (SH_C3_1 * xy * z) * sh[10 * 3];
-                res = res + (SH_C3_2 * y * (4.0f * zz - xx - yy)) * sh[11 * 3];
-                res = res + (SH_C3_3 * z * (2.0f * zz - 3.0f * xx - 3.0f * yy)) * sh[12 * 3];
-                res = res + (SH_C3_4 * x * (4.0f * zz - xx - yy)) * sh[13 * 3];
-                res = res + (SH_C3_5 * z * (xx - yy)) * sh[14 * 3];
-                res = res + (SH_C3_6 * x * (xx - 3.0f * yy)) * sh[15 * 3];
+                res = res + (SH_C3_0 * y * (3.0f * xx - yy)) * rest[8 * 3];
+                res = res + (SH_C3_1 * xy * z) * rest[9 * 3];
+                res = res + (SH_C3_2 * y * (4.0f * zz - xx - yy)) * rest[10 * 3];
+                res = res + (SH_C3_3 * z * (2.0f * zz - 3.0f * xx - 3.0f * yy)) * rest[11 * 3];
+                res = res + (SH_C3_4 * x * (4.0f * zz - xx - yy)) * rest[12 * 3];
+                res = res + (SH_C3_5 * z * (xx - yy)) * rest[13 * 3];
+                res = res + (SH_C3_6 * x * (xx - 3.0f * yy)) * rest[14 * 3];
             }
         }
     }

@@ -120,7 +120,53 @@ __device__ __forceinline__ void stage_sh_out(float* dsh, float* dsh_rest, int P,
     }
 }
 
-__global__ __launch_bounds__(kPreThreads) void k_preprocess(PreprocessParams p)
+// Split SH rows (_features_dc + _features_rest) with a 16-B aligned rest tensor: the block's rest
+// rows are one contiguous run of ng x 3(M-1) floats, copied into LDS as it lies in HBM by LDS-DMA
+// (global_load_lds_dwordx4: no VGPR destination, no per-element addressing), all in flight at once.
+// A lane then reads its row at stride 3(M-1) floats: odd for even M (45 at M = 16), so the 32-bank
+// ds_read_b32 rows of a wave never conflict.  The dc coefficients are read per lane.
+__host__ __device__ __forceinline__ bool sh_dma(const float* shs, const float* shs_rest, int M)
+{
+    return shs && shs_rest && M >= 2 && (reinterpret_cast<uintptr_t>(shs_rest) & 15) == 0;
+}
+
+typedef __attribute__((address_space(3))) void* lds_void_ptr;
+typedef __attribute__((address_space(1))) void* global_void_ptr;
+
+__device__ __forceinline__ void stage_rest_dma(const float* __restrict__ rest, int P, int M, float* lds)
+{
+    const int w = 3 * (M - 1);
+    const int g0 = blockIdx.x * kPreThreads, ng = min(kPreThreads, P - g0);
+    const int n = ng * w, n4 = n >> 2;  // g0 * w * 4 bytes is 16-B aligned: kPreThreads % 4 == 0
+    const float* src = rest + (size_t)g0 * w;
+    const int lane = threadIdx.x & 63;
+    // each wave-instruction writes 1 KiB of LDS at a wave-uniform base (+16 B per lane)
+    for (int k0 = (int)(threadIdx.x & ~63); k0 < n4; k0 += kPreThreads)
+        if (k0 + lane < n4)
+            __builtin_amdgcn_global_load_lds((global_void_ptr)(src + 4 * (k0 + lane)),
+                                             (lds_void_ptr)(lds + 4 * k0), 16, 0, 0);
+    for (int e = 4 * n4 + (int)threadIdx.x; e < n; e += kPreThreads) lds[e] = src[e];  // ragged last block
+}
+
+static size_t sh_lds_bytes(const float* shs, const float* shs_rest, int M)
+{
+    if (!shs) return 0;
+    if (sh_dma(shs, shs_rest, M)) return kPreThreads * (size_t)(3 * (M - 1)) * 4;
+    return kPreThreads * (size_t)(3 * M + 1) * 4;
+}
+
+// SH staging variants: kShLds = register-staged rows (any layout), kShDma = stage_rest_dma
+// (sh_dma() holds), kShDirect = no LDS, each lane loads its own 180-B _features_rest row
+// (M == 16; dword-aligned dwordx4 loads) -- separate instances so that one path's VGPRs do not
+// count against another
+enum ShMode { kShLds = 0, kShDma = 1, kShDirect = 2 };
+
+#ifndef LSR_PRE_DIRECT_WAVES  // measurement knob: occupancy target of the kShDirect instance (0: none)
+#define LSR_PRE_DIRECT_WAVES 0
+#endif
+template <int kSh>
+__global__ __launch_bounds__(kPreThreads) __attribute__((amdgpu_waves_per_eu(
+    kSh == kShDirect && LSR_PRE_DIRECT_WAVES > 0 ? LSR_PRE_DIRECT_WAVES : 1))) void k_preprocess(PreprocessParams p)
 {
     extern __shared__ float s_sh[];
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -133,42 +179,134 @@ __global__ __launch_bounds__(kPreThreads) void k_preprocess(PreprocessParams p)
     float cov[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     float f0 = 0.f, f1 = 0.f, f2 = 0.f;
     const bool feat = p.include_feature && p.lang;
-    if (live) {
-        px = p.means[3 * i];
-        py = p.means[3 * i + 1];
-        pz = p.means[3 * i + 2];
+    constexpr bool dma = kSh != kShLds;  // split rows, dc read per lane
+    float dc[3] = {0.f, 0.f, 0.f};
+    float rr[45];  // kShDirect: the lane's _features_rest row
+    // camera (uniform): kShDirect reads it into registers before the per-Gaussian loads, so its
+    // loads neither trail those nor wait behind them
+    const float* view = p.view;
+    const float* proj = p.proj;
+    const float* campos = p.campos;
+    float cam_view[16], cam_proj[16], cam_pos[3];
+    if (kSh == kShDirect) {
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            cam_view[k] = p.view[k];
+            cam_proj[k] = p.proj[k];
+        }
+#pragma unroll
+        for (int k = 0; k < 3; k++) cam_pos[k] = p.campos[k];
+        view = cam_view;
+        proj = cam_proj;
+        campos = cam_pos;
+    }
+    if (kSh == kShDirect) {
+        // the language step's layout (the launcher checks it): scales + rotations, the language
+        // feature, split SH rows.  Every load is unconditional (a dead lane of the last block reads
+        // Gaussian P - 1), so no branch joins sit between the loads and their registers.
+        const uint32_t ic = (uint32_t)min(i, p.P - 1), o3 = ic * 12u;
+        auto at = [](const float* base, uint32_t off) { return reinterpret_cast<const float*>(reinterpret_cast<const char*>(base) + off); };
+        px = at(p.means, o3)[0];
+        py = at(p.means, o3)[1];
+        pz = at(p.means, o3)[2];
+        q = *reinterpret_cast<const float4*>(at(p.rots, ic * 16u));
+        sx = at(p.scales, o3)[0];
+        sy = at(p.scales, o3)[1];
+        sz = at(p.scales, o3)[2];
+        opac = at(p.opac, ic * 4u)[0];
+        f0 = at(p.lang, o3)[0];
+        f1 = at(p.lang, o3)[1];
+        f2 = at(p.lang, o3)[2];
+        dc[0] = at(p.shs, o3)[0];
+        dc[1] = at(p.shs, o3)[1];
+        dc[2] = at(p.shs, o3)[2];
+        const char* row = reinterpret_cast<const char*>(p.shs_rest) + ic * 180u;
+#pragma unroll
+        for (int k = 0; k < 11; k++) {
+            const float4 v = *reinterpret_cast<const float4*>(row + 16 * k);
+            rr[4 * k] = v.x;
+            rr[4 * k + 1] = v.y;
+            rr[4 * k + 2] = v.z;
+            rr[4 * k + 3] = v.w;
+        }
+        rr[44] = *reinterpret_cast<const float*>(row + 176);
+        // a compiler-only memory clobber: the loads stay here, all in flight together, instead of
+        // being sunk into the culling branches that use them (which made three round trips: the
+        // means, then the rotation / scales behind the near-plane test, then the rest)
+        asm volatile("" ::: "memory");
+    } else if (live) {
+        // 32-bit byte offsets on uniform bases (one VGPR per row width instead of a 64-bit address
+        // per array; the launcher keeps 16 P below 2^31)
+        const uint32_t o3 = (uint32_t)i * 12u, o4 = (uint32_t)i * 16u;
+        auto at = [](const float* base, uint32_t off) { return reinterpret_cast<const float*>(reinterpret_cast<const char*>(base) + off); };
+        px = at(p.means, o3)[0];
+        py = at(p.means, o3)[1];
+        pz = at(p.means, o3)[2];
         if (p.cov_pre) {
 #pragma unroll
             for (int k = 0; k < 6; k++) cov[k] = p.cov_pre[6 * (size_t)i + k];
         } else {
-            q = *reinterpret_cast<const float4*>(p.rots + 4 * (size_t)i);
-            sx = p.scales[3 * i];
-            sy = p.scales[3 * i + 1];
-            sz = p.scales[3 * i + 2];
+            q = *reinterpret_cast<const float4*>(at(p.rots, o4));
+            sx = at(p.scales, o3)[0];
+            sy = at(p.scales, o3)[1];
+            sz = at(p.scales, o3)[2];
         }
-        opac = p.opac[i];
+        opac = at(p.opac, 4u * (uint32_t)i)[0];
         if (feat) {
-            f0 = p.lang[3 * i];
-            f1 = p.lang[3 * i + 1];
-            f2 = p.lang[3 * i + 2];
+            f0 = at(p.lang, o3)[0];
+            f1 = at(p.lang, o3)[1];
+            f2 = at(p.lang, o3)[2];
+        }
+        if (dma) {
+            dc[0] = at(p.shs, o3)[0];
+            dc[1] = at(p.shs, o3)[1];
+            dc[2] = at(p.shs, o3)[2];
         }
     }
-    if (p.shs) {
+    if (p.shs && kSh != kShDirect) {
         if (blockIdx.x * blockDim.x >= p.P) return;  // block-uniform
-        stage_sh_in<12>(p.shs, p.shs_rest, p.P, p.M, s_sh);
+        if (dma) {
+            stage_rest_dma(p.shs_rest, p.P, p.M, s_sh);
+            __builtin_amdgcn_s_waitcnt(0);  // the LDS-DMA writes have landed (vmcnt 0)
+        } else {
+            stage_sh_in<12>(p.shs, p.shs_rest, p.P, p.M, s_sh);
+        }
         __syncthreads();
     }
+    // SH -> RGB (+0.5, clamp at 0, clamp flags: gaussian_renderer/__init__.py:80 semantics)
+    float rgb[3];
+    uint32_t clamp_bits = 0;
+    auto eval_rgb = [&]() {
+        const float dox = px - campos[0], doy = py - campos[1], doz = pz - campos[2];
+        const float len = sqrtf(dot3(dox, doy, doz, dox, doy, doz));
+        const float x = dox / len, y = doy / len, z = doz / len;
+        const float* sh = kSh == kShDirect ? rr
+                        : dma ? s_sh + threadIdx.x * (3 * (p.M - 1)) : s_sh + threadIdx.x * (3 * p.M + 1) + 3;
+#pragma unroll
+        for (int ch = 0; ch < 3; ch++) {
+            const float c0 = dma ? dc[ch] : sh[ch - 3];
+            const float v = sh_eval_channel(p.D, c0, sh + ch, x, y, z) + 0.5f;
+            clamp_bits |= (v < 0.0f ? 1u : 0u) << ch;
+            rgb[ch] = fmaxf(v, 0.0f);
+        }
+    };
+#ifndef LSR_PRE_EARLY_SH  // measurement knob: kShDirect evaluates the SH before the projection
+#define LSR_PRE_EARLY_SH 0
+#endif
+    // (its 45 registers free before the projection arithmetic; culled Gaussians evaluate it too)
+    constexpr bool early = kSh == kShDirect && LSR_PRE_EARLY_SH;
+    if (early && live) eval_rgb();
     // per-thread contributions to the block partials: tile instances, super-tile entries, depth key
     uint32_t my_tiles = 0, my_supers = 0, my_key = 0xFFFFFFFFu, my_err = 0;
     bool vis = false;  // reached the end of the block below (else culled: written after it)
     if (live) do {  // `break` = culled
-    const float3 pv = xform4x3(p.view, px, py, pz);
+    const float3 pv = xform4x3(view, px, py, pz);
     if (pv.z <= 0.2f) {
         if (p.prefiltered) my_err = 0x80000000u;
         break;
     }
-    const float3 hom = xform4x3(p.proj, px, py, pz);
-    const float hw = xform4w(p.proj, px, py, pz);
+    const float3 hom = xform4x3(proj, px, py, pz);
+    const float hw = xform4w(proj, px, py, pz);
     const float p_w = 1.0f / (hw + 0.0000001f);
     const float proj_x = hom.x * p_w, proj_y = hom.y * p_w;
 
@@ -181,7 +319,7 @@ __global__ __launch_bounds__(kPreThreads) void k_preprocess(PreprocessParams p)
         }
         cov3d(sx, sy, sz, p.scale_modifier, q, cov);
     }
-    const Cov2D cv = cov2d(px, py, pz, p.focal_x, p.focal_y, p.tanfovx, p.tanfovy, cov, p.view);
+    const Cov2D cv = cov2d(px, py, pz, p.focal_x, p.focal_y, p.tanfovx, p.tanfovy, cov, view);
     const float a = cv.a, b = cv.b, c = cv.c;
     const float det = a * c - b * b;
     if (det == 0.0f) break;
@@ -199,19 +337,8 @@ __global__ __launch_bounds__(kPreThreads) void k_preprocess(PreprocessParams p)
     const uint32_t area = (uint32_t)((r4[2] - r4[0]) * (r4[3] - r4[1]));
     if (area == 0) break;
 
-    float rgb[3];
-    uint32_t clamp_bits = 0;
     if (p.shs) {
-        const float dox = px - p.campos[0], doy = py - p.campos[1], doz = pz - p.campos[2];
-        const float len = sqrtf(dot3(dox, doy, doz, dox, doy, doz));
-        const float x = dox / len, y = doy / len, z = doz / len;
-        const float* sh = s_sh + threadIdx.x * (3 * p.M + 1);
-#pragma unroll
-        for (int ch = 0; ch < 3; ch++) {
-            const float v = sh_eval_channel(p.D, sh + ch, x, y, z) + 0.5f;
-            clamp_bits |= (v < 0.0f ? 1u : 0u) << ch;
-            rgb[ch] = fmaxf(v, 0.0f);
-        }
+        if (!early) eval_rgb();
     } else {
         rgb[0] = p.colors[3 * i];
         rgb[1] = p.colors[3 * i + 1];
@@ -281,7 +408,6 @@ __global__ __launch_bounds__(kPreThreads) void k_preprocess(PreprocessParams p)
     }
 }
 
-static size_t sh_lds_bytes(const float* shs, int M) { return shs ? kPreThreads * (size_t)(3 * M + 1) * 4 : 0; }
 
 // dynamic LDS beyond the 64 KiB default (M > 20 stored SH coefficients) must be opted into
 static hipError_t allow_lds(const void* fn, size_t bytes)
@@ -294,10 +420,23 @@ static hipError_t allow_lds(const void* fn, size_t bytes)
 hipError_t launch_preprocess(const PreprocessParams& p, hipStream_t s)
 {
     if (p.P == 0) return hipSuccess;
-    hipError_t e = allow_lds((const void*)k_preprocess, sh_lds_bytes(p.shs, p.M));
+    if (p.P >= (1 << 27)) return hipErrorInvalidValue;  // k_preprocess's 32-bit row offsets
+    size_t lds = sh_lds_bytes(p.shs, p.shs_rest, p.M);
+    static const int direct = [] {  // measurement knob: LSR_PRE_SH=dma (LDS-DMA staging instead)
+        const char* v = getenv("LSR_PRE_SH");
+        return v && v[0] == 'd' && v[1] == 'm' ? 0 : 1;
+    }();
+    const int mode = !sh_dma(p.shs, p.shs_rest, p.M) ? kShLds : (direct && p.M == 16 && p.D <= 3 && p.P < (1 << 31) / 180 && !p.cov_pre && p.include_feature && p.lang)
+                   ? kShDirect : kShDma;
+    const void* fn = mode == kShDirect ? (const void*)k_preprocess<kShDirect>
+                   : mode == kShDma ? (const void*)k_preprocess<kShDma> : (const void*)k_preprocess<kShLds>;
+    if (mode == kShDirect) lds = 0;
+    hipError_t e = allow_lds(fn, lds);
     if (e != hipSuccess) return e;
     const int nb = (p.P + kPreThreads - 1) / kPreThreads;
-    hipLaunchKernelGGL(k_preprocess, dim3(nb), dim3(kPreThreads), sh_lds_bytes(p.shs, p.M), s, p);
+    if (mode == kShDirect) hipLaunchKernelGGL(k_preprocess<kShDirect>, dim3(nb), dim3(kPreThreads), 0, s, p);
+    else if (mode == kShDma) hipLaunchKernelGGL(k_preprocess<kShDma>, dim3(nb), dim3(kPreThreads), lds, s, p);
+    else hipLaunchKernelGGL(k_preprocess<kShLds>, dim3(nb), dim3(kPreThreads), lds, s, p);
     return hipGetLastError();  // the block partials are reduced by launch_publish_counters
 }
 
@@ -671,10 +810,11 @@ __device__ __forceinline__ void preprocess_backward_one(const PreprocessBwdParam
 hipError_t launch_preprocess_backward(const PreprocessBwdParams& p, hipStream_t s)
 {
     if (p.P == 0) return hipSuccess;
-    hipError_t e = allow_lds((const void*)k_preprocess_backward, sh_lds_bytes(p.shs, p.M));
+    const size_t lds = kPreThreads * (size_t)(3 * p.M + 1) * 4 * (p.shs ? 1 : 0);
+    hipError_t e = allow_lds((const void*)k_preprocess_backward, lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_preprocess_backward, dim3((p.P + kPreThreads - 1) / kPreThreads), dim3(kPreThreads),
-                       sh_lds_bytes(p.shs, p.M), s, p);
+                       lds, s, p);
     return hipGetLastError();
 }
 

@@ -46,11 +46,17 @@ FUSED_CASES = [
     dict(P=500, W=67, H=45, seed=1, sh_degree=3, active_degree=1),
     dict(P=300, W=48, H=40, seed=2, sh_degree=0),
     dict(P=600, W=80, H=64, seed=3, sh_degree=2, include_feature=False),
+    # last block of 117 Gaussians: 5265 rest floats, a float4 run plus a 1-float tail (LDS-DMA staging)
+    dict(P=501, W=64, H=48, seed=5, sh_degree=3),
+    # _features_rest not 16-B aligned: the register-staged path
+    dict(P=450, W=64, H=48, seed=6, sh_degree=3, misaligned=True),
 ]
 
 
 @pytest.mark.parametrize("case", FUSED_CASES)
 def test_fused_forward_bit_exact_and_backward(case):
+    case = dict(case)
+    misaligned = case.pop("misaligned", False)
     inc = case.get("include_feature", True)
     g, st = _raw_scene(**case)
     P, W, H = case["P"], case["W"], case["H"]
@@ -60,6 +66,10 @@ def test_fused_forward_bit_exact_and_backward(case):
     gd = g.to(DEV)
     raw = _native.RAW_OPACITY | _native.RAW_SCALES | _native.RAW_ROTATIONS | (_native.RAW_LANGUAGE if inc else 0)
     rest = gd.features_rest.contiguous() if gd.features_rest.shape[1] > 0 else None
+    if misaligned:
+        buf = torch.empty(rest.numel() + 1, device=DEV)
+        rest = buf[1:].view(rest.shape).copy_(rest)
+        assert rest.data_ptr() % 16 != 0
     out = _native.rasterize_gaussians(std, gd.xyz, gd.features_dc.contiguous(), None,
                                       gd.language_feature if inc else None, gd.opacity, gd.scaling, gd.rotation,
                                       None, raw=raw, shs_rest=rest)
