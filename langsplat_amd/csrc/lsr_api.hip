@@ -7,6 +7,7 @@
 #include <math.h>
 #include <stdio.h>
 #include <string.h>
+#include <time.h>
 
 #include <map>
 #include <mutex>
@@ -18,6 +19,53 @@
 using namespace lsr;
 
 static thread_local std::string g_last_error;
+
+// ------------------------------------------------------------------ host timeline (measurement)
+// LSR_HOST_TRACE=1: host timestamps of each lsr_forward's phases, averaged and printed at exit
+// (where the host spends the time between the counter hand-off and the next launches).
+namespace {
+struct HostTrace {
+    bool on = false;
+    static constexpr int kMarks = 7;
+    const char* names[kMarks] = {"entry->preprocess", "->depth order", "->binning alloc", "->wait returned",
+                                 "->binning enqueued", "->forward enqueued", "(unused)"};
+    double acc[kMarks] = {};
+    int64_t calls = 0;
+    HostTrace()
+    {
+        const char* v = getenv("LSR_HOST_TRACE");
+        on = v && v[0] == '1';
+    }
+    ~HostTrace()
+    {
+        if (!on || calls == 0) return;
+        fprintf(stderr, "lsr host trace over %lld forwards (us):", (long long)calls);
+        for (int i = 0; i < kMarks - 1; i++) fprintf(stderr, " %s %.2f", names[i], acc[i] / calls);
+        fprintf(stderr, "\n");
+    }
+};
+HostTrace g_host_trace;
+inline double now_us()
+{
+    timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec * 1e6 + ts.tv_nsec * 1e-3;
+}
+struct HostMarks {
+    double t[HostTrace::kMarks + 1];
+    int n = 0;
+    void mark()
+    {
+        if (g_host_trace.on && n <= HostTrace::kMarks) t[n++] = now_us();
+    }
+    ~HostMarks()
+    {
+        if (!g_host_trace.on || n < HostTrace::kMarks) return;
+        for (int i = 0; i + 1 < n; i++) g_host_trace.acc[i] += t[i + 1] - t[i];
+        g_host_trace.calls++;
+    }
+};
+}  // namespace
 
 // ------------------------------------------------------------------ opt-in event profiler
 namespace {
@@ -146,12 +194,17 @@ bool counters_arrived(const HostBlock* hb, uint32_t seq)
     return true;
 }
 
-// Waits until the counters published with `seq` arrived; a HIP error on failure.
+// Waits until the counters published with `seq` arrived; a HIP error on failure.  The stream is
+// queried only after the first millisecond of waiting (then once per ~1 ms): a query costs tens of
+// microseconds of host time, and counters landing during one were seen that much later.
 hipError_t wait_counters(const HostBlock* hb, uint32_t seq, hipStream_t stream)
 {
+    if (counters_arrived(hb, seq)) return hipSuccess;
+    double next_query = now_us() + 1000.0;
     for (uint64_t spin = 0;; spin++) {
         if (counters_arrived(hb, seq)) return hipSuccess;
-        if ((spin & 1023) == 1023) {
+        if ((spin & 255) == 255 && now_us() > next_query) {
+            next_query = now_us() + 1000.0;
             const hipError_t q = hipStreamQuery(stream);
             if (q != hipSuccess && q != hipErrorNotReady) return q;
             if (q == hipSuccess) {  // stream idle: the stores must be visible now
@@ -276,6 +329,8 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
         return LSR_OK;
     }
 
+    HostMarks hm;
+    hm.mark();
     Layout L = make_layout(P, W, H, 0, 0);
     if (L.supers > 65536) return fail(LSR_ERR_INVALID, "lsr_forward: image larger than 65536 super-tiles");
     hipError_t herr = hipSuccess;
@@ -327,6 +382,7 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
     pp.shs_rest = a->shs_rest;
     pp.partial = reinterpret_cast<uint4*>(geom + L.pre_partial);
     LSR_TRY(launch_preprocess(pp, stream), "preprocess");
+    hm.mark();
 
     // The one host wait: num_rendered R and the super-tile entries E size the binning buffer, and
     // the visible depth-key range fixes the number of depth-sort passes.  The depth sort is enqueued
@@ -339,6 +395,7 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
             "publish counters");
     const int guess = hb->depth_passes > 0 ? hb->depth_passes : 4;
     LSR_TRY(launch_depth_order(P, guess, L, geom, counters, &hb->stall, stream, debug), "depth order");
+    hm.mark();
     // the binning buffer from the last forward's size while the GPU works (the allocator callback
     // is host work that would otherwise sit between the wait and the binning launches)
     char* binning = nullptr;
@@ -347,7 +404,9 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
         binning = static_cast<char*>(alloc(user, LSR_BUF_BINNING, hb->binning_hint));
         binning_have = binning ? hb->binning_hint : 0;
     }
+    hm.mark();
     LSR_TRY(wait_counters(hb, seq, stream), "wait counters");
+    hm.mark();
     uint32_t host_cnt[8];
     for (int i = 0; i < 8; i++) host_cnt[i] = (uint32_t)hb->slot[i];
     if (host_cnt[kCntError] && s->prefiltered)
@@ -378,6 +437,7 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
     hb->hint_H = H;
     hb->binning_hint = L.binning_bytes + L.binning_bytes / 8;  // 12.5 % headroom for the next view
     LSR_TRY(launch_binning(P, R, L, geom, image, binning, &hb->stall, stream, debug), "binning");
+    hm.mark();
     RenderParams rp{};
     rp.W = W;
     rp.H = H;
@@ -406,6 +466,7 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
         rp.out_loss = a->out_loss;
     }
     LSR_TRY(launch_render_forward(rp, L.tiles, stream), "render forward");
+    hm.mark();
     return LSR_OK;
 }
 
