@@ -131,6 +131,22 @@ def algorithmic_bytes(stage, P, V, R, HW, M, color_grad=True, geometry=True, fus
     }.get(stage)
 
 
+def survey_step_bytes(P, R, HW, M, geometry):
+    """SURVEY.md §8d's implementation-independent traffic model of one rasterizer fwd+bwd,
+    bytes = P*B_G + I*B_I + HW*B_px, with B_G following the gradients the step computes: with
+    geometry gradients 312 + 36M (§8d as written); in the language step (geometry frozen) the
+    preprocess backward's reads (76 + 12M) and writes (40 + 12M) are replaced by what the
+    gradient epilogue moves (the 5-value record 20 in, dL/dmeans2D 12 + dL/dlanguage 12 out) and
+    the render backward's record is 5 values (2 x 20) instead of 12 (2 x 48); the language
+    feature's own read (12) is added in both.  B_I = 148, B_px = 64 (§8d)."""
+    sh = 12 * M
+    if geometry:
+        b_g = 312 + 3 * sh + 12
+    else:
+        b_g = (44 + sh) + 48 + 8 + 2 * 20 + (20 + 24) + 12
+    return P * b_g + R * 148 + HW * 64
+
+
 # the timed loop records the dominant kernel's events on every LIVE_EVENT_EVERY-th step
 LIVE_EVENT_EVERY = 5
 
@@ -360,6 +376,13 @@ def main():
         if valu is not None:
             roofline["valu_issue_frac"] = round(valu, 3)
             roofline["valu_source"] = vsrc
+        # north_star's "% of HBM roofline" in SURVEY.md §8d's form: the whole rasterizer fwd+bwd
+        # (every profiled stage except the optimizer) against the §8d traffic model
+        raster_stage_ms = sum(v["total_ms"] for k, v in prof.items() if k != "adam") / prof_steps
+        sb = survey_step_bytes(P, nr, W * H, M, geometry)
+        s_ach = sb / (raster_stage_ms * 1e-3) / 1e9
+        roofline["fwd_bwd_model"] = {"bytes": int(sb), "ms": round(raster_stage_ms, 4), "achieved": round(s_ach, 2),
+                                     "frac": round(s_ach / HBM_PEAK_GBS, 4), "source": "SURVEY.md §8d"}
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(cfg)

@@ -394,7 +394,10 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
     LSR_TRY(launch_publish_counters((P + kPreThreads - 1) / kPreThreads, pp.partial, counters, hb->slot, seq, stream),
             "publish counters");
     const int guess = hb->depth_passes > 0 ? hb->depth_passes : 4;
-    LSR_TRY(launch_depth_order(P, guess, L, geom, counters, &hb->stall, stream, debug), "depth order");
+    // MSD path: the bucket sort also emits the super-tile entries (into geometry arrays of fixed
+    // capacity, so no host value is needed); used below when they fitted
+    const bool fused_emit = !depth_order_uses_pass_count(P) && fused_emit_enabled();
+    LSR_TRY(launch_depth_order(P, guess, L, geom, counters, &hb->stall, stream, debug, fused_emit), "depth order");
     hm.mark();
     // the binning buffer from the last forward's size while the GPU works (the allocator callback
     // is host work that would otherwise sit between the wait and the binning launches)
@@ -427,6 +430,11 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
         }
     }
 
+    const bool emitted = fused_emit && (int64_t)host_cnt[kCntSuper] <= L.fused_cap;
+    if (fused_emit && !emitted) {  // entries beyond the fused capacity: the depth order again, unfused
+        LSR_TRY(hipMemsetAsync(geom + L.scan_regions, 0, 4 * L.zero_words, stream), "clear scan status");
+        LSR_TRY(launch_depth_order(P, guess, L, geom, counters, &hb->stall, stream, debug, false), "depth order");
+    }
     L = make_layout(P, W, H, R, (int64_t)host_cnt[kCntSuper]);
     if (!binning || L.binning_bytes > binning_have) {
         binning = static_cast<char*>(alloc(user, LSR_BUF_BINNING, L.binning_bytes));
@@ -436,7 +444,7 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
     hb->hint_W = W;
     hb->hint_H = H;
     hb->binning_hint = L.binning_bytes + L.binning_bytes / 8;  // 12.5 % headroom for the next view
-    LSR_TRY(launch_binning(P, R, L, geom, image, binning, &hb->stall, stream, debug), "binning");
+    LSR_TRY(launch_binning(P, R, L, geom, image, binning, &hb->stall, stream, debug, emitted), "binning");
     hm.mark();
     RenderParams rp{};
     rp.W = W;

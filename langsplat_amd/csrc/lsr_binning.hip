@@ -371,13 +371,32 @@ __device__ __forceinline__ void msd_digit(const uint32_t* kxf, int& shift, int& 
     nbits = bits - shift;
 }
 
+// Word ranges a kernel clears with grid-stride stores besides its own work (n = 0: none).  The
+// binning's first launch clears the tables its later kernels accumulate into or leave partly
+// unwritten (tile / super-tile ranges, the segment count table, the scans' status words).
+struct ZeroList {
+    uint32_t* p[4];
+    int n[4];
+};
+
+__device__ __forceinline__ void zero_words_strided(const ZeroList& z)
+{
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    const int stride = gridDim.x * blockDim.x;
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+        for (int w = r; w < z.n[k]; w += stride) z.p[k][w] = 0u;
+}
+
 template <int kItems>
 __global__ __launch_bounds__(kRadixThreads) void k_radix_hist(const uint32_t* __restrict__ keys, int n, int shift,
                                                               int nbits, uint32_t* __restrict__ hist, int nblk,
-                                                              const uint32_t* __restrict__ kxf, int remap, int msd)
+                                                              const uint32_t* __restrict__ kxf, int remap, int msd,
+                                                              ZeroList zero)
 {
     constexpr int kWaves = kRadixThreads / 64;
     __shared__ uint32_t wcnt[kWaves][256];
+    zero_words_strided(zero);
     if (msd) msd_digit(kxf, shift, nbits);
     const int blk = xcd_tile(nblk, remap);
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
@@ -554,7 +573,8 @@ static hipError_t radix_sort(const uint32_t* k0, const uint32_t* v0, int n, int 
                              uint32_t* vA, uint32_t* kB, uint32_t* vB, uint32_t* hist, uint32_t* hist_scan,
                              uint32_t* scan_regions, size_t region_words, uint32_t* stall, hipStream_t s, bool debug,
                              int* passes_out,
-                             const uint32_t* kxf = nullptr, ScatterTail last = ScatterTail{nullptr, nullptr, nullptr})
+                             const uint32_t* kxf = nullptr, ScatterTail last = ScatterTail{nullptr, nullptr, nullptr},
+                             ZeroList zero = ZeroList{})
 {
     const bool small = radix_small(n);
     const int tile = kRadixThreads * (small ? 4 : 16);
@@ -573,12 +593,13 @@ static hipError_t radix_sort(const uint32_t* k0, const uint32_t* v0, int n, int 
         const int nbits = (total_bits - shift) < 8 ? (total_bits - shift) : 8;
         uint32_t* kout = (pass & 1) ? kA : kB;
         uint32_t* vout = (pass & 1) ? vA : vB;
+        const ZeroList z = pass == 0 ? zero : ZeroList{};
         if (small)
             hipLaunchKernelGGL(k_radix_hist<4>, dim3(nblk), dim3(kRadixThreads), 0, s, kin, n, shift, nbits, hist, nblk,
-                               pass == 0 ? kxf : nullptr, remap, 0);
+                               pass == 0 ? kxf : nullptr, remap, 0, z);
         else
             hipLaunchKernelGGL(k_radix_hist<16>, dim3(nblk), dim3(kRadixThreads), 0, s, kin, n, shift, nbits, hist,
-                               nblk, pass == 0 ? kxf : nullptr, remap, 0);
+                               nblk, pass == 0 ? kxf : nullptr, remap, 0, z);
         if ((e = post(debug, s)) != hipSuccess) return e;
         if ((e = scan_exclusive(hist, hist_scan, (1 << nbits) * nblk, scan_regions + pass * region_words, nullptr,
                                 stall, s, debug)) != hipSuccess)
@@ -807,6 +828,93 @@ __device__ __forceinline__ uint32_t scan1024(uint32_t v, uint32_t* wsum, uint32_
     return before + x - v;
 }
 
+// Fused super-tile emission (round 2).  With `keys` set, the bucket workgroups also write what
+// k_emit_super would: each visible Gaussian's super-tile entries, in depth order, at the exclusive
+// prefix of the entry counts.  Every workgroup publishes its bucket's entry total ({flag, total} in
+// one 64-bit word) as soon as it has it, then sums its predecessors' words into its base (an LDS
+// bucket after its sort; a bucket sorted in global memory counts its entries before sorting).
+// Buckets are taken by ticket, so every predecessor of a waiting workgroup is already running, and
+// no workgroup waits before it has published.  A
+// wait that reaches the spin bound computes the base from the inputs instead (same value) and flags
+// the stall.  A workgroup whose entries would pass `cap` writes none: the host sees E > cap after
+// its wait and runs the depth order again without emission, then k_emit_super.  With emission the
+// depth-order arrays k_emit_super reads (sorted ids, ranked rectangles, local offsets) are not
+// written.
+struct BucketEmit {
+    uint32_t* keys;  // null: no emission
+    uint32_t* vals;
+    uint32_t cap;
+    uint64_t* status;  // 256 words + the ticket (status[256]), zero at launch
+    int sgx;
+    uint32_t* stall;
+    uint32_t spin_limit;
+    const uint32_t* depth_key;  // stall fallback: the entries of all Gaussians in lower buckets
+    const uint2* rect;
+    int P;
+};
+
+__device__ __forceinline__ void emit_entries(const BucketEmit& em, uint32_t o, uint32_t g, uint2 rc)
+{
+    if (rc.x == rc.y) return;  // culled: no entries
+    int sx0, sy0, sx1, sy1;
+    super_rect(rc, sx0, sy0, sx1, sy1);
+    for (int y = sy0; y < sy1; y++)
+        for (int x = sx0; x < sx1; x++) {
+            em.keys[o] = entry_key(rc, x, y, em.sgx);
+            em.vals[o] = g;
+            o++;
+        }
+}
+
+__device__ __forceinline__ void publish_bucket_total(const BucketEmit& em, int d, uint32_t total)
+{
+    if (em.keys && threadIdx.x == 0)
+        __hip_atomic_store(&em.status[d], kFlagAgg | (uint64_t)total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The entry base of bucket d: the sum of the totals of buckets 0..d-1 (every thread calls it).
+__device__ uint32_t bucket_entry_base(const BucketEmit& em, int d, const uint32_t* kxf, uint32_t* wsum)
+{
+    __shared__ uint32_t s_base;
+    __shared__ int s_ok;
+    const int t = threadIdx.x;
+    if (t < 64) {
+        uint32_t part = 0, spins = 0;
+        bool ok = true;
+        for (int b0 = 0; b0 < d && ok; b0 += 64) {
+            const int b = b0 + t;
+            uint64_t w = b < d ? __hip_atomic_load(&em.status[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kFlagAgg;
+            while (em.spin_limit == 0u || __ballot((w >> 62) == 0ull) != 0ull) {
+                if (em.spin_limit == 0u || ++spins > em.spin_limit) {
+                    ok = false;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+                if ((w >> 62) == 0ull) w = __hip_atomic_load(&em.status[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            part += (uint32_t)w;
+        }
+        part = wave_sum(part);
+        if (t == 0) {
+            s_base = part;
+            s_ok = ok ? 1 : 0;
+        }
+    }
+    __syncthreads();
+    if (s_ok) return s_base;
+    // stalled: the entries of every Gaussian whose top digit is below d, from the inputs
+    int shift, nbits;
+    msd_digit(kxf, shift, nbits);
+    const uint32_t mask = (1u << nbits) - 1u;
+    uint32_t part = 0;
+    for (int g = t; g < em.P; g += kBucketThreads)
+        if (((key_xf(em.depth_key[g], kxf) >> shift) & mask) < (uint32_t)d) part += super_count(em.rect[g]);
+    uint32_t tot;
+    scan1024(part, wsum, &tot);
+    if (t == 0) note_stall(em.stall);
+    return tot;
+}
+
 // One workgroup per bucket (top-digit value).  keys / ids: the MSD pass's output (transformed keys,
 // bucket-contiguous, id order inside a bucket; rect_ranked holds the rectangles in the same
 // layout); hist_scan: its scanned [digit][block] histogram, whose digit starts are the bucket
@@ -828,7 +936,7 @@ void k_depth_bucket_sort(
     int n, uint32_t* __restrict__ keys, uint32_t* __restrict__ ids, const uint32_t* __restrict__ hist_scan, int nblk,
     const uint32_t* __restrict__ kxf, const uint2* __restrict__ rect, uint32_t* __restrict__ sorted_ids,
     uint2* __restrict__ rect_ranked, uint32_t* __restrict__ local_off, uint32_t* __restrict__ totals,
-    uint32_t* __restrict__ scratch_k, int timeline)
+    uint32_t* __restrict__ scratch_k, int timeline, BucketEmit em)
 {
     const uint64_t t_start = timeline ? wall_clock64() : 0;
     struct TimelineGuard {  // written when the workgroup leaves, on every path
@@ -858,8 +966,14 @@ void k_depth_bucket_sort(
     } guard{timeline, t_start, 0, {0u, 0u, 0u, 0u}};
     extern __shared__ uint4 s_bucket_raw[];
     BucketLds& L = *reinterpret_cast<BucketLds*>(s_bucket_raw);
-    const int d = (int)blockIdx.x;
     const int t = threadIdx.x;
+    int d = (int)blockIdx.x;
+    if (em.keys) {  // fused emission: buckets by ticket (a waiting workgroup's predecessors run)
+        __shared__ int s_d;
+        if (t == 0) s_d = (int)atomicAdd(reinterpret_cast<uint32_t*>(em.status + 256), 1u);
+        __syncthreads();
+        d = s_d;
+    }
     // bucket range: both scanned starts are loaded (in bounds: the histogram has 256 digit rows)
     // together with the width (kxf), then discarded for digits beyond the width, whose histogram
     // rows the MSD pass did not write
@@ -876,6 +990,7 @@ void k_depth_bucket_sort(
     guard.nb = nb;
     if (nb <= 0) {  // no such top digit, or no key in it
         if (t == 0) totals[d] = 0u;
+        publish_bucket_total(em, d, 0u);
         return;
     }
     const int lowbits = shift;  // the bits below the top digit (equal top digits inside a bucket)
@@ -966,9 +1081,11 @@ void k_depth_bucket_sort(
         for (int r = 0; r < kBucketRounds; r++) {
             const int i = t + r * kBucketThreads;
             if (i < nb) {
-                const uint32_t o = start + (uint32_t)i;
-                sorted_ids[o] = id[r];
-                rect_ranked[o] = rc[r];
+                if (!em.keys) {  // fused emission: no later kernel reads the depth-order arrays
+                    const uint32_t o = start + (uint32_t)i;
+                    sorted_ids[o] = id[r];
+                    rect_ranked[o] = rc[r];
+                }
                 X[i] = super_count(rc[r]);
             }
         }
@@ -991,31 +1108,61 @@ void k_depth_bucket_sort(
         }
         if (t == 0) totals[d] = tot;
         __syncthreads();
+        if (!em.keys) {
+#pragma unroll
+            for (int r = 0; r < kBucketRounds; r++) {
+                const int i = t + r * kBucketThreads;
+                if (i < nb) local_off[start + i] = X[i];
+            }
+            return;
+        }
+        // the total is published once known (after the sort): a workgroup waiting for its base waits
+        // for the slowest predecessor's sort, which with buckets of similar size ends about when
+        // its own does (publishing before the sort put a rectangle load and a scan on every
+        // workgroup's critical path instead)
+        publish_bucket_total(em, d, tot);
+        const uint32_t ebase = bucket_entry_base(em, d, kxf, L.wsum);
+        if ((uint64_t)ebase + tot > (uint64_t)em.cap) return;  // over capacity: the host re-runs unfused
 #pragma unroll
         for (int r = 0; r < kBucketRounds; r++) {
             const int i = t + r * kBucketThreads;
-            if (i < nb) local_off[start + i] = X[i];
+            if (i < nb) emit_entries(em, ebase + X[i], id[r], rc[r]);
         }
         return;
     }
     // beyond LDS: global passes between (keys, ids) and (scratch_k, sorted_ids) over the bucket
+    uint32_t etot = 0;
+    if (em.keys) {  // the bucket's entry total first (bucket layout: any order gives the same sum)
+        uint32_t part = 0;
+        for (int i = t; i < nb; i += kBucketThreads) part += super_count(rect_ranked[start + i]);
+        scan1024(part, L.wsum, &etot);
+        publish_bucket_total(em, d, etot);
+    }
     const int res = bucket_global_sort(L, keys + start, ids + start, scratch_k + start, sorted_ids + start, nb,
                                        lowbits);
     const uint32_t* rid = res ? sorted_ids + start : ids + start;
+    const uint32_t ebase = em.keys ? bucket_entry_base(em, d, kxf, L.wsum) : 0u;
+    const bool emit = em.keys && (uint64_t)ebase + etot <= (uint64_t)em.cap;
     uint32_t carry = 0;
     for (int c0 = 0; c0 < nb; c0 += kBucketThreads) {  // in order, 1024 positions at a time
         const int i = c0 + t;
-        uint32_t cnt = 0;
+        uint32_t cnt = 0, g = 0;
+        uint2 rc = make_uint2(0u, 0u);
         if (i < nb) {
-            const uint32_t g = rid[i];
-            const uint2 rc = rect[g];
-            sorted_ids[start + i] = g;  // in place when rid aliases sorted_ids
-            rect_ranked[start + i] = rc;
+            g = rid[i];
+            rc = rect[g];
+            if (!em.keys) {
+                sorted_ids[start + i] = g;  // in place when rid aliases sorted_ids
+                rect_ranked[start + i] = rc;
+            }
             cnt = super_count(rc);
         }
         uint32_t tot;
         const uint32_t ex = scan1024(cnt, L.wsum, &tot);
-        if (i < nb) local_off[start + i] = carry + ex;
+        if (i < nb) {
+            if (!em.keys) local_off[start + i] = carry + ex;
+            if (emit) emit_entries(em, ebase + carry + ex, g, rc);
+        }
         carry += tot;
     }
     if (t == 0) totals[d] = carry;
@@ -1053,8 +1200,17 @@ bool depth_order_uses_pass_count(int P)
 
 // ---------------------------------------------------------------- depth order + super-tile counts
 
+bool fused_emit_enabled()
+{
+    static const bool v = [] {
+        const char* e = getenv("LSR_FUSED_EMIT");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+
 hipError_t launch_depth_order(int P, int passes, const Layout& L, char* geom, uint32_t* counters, uint32_t* stall,
-                              hipStream_t s, bool debug)
+                              hipStream_t s, bool debug, bool fused_emit)
 {
     if (P == 0) return hipSuccess;
     uint32_t* hist = reinterpret_cast<uint32_t*>(geom + L.radix_hist);
@@ -1085,10 +1241,10 @@ hipError_t launch_depth_order(int P, int passes, const Layout& L, char* geom, ui
         const int nblk = (P + kRadixThreads * (small ? 4 : 16) - 1) / (kRadixThreads * (small ? 4 : 16));
         if (small)
             hipLaunchKernelGGL(k_radix_hist<4>, dim3(nblk), dim3(kRadixThreads), 0, s, keys, P, 0, 8, hist, nblk, kxf,
-                               remap, 1);
+                               remap, 1, ZeroList{});
         else
             hipLaunchKernelGGL(k_radix_hist<16>, dim3(nblk), dim3(kRadixThreads), 0, s, keys, P, 0, 8, hist, nblk, kxf,
-                               remap, 1);
+                               remap, 1, ZeroList{});
         if ((e = post(debug, s)) != hipSuccess) return e;
         if ((e = scan_exclusive(hist, hist_scan, 256 * nblk, regions, nullptr, stall, s, debug)) != hipSuccess)
             return e;
@@ -1101,10 +1257,24 @@ hipError_t launch_depth_order(int P, int passes, const Layout& L, char* geom, ui
             hipLaunchKernelGGL((k_radix_scatter<16, true>), dim3(nblk), dim3(kRadixThreads), 0, s, keys,
                                (const uint32_t*)nullptr, P, 0, 8, hist_scan, nblk, kb, vb, kxf, carry, remap, 1);
         if ((e = post(debug, s)) != hipSuccess) return e;
-        // bucket-local offsets into super_offset, bucket totals for k_emit_super (no P-long scan)
+        // bucket-local offsets into super_offset, bucket totals for k_emit_super (no P-long scan);
+        // with fused emission also the super-tile entries themselves
+        BucketEmit em{};
+        if (fused_emit) {
+            em.keys = reinterpret_cast<uint32_t*>(geom + L.fused_keys);
+            em.vals = reinterpret_cast<uint32_t*>(geom + L.fused_vals);
+            em.cap = (uint32_t)L.fused_cap;
+            em.status = reinterpret_cast<uint64_t*>(geom + L.bucket_status);
+            em.sgx = L.sgx;
+            em.stall = stall;
+            em.spin_limit = stall_spin_limit();
+            em.depth_key = keys;
+            em.rect = tail.rect;
+            em.P = P;
+        }
         hipLaunchKernelGGL(k_depth_bucket_sort, dim3(256), dim3(kBucketThreads), kBucketLdsBytes, s, P, kb, vb,
                            (const uint32_t*)hist_scan, nblk, kxf, tail.rect, va, tail.rect_ranked, off,
-                           reinterpret_cast<uint32_t*>(geom + L.bucket_totals), ka, bucket_timeline_on());
+                           reinterpret_cast<uint32_t*>(geom + L.bucket_totals), ka, bucket_timeline_on(), em);
         return post(debug, s);
     }
     hipError_t e = (passes & 1)
@@ -1549,7 +1719,7 @@ static MsdOffsets msd_offsets(int P, const Layout& L, char* geom, char* image)
 }
 
 hipError_t launch_binning(int P, int64_t R, const Layout& L, char* geom, char* image, char* binning, uint32_t* stall,
-                          hipStream_t s, bool debug)
+                          hipStream_t s, bool debug, bool emitted)
 {
     uint2* ranges = reinterpret_cast<uint2*>(image + L.ranges);
     if (R == 0) return hipMemsetAsync(ranges, 0, 8 * (size_t)L.tiles, s);
@@ -1566,18 +1736,30 @@ hipError_t launch_binning(int P, int64_t R, const Layout& L, char* geom, char* i
     uint32_t* table = reinterpret_cast<uint32_t*>(binning + L.seg_table);
     uint32_t* pl = reinterpret_cast<uint32_t*>(binning + L.point_list);
     hipError_t e;
-    hipLaunchKernelGGL(k_emit_super, dim3((P + 255) / 256), dim3(256), 0, s, P, L.sgx,
-                       reinterpret_cast<const uint32_t*>(geom + L.sorted_ids),
-                       reinterpret_cast<const uint32_t*>(geom + L.super_offset),
-                       reinterpret_cast<const uint2*>(geom + L.rect_ranked), kA, vA,
-                       reinterpret_cast<uint32_t*>(ranges), 2 * L.tiles, reinterpret_cast<uint32_t*>(sranges),
-                       2 * L.supers, table, (int)L.seg_table_words, regions,
-                       (int)((L.super_passes + 1) * L.scan_region_bin), msd_offsets(P, L, geom, image));
-    if ((e = post(debug, s)) != hipSuccess) return e;
+    // the tables the kernels below accumulate into or leave partly unwritten, cleared by
+    // k_emit_super or (fused emission) by the super-tile sort's first histogram launch
+    const ZeroList zero{{reinterpret_cast<uint32_t*>(ranges), reinterpret_cast<uint32_t*>(sranges), table, regions},
+                        {2 * L.tiles, 2 * L.supers, (int)L.seg_table_words,
+                         (int)((L.super_passes + 1) * L.scan_region_bin)}};
+    const uint32_t* k0 = kA;
+    const uint32_t* v0 = vA;
+    if (emitted) {  // the depth order's bucket sort wrote the entries
+        k0 = reinterpret_cast<const uint32_t*>(geom + L.fused_keys);
+        v0 = reinterpret_cast<const uint32_t*>(geom + L.fused_vals);
+    } else {
+        hipLaunchKernelGGL(k_emit_super, dim3((P + 255) / 256), dim3(256), 0, s, P, L.sgx,
+                           reinterpret_cast<const uint32_t*>(geom + L.sorted_ids),
+                           reinterpret_cast<const uint32_t*>(geom + L.super_offset),
+                           reinterpret_cast<const uint2*>(geom + L.rect_ranked), kA, vA, zero.p[0], zero.n[0],
+                           zero.p[1], zero.n[1], zero.p[2], zero.n[2], zero.p[3], zero.n[3],
+                           msd_offsets(P, L, geom, image));
+        if ((e = post(debug, s)) != hipSuccess) return e;
+    }
     int passes = 0;
     uint32_t* bin_hist_scan = reinterpret_cast<uint32_t*>(binning + L.bin_radix_hist_scan);
-    e = radix_sort(kA, vA, (int)E, L.super_bits, kA, vA, kB, vB, reinterpret_cast<uint32_t*>(binning + L.bin_radix_hist),
-                   bin_hist_scan, regions, L.scan_region_bin, stall, s, debug, &passes);
+    e = radix_sort(k0, v0, (int)E, L.super_bits, kA, vA, kB, vB, reinterpret_cast<uint32_t*>(binning + L.bin_radix_hist),
+                   bin_hist_scan, regions, L.scan_region_bin, stall, s, debug, &passes, nullptr,
+                   ScatterTail{nullptr, nullptr, nullptr}, emitted ? zero : ZeroList{});
     if (e != hipSuccess) return e;
     const uint32_t* skeys = (passes & 1) ? kB : kA;
     const uint32_t* svals = (passes & 1) ? vB : vA;

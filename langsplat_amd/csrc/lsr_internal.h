@@ -37,6 +37,7 @@ constexpr int kSuper = 8;          // super-tile = kSuper x kSuper tiles (64-bit
 constexpr int kSegEntries = 512;   // super-tile list entries per binning workgroup
 constexpr int kGradStride = 16;                          // floats per Gaussian grad record
 constexpr int kGradStrideLang = 8;  // without geometry gradients: {dxy, dlang} in slots 0..4 (32 B)
+constexpr int kFusedEntries = 3;    // capacity of the fused super-tile emission, entries per Gaussian
 
 size_t radix_hist_words(int64_t n);   // per-block digit histograms for n keys
 size_t scan_region_words(int64_t n);  // look-back status + ticket of one scan of n words
@@ -50,6 +51,10 @@ struct Layout {
     size_t loss_words;        // fused loss: per-workgroup / per-group words and tickets, after the scan regions
     size_t zero_words;        // u32 words preprocess clears from scan_regions (scan status + loss words)
     size_t bucket_totals;     // MSD depth order: super-tile entries per top-digit bucket (256 u32)
+    size_t bucket_status;     // MSD depth order with fused emission: 256 {flag, bucket total} u64 words
+                              // + the bucket ticket, inside the range preprocess clears
+    size_t fused_keys, fused_vals;  // the super-tile entries the bucket sort emits (fused_cap each)
+    int64_t fused_cap;
     size_t grad_records;      // P x kGradStrideLang floats: the language step's gradient records (cleared
                               // by the render forward under LSR_FWD_ZERO_GRAD_RECORDS)
     size_t geom_bytes;
@@ -94,11 +99,17 @@ inline Layout make_layout(int P, int W, int H, int64_t R, int64_t E)
         const size_t gx = (size_t)(W + kTile - 1) / kTile, gy = (size_t)(H + kTile - 1) / kTile;
         const size_t loss_bytes = 8 * gx * gy;  // one word per render forward workgroup
         L.loss_words = take(loss_bytes);
-        L.zero_words = (L.loss_words + loss_bytes - L.scan_regions + 3) / 4;
+        L.bucket_status = take(8 * 257);
+        L.zero_words = (L.bucket_status + 8 * 257 - L.scan_regions + 3) / 4;
     }
     L.rect_ranked = take(8 * p);
     L.grad_records = take(4 * kGradStrideLang * p);
     L.bucket_totals = take(4 * 256);
+    // E is ~1.5 per visible Gaussian at 1080p; a view with more than kFusedEntries per Gaussian
+    // falls back to k_emit_super after the host wait
+    L.fused_cap = (int64_t)kFusedEntries * (int64_t)p;
+    L.fused_keys = take(4 * (size_t)L.fused_cap);
+    L.fused_vals = take(4 * (size_t)L.fused_cap);
     L.pre_partial = take(16 * ((p + kPreThreads - 1) / kPreThreads));
     L.geom_bytes = o;
 
@@ -220,14 +231,19 @@ hipError_t launch_mark_visible(int P, const float* means, const float* view, con
 // depth sort of all P Gaussians by (depth key, id) on `passes` 8-bit digits of the key minus the
 // smallest visible key (counters[kCntKeyMin/Max], from launch_preprocess) -> sorted_ids; per-Gaussian
 // super-tile entry offsets in that order
+// fused_emit (MSD path only): the bucket sort also writes the super-tile entries into L.fused_keys /
+// fused_vals when they fit (E <= L.fused_cap), so k_emit_super is not launched
 hipError_t launch_depth_order(int P, int passes, const Layout& L, char* geom, uint32_t* counters, uint32_t* stall,
-                              hipStream_t s, bool debug);
+                              hipStream_t s, bool debug, bool fused_emit = false);
 // false: the depth order reads its pass count on the device (MSD pass + per-bucket LDS sort) and
 // ignores `passes`; true (large P): LSD passes, `passes` must cover the visible key range
 bool depth_order_uses_pass_count(int P);
-// super-tile lists, per-(tile, segment) counts, scanned bases -> point_list and tile ranges
+// LSR_FUSED_EMIT=0 turns the fused super-tile emission off (measurement knob, read once)
+bool fused_emit_enabled();
+// super-tile lists, per-(tile, segment) counts, scanned bases -> point_list and tile ranges.
+// emitted: the depth order's bucket sort already wrote the E entries into L.fused_keys / fused_vals.
 hipError_t launch_binning(int P, int64_t R, const Layout& L, char* geom, char* image, char* binning, uint32_t* stall,
-                          hipStream_t s, bool debug);
+                          hipStream_t s, bool debug, bool emitted = false);
 
 // Look-back stall handling (k_scan, k_masked_l1_forward).  A single-pass look-back polls at most
 // stall_spin_limit() times for a predecessor's value; past that it computes the value itself from

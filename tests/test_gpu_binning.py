@@ -43,3 +43,27 @@ def test_super_tile_counts(W, H, supers):
     run, std, ind, out = check_forward_exact(st, inp)
     assert out[0] > 0
     check_backward(st, inp, run, out)
+
+
+def test_fused_emission_over_capacity():
+    """The depth sort's bucket workgroups write the super-tile entries themselves, into arrays of
+    kFusedEntries (3) entries per Gaussian (lsr_internal.h).  A view whose Gaussians meet more
+    super-tiles than that (E > 3 P) emits nothing there and takes k_emit_super after the host wait.
+    Large Gaussians on a 1280x720 image: both the forward and the backward stay exact."""
+    from tests.test_gpu_parity import state
+    P, W, H = 300, 1280, 720
+    g = torch.Generator().manual_seed(41)
+    cam = make_cameras(1, W, H)[0]
+    tx, ty = math.tan(cam.FoVx * 0.5), math.tan(cam.FoVy * 0.5)
+    d = 3.0 + torch.rand(P, generator=g) * 2.0
+    u, v = torch.rand(P, generator=g) * 2 - 1, torch.rand(P, generator=g) * 2 - 1
+    means = torch.stack([u * d * tx * 0.8, v * d * ty * 0.8, d - 4.0], 1)
+    inp = dict(means3D=means, opacities=torch.rand((P, 1), generator=g) * 0.3 + 0.05,
+               colors_precomp=torch.rand((P, 3), generator=g),
+               language_feature_precomp=torch.nn.functional.normalize(torch.randn((P, 3), generator=g)),
+               scales=0.15 + 0.15 * torch.rand((P, 3), generator=g),
+               rotations=torch.nn.functional.normalize(torch.randn((P, 4), generator=g)))
+    st = settings_for(cam, sh_degree=0)
+    run, std, ind, out = check_forward_exact(st, inp)
+    assert state(out, P, W, H)["counters"][4] > 3 * P  # E: beyond the fused capacity
+    check_backward(st, inp, run, out)
