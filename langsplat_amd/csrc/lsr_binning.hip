@@ -1597,13 +1597,21 @@ __global__ __launch_bounds__(256) void k_bin_count_fused(int S, int sgx, int sgy
     c.e1 = min(sr[s].y, c.e0 + (uint32_t)kSegEntries);
     c.nseg = super_segments(sr[s]);
     c.colpre = scol[s];
+    // the segment's (at most 2 x 256) keys loaded together: one memory round trip
+    constexpr int kBatches = kSegEntries / 256;
+    uint32_t kq[kBatches];
+#pragma unroll
+    for (int q = 0; q < kBatches; q++) {
+        const uint32_t e = c.e0 + (uint32_t)(q * 256 + t);
+        kq[q] = e < c.e1 ? keys[e] : 0u;
+    }
     if (t < 64) cnt[t] = 0;
     __syncthreads();
     uint32_t mine = 0;  // lane l: entries of this wave covering local tile l
-    for (uint32_t b = c.e0 + (t & ~63u); b < c.e1; b += 256) {
-        const uint32_t e = b + (t & 63);
-        const uint64_t m = e < c.e1 ? entry_mask(keys[e]) : 0ull;
-        mine += (uint32_t)__popcll(transpose64(m));
+#pragma unroll
+    for (int q = 0; q < kBatches; q++) {
+        const uint32_t e = c.e0 + (uint32_t)(q * 256 + t);
+        mine += (uint32_t)__popcll(transpose64(e < c.e1 ? entry_mask(kq[q]) : 0ull));
     }
     atomicAdd(&cnt[t & 63], mine);
     __syncthreads();
@@ -1633,6 +1641,16 @@ __global__ __launch_bounds__(256) void k_bin_emit(int S, int sgx, int gx, int gy
     if (!block_segment(S, seg_base, &s, &seg)) return;
     const SegmentCtx c = segment_ctx(s, seg, sgx, sranges, col_prefix);
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+    // both batches' entries loaded up front (a segment is at most kSegEntries = 2 x 256 entries):
+    // one memory round trip instead of one per batch
+    constexpr int kBatches = kSegEntries / 256;
+    uint32_t gq[kBatches], kq[kBatches];
+#pragma unroll
+    for (int q = 0; q < kBatches; q++) {
+        const uint32_t e = c.e0 + (uint32_t)(q * 256 + t);
+        gq[q] = e < c.e1 ? vals[e] : 0u;
+        kq[q] = e < c.e1 ? keys[e] : 0u;
+    }
     if (t < 64) {
         int gt = 0;
         const int64_t slot = table_slot(c, t, gx, gy, row_prefix, &gt);
@@ -1644,14 +1662,13 @@ __global__ __launch_bounds__(256) void k_bin_emit(int S, int sgx, int gx, int gy
             if (r.y > r.x) schedule_tile(sched_counts, sched_lists, gx * gy, gt, r.y - r.x);
         }
     }
-    for (uint32_t b = c.e0; b < c.e1; b += 256) {
+#pragma unroll
+    for (int q = 0; q < kBatches; q++) {
+        const uint32_t b = c.e0 + (uint32_t)(q * 256);
+        if (b >= c.e1) break;  // block-uniform
         const uint32_t e = b + t;
-        uint32_t g = 0;
-        uint64_t m = 0ull;
-        if (e < c.e1) {
-            g = vals[e];
-            m = entry_mask(keys[e]);
-        }
+        const uint32_t g = gq[q];
+        const uint64_t m = e < c.e1 ? entry_mask(kq[q]) : 0ull;
         colw[wave][lane] = transpose64(m);
         sg[wave][lane] = g;
         __syncthreads();

@@ -8,6 +8,7 @@ rounds=${3:-2}
 mkdir -p gpurun_out
 for r in $(seq 1 "$rounds"); do
     for v in $vals; do
-        env "$var=$v" timeout -k 10 120 python bench.py --no-cpu-baseline > "gpurun_out/ab_${var}_${v}_${r}.log" 2>&1
+        tag=$(basename "$v")
+        env "$var=$v" timeout -k 10 120 python bench.py --no-cpu-baseline > "gpurun_out/ab_${var}_${tag}_${r}.log" 2>&1
     done
 done
