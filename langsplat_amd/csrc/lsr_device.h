@@ -55,12 +55,13 @@ __device__ __forceinline__ float expf_exact(float x)
 }
 
 // expf_exact without the underflow branch, for the render loops: every alpha they use comes from a
-// power >= the cutoff of power_cutoff (> -6), where the two are the same operation sequence; the
-// clamp only keeps lanes whose result is discarded finite.  Branch-free, so the chains of
-// neighbouring list entries interleave.
+// power >= the cutoff of power_cutoff (> -6 for opacities up to 1e30), where the two are the same
+// operation sequence.  Lanes below the cutoff get a meaningless value that no test lets through
+// (the cutoff test rejects them whatever the alpha), so there is no clamp (it cost 3 VALU per
+// pair of entries in the forward walk).  Branch-free, so the chains of neighbouring list entries
+// interleave.
 __device__ __forceinline__ float expf_exact_render(float x)
 {
-    x = __builtin_fmaxf(x, -87.0f);
     const float t = __builtin_fmaf(x, 1.44269504088896341f, kExpShift);
     const float n = t - kExpShift;
     float r = __builtin_fmaf(n, -0.693145751953125f, x);
@@ -88,7 +89,6 @@ __device__ __forceinline__ lsr_f2 make_f2(float x, float y)
 }
 __device__ __forceinline__ lsr_f2 expf_exact_render2(lsr_f2 x)
 {
-    x = __builtin_elementwise_max(x, (lsr_f2)(-87.0f));
     const lsr_f2 t = __builtin_elementwise_fma(x, (lsr_f2)(1.44269504088896341f), (lsr_f2)(kExpShift));
     const lsr_f2 n = t - kExpShift;
     lsr_f2 r = __builtin_elementwise_fma(n, (lsr_f2)(-0.693145751953125f), x);

@@ -375,7 +375,9 @@ __global__ __launch_bounds__(kTilePixels) void k_render_forward(RenderParams p)
     __shared__ float4 sC[kThreads];  // r, g, b, f0
     __shared__ float4 sF[kThreads];  // f1, f2, -, -  (16-B slots: every record of slot s at byte 16 s)
     __shared__ uint8_t sM[kThreads];  // entry_cover mask
-    __shared__ uint16_t sL[kThreads / 64][kThreads];  // per-wave culled slot lists, as byte offsets 16 s
+    // per-wave culled slot lists, as byte offsets 16 s; slot n holds offset 0, so the walk reads the
+    // second entry of a pair without testing i + 1 < n (its result is discarded then)
+    __shared__ uint16_t sL[kThreads / 64][kThreads + 1];
     __shared__ uint32_t s_last;
 
     const int T = p.gx * p.gy;
@@ -441,6 +443,7 @@ __global__ __launch_bounds__(kTilePixels) void k_render_forward(RenderParams p)
         const int cnt = (int)min((uint32_t)kThreads, end - base);
         const int n = __builtin_amdgcn_readfirstlane(
             wave_compact(sM, cnt, 1u << wave, lane, sL[wave]));
+        if (lane == 0) sL[wave][n] = 0;
         __syncthreads();  // list visible to the wave's other lanes
         if (kStats) ph.lap(ph.compact);
         if (idx + kThreads < end) g_next = p.point_list[idx + kThreads];
@@ -457,7 +460,7 @@ __global__ __launch_bounds__(kTilePixels) void k_render_forward(RenderParams p)
             if (__ballot(q.T > 0.0f) == 0ull) break;
             const uint32_t o0 = sL[wave][i];
             const bool has1 = i + 1 < n;
-            const uint32_t o1 = has1 ? sL[wave][i + 1] : o0;
+            const uint32_t o1 = sL[wave][i + 1];
             const float4 A0 = *reinterpret_cast<const float4*>(cA + o0), B0 = *reinterpret_cast<const float4*>(cB + o0);
             const float4 A1 = *reinterpret_cast<const float4*>(cA + o1), B1 = *reinterpret_cast<const float4*>(cB + o1);
             // per entry {dx, dy} and {A.z dx, A.w dy} as packed ops on the record's own register pairs
