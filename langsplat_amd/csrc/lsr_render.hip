@@ -466,8 +466,10 @@ __global__ __launch_bounds__(kTilePixels) void k_render_forward(RenderParams p)
             // per entry {dx, dy} and {A.z dx, A.w dy} as packed ops on the record's own register pairs
             const lsr_f2 d0 = make_f2(A0.x, A0.y) - pxy, d1 = make_f2(A1.x, A1.y) - pxy;
             const lsr_f2 m0 = make_f2(A0.z, A0.w) * d0, m1 = make_f2(A1.z, A1.w) * d1;
-            const float pw0 = fma_(m0.x, d0.x, fma_(m0.y, d0.y, -((B0.x * d0.x) * d0.y)));
-            const float pw1 = fma_(m1.x, d1.x, fma_(m1.y, d1.y, -((B1.x * d1.x) * d1.y)));
+            // power = dx (A.z dx - conic.y dy) + (A.w dy) dy: 4 operations after {A.z dx, A.w dy}
+            // (the oracle's render_pixel / backward_pixel and the backward walk use the same order)
+            const float pw0 = fma_(d0.x, fma_(-B0.x, d0.y, m0.x), m0.y * d0.y);
+            const float pw1 = fma_(d1.x, fma_(-B1.x, d1.y, m1.x), m1.y * d1.y);
             const lsr_f2 G2 = expf_exact_render2(make_f2(pw0, pw1));
             const float al0 = fminf(0.99f, B0.y * G2.x);
             const float al1 = fminf(0.99f, B1.y * G2.y);
@@ -926,7 +928,7 @@ __device__ __forceinline__ void bwd_walk_entry(BwdPixel& q, const BwdEntry& E, i
     const float4& A = E.A;
     const float4& B = E.B;
     const float dx = A.x - pfx, dy = A.y - pfy;
-    const float pw = fma_(A.z * dx, dx, fma_(A.w * dy, dy, -((B.x * dx) * dy)));
+    const float pw = fma_(dx, fma_(-B.x, dy, A.z * dx), (A.w * dy) * dy);  // the forward's order
     bool h = kk < (int)q.last && pw <= 0.0f && pw >= B.z;
     if (__ballot(h) == 0ull) return;  // wave-uniform skip
     // hardware exp (a few ulp): gradients need 1e-4.  Only the 1/255 skip decision must equal the

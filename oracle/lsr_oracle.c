@@ -385,7 +385,7 @@ static void render_pixel(const lso_state* st, int tile, int px, int py, float* C
         const float* co = st->conic_o + 4 * g;
         float dx = st->xy[2 * g] - pfx, dy = st->xy[2 * g + 1] - pfy;
         float hx = -0.5f * co[0], hz = -0.5f * co[2];
-        float power = fmaf(hx * dx, dx, fmaf(hz * dy, dy, -((co[1] * dx) * dy)));
+        float power = fmaf(dx, fmaf(-co[1], dy, hx * dx), (hz * dy) * dy);
         if (power > 0.0f) continue;
         float alpha = fminf(0.99f, co[3] * lso_expf(power));
         if (alpha < 1.0f / 255.0f) continue;
@@ -644,7 +644,7 @@ static void backward_pixel(const lso_state* st, int tile, int px, int py, const 
         const float* co = st->conic_o + 4 * g;
         float dx = st->xy[2 * g] - pfx, dy = st->xy[2 * g + 1] - pfy;
         float hx = -0.5f * co[0], hz = -0.5f * co[2];
-        float power = fmaf(hx * dx, dx, fmaf(hz * dy, dy, -((co[1] * dx) * dy)));
+        float power = fmaf(dx, fmaf(-co[1], dy, hx * dx), (hz * dy) * dy);
         if (power > 0.0f) continue;
         float G = lso_expf(power);
         float alpha = fminf(0.99f, co[3] * G);
