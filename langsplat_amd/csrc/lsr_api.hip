@@ -464,7 +464,7 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
     rp.out_lang = a->out_language_feature;
     if (a->flags & LSR_FWD_ZERO_GRAD_RECORDS) {
         rp.zero_records = reinterpret_cast<float4*>(geom + L.grad_records);
-        rp.zero_records_n4 = (int64_t)P * kGradStrideLang / 4;
+        rp.zero_records_n4 = ((int64_t)P * kGradStrideLang + 3) / 4;
     }
     if (a->out_loss && rp.include_feature) {
         rp.loss_gt = a->loss_target;
@@ -509,7 +509,7 @@ int32_t lsr_backward(const lsr_settings* s, const lsr_backward_args* a, lsr_allo
     char* geom = static_cast<char*>(a->geom_buffer);
     char* image = static_cast<char*>(a->image_buffer);
     char* binning = static_cast<char*>(a->binning_buffer);
-    // the render backward's 5-value form (no geometry, no colour gradient) keeps 32-B records; the
+    // the render backward's 5-value form (no geometry, no colour gradient) keeps 20-B records; the
     // first backward of a forward that cleared them (LSR_FWD_ZERO_GRAD_RECORDS) uses them directly
     const bool compact = !geometry && !a->dL_dout_color;
     const int stride = compact ? kGradStrideLang : kGradStride;

@@ -36,7 +36,7 @@ constexpr int kPreThreads = LSR_PRE_THREADS;
 constexpr int kSuper = 8;          // super-tile = kSuper x kSuper tiles (64-bit tile masks)
 constexpr int kSegEntries = 512;   // super-tile list entries per binning workgroup
 constexpr int kGradStride = 16;                          // floats per Gaussian grad record
-constexpr int kGradStrideLang = 8;  // without geometry gradients: {dxy, dlang} in slots 0..4 (32 B)
+constexpr int kGradStrideLang = 5;  // without geometry gradients: {dxy, dlang}, packed 20-B records
 constexpr int kFusedEntries = 3;    // capacity of the fused super-tile emission, entries per Gaussian
 
 size_t radix_hist_words(int64_t n);   // per-block digit histograms for n keys
@@ -103,7 +103,7 @@ inline Layout make_layout(int P, int W, int H, int64_t R, int64_t E)
         L.zero_words = (L.bucket_status + 8 * 257 - L.scan_regions + 3) / 4;
     }
     L.rect_ranked = take(8 * p);
-    L.grad_records = take(4 * kGradStrideLang * p);
+    L.grad_records = take(4 * kGradStrideLang * p + 16);  // + padding: cleared as whole float4s
     L.bucket_totals = take(4 * 256);
     // E is ~1.5 per visible Gaussian at 1080p; a view with more than kFusedEntries per Gaussian
     // falls back to k_emit_super after the host wait

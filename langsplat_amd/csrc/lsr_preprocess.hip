@@ -832,10 +832,18 @@ __global__ __launch_bounds__(256) void k_grad_epilogue(int P, const int* __restr
     // every load is issued up front (one memory round trip): the records of culled Gaussians are
     // zero (the backward zero-fills them and adds nothing), radii only selects the zero result
     const int rad = radii[i];
-    // stride kGradStrideLang: {dx, dy, l0, l1}{l2, -, -, -}; kGradStride: the full record
-    const float4* g4 = reinterpret_cast<const float4*>(grad + (size_t)i * stride);
-    const float4 ga = g4[0];
-    const float4 gb = stride == kGradStrideLang ? g4[1] : g4[2];
+    // stride kGradStrideLang: the packed 20-B record {dx, dy, l0, l1, l2} (consecutive lanes read
+    // consecutive records: 20 B per Gaussian of HBM traffic); kGradStride: the full 64-B record
+    float4 ga, gb;
+    if (stride == kGradStrideLang) {
+        const float* r = grad + (size_t)i * kGradStrideLang;
+        ga = make_float4(r[0], r[1], r[2], r[3]);
+        gb = make_float4(r[4], 0.f, 0.f, 0.f);
+    } else {
+        const float4* g4 = reinterpret_cast<const float4*>(grad + (size_t)i * stride);
+        ga = g4[0];
+        gb = g4[2];
+    }
     const bool raw = raw_lang && lang && dlang;
     const float l0 = raw ? lang[i3] : 0.f, l1 = raw ? lang[i3 + 1] : 0.f, l2 = raw ? lang[i3 + 2] : 0.f;
     const bool live = rad > 0;

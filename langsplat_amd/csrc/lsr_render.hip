@@ -1093,7 +1093,7 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
                 const float val = sG[e * kGS + gslot<kColor, k5>(c)] * fscale;
                 if (val != 0.0f) {  // the id again from point_list (an L2 hit; saves 1 KB of LDS)
                     const uint32_t g = p.point_list[start + (uint32_t)(maxl - 1 - (done_cnt + e))];
-                    if (k5)  // compact 32-B record: the five values in slots 0..4
+                    if (k5)  // packed 20-B record: the five values in slots 0..4
                         atomicAdd(&p.grad[(size_t)g * kGradStrideLang + gslot<kColor, k5>(c)], val);
                     else
                         atomicAdd(&p.grad[(size_t)g * kGradStride + c], val);
