@@ -271,7 +271,7 @@ def main():
         if bucket is not None:
             bucket.all_reduce(average=True)
         optim.step()
-        optim.zero_grad(set_to_none=bucket is None)
+        optim.zero_grad(set_to_none=bucket is None or bucket.direct)
         return loss
 
     # blends and instance counts of this view (constant over steps: geometry is frozen)

@@ -30,25 +30,36 @@ def init_from_env(backend: str = None):
 
 
 class GradBucket:
-    """Flat fp32 buffer backing the .grad of every trainable parameter.
+    """The trainable parameters' gradients as ONE all-reduce buffer.
 
-    Call after the parameters exist and before the first backward.  Keep it by using
+    Several parameters (RGB mode: six groups): a flat fp32 buffer whose slices ARE the .grad
+    tensors.  Call after the parameters exist and before the first backward, and keep it by using
     optimizer.zero_grad(set_to_none=False) (a None .grad would detach the parameter from the
-    bucket); `zero()` does the same for the whole bucket in one memset.
+    bucket); `zero()` clears the whole bucket in one memset.
+
+    One parameter (LangSplat's language-feature step, scene/gaussian_model.py:203-217): `direct`
+    mode, no buffer of its own.  The .grad tensor autograd leaves (with zero_grad(set_to_none=True)
+    it is the rasterizer backward's own output, handed over without a copy) is contiguous and is
+    reduced in place -- no per-step memset of a bucket and no accumulate-add into it.
     """
 
     def __init__(self, params: Iterable[torch.nn.Parameter]):
         self.params: List[torch.Tensor] = [p for p in params if p.requires_grad]
         if not self.params:
             raise ValueError("GradBucket: no trainable parameters")
-        dev = self.params[0].device
-        total = sum(p.numel() for p in self.params)
-        self.flat = torch.zeros((total,), dtype=torch.float32, device=dev)
-        self.views = []
-        off = 0
         for p in self.params:
             if p.dtype != torch.float32:
                 raise TypeError("GradBucket expects fp32 parameters")
+        self.direct = len(self.params) == 1
+        self.flat = None
+        self.views = []
+        if self.direct:
+            return
+        dev = self.params[0].device
+        total = sum(p.numel() for p in self.params)
+        self.flat = torch.zeros((total,), dtype=torch.float32, device=dev)
+        off = 0
+        for p in self.params:
             v = self.flat[off:off + p.numel()].view_as(p)
             p.grad = v
             self.views.append(v)
@@ -56,25 +67,38 @@ class GradBucket:
 
     @property
     def nbytes(self) -> int:
-        return self.flat.numel() * 4
+        return sum(p.numel() for p in self.params) * 4
 
     def attached(self) -> bool:
+        if self.direct:
+            g = self.params[0].grad
+            return g is not None and g.is_contiguous()
         return all(p.grad is not None and p.grad.data_ptr() == v.data_ptr() for p, v in zip(self.params, self.views))
 
     def zero(self):
+        if self.direct:
+            if self.params[0].grad is not None:
+                self.params[0].grad.zero_()
+            return
         self.flat.zero_()
+
+    def buffer(self) -> torch.Tensor:
+        """The tensor the collective reduces (the flat bucket, or the one parameter's .grad)."""
+        return self.params[0].grad if self.direct else self.flat
 
     def all_reduce(self, average: bool = True, group=None):
         """SUM over ranks (then / world_size when average) -- the one collective of a step."""
         if not (dist.is_available() and dist.is_initialized()):
             return
         if not self.attached():
-            raise RuntimeError("GradBucket: a parameter's .grad no longer aliases the bucket "
-                               "(use zero_grad(set_to_none=False))")
+            raise RuntimeError("GradBucket: no gradient to reduce -- the parameter's .grad is missing or not "
+                               "contiguous (direct mode), or no longer aliases the bucket (use "
+                               "zero_grad(set_to_none=False) with several parameters)")
+        buf = self.buffer()
         if average and dist.get_backend(group) == "nccl":
             # RCCL's ncclAvg: the division is part of the collective (no separate scaling kernel)
-            dist.all_reduce(self.flat, op=dist.ReduceOp.AVG, group=group)
+            dist.all_reduce(buf, op=dist.ReduceOp.AVG, group=group)
             return
-        dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group)
+        dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
         if average:
-            self.flat.mul_(1.0 / dist.get_world_size(group))
+            buf.mul_(1.0 / dist.get_world_size(group))

@@ -60,6 +60,20 @@ def _worker(rank, world, port, out_dir):
             raise AssertionError("expected RuntimeError")
         except RuntimeError:
             pass
+        # one trainable parameter (the language-feature step): direct mode reduces the .grad
+        # autograd left (zero_grad(set_to_none=True): a fresh tensor each step) in place
+        lang1 = torch.nn.Parameter(torch.zeros((150, 3)))
+        direct = GradBucket([lang1, frozen])
+        assert direct.direct and direct.flat is None and direct.nbytes == 150 * 3 * 4
+        lang1.grad = gl.clone()
+        direct.all_reduce(average=False)
+        np.save(os.path.join(out_dir, f"direct_{rank}.npy"), lang1.grad.numpy())
+        lang1.grad = None  # set_to_none: nothing to reduce is an error, not a silent no-op
+        try:
+            direct.all_reduce()
+            raise AssertionError("expected RuntimeError")
+        except RuntimeError:
+            pass
     finally:
         dist.destroy_process_group()
 
@@ -74,6 +88,7 @@ def test_allreduced_bucket_equals_sum_of_view_gradients(tmp_path, world):
         np.testing.assert_allclose(np.load(tmp_path / f"lang_{r}.npy"), ref_l, rtol=1e-5, atol=1e-8)
         np.testing.assert_allclose(np.load(tmp_path / f"opac_{r}.npy"), ref_o, rtol=1e-5, atol=1e-8)
         np.testing.assert_allclose(np.load(tmp_path / f"lang_avg_{r}.npy"), ref_l / world, rtol=1e-5, atol=1e-8)
+        np.testing.assert_allclose(np.load(tmp_path / f"direct_{r}.npy"), ref_l, rtol=1e-5, atol=1e-8)
     # the ranks agree bit for bit (one collective, same result everywhere; float sums in ring order)
     for r in range(1, world):
         assert np.array_equal(np.load(tmp_path / f"lang_{r}.npy"), np.load(tmp_path / "lang_0.npy"))

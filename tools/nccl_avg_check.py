@@ -14,7 +14,11 @@ torch.cuda.set_device(0)
 dist.init_process_group("nccl")
 from langsplat_amd.distributed import GradBucket
 p = torch.nn.Parameter(torch.zeros(1000, 3, device="cuda"))
-b = GradBucket([p]); b.flat.fill_(2.0)
+q = torch.nn.Parameter(torch.zeros(10, 1, device="cuda"))
+b = GradBucket([p, q]); b.flat.fill_(2.0)  # flat bucket (several parameters)
 b.all_reduce(average=True); torch.cuda.synchronize()
 print("avg ok", dist.get_backend(), float(b.flat[0]), torch.equal(b.flat, torch.full_like(b.flat, 2.0)))
+d = GradBucket([p]); p.grad = torch.full((1000, 3), 2.0, device="cuda")  # direct mode (one parameter)
+d.all_reduce(average=True); torch.cuda.synchronize()
+print("direct avg ok", torch.equal(p.grad, torch.full_like(p.grad, 2.0)))
 dist.destroy_process_group()
