@@ -1508,7 +1508,10 @@ __global__ __launch_bounds__(256) void k_bin_count(int S, int sgx, int gx, int g
 // rank in tile l is popcount(column & lanes below) past the lower waves' columns.  The batch's
 // output is up to 64 contiguous runs (one per tile); it is staged in LDS tile-major and written
 // with consecutive lanes on consecutive addresses (batches over kStage instances store directly).
-constexpr int kStage = 4096;
+#ifndef LSR_BIN_STAGE  // staging capacity in instances (LDS: 5 B each); measurement knob
+#define LSR_BIN_STAGE 4096
+#endif
+constexpr int kStage = LSR_BIN_STAGE;
 
 // k_bin_count with the segment setup folded in, for a super-tile sort of ONE radix pass (S <= 256
 // super-tiles): the super-tile ranges are then the digit starts of the scanned [digit][block]

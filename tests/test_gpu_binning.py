@@ -4,7 +4,8 @@ The super-tile sort (lsr_binning.hip) is one 8-bit radix pass when the image has
 super-tiles of 8 x 8 tiles (1080p: 135), and then takes the fused count kernel
 (k_bin_count_fused: super-tile ranges straight from the scanned radix histogram); beyond 256
 super-tiles it takes two passes and the k_super_ranges / k_seg_setup kernels.  Both must give the
-oracle's per-tile lists, ranges and images bit for bit.
+oracle's per-tile lists, ranges and images bit for bit (up to 2188 super-tiles: a 140000 x 200
+image).
 """
 import math
 
@@ -35,7 +36,7 @@ def strip_scene(P, W, H, seed):
     return settings_for(cam, sh_degree=0), inp
 
 
-@pytest.mark.parametrize("W,H,supers", [(2000, 250, 32), (8192, 72, 64), (33000, 64, 258)])
+@pytest.mark.parametrize("W,H,supers", [(2000, 250, 32), (8192, 72, 64), (33000, 64, 258), (140000, 200, 2188)])
 def test_super_tile_counts(W, H, supers):
     st, inp = strip_scene(3000, W, H, seed=W + H)
     gx, gy = (W + 15) // 16, (H + 15) // 16
