@@ -768,7 +768,7 @@ __device__ __forceinline__ void bwd_pixel_init(BwdPixel& q, const RenderParams& 
 // (flush_scale): v[0] = dL/dmean2D.x / (2 ddelx_dx), v[1] likewise, v[2..4] = -2 dL/dconic.
 // A = {x, y, -conic.x / 2, -conic.z / 2}, B = {conic.y, opacity, .., ..}, hB = -conic.y / 2.
 template <bool kFeat, bool kColor, bool kGeo>
-__device__ __forceinline__ void bwd_pixel_blend(BwdPixel& q, float G, float alpha, float dx, float dy,
+__device__ __forceinline__ void bwd_pixel_blend(BwdPixel& q, float G, float og, float alpha, float dx, float dy,
                                                 const float4& A, const float4& B, const float3& C, const float3& F,
                                                 float hB, float (&v)[12])
 {
@@ -814,8 +814,8 @@ __device__ __forceinline__ void bwd_pixel_blend(BwdPixel& q, float G, float alph
     }
     // dL/dalpha = T (sum) - T_final / (1 - alpha) (bg . dL/dpix); bg_term = -T_final (bg . dL/dpix)
     dL_dalpha = kColor ? fma_(q.bg_term, inv_one_m, dL_dalpha * q.T) : dL_dalpha * q.T;
-    const float dL_dG = B.y * dL_dalpha;
-    if (kGeo) {  // conic and opacity partials: only the geometry gradients use them
+    if (kGeo) {
+        const float dL_dG = B.y * dL_dalpha;  // conic and opacity partials: only the geometry gradients use them
         const float ga = (G * dx) * dL_dG, gb = (G * dy) * dL_dG;
         // dG/ddelx dL/dG = -(ga conic.x + gb conic.y) = 2 (ga A.z - gb conic.y / 2), likewise y
         v[0] = fma_(-0.5f, gb * B.x, ga * A.z);
@@ -826,8 +826,10 @@ __device__ __forceinline__ void bwd_pixel_blend(BwdPixel& q, float G, float alph
         v[5] = G * dL_dalpha;
     } else {
         // the same two values factored as G dL/dG (A.z dx - conic.y dy / 2) and likewise y:
-        // A.z dx, A.w dy and conic.y dx are the power's own products (shared by CSE)
-        const float sG = G * dL_dG;
+        // A.z dx, A.w dy and conic.y dx are the power's own products (shared by CSE).
+        // G dL/dG = G o dL/dalpha with og = o G, the product the alpha was clamped from: one
+        // multiply instead of two (dL/dG itself is not needed here)
+        const float sG = og * dL_dalpha;
         v[0] = sG * fma_(hB, dy, A.z * dx);  // hB = -conic.y / 2
         v[1] = sG * fma_(-0.5f, B.x * dx, A.w * dy);
         v[2] = v[3] = v[4] = v[5] = 0.0f;
@@ -934,12 +936,14 @@ __device__ __forceinline__ void bwd_walk_entry(BwdPixel& q, const BwdEntry& E, i
     // hardware exp (a few ulp): gradients need 1e-4.  Only the 1/255 skip decision must equal the
     // forward's, so alphas within 1e-6 of it use the exact exp.
     float G = __expf(pw);
-    float al = fminf(0.99f, B.y * G);
+    float og = B.y * G;
+    float al = fminf(0.99f, og);
     const bool near = fabsf(al - 1.0f / 255.0f) < 1e-6f;
     if (__ballot(near) != 0ull) {  // wave-uniform: keeps the exact exp off the hot path
         if (near) {
             G = expf_exact(pw);
-            al = fminf(0.99f, B.y * G);
+            og = B.y * G;
+            al = fminf(0.99f, og);
         }
     }
     h = h && al >= 1.0f / 255.0f;
@@ -954,7 +958,7 @@ __device__ __forceinline__ void bwd_walk_entry(BwdPixel& q, const BwdEntry& E, i
             atomicAdd(&s_stat[8 + nh], 1u);
         }
     }
-    if (!h) al = G = 0.0f;
+    if (!h) al = G = og = 0.0f;
     float3 C = make_float3(0.f, 0.f, 0.f), F = make_float3(0.f, 0.f, 0.f);
     if (kColor) {
         C = make_float3(E.C.x, E.C.y, E.C.z);
@@ -963,7 +967,8 @@ __device__ __forceinline__ void bwd_walk_entry(BwdPixel& q, const BwdEntry& E, i
         F = kGeo ? make_float3(E.F.x, B.w, E.F.y) : make_float3(E.F.x, E.F.y, E.F.z);
     }
     float v[12];
-    bwd_pixel_blend<kFeat, kColor, kGeo>(q, G, al, dx, dy, A, B, C, F, (kColor || kGeo) ? -0.5f * B.x : E.F.w, v);
+    bwd_pixel_blend<kFeat, kColor, kGeo>(q, G, og, al, dx, dy, A, B, C, F, (kColor || kGeo) ? -0.5f * B.x : E.F.w,
+                                         v);
     if (k5) {
         const float tot = wave_reduce_scatter5(v, lane);
         if (scatter_writer5(lane)) atomicAdd(sG + (uint32_t)(j * kGS), tot);  // sG: this lane's slot
