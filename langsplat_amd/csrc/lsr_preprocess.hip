@@ -426,7 +426,7 @@ hipError_t launch_preprocess(const PreprocessParams& p, hipStream_t s)
         const char* v = getenv("LSR_PRE_SH");
         return v && v[0] == 'd' && v[1] == 'm' ? 0 : 1;
     }();
-    const int mode = !sh_dma(p.shs, p.shs_rest, p.M) ? kShLds : (direct && p.M == 16 && p.D <= 3 && p.P < (1 << 31) / 180 && !p.cov_pre && p.include_feature && p.lang)
+    const int mode = !sh_dma(p.shs, p.shs_rest, p.M) ? kShLds : (direct && p.M == 16 && p.D <= 3 && (int64_t)p.P * 180 < (int64_t)1 << 31 && !p.cov_pre && p.include_feature && p.lang)
                    ? kShDirect : kShDma;
     const void* fn = mode == kShDirect ? (const void*)k_preprocess<kShDirect>
                    : mode == kShDma ? (const void*)k_preprocess<kShDma> : (const void*)k_preprocess<kShLds>;

@@ -2,7 +2,7 @@
 host wall time per step, split into the time spent waiting on the GPU (the counter hand-off inside
 lsr_forward, synchronize) and the rest (Python, autograd, launches).
 
-    python tools/host_profile.py [steps]
+    python tools/host_profile.py [steps] [config]
 """
 import cProfile
 import os
@@ -24,7 +24,7 @@ from langsplat_amd.synthetic import CONFIGS, make_cameras, make_gaussians  # noq
 def main():
     steps = int(sys.argv[1]) if len(sys.argv) > 1 else 50
     dev = torch.device("cuda", 0)
-    c = CONFIGS["C3"]
+    c = CONFIGS[sys.argv[2] if len(sys.argv) > 2 else "C3"]
     params = make_gaussians(c["P"], seed=0, sh_degree=c["sh_degree"]).to(dev)
     model = bench.Model(params, include_feature=True)
     cam = make_cameras(1, c["width"], c["height"], device=dev)[0]
