@@ -157,7 +157,7 @@ DOMINANT_STAGE = "render backward"
 # k_render_backward<kStats, kFeat, kColor, kGeo>; the language step runs kColor = kGeo = false)
 STAGE_KERNEL = {"render backward": "lsr::k_render_backward<false, true, false, false>",
                 "render forward": "lsr::k_render_forward<false, true, true>",
-                "preprocess": "lsr::k_preprocess<1>", "preprocess backward": "lsr::k_preprocess_backward"}
+                "preprocess": "lsr::k_preprocess<2>", "preprocess backward": "lsr::k_preprocess_backward"}
 
 
 def pmc_traffic(stage):
