@@ -54,18 +54,19 @@ __device__ __forceinline__ float expf_exact(float x)
     return p * exp_scale(t);
 }
 
-// expf_exact without the underflow branch, for the render loops: every alpha they use comes from a
-// power >= the cutoff of power_cutoff (> -6 for opacities up to 1e30), where the two are the same
-// operation sequence.  Lanes below the cutoff get a meaningless value that no test lets through
-// (the cutoff test rejects them whatever the alpha), so there is no clamp (it cost 3 VALU per
+// The render loops' exp (oracle lso_expf_render): expf_exact's polynomial after a one-constant
+// range reduction (one FMA instead of two; <= 2 ulp for x >= -20, and every alpha the loops use
+// comes from a power >= the cutoff of power_cutoff, > -6 for opacities up to 1e30), and no
+// underflow branch.  Lanes below the cutoff get a meaningless value that no test lets through (the
+// cutoff test rejects them whatever the alpha), so there is no clamp either (it cost 3 VALU per
 // pair of entries in the forward walk).  Branch-free, so the chains of neighbouring list entries
 // interleave.
 __device__ __forceinline__ float expf_exact_render(float x)
 {
     const float t = __builtin_fmaf(x, 1.44269504088896341f, kExpShift);
     const float n = t - kExpShift;
-    float r = __builtin_fmaf(n, -0.693145751953125f, x);
-    r = __builtin_fmaf(n, -1.42860682030941723212e-6f, r);
+    // one-constant reduction (oracle lso_expf_render): |n| <= 8 on the compositing domain
+    const float r = __builtin_fmaf(n, -0.693147182464599609375f, x);
     float p = 1.38145383e-3f;  // degree 6 (oracle lso_expf): c0 = c1 = 1, c2..c6 fitted
     p = __builtin_fmaf(p, r, 8.36874545e-3f);
     p = __builtin_fmaf(p, r, 4.16683890e-2f);
@@ -90,8 +91,7 @@ __device__ __forceinline__ lsr_f2 expf_exact_render2(lsr_f2 x)
 {
     const lsr_f2 t = __builtin_elementwise_fma(x, (lsr_f2)(1.44269504088896341f), (lsr_f2)(kExpShift));
     const lsr_f2 n = t - kExpShift;
-    lsr_f2 r = __builtin_elementwise_fma(n, (lsr_f2)(-0.693145751953125f), x);
-    r = __builtin_elementwise_fma(n, (lsr_f2)(-1.42860682030941723212e-6f), r);
+    const lsr_f2 r = __builtin_elementwise_fma(n, (lsr_f2)(-0.693147182464599609375f), x);
     lsr_f2 p = (lsr_f2)(1.38145383e-3f);
     p = __builtin_elementwise_fma(p, r, (lsr_f2)(8.36874545e-3f));
     p = __builtin_elementwise_fma(p, r, (lsr_f2)(4.16683890e-2f));

@@ -941,7 +941,7 @@ __device__ __forceinline__ void bwd_walk_entry(BwdPixel& q, const BwdEntry& E, i
     const bool near = fabsf(al - 1.0f / 255.0f) < 1e-6f;
     if (__ballot(near) != 0ull) {  // wave-uniform: keeps the exact exp off the hot path
         if (near) {
-            G = expf_exact(pw);
+            G = expf_exact_render(pw);  // the forward's exp (pw >= cutoff > -6 here)
             og = B.y * G;
             al = fminf(0.99f, og);
         }

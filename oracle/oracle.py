@@ -65,6 +65,8 @@ def lib():
         L.lso_free.argtypes = [ctypes.c_void_p]
         L.lso_expf.restype = ctypes.c_float
         L.lso_expf.argtypes = [ctypes.c_float]
+        L.lso_expf_render.restype = ctypes.c_float
+        L.lso_expf_render.argtypes = [ctypes.c_float]
         L.lso_sh_eval.restype = None
         L.lso_sh_eval.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         L.lso_sh_backward.restype = None
@@ -227,6 +229,11 @@ def forward(settings, **kw) -> OracleRun:
 
 def expf(x: float) -> float:
     return float(lib().lso_expf(float(x)))
+
+
+def expf_render(x: float) -> float:
+    """The compositing loops' exp (lsr_oracle.c lso_expf_render; x >= -20)."""
+    return float(lib().lso_expf_render(float(x)))
 
 
 def sh_eval(deg: int, sh: np.ndarray, dirs: np.ndarray) -> np.ndarray:

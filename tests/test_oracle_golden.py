@@ -80,6 +80,18 @@ def test_expf_restatement_accuracy():
     assert oracle.expf(-100.0) == 0.0
 
 
+def test_expf_render_restatement_accuracy():
+    """The compositing loops' exp (one-constant range reduction) is within 2 ulp of the true exp
+    wherever they use it (power >= ln(1/255) - 0.01 > -6), and beyond, down to -20."""
+    xs = np.concatenate([np.linspace(-20.0, 0.0, 40001, dtype=np.float32),
+                         -np.logspace(-8, 1.3, 2001).astype(np.float32)])
+    ours = np.array([oracle.expf_render(float(x)) for x in xs], dtype=np.float32)
+    ref = np.exp(xs.astype(np.float64))
+    ulp = np.spacing(ref.astype(np.float32)).astype(np.float64)
+    assert np.max(np.abs(ours - ref) / ulp) <= 2.0
+    assert oracle.expf_render(0.0) == 1.0
+
+
 def test_cov3d_is_rssr():
     """Sigma = R S S^T R^T (scene/gaussian_model.py:27-31 with utils/general_utils.py:78-110)."""
     g = torch.Generator().manual_seed(3)
