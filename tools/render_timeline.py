@@ -64,6 +64,10 @@ def analyse(name, recs, info=None):
           f"peak concurrency {peak} ({peak / max(ncu, 1):.1f}/CU)")
     print(f"  sum of workgroup time / (span x peak) = {busy / (span * peak):.3f}; "
           f"span below 1/2 peak: {below[0.5] / span:.3f}, below 1/4 peak: {below[0.25] / span:.3f}")
+    tot = {k: sum(ph.get(k, 0) for ph in phases.values()) for k in ("load", "compact", "walk")}
+    if sum(tot.values()):
+        print("  phases summed over workgroups: " + ", ".join(f"{k} {100.0 * v / busy:.1f}%" for k, v in tot.items())
+              + " of workgroup time")
     dur.sort(reverse=True)
     mean = busy / len(dur)
     print(f"  workgroup time: mean {mean * TICK_US:.1f} us, max {dur[0][0] * TICK_US:.1f} us")
