@@ -981,6 +981,9 @@ __device__ __forceinline__ void bwd_walk_entry(BwdPixel& q, const BwdEntry& E, i
     }
 }
 
+#ifndef LSR_BWD_NOFLUSH  // measurement only: 1 drops the flush atomics (wrong gradients)
+#define LSR_BWD_NOFLUSH 0
+#endif
 template <bool kStats, bool kFeat, bool kColor, bool kGeo>
 __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
 {
@@ -1002,6 +1005,7 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
     __shared__ float sG[kThreads * kGS];  // per-entry gradient sums of the tile
     __shared__ uint8_t sM[kThreads];     // wave_cover mask (& the waves' contributor bounds)
     __shared__ uint32_t s_wmax[kThreads / 64];
+    __shared__ uint32_t s_gid[k5 ? kThreads : 1];  // the language step's flush: the batch's Gaussian ids
 
     const uint64_t t_start = kStats ? wall_clock64() : 0;
     int tile = (int)blockIdx.x;
@@ -1046,6 +1050,7 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
         uint32_t cover = 0;
         if (kload >= 0) {
             const uint32_t g = p.point_list[start + (uint32_t)kload];
+            if (k5) s_gid[t] = g;
             const float4 a = p.record[3 * (size_t)g];
             const float4 b = p.record[3 * (size_t)g + 1];
             const float4 c = p.record[3 * (size_t)g + 2];
@@ -1093,13 +1098,23 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
             s_stat[6] += 1u;           // batches
             s_bmax = 0u;
         }
+        if (k5) {
+            // the language step's flush: the batch's 5 x cnt values on consecutive threads (every
+            // lane active), the ids from LDS (no dependent global load before each atomic)
+            for (int slot = t; slot < cnt * 5; slot += kThreads) {
+                const int e = slot / 5, c = slot - 5 * e;  // value slot c: dxy (0, 1), language (2..4)
+                const float val = sG[slot] * (c == 0 ? (float)p.W : c == 1 ? (float)p.H : 1.0f);
+                if (val != 0.0f && !LSR_BWD_NOFLUSH) atomicAdd(&p.grad[(size_t)s_gid[e] * kGradStrideLang + c], val);
+            }
+            continue;
+        }
         // flush: 16 lanes per entry (12 active) -> one 48-byte atomic row per (tile, Gaussian)
         for (int slot = t; slot < cnt * 16; slot += kThreads) {
             const int e = slot >> 4, c = slot & 15;
             if (c < 12) {
                 if (!gvalue<kColor, kGeo>(c)) continue;  // a value this variant does not produce
                 const float val = sG[e * kGS + gslot<kColor, k5>(c)] * fscale;
-                if (val != 0.0f) {  // the id again from point_list (an L2 hit; saves 1 KB of LDS)
+                if (val != 0.0f && !LSR_BWD_NOFLUSH) {  // the id again from point_list (an L2 hit; saves 1 KB of LDS)
                     const uint32_t g = p.point_list[start + (uint32_t)(maxl - 1 - (done_cnt + e))];
                     if (k5)  // packed 20-B record: the five values in slots 0..4
                         atomicAdd(&p.grad[(size_t)g * kGradStrideLang + gslot<kColor, k5>(c)], val);
