@@ -454,6 +454,7 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
     rp.include_feature = (s->include_feature && a->language_feature) ? 1 : 0;
     rp.ranges = reinterpret_cast<const uint2*>(image + L.ranges);
     rp.point_list = reinterpret_cast<const uint32_t*>(binning + L.point_list);
+    rp.cover = reinterpret_cast<uint8_t*>(binning + L.cover);
     rp.record = reinterpret_cast<const float4*>(geom + L.record);
     rp.bg = s->bg;
     rp.final_T = reinterpret_cast<float*>(image + L.final_T);
@@ -530,6 +531,7 @@ int32_t lsr_backward(const lsr_settings* s, const lsr_backward_args* a, lsr_allo
     rp.include_feature = (s->include_feature && a->language_feature) ? 1 : 0;
     rp.ranges = reinterpret_cast<const uint2*>(image + L.ranges);
     rp.point_list = reinterpret_cast<const uint32_t*>(binning + L.point_list);
+    rp.cover = reinterpret_cast<uint8_t*>(binning + L.cover);
     rp.record = reinterpret_cast<const float4*>(geom + L.record);
     rp.bg = s->bg;
     rp.final_T = reinterpret_cast<float*>(image + L.final_T);

@@ -62,7 +62,7 @@ struct Layout {
     size_t counters, ranges, final_T, n_contrib, tile_lists, loss_partial, loss_code;
     size_t image_bytes;
     // binning (point_list per tile instance, the rest per super-tile entry / segment)
-    size_t point_list, super_keys, super_vals, alt_keys, alt_vals, bin_radix_hist, bin_radix_hist_scan;
+    size_t point_list, cover, super_keys, super_vals, alt_keys, alt_vals, bin_radix_hist, bin_radix_hist_scan;
     size_t bin_scan_regions, super_ranges, seg_base, col_prefix, row_prefix, seg_table, seg_table_scan;
     size_t scan_region_bin;   // u32 words per binning scan region
     size_t seg_table_words;   // (tile, segment) count table incl. one trailing slot
@@ -141,6 +141,7 @@ inline Layout make_layout(int P, int W, int H, int64_t R, int64_t E)
     L.seg_blocks = (int64_t)((e + kSegEntries - 1) / kSegEntries) + L.supers;
     L.seg_table_words = 64 * (size_t)L.seg_blocks + 1;
     L.point_list = take(4 * r);
+    L.cover = take(r);  // right after point_list: its offset depends on R only (the backward has no E)
     L.super_keys = take(4 * e);
     L.super_vals = take(4 * e);
     L.alt_keys = take(4 * e);
@@ -194,6 +195,9 @@ struct RenderParams {
     int W, H, gx, gy, include_feature;
     const uint2* ranges;
     const uint32_t* point_list;
+    // per list instance: the 4-bit mask of the tile's wave blocks it can reach (entry_cover), written
+    // by the forward for every instance it loads and read by the backward instead of recomputing it
+    uint8_t* cover;
     const float4* record;
     const float* bg;
     float* final_T;

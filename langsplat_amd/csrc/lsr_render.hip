@@ -439,7 +439,9 @@ __global__ __launch_bounds__(kTilePixels) void k_render_forward(RenderParams p)
             sB[t] = make_float4(a.w, b.y, cut, 0.0f);
             sC[t] = make_float4(b.z, b.w, c.x, c.y);
             sF[t] = make_float4(c.z, c.w, 0.0f, 0.0f);
-            sM[t] = (uint8_t)entry_cover(a.x, a.y, a.z, a.w, b.x, cut, tx0, ty0);
+            const uint8_t m = (uint8_t)entry_cover(a.x, a.y, a.z, a.w, b.x, cut, tx0, ty0);
+            sM[t] = m;
+            p.cover[idx] = m;  // for the backward (coalesced: one byte per thread)
         }
         __syncthreads();
         if (kStats) ph.lap(ph.load);
@@ -1068,7 +1070,9 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
             }
             const uint32_t k = (uint32_t)kload;
             const uint32_t live = (k < w0 ? 1u : 0u) | (k < w1 ? 2u : 0u) | (k < w2 ? 4u : 0u) | (k < w3 ? 8u : 0u);
-            cover = entry_cover(a.x, a.y, a.z, a.w, b.x, cut, tx0, ty0) & live;
+            // the forward's mask of this instance (it loaded every instance below any pixel's
+            // contributor count): the same function of the same inputs, not recomputed
+            cover = (uint32_t)p.cover[start + k] & live;
         }
         sM[t] = (uint8_t)cover;
         for (int i = t; i < kThreads * kGS; i += kThreads) sG[i] = 0.f;
