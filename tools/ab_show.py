@@ -11,5 +11,5 @@ for f in sorted(glob.glob(f"gpurun_out/ab_{var}_*.log")):
         continue
     d = json.loads(lines[-1])
     st = d["stages_ms_per_step"]
-    print(f.split("/")[-1], d["ms_per_step"], "%.3e" % d["value"],
+    print(f.split("/")[-1], d["ms_per_step"], "all-grads", d.get("ms_per_step_all_gradients"), "%.3e" % d["value"],
           " ".join(f"{k[:10]}={v * 1000:.1f}" for k, v in st.items()))
