@@ -1026,7 +1026,6 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
     const float tx0 = (float)(tx * kTile), ty0 = (float)(ty * kTile);
     const size_t HW = (size_t)p.W * p.H;
     const uint32_t start = p.ranges[tile].x;
-    const float fscale = flush_scale(t & 15, p.W, p.H);  // this thread's flush slot is always t & 15
 
     BwdPixel q;
     bwd_pixel_init<kFeat, kColor>(q, p, px < p.W && py < p.H, (size_t)py * p.W + px, HW);
@@ -1102,29 +1101,22 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
             s_stat[6] += 1u;           // batches
             s_bmax = 0u;
         }
-        if (k5) {
-            // the language step's flush: the batch's 5 x cnt values on consecutive threads (every
-            // lane active), the ids from LDS (no dependent global load before each atomic)
-            for (int slot = t; slot < cnt * 5; slot += kThreads) {
-                const int e = slot / 5, c = slot - 5 * e;  // value slot c: dxy (0, 1), language (2..4)
-                const float val = sG[slot] * (c == 0 ? (float)p.W : c == 1 ? (float)p.H : 1.0f);
-                if (val != 0.0f && !LSR_BWD_NOFLUSH) atomicAdd(&p.grad[(size_t)s_gid[e] * kGradStrideLang + c], val);
-            }
-            continue;
-        }
-        // flush: 16 lanes per entry (12 active) -> one 48-byte atomic row per (tile, Gaussian)
-        for (int slot = t; slot < cnt * 16; slot += kThreads) {
-            const int e = slot >> 4, c = slot & 15;
-            if (c < 12) {
-                if (!gvalue<kColor, kGeo>(c)) continue;  // a value this variant does not produce
-                const float val = sG[e * kGS + gslot<kColor, k5>(c)] * fscale;
-                if (val != 0.0f && !LSR_BWD_NOFLUSH) {  // the id again from point_list (an L2 hit; saves 1 KB of LDS)
-                    const uint32_t g = p.point_list[start + (uint32_t)(maxl - 1 - (done_cnt + e))];
-                    if (k5)  // packed 20-B record: the five values in slots 0..4
-                        atomicAdd(&p.grad[(size_t)g * kGradStrideLang + gslot<kColor, k5>(c)], val);
-                    else
-                        atomicAdd(&p.grad[(size_t)g * kGradStride + c], val);
-                }
+        // flush: the batch's kGS x cnt tile sums on consecutive threads (every lane busy) -> one
+        // atomic row per (tile, Gaussian).  The language step keeps the batch's ids in LDS (no
+        // dependent global load before each atomic); the other variants, whose LDS is at the
+        // occupancy limit, read them again from point_list (an L2 hit).
+        for (int slot = t; slot < cnt * kGS; slot += kThreads) {
+            const int e = slot / kGS, cs = slot - kGS * e;
+            const float v = sG[slot];
+            if (v == 0.0f || LSR_BWD_NOFLUSH) continue;
+            if (k5) {  // packed 20-B record: dxy in slots 0, 1, the language feature in 2..4
+                const float val = v * (cs == 0 ? (float)p.W : cs == 1 ? (float)p.H : 1.0f);
+                atomicAdd(&p.grad[(size_t)s_gid[e] * kGradStrideLang + cs], val);
+            } else {
+                const int c = (kColor || cs < 6) ? cs : cs + 3;  // gslot's inverse
+                if (!gvalue<kColor, kGeo>(c)) continue;          // a value this variant does not produce
+                const uint32_t g = p.point_list[start + (uint32_t)(maxl - 1 - (done_cnt + e))];
+                atomicAdd(&p.grad[(size_t)g * kGradStride + c], v * flush_scale(c, p.W, p.H));
             }
         }
     }
