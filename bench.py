@@ -160,66 +160,86 @@ STAGE_KERNEL = {"render backward": "lsr::k_render_backward<false, true, false, f
                 "preprocess": "lsr::k_preprocess<2>", "preprocess backward": "lsr::k_preprocess_backward"}
 
 
-def pmc_traffic(stage):
-    """HBM bytes per launch of the stage's kernel from the newest committed rocprofv3 PMC summary
-    (profiles/*_summary.json, tools/prof_summary.py: FETCH_SIZE x2 + WRITE_SIZE, gfx950 correction),
-    or (None, None) when no profile covers it."""
-    import glob
-    kern = STAGE_KERNEL.get(stage)
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9]*_summary.json")))  # by round tag
-    for f in reversed(files):
-        try:
-            d = json.load(open(f))["kernels"].get(kern, {})
-        except (OSError, ValueError, KeyError):
-            continue
-        if "hbm_bytes_per_launch" in d:
-            return float(d["hbm_bytes_per_launch"]), os.path.relpath(f, ROOT)
-    return None, None
+# profiles this round's bench reads its PMC figures from: profiles/<ROUND>_<config>_{summary,valu}.json
+# (tools/profile_round.sh + tools/prof_summary.py, tools/pmc_valu.sh + tools/valu_summary.py).  A
+# profile of another round or another config is never used: its field is then null.
+ROUND = "r03"
+CUS = 256
+CLOCK_HZ = 2.4e9  # MI355X_MICROARCH.md: max engine clock (what the PMC runs' GRBM_GUI_ACTIVE / time gives)
+# wave64 VALU instructions a CU can issue per cycle: 4 SIMD-32 units, each one wave64 instruction per
+# 2 cycles when two or more waves alternate (MI355X_MICROARCH.md "Wave scheduling"; tools/valu_peak.hip
+# measures it: profiles/r03_valu_peak.txt)
+VALU_PEAK_PER_CU_CYCLE = 2.0
 
 
-def pmc_valu(stage):
-    """VALU instructions issued per CU per cycle by the stage's kernel (at most 1: a CU issues one
-    wave64 VALU instruction per cycle) from the newest committed profiles/*_valu.json
-    (tools/valu_summary.py over tools/pmc_valu.sh), or (None, None)."""
-    import glob
-    kern = STAGE_KERNEL.get(stage)
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9]*_valu.json")))  # by round tag
-    for f in reversed(files):
-        try:
-            d = json.load(open(f))["kernels"].get(kern, {})
-        except (OSError, ValueError, KeyError):
-            continue
-        if "valu_per_cu_cycle" in d:
-            return float(d["valu_per_cu_cycle"]), os.path.relpath(f, ROOT)
-    return None, None
+def _profile(kind, cfg):
+    path = os.path.join(ROOT, "profiles", f"{ROUND}_{cfg}_{kind}.json")
+    try:
+        return json.load(open(path))["kernels"], os.path.relpath(path, ROOT)
+    except (OSError, ValueError, KeyError):
+        return None, None
+
+
+def pmc_traffic(stage, cfg):
+    """HBM bytes per launch of the stage's kernel from this round's PMC summary of this config
+    (FETCH_SIZE + WRITE_SIZE passes, gfx950 correction: tools/prof_summary.py), or (None, None)."""
+    k, src = _profile("summary", cfg)
+    d = (k or {}).get(STAGE_KERNEL.get(stage), {})
+    return (float(d["hbm_bytes_per_launch"]), src) if "hbm_bytes_per_launch" in d else (None, None)
+
+
+def pmc_valu(stage, cfg):
+    """SQ_INSTS_VALU per launch of the stage's kernel (and the PMC run's own per-CU-cycle rate) from
+    this round's profiles/<ROUND>_<cfg>_valu.json (tools/valu_summary.py), or (None, None, None)."""
+    k, src = _profile("valu", cfg)
+    d = (k or {}).get(STAGE_KERNEL.get(stage), {})
+    if d.get("valu_insts") is None:
+        return None, None, None
+    return float(d["valu_insts"]), d.get("valu_per_cu_cycle"), src
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
 
 
 def cpu_baseline(cfg, seconds_budget=25.0):
-    """Oracle (oracle/lsr_oracle.c, 1 thread) fwd+bwd on a bounded sample of the same workload:
-    the first P/2 Gaussians of the C3 scene, same camera and resolution (~15 s single-threaded)."""
+    """The C oracle (oracle/lsr_oracle.c, OpenMP over tiles on all the threads OMP_NUM_THREADS grants)
+    on the FULL workload config: the same scene, camera and resolution, one forward + full backward
+    (every gradient) per run, runs repeated while within the budget (at most 3), median rate."""
     from oracle import oracle
     from tests.scenes import settings_for
     c = CONFIGS[cfg]
-    frac = 2
-    Ps = c["P"] // frac
     g = make_gaussians(c["P"], seed=0)
-    cam = make_cameras(1, c["width"], c["height"])[0]
+    cam = make_cameras(c["views"], c["width"], c["height"])[0]
     st = settings_for(cam, sh_degree=3)
     with torch.no_grad():
-        inp = {k: (v[:Ps].contiguous() if v.dim() and v.shape[0] == c["P"] else v)
-               for k, v in activated_inputs(g).items()}
+        inp = {k: v.contiguous() for k, v in activated_inputs(g).items()}
     H, W = c["height"], c["width"]
     gen = torch.Generator().manual_seed(1)
     gcol = torch.randn((3, H, W), generator=gen) / (3 * H * W)
     glang = torch.randn((3, H, W), generator=gen) / (3 * H * W)
-    t0 = time.perf_counter()
-    run = oracle.forward(st, **inp)
-    run.backward(gcol, glang)
-    dt = time.perf_counter() - t0
-    blends = run.blends
-    return {"value": blends / dt, "unit": "blends/s", "cores": 1, "kind": "port",
-            "sample": f"{cfg} scene, first {Ps} of {c['P']} Gaussians, {W}x{H}, one fwd+bwd "
-                      f"({blends} blends, {dt:.1f} s, single-threaded C oracle)"}
+    times, blends = [], 0
+    t_start = time.perf_counter()
+    while len(times) < 3 and (not times or time.perf_counter() - t_start + times[-1] < seconds_budget):
+        t0 = time.perf_counter()
+        run = oracle.forward(st, **inp)
+        run.backward(gcol, glang)
+        times.append(time.perf_counter() - t0)
+        blends = run.blends
+        del run
+    dt = sorted(times)[len(times) // 2]
+    threads = oracle.num_threads()
+    return {"value": round(blends / dt, 1), "unit": "blends/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(),
+            "sample": f"{cfg} full scene ({c['P']} Gaussians, {W}x{H}, camera 0), forward + full backward "
+                      f"(every gradient), {blends} blends, median of {len(times)} run(s) "
+                      f"({', '.join(f'{t:.2f}' for t in times)} s), C oracle on {threads} OpenMP threads"}
 
 
 def main():
@@ -315,6 +335,16 @@ def main():
     elapsed = time.perf_counter() - t0
     _native.profile_enable(False)
     dom = _native.profile_report().get(DOMINANT_STAGE, {"avg_ms": float("nan")})
+    # the same steps with train.py:108's loss.item() after each (a device-to-host sync per step: the
+    # host cannot run ahead into the next step), reported beside `value` as ms_per_step_with_sync
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ts = time.perf_counter()
+    for _ in range(args.steps):
+        step().item()
+    torch.cuda.synchronize()
+    elapsed_sync = time.perf_counter() - ts
     # the same step with every geometry gradient computed although no parameter needs one (what the
     # reference extension does; LSR_ALL_GRADS=1): reported beside, never as `value`
     _native.FORCE_GEOMETRY_GRADS = True
@@ -365,17 +395,27 @@ def main():
                                   fused_loss=fused)
     roofline = None
     if bytes_dom is not None:
-        achieved = bytes_dom / (dom["avg_ms"] * 1e-3) / 1e9
-        traffic, src = pmc_traffic(dom_name)
-        roofline = {"bound": "hbm", "kernel": dom_name, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                    "traffic": None if traffic is None else int(traffic), "traffic_source": src,
-                    "avg_ms": round(dom["avg_ms"], 4), "bytes_per_launch": int(bytes_dom)}
-        # what actually bounds it: the render kernels are VALU-issue-bound
-        valu, vsrc = pmc_valu(dom_name)
-        if valu is not None:
-            roofline["valu_issue_frac"] = round(valu, 3)
-            roofline["valu_source"] = vsrc
+        avg_s = dom["avg_ms"] * 1e-3
+        # HBM view (SURVEY.md §8d's per-unit bytes): algorithmic bytes / live launch time,
+        # and the HBM bytes the PMC passes of this round and config measured for the same kernel
+        traffic, tsrc = pmc_traffic(dom_name, cfg)
+        hbm = {"bound": "hbm", "achieved": round(bytes_dom / avg_s / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+               "frac": round(bytes_dom / avg_s / 1e9 / HBM_PEAK_GBS, 4), "bytes_per_launch": int(bytes_dom),
+               "traffic": None if traffic is None else int(traffic), "traffic_source": tsrc,
+               "traffic_frac": None if traffic is None else round(traffic / avg_s / 1e9 / HBM_PEAK_GBS, 4)}
+        # what bounds the render kernels is instruction issue, not HBM: the headline is
+        # the VALU issue rate, SQ_INSTS_VALU per launch (this round's PMC pass of this config) over the
+        # live launch time, against the chip's wave64 VALU issue peak
+        insts, pmc_rate, vsrc = pmc_valu(dom_name, cfg)
+        if insts is not None:
+            achieved = insts / CUS / (avg_s * CLOCK_HZ)
+            roofline = {"bound": "valu", "kernel": dom_name, "achieved": round(achieved, 4),
+                        "peak": VALU_PEAK_PER_CU_CYCLE, "unit": "wave64 VALU instructions / CU / cycle",
+                        "frac": round(achieved / VALU_PEAK_PER_CU_CYCLE, 4), "traffic": hbm["traffic"],
+                        "avg_ms": round(dom["avg_ms"], 4), "valu_insts_per_launch": int(insts),
+                        "valu_source": vsrc, "pmc_run_valu_per_cu_cycle": pmc_rate, "hbm": hbm}
+        else:  # no VALU profile of this round and config: the HBM view is the headline
+            roofline = dict(hbm, kernel=dom_name, avg_ms=round(dom["avg_ms"], 4), valu_source=None)
         # north_star's "% of HBM roofline" in SURVEY.md §8d's form: the whole rasterizer fwd+bwd
         # (every profiled stage except the optimizer) against the §8d traffic model
         raster_stage_ms = sum(v["total_ms"] for k, v in prof.items() if k != "adam") / prof_steps
@@ -407,6 +447,7 @@ def main():
                    "gradients": "all geometry" if _native.FORCE_GEOMETRY_GRADS else
                                 "as needed: means2D + language feature (geometry frozen, "
                                 "scene/gaussian_model.py:203-217)"},
+        "ms_per_step_with_sync": round(1000.0 * elapsed_sync / args.steps, 4),
         "ms_per_step_all_gradients": round(1000.0 * elapsed_all / args.steps, 4),
         "raster_ms_per_step": round(raster_ms, 4),
         "stages_ms_per_step": {k: round(v["total_ms"] / prof_steps, 4) for k, v in sorted(prof.items())},

@@ -46,6 +46,9 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 
 #define BLOCK_X 16
 #define BLOCK_Y 16
@@ -67,10 +70,19 @@ typedef struct lso_settings {
     float viewmatrix[16];
     float projmatrix[16];
     float campos[3];
+    /* arithmetic form (see "Upstream forms" below): 0 = the kernels' operation sequence (the
+       bit-exact contract), 1 = upstream's source expressions, one rounding per operation,
+       2 = the same expressions with nvcc-style multiply-add contraction */
+    int32_t form;
 } lso_settings;
+
+#define LSO_FORM_KERNEL 0
+#define LSO_FORM_UPSTREAM 1
+#define LSO_FORM_UPSTREAM_FMA 2
 
 typedef struct lso_state {
     lso_settings s;
+    int form;
     int P, M, gx, gy;
     int has_shs, has_colors, has_cov, has_lang;
     /* private copies of the inputs (the backward re-reads them) */
@@ -247,6 +259,189 @@ static void cov2d(const float* mean, float fx, float fy, float tanfovx, float ta
 }
 
 /* ------------------------------------------------------------------------------------------ */
+/* Upstream forms (a number for the unpinned core)                          */
+/* ------------------------------------------------------------------------------------------ */
+/* The kernels and form 0 evaluate kernel-shaped expressions (the 4-op power, the shared exp
+ * restatement, A = J W with b = A1 (S A0), f (alpha T)).  Forms 1 and 2 evaluate instead the
+ * expressions of the published 3DGS rasterizer that the absent submodule forks, as its source
+ * writes them:
+ *   - transformPoint4x3/4x4: m[0] x + m[4] y + m[8] z + m[12], left to right;
+ *   - computeCov3D with glm: R from the quaternion, M = S R, Sigma = M^T M (glm's column-major
+ *     products, each a left-to-right sum over k);
+ *   - computeCov2D with glm: T = W J, cov = T^T V^T T evaluated left to right, +0.3 on the diagonal;
+ *     det = a c - b b, conic, mid, lambda, radius as written;
+ *   - computeColorFromSH: dir / glm::length(dir) (length = sqrt of the left-to-right dot), the basis
+ *     sums as written;
+ *   - renderCUDA: power = -0.5f (c.x dx dx + c.z dy dy) - c.y dx dy, alpha = min(0.99, o exp(power))
+ *     with exp correctly rounded ((float)exp((double)x): CUDA's expf is within 2 ulp, so the
+ *     nearest float is the best single stand-in), C += f alpha T (as (f alpha) T);
+ *   - the backward renderCUDA's power, G = exp(power) and dG/ddelta = -gdx c.x - gdy c.y as written.
+ * Form 1 rounds every operation.  Form 2 contracts a*b+c / a*b-c into one fma where nvcc's
+ * default -fmad=true would: following LLVM's DAG combiner, in x*y + u*v the LEFT product is fused
+ * (fma(x, y, u*v)), in s + x*y and s - x*y the product is fused into the sum.  Which products
+ * upstream's compiler really fused is not knowable here; the two forms bracket the plausible
+ * arithmetic.  Everything else (the tile rectangle, ndc2Pix, the preprocess backward's chain rule,
+ * the SH and covariance backward) is shared with form 0, whose sequence there already follows the
+ * upstream source.  tests/test_gpu_upstream_form.py reports and bounds HIP vs forms 1 and 2. */
+
+static inline float u_sum2(int f, float a0, float b0, float a1, float b1)
+{
+    return f == LSO_FORM_UPSTREAM_FMA ? fmaf(a0, b0, a1 * b1) : a0 * b0 + a1 * b1;
+}
+
+static inline float u_sum3(int f, float a0, float b0, float a1, float b1, float a2, float b2)
+{
+    return f == LSO_FORM_UPSTREAM_FMA ? fmaf(a2, b2, fmaf(a0, b0, a1 * b1)) : (a0 * b0 + a1 * b1) + a2 * b2;
+}
+
+/* a*b - c*d */
+static inline float u_diffp(int f, float a, float b, float c, float d)
+{
+    return f == LSO_FORM_UPSTREAM_FMA ? fmaf(a, b, -(c * d)) : a * b - c * d;
+}
+
+/* a*b - s */
+static inline float u_prodsub(int f, float a, float b, float s)
+{
+    return f == LSO_FORM_UPSTREAM_FMA ? fmaf(a, b, -s) : a * b - s;
+}
+
+/* s + a*b */
+static inline float u_addp(int f, float s, float a, float b)
+{
+    return f == LSO_FORM_UPSTREAM_FMA ? fmaf(a, b, s) : s + a * b;
+}
+
+/* s - a*b */
+static inline float u_subp(int f, float s, float a, float b)
+{
+    return f == LSO_FORM_UPSTREAM_FMA ? fmaf(-a, b, s) : s - a * b;
+}
+
+static inline float u_exp(float x) { return (float)exp((double)x); }
+
+static inline void u_xform4x3(int f, const float* m, const float* p, float* o)
+{
+    for (int r = 0; r < 3; r++) o[r] = u_sum3(f, m[r], p[0], m[4 + r], p[1], m[8 + r], p[2]) + m[12 + r];
+}
+
+static inline void u_xform4x4(int f, const float* m, const float* p, float* o)
+{
+    for (int r = 0; r < 4; r++) o[r] = u_sum3(f, m[r], p[0], m[4 + r], p[1], m[8 + r], p[2]) + m[12 + r];
+}
+
+/* computeCov3D with glm (column-major g[c][r]): R's columns from the quaternion, M = S R,
+ * Sigma = M^T M: Sigma[c][r] = sum_k M[r][k] M[c][k]. */
+static void u_cov3d(int f, const float* scale, float mod, const float* q, float* cov)
+{
+    const float r = q[0], x = q[1], y = q[2], z = q[3];
+    float R[3][3];
+    R[0][0] = u_subp(f, 1.f, 2.f, u_sum2(f, y, y, z, z));
+    R[0][1] = 2.f * u_diffp(f, x, y, r, z);
+    R[0][2] = 2.f * u_sum2(f, x, z, r, y);
+    R[1][0] = 2.f * u_sum2(f, x, y, r, z);
+    R[1][1] = u_subp(f, 1.f, 2.f, u_sum2(f, x, x, z, z));
+    R[1][2] = 2.f * u_diffp(f, y, z, r, x);
+    R[2][0] = 2.f * u_diffp(f, x, z, r, y);
+    R[2][1] = 2.f * u_sum2(f, y, z, r, x);
+    R[2][2] = u_subp(f, 1.f, 2.f, u_sum2(f, x, x, y, y));
+    const float s[3] = {mod * scale[0], mod * scale[1], mod * scale[2]};
+    float M[3][3];
+    for (int c = 0; c < 3; c++)
+        for (int k = 0; k < 3; k++) M[c][k] = s[k] * R[c][k]; /* S diagonal: the zero terms add +-0 */
+#define SIG(c, r) u_sum3(f, M[r][0], M[c][0], M[r][1], M[c][1], M[r][2], M[c][2])
+    cov[0] = SIG(0, 0);
+    cov[1] = SIG(0, 1);
+    cov[2] = SIG(0, 2);
+    cov[3] = SIG(1, 1);
+    cov[4] = SIG(1, 2);
+    cov[5] = SIG(2, 2);
+#undef SIG
+}
+
+/* computeCov2D with glm.  Outputs as cov2d(): the clamped t, the T = W J columns 0/1 in A (the
+ * 2x3 the preprocess backward uses: A[c][k] = T[c][k]) and abc = (a + 0.3, b, c + 0.3). */
+static void u_cov2d(int f, const float* mean, float fx, float fy, float tanfovx, float tanfovy, const float* cov,
+                    const float* view, float* t, float A[2][3], float* abc, float* txtz_out, float* tytz_out)
+{
+    u_xform4x3(f, view, mean, t);
+    const float limx = 1.3f * tanfovx, limy = 1.3f * tanfovy;
+    const float txtz = t[0] / t[2], tytz = t[1] / t[2];
+    t[0] = fminf(limx, fmaxf(-limx, txtz)) * t[2];
+    t[1] = fminf(limy, fmaxf(-limy, tytz)) * t[2];
+    const float j00 = fx / t[2], j02 = -(fx * t[0]) / (t[2] * t[2]);
+    const float j11 = fy / t[2], j12 = -(fy * t[1]) / (t[2] * t[2]);
+    /* W[c][r] = view[4 r + c]; T[c][r] = W[0][r] J[c][0] + W[1][r] J[c][1] + W[2][r] J[c][2] with
+       J[0] = (j00, 0, j02), J[1] = (0, j11, j12): the zero product adds +-0 to the first nonzero
+       one, and the last product is the one contracted into the sum */
+    for (int r = 0; r < 3; r++) {
+        A[0][r] = u_addp(f, view[4 * r] * j00, view[4 * r + 2], j02);
+        A[1][r] = u_addp(f, view[4 * r + 1] * j11, view[4 * r + 2], j12);
+    }
+    const float V[3][3] = {{cov[0], cov[1], cov[2]}, {cov[1], cov[3], cov[4]}, {cov[2], cov[4], cov[5]}};
+    /* X = T^T V: X[k][r] = sum_j T[r][j] V[k][j];  cov2D[c][r] = sum_k X[k][r] T[c][k] */
+    float X0[3], X1[3];
+    for (int k = 0; k < 3; k++) {
+        X0[k] = u_sum3(f, A[0][0], V[k][0], A[0][1], V[k][1], A[0][2], V[k][2]);
+        X1[k] = u_sum3(f, A[1][0], V[k][0], A[1][1], V[k][1], A[1][2], V[k][2]);
+    }
+    abc[0] = u_sum3(f, X0[0], A[0][0], X0[1], A[0][1], X0[2], A[0][2]) + 0.3f;
+    abc[1] = u_sum3(f, X1[0], A[0][0], X1[1], A[0][1], X1[2], A[0][2]);
+    abc[2] = u_sum3(f, X1[0], A[1][0], X1[1], A[1][1], X1[2], A[1][2]) + 0.3f;
+    if (txtz_out) *txtz_out = txtz;
+    if (tytz_out) *tytz_out = tytz;
+}
+
+/* computeColorFromSH as written, including the + 0.5 (form 1: lso_sh_eval's sequence; form 2
+ * contracted: at degree 0 the + 0.5 meets the product SH_C0 sh[0] itself, above it the first
+ * subtraction does) */
+static void u_sh_eval(int f, int deg, const float* sh, const float* mean, const float* campos, float* out)
+{
+    float d[3] = {mean[0] - campos[0], mean[1] - campos[1], mean[2] - campos[2]};
+    const float len = sqrtf(u_sum3(f, d[0], d[0], d[1], d[1], d[2], d[2]));
+    const float x = d[0] / len, y = d[1] / len, z = d[2] / len;
+    const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+    for (int c = 0; c < 3; c++) {
+        const float* s = sh + c;
+        if (deg == 0) {
+            out[c] = u_addp(f, 0.5f, SH_C0, s[0]);
+            continue;
+        }
+        float res;
+        {
+            res = u_diffp(f, SH_C0, s[0], SH_C1 * y, s[1 * 3]);
+            res = u_addp(f, res, SH_C1 * z, s[2 * 3]);
+            res = u_subp(f, res, SH_C1 * x, s[3 * 3]);
+            if (deg > 1) {
+                res = u_addp(f, res, SH_C2[0] * xy, s[4 * 3]);
+                res = u_addp(f, res, SH_C2[1] * yz, s[5 * 3]);
+                res = u_addp(f, res, SH_C2[2] * (u_subp(f, -xx, -2.0f, zz) - yy), s[6 * 3]);
+                res = u_addp(f, res, SH_C2[3] * xz, s[7 * 3]);
+                res = u_addp(f, res, SH_C2[4] * (xx - yy), s[8 * 3]);
+                if (deg > 2) {
+                    res = u_addp(f, res, SH_C3[0] * y * u_subp(f, -yy, -3.0f, xx), s[9 * 3]);
+                    res = u_addp(f, res, SH_C3[1] * xy * z, s[10 * 3]);
+                    res = u_addp(f, res, SH_C3[2] * y * (u_subp(f, -xx, -4.0f, zz) - yy), s[11 * 3]);
+                    res = u_addp(f, res, SH_C3[3] * z * u_subp(f, u_diffp(f, 2.0f, zz, 3.0f, xx), 3.0f, yy),
+                                 s[12 * 3]);
+                    res = u_addp(f, res, SH_C3[4] * x * (u_subp(f, -xx, -4.0f, zz) - yy), s[13 * 3]);
+                    res = u_addp(f, res, SH_C3[5] * z * (xx - yy), s[14 * 3]);
+                    res = u_addp(f, res, SH_C3[6] * x * u_subp(f, xx, 3.0f, yy), s[15 * 3]);
+                }
+            }
+        }
+        out[c] = res + 0.5f;
+    }
+}
+
+/* renderCUDA's power as written: -0.5f * (c.x dx dx + c.z dy dy) - c.y dx dy */
+static inline float u_power(int f, const float* co, float dx, float dy)
+{
+    const float inner = u_sum2(f, co[0] * dx, dx, co[2] * dy, dy);
+    return u_diffp(f, -0.5f, inner, co[1] * dx, dy);
+}
+
+/* ------------------------------------------------------------------------------------------ */
 /* SH -> RGB (utils/sh_utils.py:57-112; +0.5 and clamp as gaussian_renderer/__init__.py:80)   */
 /* ------------------------------------------------------------------------------------------ */
 
@@ -305,47 +500,60 @@ static void* xcopy(const void* src, size_t bytes)
     return d;
 }
 
-typedef struct { uint64_t key; uint32_t id; } inst_t;
-
-static int inst_cmp(const void* a, const void* b)
+/* the per-Gaussian state's covariance inputs in the state's arithmetic form */
+static void cov3d_of(const lso_state* st, int i, float* cov_local, const float** cov)
 {
-    const inst_t* x = (const inst_t*)a;
-    const inst_t* y = (const inst_t*)b;
-    if (x->key != y->key) return x->key < y->key ? -1 : 1;
-    return x->id < y->id ? -1 : (x->id > y->id);
+    if (st->has_cov) {
+        *cov = st->cov_pre + 6 * i;
+    } else if (st->form == LSO_FORM_KERNEL) {
+        lso_cov3d(st->scales + 3 * i, st->s.scale_modifier, st->rots + 4 * i, cov_local);
+        *cov = cov_local;
+    } else {
+        u_cov3d(st->form, st->scales + 3 * i, st->s.scale_modifier, st->rots + 4 * i, cov_local);
+        *cov = cov_local;
+    }
+}
+
+static void cov2d_of(const lso_state* st, const float* mean, float fx, float fy, const float* cov, float* t,
+                     float A[2][3], float* abc, float* txtz, float* tytz)
+{
+    const lso_settings* s = &st->s;
+    if (st->form == LSO_FORM_KERNEL)
+        cov2d(mean, fx, fy, s->tanfovx, s->tanfovy, cov, s->viewmatrix, t, A, abc, txtz, tytz);
+    else
+        u_cov2d(st->form, mean, fx, fy, s->tanfovx, s->tanfovy, cov, s->viewmatrix, t, A, abc, txtz, tytz);
 }
 
 static void preprocess_one(lso_state* st, int i, float focal_x, float focal_y)
 {
     const lso_settings* s = &st->s;
     const int W = s->image_width, H = s->image_height;
+    const int f = st->form;
     st->radii[i] = 0;
     st->tiles[i] = 0;
     const float* p = st->means + 3 * i;
     float pv[3];
-    xform4x3(s->viewmatrix, p, pv);
+    if (f == LSO_FORM_KERNEL) xform4x3(s->viewmatrix, p, pv);
+    else u_xform4x3(f, s->viewmatrix, p, pv);
     if (pv[2] <= 0.2f) return; /* near cull */
     float hom[4];
-    xform4x4(s->projmatrix, p, hom);
+    if (f == LSO_FORM_KERNEL) xform4x4(s->projmatrix, p, hom);
+    else u_xform4x4(f, s->projmatrix, p, hom);
     float p_w = 1.0f / (hom[3] + 0.0000001f);
     float proj_x = hom[0] * p_w, proj_y = hom[1] * p_w;
 
     float cov_local[6];
     const float* cov;
-    if (st->has_cov) cov = st->cov_pre + 6 * i;
-    else {
-        lso_cov3d(st->scales + 3 * i, s->scale_modifier, st->rots + 4 * i, cov_local);
-        cov = cov_local;
-    }
+    cov3d_of(st, i, cov_local, &cov);
     float t[3], A[2][3], abc[3];
-    cov2d(p, focal_x, focal_y, s->tanfovx, s->tanfovy, cov, s->viewmatrix, t, A, abc, NULL, NULL);
+    cov2d_of(st, p, focal_x, focal_y, cov, t, A, abc, NULL, NULL);
     float a = abc[0], b = abc[1], c = abc[2];
-    float det = a * c - b * b;
+    float det = f == LSO_FORM_KERNEL ? a * c - b * b : u_diffp(f, a, c, b, b);
     if (det == 0.0f) return;
     float det_inv = 1.f / det;
     float cx = c * det_inv, cy = -b * det_inv, cz = a * det_inv;
     float mid = 0.5f * (a + c);
-    float disc = fmaxf(0.1f, mid * mid - det);
+    float disc = fmaxf(0.1f, f == LSO_FORM_KERNEL ? mid * mid - det : u_prodsub(f, mid, mid, det));
     float sq = sqrtf(disc);
     float l1 = mid + sq, l2 = mid - sq;
     float my_radius = ceilf(3.f * sqrtf(fmaxf(l1, l2)));
@@ -364,10 +572,15 @@ static void preprocess_one(lso_state* st, int i, float focal_x, float focal_y)
 
     if (st->has_shs) {
         float dir_orig[3], dir[3], res[3];
-        view_dir(p, s->campos, dir_orig, dir);
-        lso_sh_eval(s->sh_degree, st->shs + (size_t)i * st->M * 3, dir, res);
+        if (f == LSO_FORM_KERNEL) {
+            view_dir(p, s->campos, dir_orig, dir);
+            lso_sh_eval(s->sh_degree, st->shs + (size_t)i * st->M * 3, dir, res);
+            for (int ch = 0; ch < 3; ch++) res[ch] = res[ch] + 0.5f;
+        } else {
+            u_sh_eval(f, s->sh_degree, st->shs + (size_t)i * st->M * 3, p, s->campos, res);
+        }
         for (int ch = 0; ch < 3; ch++) {
-            float v = res[ch] + 0.5f;
+            float v = res[ch];
             st->clamped[3 * i + ch] = v < 0.0f;
             st->rgb[3 * i + ch] = fmaxf(v, 0.0f);
         }
@@ -428,6 +641,56 @@ static void render_pixel(const lso_state* st, int tile, int px, int py, float* C
     *last_out = last;
 }
 
+/* render_pixel in an upstream form (see "Upstream forms") */
+static void render_pixel_upstream(const lso_state* st, int tile, int px, int py, float* C, float* F,
+                                  float* T_out, uint32_t* last_out)
+{
+    const int f = st->form;
+    const float pfx = (float)px, pfy = (float)py;
+    float T = 1.0f;
+    uint32_t contributor = 0, last = 0;
+    C[0] = C[1] = C[2] = 0.f;
+    F[0] = F[1] = F[2] = 0.f;
+    const int feat = st->s.include_feature && st->has_lang;
+    for (uint32_t k = st->ranges[2 * tile]; k < st->ranges[2 * tile + 1]; k++) {
+        contributor++;
+        uint32_t g = st->point_list[k];
+        const float* co = st->conic_o + 4 * g;
+        const float dx = st->xy[2 * g] - pfx, dy = st->xy[2 * g + 1] - pfy;
+        const float power = u_power(f, co, dx, dy);
+        if (power > 0.0f) continue;
+        const float alpha = fminf(0.99f, co[3] * u_exp(power));
+        if (alpha < 1.0f / 255.0f) continue;
+        const float test_T = T * (1 - alpha);
+        if (test_T < 0.0001f) break;
+        for (int ch = 0; ch < 3; ch++) C[ch] = u_addp(f, C[ch], st->rgb[3 * g + ch] * alpha, T);
+        if (feat)
+            for (int ch = 0; ch < 3; ch++) F[ch] = u_addp(f, F[ch], st->lang[3 * g + ch] * alpha, T);
+        T = test_T;
+        last = contributor;
+    }
+    *T_out = T;
+    *last_out = last;
+}
+
+static int lso_threads(void)
+{
+#ifdef _OPENMP
+    return omp_get_max_threads();
+#else
+    return 1;
+#endif
+}
+
+/* threads the oracle's parallel loops use (OMP_NUM_THREADS; bench.py's cpu_baseline reports it) */
+int lso_num_threads(void) { return lso_threads(); }
+
+static int tile_inst_cmp(const void* a, const void* b)
+{
+    const uint64_t x = *(const uint64_t*)a, y = *(const uint64_t*)b;
+    return x < y ? -1 : (x > y);
+}
+
 lso_state* lso_forward(const lso_settings* s, int P, int M, const float* means3D,
                        const float* shs, const float* colors_precomp, const float* lang,
                        const float* opacities, const float* scales, const float* rotations,
@@ -436,6 +699,7 @@ lso_state* lso_forward(const lso_settings* s, int P, int M, const float* means3D
 {
     lso_state* st = (lso_state*)calloc(1, sizeof(lso_state));
     st->s = *s;
+    st->form = (s->form == LSO_FORM_UPSTREAM || s->form == LSO_FORM_UPSTREAM_FMA) ? s->form : LSO_FORM_KERNEL;
     st->P = P;
     st->M = M;
     const int W = s->image_width, H = s->image_height;
@@ -473,54 +737,71 @@ lso_state* lso_forward(const lso_settings* s, int P, int M, const float* means3D
 
     const float focal_y = (float)H / (2.0f * s->tanfovy);
     const float focal_x = (float)W / (2.0f * s->tanfovx);
+#pragma omp parallel for schedule(static)
     for (int i = 0; i < P; i++) preprocess_one(st, i, focal_x, focal_y);
     memcpy(radii_out, st->radii, sizeof(int32_t) * (size_t)P);
 
-    /* duplicate with keys (tile << 32 | depth bits), stable sort => (tile, depth, id) order */
+    /* duplicate with keys (tile << 32 | depth bits) and sort (stable: equal keys keep id order),
+       i.e. the (tile, depth, id) order: a counting sort by tile in id order, then each tile's run
+       sorted on (depth bits << 32 | id) -- the same order as one sort of the 64-bit keys */
     int64_t R = 0;
     for (int i = 0; i < P; i++) R += st->tiles[i];
     st->R = R;
-    inst_t* inst = (inst_t*)malloc(sizeof(inst_t) * (size_t)(R + 1));
-    int64_t o = 0;
+    uint32_t* tile_count = (uint32_t*)calloc((size_t)T_tiles + 1, sizeof(uint32_t));
     for (int i = 0; i < P; i++) {
         if (st->tiles[i] == 0) continue;
         int r4[4];
         tile_rect(st, i, r4);
         for (int y = r4[1]; y < r4[3]; y++)
-            for (int x = r4[0]; x < r4[2]; x++) {
-                inst[o].key = ((uint64_t)(uint32_t)(y * st->gx + x) << 32) | f2bits(st->depth[i]);
-                inst[o].id = (uint32_t)i;
-                o++;
-            }
+            for (int x = r4[0]; x < r4[2]; x++) tile_count[y * st->gx + x]++;
     }
-    qsort(inst, (size_t)R, sizeof(inst_t), inst_cmp);
+    int64_t acc = 0;
+    for (int t = 0; t < T_tiles; t++) {
+        st->ranges[2 * t] = (uint32_t)acc;
+        acc += tile_count[t];
+        st->ranges[2 * t + 1] = (uint32_t)acc;
+        tile_count[t] = st->ranges[2 * t]; /* now the write cursor */
+    }
+    uint64_t* inst = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)(R + 1));
+    for (int i = 0; i < P; i++) {
+        if (st->tiles[i] == 0) continue;
+        int r4[4];
+        tile_rect(st, i, r4);
+        const uint64_t key = ((uint64_t)f2bits(st->depth[i]) << 32) | (uint32_t)i;
+        for (int y = r4[1]; y < r4[3]; y++)
+            for (int x = r4[0]; x < r4[2]; x++) inst[tile_count[y * st->gx + x]++] = key;
+    }
+    free(tile_count);
+#pragma omp parallel for schedule(dynamic, 16)
+    for (int t = 0; t < T_tiles; t++) {
+        const uint32_t a = st->ranges[2 * t], b = st->ranges[2 * t + 1];
+        if (b - a > 1) qsort(inst + a, b - a, sizeof(uint64_t), tile_inst_cmp);
+    }
     st->point_list = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)(R + 1));
-    for (int64_t k = 0; k < R; k++) {
-        st->point_list[k] = inst[k].id;
-        uint32_t t = (uint32_t)(inst[k].key >> 32);
-        if (k == 0 || (uint32_t)(inst[k - 1].key >> 32) != t) st->ranges[2 * t] = (uint32_t)k;
-        if (k == R - 1 || (uint32_t)(inst[k + 1].key >> 32) != t) st->ranges[2 * t + 1] = (uint32_t)(k + 1);
-    }
+    for (int64_t k = 0; k < R; k++) st->point_list[k] = (uint32_t)inst[k];
     free(inst);
 
     const size_t HW = (size_t)W * H;
-    for (int ty = 0; ty < st->gy; ty++)
-        for (int tx = 0; tx < st->gx; tx++) {
-            int tile = ty * st->gx + tx;
-            for (int py = ty * BLOCK_Y; py < ty * BLOCK_Y + BLOCK_Y && py < H; py++)
-                for (int px = tx * BLOCK_X; px < tx * BLOCK_X + BLOCK_X && px < W; px++) {
-                    float C[3], F[3], T;
-                    uint32_t last;
-                    render_pixel(st, tile, px, py, C, F, &T, &last);
-                    size_t pix = (size_t)py * W + px;
-                    st->final_T[pix] = T;
-                    st->n_contrib[pix] = last;
-                    for (int ch = 0; ch < 3; ch++) {
-                        out_color[ch * HW + pix] = fmaf(T, s->bg[ch], C[ch]);
-                        out_lang[ch * HW + pix] = F[ch];
-                    }
+    const int upstream = st->form != LSO_FORM_KERNEL;
+#pragma omp parallel for schedule(dynamic, 4)
+    for (int tile = 0; tile < T_tiles; tile++) {
+        const int ty = tile / st->gx, tx = tile % st->gx;
+        for (int py = ty * BLOCK_Y; py < ty * BLOCK_Y + BLOCK_Y && py < H; py++)
+            for (int px = tx * BLOCK_X; px < tx * BLOCK_X + BLOCK_X && px < W; px++) {
+                float C[3], F[3], T;
+                uint32_t last;
+                if (upstream) render_pixel_upstream(st, tile, px, py, C, F, &T, &last);
+                else render_pixel(st, tile, px, py, C, F, &T, &last);
+                size_t pix = (size_t)py * W + px;
+                st->final_T[pix] = T;
+                st->n_contrib[pix] = last;
+                for (int ch = 0; ch < 3; ch++) {
+                    out_color[ch * HW + pix] = upstream ? u_addp(st->form, C[ch], T, s->bg[ch])
+                                                        : fmaf(T, s->bg[ch], C[ch]);
+                    out_lang[ch * HW + pix] = F[ch];
                 }
-        }
+            }
+    }
     return st;
 }
 
@@ -647,13 +928,16 @@ void lso_cov3d_backward(const float* scale, float mod, const float* rot, const f
               2.f * y * (dR[2][1] + dR[1][2]) - 4.f * z * (dR[1][1] + dR[0][0]);
 }
 
-/* Per-pixel backward contributions, back to front (upstream BACKWARD::renderCUDA) */
+/* Per-pixel backward contributions, back to front (upstream BACKWARD::renderCUDA).  g holds 12
+ * doubles per Gaussian: dxy 0-1, dconic 2-4, dopacity 5, drgb 6-8, dlang 9-11.  Forms 1 and 2
+ * evaluate upstream's power, G = exp(power) and sums as written ("Upstream forms"). */
 static void backward_pixel(const lso_state* st, int tile, int px, int py, const float* dpix,
-                           const float* dpixF, double* g_xy, double* g_conic, double* g_opac,
-                           double* g_rgb, double* g_lang)
+                           const float* dpixF, double* gacc)
 {
     const lso_settings* s = &st->s;
     const int W = s->image_width, H = s->image_height;
+    const int form = st->form;
+    const int up = form != LSO_FORM_KERNEL;
     const size_t pix = (size_t)py * W + px;
     const float T_final = st->final_T[pix];
     float T = T_final;
@@ -663,16 +947,26 @@ static void backward_pixel(const lso_state* st, int tile, int px, int py, const 
     const int feat = s->include_feature && st->has_lang;
     float acc[3] = {0, 0, 0}, accF[3] = {0, 0, 0}, last_c[3] = {0, 0, 0}, last_f[3] = {0, 0, 0};
     float last_alpha = 0.0f;
-    float bg_dot = fmaf(s->bg[2], dpix[2], fmaf(s->bg[1], dpix[1], s->bg[0] * dpix[0]));
+    float bg_dot = up ? u_addp(form, u_addp(form, u_addp(form, 0.0f, s->bg[0], dpix[0]), s->bg[1], dpix[1]),
+                               s->bg[2], dpix[2])
+                      : fmaf(s->bg[2], dpix[2], fmaf(s->bg[1], dpix[1], s->bg[0] * dpix[0]));
     const uint32_t start = st->ranges[2 * tile];
     for (int64_t j = (int64_t)last - 1; j >= 0; j--) {
         uint32_t g = st->point_list[start + j];
+        double* ga = gacc + 12 * (size_t)g;
         const float* co = st->conic_o + 4 * g;
         float dx = st->xy[2 * g] - pfx, dy = st->xy[2 * g + 1] - pfy;
-        float hx = -0.5f * co[0], hz = -0.5f * co[2];
-        float power = fmaf(dx, fmaf(-co[1], dy, hx * dx), (hz * dy) * dy);
-        if (power > 0.0f) continue;
-        float G = lso_expf_render(power);
+        float power, G;
+        if (up) {
+            power = u_power(form, co, dx, dy);
+            if (power > 0.0f) continue;
+            G = u_exp(power);
+        } else {
+            float hx = -0.5f * co[0], hz = -0.5f * co[2];
+            power = fmaf(dx, fmaf(-co[1], dy, hx * dx), (hz * dy) * dy);
+            if (power > 0.0f) continue;
+            G = lso_expf_render(power);
+        }
         float alpha = fminf(0.99f, co[3] * G);
         if (alpha < 1.0f / 255.0f) continue;
         float one_m = 1.0f - alpha;
@@ -682,33 +976,36 @@ static void backward_pixel(const lso_state* st, int tile, int px, int py, const 
         float oml = 1.0f - last_alpha;
         for (int ch = 0; ch < 3; ch++) {
             float c = st->rgb[3 * g + ch];
-            acc[ch] = fmaf(last_alpha, last_c[ch], oml * acc[ch]);
+            acc[ch] = up ? u_sum2(form, last_alpha, last_c[ch], oml, acc[ch])
+                         : fmaf(last_alpha, last_c[ch], oml * acc[ch]);
             last_c[ch] = c;
-            dL_dalpha = fmaf(c - acc[ch], dpix[ch], dL_dalpha);
-            g_rgb[3 * g + ch] += (double)(dchannel_dcolor * dpix[ch]);
+            dL_dalpha = up ? u_addp(form, dL_dalpha, c - acc[ch], dpix[ch]) : fmaf(c - acc[ch], dpix[ch], dL_dalpha);
+            ga[6 + ch] += (double)(dchannel_dcolor * dpix[ch]);
         }
         if (feat) {
             for (int ch = 0; ch < 3; ch++) {
                 float f = st->lang[3 * g + ch];
-                accF[ch] = fmaf(last_alpha, last_f[ch], oml * accF[ch]);
+                accF[ch] = up ? u_sum2(form, last_alpha, last_f[ch], oml, accF[ch])
+                              : fmaf(last_alpha, last_f[ch], oml * accF[ch]);
                 last_f[ch] = f;
-                dL_dalpha = fmaf(f - accF[ch], dpixF[ch], dL_dalpha);
-                g_lang[3 * g + ch] += (double)(dchannel_dcolor * dpixF[ch]);
+                dL_dalpha = up ? u_addp(form, dL_dalpha, f - accF[ch], dpixF[ch])
+                               : fmaf(f - accF[ch], dpixF[ch], dL_dalpha);
+                ga[9 + ch] += (double)(dchannel_dcolor * dpixF[ch]);
             }
         }
         dL_dalpha = dL_dalpha * T;
         last_alpha = alpha;
-        dL_dalpha = fmaf(-T_final / one_m, bg_dot, dL_dalpha);
+        dL_dalpha = up ? u_addp(form, dL_dalpha, -T_final / one_m, bg_dot) : fmaf(-T_final / one_m, bg_dot, dL_dalpha);
         float dL_dG = co[3] * dL_dalpha;
         float gdx = G * dx, gdy = G * dy;
-        float dG_ddelx = -gdx * co[0] - gdy * co[1];
-        float dG_ddely = -gdy * co[2] - gdx * co[1];
-        g_xy[2 * g] += (double)(dL_dG * dG_ddelx * ddelx_dx);
-        g_xy[2 * g + 1] += (double)(dL_dG * dG_ddely * ddely_dy);
-        g_conic[3 * g + 0] += (double)(-0.5f * gdx * dx * dL_dG);
-        g_conic[3 * g + 1] += (double)(-0.5f * gdx * dy * dL_dG);
-        g_conic[3 * g + 2] += (double)(-0.5f * gdy * dy * dL_dG);
-        g_opac[g] += (double)(G * dL_dalpha);
+        float dG_ddelx = up ? u_diffp(form, -gdx, co[0], gdy, co[1]) : -gdx * co[0] - gdy * co[1];
+        float dG_ddely = up ? u_diffp(form, -gdy, co[2], gdx, co[1]) : -gdy * co[2] - gdx * co[1];
+        ga[0] += (double)(dL_dG * dG_ddelx * ddelx_dx);
+        ga[1] += (double)(dL_dG * dG_ddely * ddely_dy);
+        ga[2] += (double)(-0.5f * gdx * dx * dL_dG);
+        ga[3] += (double)(-0.5f * gdx * dy * dL_dG);
+        ga[4] += (double)(-0.5f * gdy * dy * dL_dG);
+        ga[5] += (double)(G * dL_dalpha);
     }
 }
 
@@ -723,13 +1020,9 @@ static void preprocess_backward_one(const lso_state* st, int i, float focal_x, f
     /* ---- cov2D backward ---- */
     float cov_local[6];
     const float* cov;
-    if (st->has_cov) cov = st->cov_pre + 6 * i;
-    else {
-        lso_cov3d(st->scales + 3 * i, s->scale_modifier, st->rots + 4 * i, cov_local);
-        cov = cov_local;
-    }
+    cov3d_of(st, i, cov_local, &cov);
     float t[3], A[2][3], abc[3], txtz, tytz;
-    cov2d(p, focal_x, focal_y, s->tanfovx, s->tanfovy, cov, s->viewmatrix, t, A, abc, &txtz, &tytz);
+    cov2d_of(st, p, focal_x, focal_y, cov, t, A, abc, &txtz, &tytz);
     const float limx = 1.3f * s->tanfovx, limy = 1.3f * s->tanfovy;
     const float x_grad_mul = (txtz < -limx || txtz > limx) ? 0.0f : 1.0f;
     const float y_grad_mul = (tytz < -limy || tytz > limy) ? 0.0f : 1.0f;
@@ -786,7 +1079,8 @@ static void preprocess_backward_one(const lso_state* st, int i, float focal_x, f
     /* ---- screen-space mean backward ---- */
     const float* m = s->projmatrix;
     float hom[4];
-    xform4x4(m, p, hom);
+    if (st->form == LSO_FORM_KERNEL) xform4x4(m, p, hom);
+    else u_xform4x4(st->form, m, p, hom);
     float m_w = 1.0f / (hom[3] + 0.0000001f);
     float mul1 = hom[0] * m_w * m_w;
     float mul2 = hom[1] * m_w * m_w;
@@ -834,49 +1128,55 @@ void lso_backward(const lso_state* st, const float* dL_dcolor, const float* dL_d
     if (dL_drot) memset(dL_drot, 0, sizeof(float) * 4 * (size_t)P);
     if (P == 0) return;
 
-    double* g_xy = (double*)calloc(2 * (size_t)P, sizeof(double));
-    double* g_conic = (double*)calloc(3 * (size_t)P, sizeof(double));
-    double* g_opac = (double*)calloc((size_t)P, sizeof(double));
-    double* g_rgb = (double*)calloc(3 * (size_t)P, sizeof(double));
-    double* g_lang = (double*)calloc(3 * (size_t)P, sizeof(double));
-    for (int ty = 0; ty < st->gy; ty++)
-        for (int tx = 0; tx < st->gx; tx++) {
-            int tile = ty * st->gx + tx;
-            for (int py = ty * BLOCK_Y; py < ty * BLOCK_Y + BLOCK_Y && py < H; py++)
-                for (int px = tx * BLOCK_X; px < tx * BLOCK_X + BLOCK_X && px < W; px++) {
-                    size_t pix = (size_t)py * W + px;
-                    float dpix[3] = {dL_dcolor[pix], dL_dcolor[HW + pix], dL_dcolor[2 * HW + pix]};
-                    float dpixF[3] = {0, 0, 0};
-                    if (dL_dlang) {
-                        dpixF[0] = dL_dlang[pix];
-                        dpixF[1] = dL_dlang[HW + pix];
-                        dpixF[2] = dL_dlang[2 * HW + pix];
-                    }
-                    backward_pixel(st, tile, px, py, dpix, dpixF, g_xy, g_conic, g_opac, g_rgb, g_lang);
+    /* per-thread accumulators (12 doubles per Gaussian), tiles dealt round-robin (a fixed
+       assignment for a given thread count), then summed over threads in thread order */
+    const int nth = lso_threads();
+    double* gacc = (double*)calloc((size_t)nth * 12 * (size_t)P, sizeof(double));
+    const int T_tiles = st->gx * st->gy;
+#pragma omp parallel for schedule(static, 1) num_threads(nth)
+    for (int tile = 0; tile < T_tiles; tile++) {
+#ifdef _OPENMP
+        double* mine = gacc + (size_t)omp_get_thread_num() * 12 * (size_t)P;
+#else
+        double* mine = gacc;
+#endif
+        const int ty = tile / st->gx, tx = tile % st->gx;
+        for (int py = ty * BLOCK_Y; py < ty * BLOCK_Y + BLOCK_Y && py < H; py++)
+            for (int px = tx * BLOCK_X; px < tx * BLOCK_X + BLOCK_X && px < W; px++) {
+                size_t pix = (size_t)py * W + px;
+                float dpix[3] = {dL_dcolor[pix], dL_dcolor[HW + pix], dL_dcolor[2 * HW + pix]};
+                float dpixF[3] = {0, 0, 0};
+                if (dL_dlang) {
+                    dpixF[0] = dL_dlang[pix];
+                    dpixF[1] = dL_dlang[HW + pix];
+                    dpixF[2] = dL_dlang[2 * HW + pix];
                 }
-        }
+                backward_pixel(st, tile, px, py, dpix, dpixF, mine);
+            }
+    }
     const float focal_y = (float)H / (2.0f * s->tanfovy);
     const float focal_x = (float)W / (2.0f * s->tanfovx);
+#pragma omp parallel for schedule(static)
     for (int i = 0; i < P; i++) {
         if (!(st->radii[i] > 0)) continue;
-        float dxy[2] = {(float)g_xy[2 * i], (float)g_xy[2 * i + 1]};
-        float dconic[3] = {(float)g_conic[3 * i], (float)g_conic[3 * i + 1], (float)g_conic[3 * i + 2]};
-        float drgb[3] = {(float)g_rgb[3 * i], (float)g_rgb[3 * i + 1], (float)g_rgb[3 * i + 2]};
+        double gsum[12];
+        for (int k = 0; k < 12; k++) gsum[k] = gacc[12 * (size_t)i + k];
+        for (int t = 1; t < nth; t++)
+            for (int k = 0; k < 12; k++) gsum[k] += gacc[((size_t)t * P + i) * 12 + k];
+        float dxy[2] = {(float)gsum[0], (float)gsum[1]};
+        float dconic[3] = {(float)gsum[2], (float)gsum[3], (float)gsum[4]};
+        float drgb[3] = {(float)gsum[6], (float)gsum[7], (float)gsum[8]};
         dL_dmeans2D[3 * i] = dxy[0];
         dL_dmeans2D[3 * i + 1] = dxy[1];
         for (int ch = 0; ch < 3; ch++) {
             dL_dcolors[3 * i + ch] = drgb[ch];
-            dL_dlang_out[3 * i + ch] = (float)g_lang[3 * i + ch];
+            dL_dlang_out[3 * i + ch] = (float)gsum[9 + ch];
         }
-        dL_dopacity[i] = (float)g_opac[i];
+        dL_dopacity[i] = (float)gsum[5];
         preprocess_backward_one(st, i, focal_x, focal_y, dxy, dconic, drgb, dL_dmeans3D, dL_dcov3D,
                                 dL_dsh, dL_dscales, dL_drot);
     }
-    free(g_xy);
-    free(g_conic);
-    free(g_opac);
-    free(g_rgb);
-    free(g_lang);
+    free(gacc);
 }
 
 /* ------------------------------------------------------------------------------------------ */

@@ -37,7 +37,13 @@ class _Settings(ctypes.Structure):
         ("viewmatrix", ctypes.c_float * 16),
         ("projmatrix", ctypes.c_float * 16),
         ("campos", ctypes.c_float * 3),
+        ("form", ctypes.c_int32),
     ]
+
+# arithmetic forms of lsr_oracle.c ("Upstream forms"): KERNEL is the kernels' operation sequence
+# (the bit-exact contract); UPSTREAM / UPSTREAM_FMA evaluate the published rasterizer's source
+# expressions, without / with nvcc-style multiply-add contraction
+FORM_KERNEL, FORM_UPSTREAM, FORM_UPSTREAM_FMA = 0, 1, 2
 
 
 def build(force: bool = False) -> str:
@@ -79,6 +85,8 @@ def lib():
         L.lso_activate.argtypes = [ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 8
         L.lso_activate_backward.restype = None
         L.lso_activate_backward.argtypes = [ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 12
+        L.lso_num_threads.restype = ctypes.c_int
+        L.lso_num_threads.argtypes = []
         L.lso_knn_mean_dist3.restype = None
         L.lso_knn_mean_dist3.argtypes = [ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]
         L.lso_cov3d_backward.restype = None
@@ -103,9 +111,10 @@ def _ptr(a):
     return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
 
 
-def make_settings(s) -> _Settings:
+def make_settings(s, form: int = FORM_KERNEL) -> _Settings:
     """From a GaussianRasterizationSettings-like object (fields of gaussian_renderer/__init__.py:37-51)."""
     out = _Settings()
+    out.form = int(form)
     out.image_height = int(s.image_height)
     out.image_width = int(s.image_width)
     out.tanfovx = float(s.tanfovx)
@@ -130,10 +139,12 @@ class OracleRun:
     }
 
     def __init__(self, settings, means3D, opacities, shs=None, colors_precomp=None,
-                 language_feature_precomp=None, scales=None, rotations=None, cov3D_precomp=None):
+                 language_feature_precomp=None, scales=None, rotations=None, cov3D_precomp=None,
+                 form=FORM_KERNEL):
         L = lib()
         self.settings = settings
-        st = make_settings(settings)
+        self.form = int(form)
+        st = make_settings(settings, form)
         self._st = st
         H, W = st.image_height, st.image_width
         self.H, self.W = H, W
@@ -225,6 +236,11 @@ class OracleRun:
 
 def forward(settings, **kw) -> OracleRun:
     return OracleRun(settings, **kw)
+
+
+def num_threads() -> int:
+    """Threads of the oracle's OpenMP loops (OMP_NUM_THREADS, else the host's cores)."""
+    return int(lib().lso_num_threads())
 
 
 def expf(x: float) -> float:
