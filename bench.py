@@ -106,6 +106,92 @@ class Opt:
     include_feature = True
 
 
+class OptRGB:
+    """arguments/__init__.py:74-94 OptimizationParams for the RGB stage (include_feature=False)."""
+    include_feature = False
+    position_lr_init = 0.00016
+    feature_lr = 0.0025
+    opacity_lr = 0.05
+    scaling_lr = 0.005
+    rotation_lr = 0.001
+    lambda_dssim = 0.2
+
+
+def _ssim_window(window_size, channel, device):
+    """utils/loss_utils.py:24-33: the 11 x 11 Gaussian window (sigma 1.5), one per channel."""
+    x = torch.arange(window_size, dtype=torch.float64) - window_size // 2
+    g = torch.exp(-x * x / (2 * 1.5 ** 2))
+    g = (g / g.sum()).float().unsqueeze(1)
+    w = g.mm(g.t()).unsqueeze(0).unsqueeze(0)
+    return w.expand(channel, 1, window_size, window_size).contiguous().to(device)
+
+
+def ssim(img1, img2, window_size=11):
+    """utils/loss_utils.py:35-63 (size_average=True) as torch ops: the RGB stage's loss consumer of
+    the rasterizer output (outside the hot path; MIOpen convolutions here)."""
+    F = torch.nn.functional
+    channel = img1.size(-3)
+    w = _ssim_window(window_size, channel, img1.device).type_as(img1)
+    pad = window_size // 2
+    mu1 = F.conv2d(img1, w, padding=pad, groups=channel)
+    mu2 = F.conv2d(img2, w, padding=pad, groups=channel)
+    mu1_sq, mu2_sq, mu1_mu2 = mu1.pow(2), mu2.pow(2), mu1 * mu2
+    s1 = F.conv2d(img1 * img1, w, padding=pad, groups=channel) - mu1_sq
+    s2 = F.conv2d(img2 * img2, w, padding=pad, groups=channel) - mu2_sq
+    s12 = F.conv2d(img1 * img2, w, padding=pad, groups=channel) - mu1_mu2
+    C1, C2 = 0.01 ** 2, 0.03 ** 2
+    m = ((2 * mu1_mu2 + C1) * (2 * s12 + C2)) / ((mu1_sq + mu2_sq + C1) * (s1 + s2 + C2))
+    return m.mean()
+
+
+class RGBStep:
+    """The RGB stage's train step (train.py:76-138 with include_feature=False): render, the loss of
+    train.py:100-103 ((1 - lambda_dssim) L1 + lambda_dssim (1 - SSIM) on the colour image), backward
+    through every geometry / appearance gradient, the densification statistics of train.py:125-126
+    (one kernel), Adam over the six groups of scene/gaussian_model.py:219-226 (one launch), zero_grad.
+    N > 1: the six gradients and the statistics in one GradBucket all-reduce, max radii by MAX."""
+
+    def __init__(self, params, cam, gt_image, bucket_world=1, spatial_lr_scale=1.0):
+        self.model = Model(params, include_feature=False)
+        self.cam, self.gt = cam, gt_image
+        P = params.P
+        dev = params.xyz.device
+        o = OptRGB
+        m = self.model
+        groups = [{"params": [m._xyz], "lr": o.position_lr_init * spatial_lr_scale, "name": "xyz"},
+                  {"params": [m._features_dc], "lr": o.feature_lr, "name": "f_dc"},
+                  {"params": [m._features_rest], "lr": o.feature_lr / 20.0, "name": "f_rest"},
+                  {"params": [m._opacity], "lr": o.opacity_lr, "name": "opacity"},
+                  {"params": [m._scaling], "lr": o.scaling_lr, "name": "scaling"},
+                  {"params": [m._rotation], "lr": o.rotation_lr, "name": "rotation"}]
+        self.optim = AmdAdam(groups, lr=0.0, eps=1e-15)
+        # scene/gaussian_model.py:196-201 training_setup state of the densification statistics
+        self.max_radii2D = torch.zeros((P,), device=dev)
+        self.xyz_gradient_accum = torch.zeros((P, 1), device=dev)
+        self.denom = torch.zeros((P, 1), device=dev)
+        self.bucket = GradBucket(m.trainable(), densify_points=P) if bucket_world > 1 else None
+        self.bg = torch.zeros(3, device=dev)
+
+    def __call__(self):
+        pkg = render(self.cam, self.model, Pipe, self.bg, OptRGB)
+        image = pkg["render"]
+        Ll1 = torch.abs(image - self.gt).mean()
+        loss = (1.0 - OptRGB.lambda_dssim) * Ll1 + OptRGB.lambda_dssim * (1.0 - ssim(image, self.gt))
+        loss.backward()
+        vgrad = pkg["viewspace_points"].grad
+        if self.bucket is None:
+            _native.densification_stats(pkg["radii"], vgrad, self.max_radii2D, self.xyz_gradient_accum, self.denom)
+            self.optim.step()
+            self.optim.zero_grad(set_to_none=True)
+        else:
+            self.bucket.stage_densification(pkg["radii"], vgrad, self.max_radii2D)
+            self.bucket.all_reduce(average=True)
+            self.bucket.apply_densification(self.xyz_gradient_accum, self.denom)
+            self.optim.step()
+            self.bucket.zero()
+        return loss
+
+
 def algorithmic_bytes(stage, P, V, R, HW, M, color_grad=True, geometry=True, fused_loss=False):
     """Compulsory HBM bytes per launch of each stage (SURVEY.md §8d per-unit model).
     The render backward's per-pixel and per-Gaussian terms follow its variant: dL/dcolor is read
@@ -360,6 +446,24 @@ def main():
     elapsed_all = time.perf_counter() - t1
     gc.enable()
     _native.FORCE_GEOMETRY_GRADS = os.environ.get("LSR_ALL_GRADS", "0") == "1"
+    # the RGB stage's step on the same scene and view (all six groups trainable, L1 + SSIM, densification
+    # statistics): reported beside, never as `value`
+    rgb_ms = None
+    if os.environ.get("LSR_BENCH_RGB", "1") != "0":
+        gtimg = torch.rand((3, H, W), generator=torch.Generator().manual_seed(200 + view)).to(dev)
+        rgb = RGBStep(make_gaussians(P, seed=0, sh_degree=c["sh_degree"]).to(dev), cam, gtimg, bucket_world=world)
+        for _ in range(3):
+            rgb()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        rgb_steps = max(1, args.steps // 2)
+        for _ in range(rgb_steps):
+            rgb()
+        torch.cuda.synchronize()
+        rgb_ms = 1000.0 * (time.perf_counter() - t2) / rgb_steps
+        del rgb
     # stage breakdown: a separate, untimed pass with every stage profiled
     prof_steps = min(args.steps, 10)
     _native.profile_enable(True)
@@ -449,6 +553,7 @@ def main():
                                 "scene/gaussian_model.py:203-217)"},
         "ms_per_step_with_sync": round(1000.0 * elapsed_sync / args.steps, 4),
         "ms_per_step_all_gradients": round(1000.0 * elapsed_all / args.steps, 4),
+        "ms_per_step_rgb": None if rgb_ms is None else round(rgb_ms, 4),
         "raster_ms_per_step": round(raster_ms, 4),
         "stages_ms_per_step": {k: round(v["total_ms"] / prof_steps, 4) for k, v in sorted(prof.items())},
         "roofline": roofline,

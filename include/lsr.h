@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define LSR_ABI_VERSION 6
+#define LSR_ABI_VERSION 7
 
 enum lsr_status {
     LSR_OK = 0,
@@ -74,11 +74,15 @@ enum lsr_raw_flags {
     LSR_RAW_LANGUAGE = 8    /* language_feature = _language_feature: x / (||x|| + 1e-9)             */
 };
 
-/* The language step's backward (no geometry gradient, no colour gradient) accumulates 32-byte
+/* The language step's backward (no geometry gradient, no colour gradient) accumulates 20-byte
  * per-Gaussian gradient records that must start at zero.  With LSR_FWD_ZERO_GRAD_RECORDS the
  * forward clears them inside its compositing kernel (stores beside a VALU-bound loop: no separate
  * memset launch) in the geometry buffer; the FIRST backward of that forward then passes
- * LSR_BWD_RECORDS_ZEROED and uses them as they are.  Any other backward clears its own records. */
+ * LSR_BWD_RECORDS_ZEROED and uses them as they are.  Any other backward clears its own records.
+ * LSR_BWD_RECORDS_ZEROED is only valid for the first backward of a forward that passed
+ * LSR_FWD_ZERO_GRAD_RECORDS, and lsr_backward_args.dL_dloss only for a forward that fused the loss
+ * (out_loss set): the forward records both in its image buffer, and with settings.debug the
+ * backward checks them and fails with LSR_ERR_INVALID instead of reading stale records or codes. */
 enum lsr_forward_flags { LSR_FWD_ZERO_GRAD_RECORDS = 1 };
 enum lsr_backward_flags { LSR_BWD_RECORDS_ZEROED = 1 };
 
@@ -189,7 +193,7 @@ typedef struct lsr_state_layout {
     size_t sorted_ids;     /* uint32[P]  Gaussians by (depth, id); culled ones tie with the farthest */
     size_t super_offset;   /* uint32[P]  first super-tile entry of the Gaussian of depth rank r */
     /* image buffer */
-    size_t counters;       /* uint32[16] {reserved, num_rendered, error, reserved, super entries, ...} */
+    size_t counters;       /* uint32[16] {reserved, num_rendered, error, forward flags, super entries, ...} */
     size_t ranges;         /* uint32[2T] [start, end) of each tile in point_list */
     size_t final_T;        /* float[H*W] */
     size_t n_contrib;      /* uint32[H*W] */
@@ -201,9 +205,11 @@ typedef struct lsr_state_layout {
 int32_t lsr_abi_version(void);
 const char* lsr_last_error(void);
 
-/* Sizes (bytes) of the forward scratch buffers (binning: an upper bound for any scene with
- * num_rendered tile instances; the forward requests the exact size). */
-size_t lsr_geom_bytes(int32_t P);
+/* Sizes (bytes) of the forward scratch buffers, exactly what lsr_forward requests for the geometry
+ * and image buffers (the geometry buffer holds one fused-loss word per tile, so it depends on the
+ * image size too); binning: an upper bound for any scene with num_rendered tile instances (the
+ * forward requests the size its super-tile entry count needs, at most this). */
+size_t lsr_geom_bytes(int32_t P, int32_t width, int32_t height);
 size_t lsr_image_bytes(int32_t width, int32_t height);
 size_t lsr_binning_bytes(int32_t width, int32_t height, int64_t num_rendered);
 size_t lsr_backward_bytes(int32_t P);
@@ -304,6 +310,29 @@ int32_t lsr_debug_bucket_timeline(uint32_t* out, int32_t n);
  * schedules, scene/gaussian_model.py:231-241). */
 int32_t lsr_adam_step(int64_t n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq, double lr,
                       double beta1, double beta2, double eps, int64_t step, void* stream);
+
+/* The same step for several tensors in ONE launch (RGB mode's six parameter groups,
+ * scene/gaussian_model.py:219-226, each with its own lr, betas, eps and step count, i.e. torch's
+ * per-parameter state).  Every gradient is multiplied by grad_scale first (e.g. the 1 / N of a
+ * gradient all-reduced as a SUM over N ranks; 1 = none). */
+typedef struct lsr_adam_tensor {
+    int64_t n;
+    float* param;
+    const float* grad;
+    float* exp_avg;
+    float* exp_avg_sq;
+    double lr, beta1, beta2, eps;
+    int64_t step;                /* 1-based, after this update */
+} lsr_adam_tensor;
+int32_t lsr_adam_multi(int32_t count, const lsr_adam_tensor* tensors, float grad_scale, void* stream);
+
+/* Densification statistics of one rendered view, one pass (train.py:125-126 with
+ * GaussianModel.add_densification_stats, scene/gaussian_model.py:480-482), for Gaussians with
+ * radii > 0:  max_radii2D = max(max_radii2D, radii);  xyz_gradient_accum += ||dL_dmeans2D[:, :2]||;
+ * denom += 1.  dL_dmeans2D is P x 3 (viewspace_points.grad); the three outputs are P floats each
+ * (the reference's (P,) and (P, 1) tensors); any of them may be NULL (not updated). */
+int32_t lsr_densification_stats(int32_t P, const int32_t* radii, const float* dL_dmeans2D, float* max_radii2D,
+                                float* xyz_gradient_accum, float* denom, void* stream);
 
 /* ---- point-cloud initialisation --------------------------------------
  * simple-knn's distCUDA2 (scene/gaussian_model.py:20,180): for each of the N points (N x 3 fp32),

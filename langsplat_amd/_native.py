@@ -22,7 +22,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LSR_LIB") or os.path.join(_HERE, "liblsr.so")
 
 LSR_BUF_GEOM, LSR_BUF_BINNING, LSR_BUF_IMAGE, LSR_BUF_BACKWARD = 0, 1, 2, 3
-ABI_VERSION = 6
+ABI_VERSION = 7
 # lsr_raw_flags (include/lsr.h): inputs are GaussianModel's raw parameters
 RAW_OPACITY, RAW_SCALES, RAW_ROTATIONS, RAW_LANGUAGE = 1, 2, 4, 8
 FWD_ZERO_GRAD_RECORDS = 1  # lsr_forward_flags
@@ -78,13 +78,19 @@ class LsrKernelStat(ctypes.Structure):
     _fields_ = [("name", ctypes.c_char * 32), ("launches", ctypes.c_int64), ("total_ms", ctypes.c_double)]
 
 
+class LsrAdamTensor(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int64), ("param", _vp), ("grad", _vp), ("exp_avg", _vp), ("exp_avg_sq", _vp),
+                ("lr", ctypes.c_double), ("beta1", ctypes.c_double), ("beta2", ctypes.c_double),
+                ("eps", ctypes.c_double), ("step", ctypes.c_int64)]
+
+
 ALLOC_FN = ctypes.CFUNCTYPE(_vp, _vp, ctypes.c_int32, ctypes.c_size_t)
 
 # symbol -> (restype, argtypes); must cover every function declared in include/lsr.h
 SIGNATURES = {
     "lsr_abi_version": (ctypes.c_int32, []),
     "lsr_last_error": (ctypes.c_char_p, []),
-    "lsr_geom_bytes": (ctypes.c_size_t, [ctypes.c_int32]),
+    "lsr_geom_bytes": (ctypes.c_size_t, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
     "lsr_image_bytes": (ctypes.c_size_t, [ctypes.c_int32, ctypes.c_int32]),
     "lsr_binning_bytes": (ctypes.c_size_t, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int64]),
     "lsr_backward_bytes": (ctypes.c_size_t, [ctypes.c_int32]),
@@ -97,6 +103,8 @@ SIGNATURES = {
     "lsr_mark_visible": (ctypes.c_int32, [ctypes.c_int32, _vp, _vp, _vp, _vp, _vp]),
     "lsr_adam_step": (ctypes.c_int32, [ctypes.c_int64, _vp, _vp, _vp, _vp, ctypes.c_double, ctypes.c_double,
                                        ctypes.c_double, ctypes.c_double, ctypes.c_int64, _vp]),
+    "lsr_adam_multi": (ctypes.c_int32, [ctypes.c_int32, ctypes.POINTER(LsrAdamTensor), ctypes.c_float, _vp]),
+    "lsr_densification_stats": (ctypes.c_int32, [ctypes.c_int32, _vp, _vp, _vp, _vp, _vp, _vp]),
     "lsr_dist_cuda2": (ctypes.c_int32, [ctypes.c_int64, _vp, _vp, ALLOC_FN, _vp, _vp]),
     "lsr_masked_l1_scratch_bytes": (ctypes.c_size_t, [ctypes.c_int32, ctypes.c_int64]),
     "lsr_masked_l1_forward": (ctypes.c_int32, [ctypes.c_int32, ctypes.c_int64, _vp, _vp, _vp, ctypes.c_int32, _vp, _vp,
@@ -440,6 +448,26 @@ def rasterize_gaussians_backward(rs, means3D, shs, colors_precomp, language_feat
     with _on_device(device), alloc:
         _check(lib.lsr_backward(ctypes.byref(s), ctypes.byref(a), _ALLOC_CB, None, _stream(device)), "lsr_backward")
     return g
+
+
+def densification_stats(radii, dmeans2D, max_radii2D=None, xyz_gradient_accum=None, denom=None):
+    """train.py:125-126 in one kernel (include/lsr.h lsr_densification_stats), in place: for radii > 0,
+    max_radii2D = max(max_radii2D, radii), xyz_gradient_accum += ||dmeans2D[:, :2]||, denom += 1."""
+    lib = load()
+    P = int(radii.shape[0])
+    outs = []
+    for t, shape in ((max_radii2D, (P,)), (xyz_gradient_accum, (P, 1)), (denom, (P, 1))):
+        if t is not None and (t.dtype != torch.float32 or not t.is_contiguous() or t.numel() != P):
+            raise ValueError(f"densification_stats: expected a contiguous fp32 tensor of {shape}")
+        outs.append(_ptr(t))
+    if radii.dtype != torch.int32 or not radii.is_contiguous():
+        raise ValueError("densification_stats: radii must be a contiguous int32 tensor")
+    g = _f32c(dmeans2D.detach())
+    if tuple(g.shape) != (P, 3):
+        raise ValueError("densification_stats: dmeans2D must be (P, 3)")
+    with _on_device(radii.device):
+        _check(lib.lsr_densification_stats(P, _ptr(radii), _ptr(g), *outs, _stream(radii.device)),
+               "lsr_densification_stats")
 
 
 def mark_visible(means3D, viewmatrix, projmatrix):

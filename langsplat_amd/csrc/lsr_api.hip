@@ -240,13 +240,28 @@ static int32_t fail(int32_t code, const char* what, hipError_t e = hipSuccess)
         if (_e != hipSuccess) return fail(LSR_ERR_HIP, what, _e);            \
     } while (0)
 
+static AdamScalars adam_scalars(double lr, double beta1, double beta2, double eps, int64_t step)
+{
+    // torch/optim/adam.py _single_tensor_adam: Python-float scalars, cast where they meet tensors
+    const double bc1 = 1.0 - pow(beta1, (double)step);
+    const double bc2 = 1.0 - pow(beta2, (double)step);
+    AdamScalars a;
+    a.w1 = (float)(1.0 - beta1);
+    a.beta2 = (float)beta2;
+    a.w2 = (float)(1.0 - beta2);
+    a.inv_bc2_sqrt = 1.0f / (float)sqrt(bc2);
+    a.eps = (float)eps;
+    a.neg_step_size = (float)(-(lr / bc1));
+    return a;
+}
+
 extern "C" {
 
 int32_t lsr_abi_version(void) { return LSR_ABI_VERSION; }
 
 const char* lsr_last_error(void) { return g_last_error.c_str(); }
 
-size_t lsr_geom_bytes(int32_t P) { return make_layout(P, 0, 0, 0, 0).geom_bytes; }
+size_t lsr_geom_bytes(int32_t P, int32_t width, int32_t height) { return make_layout(P, width, height, 0, 0).geom_bytes; }
 
 size_t lsr_image_bytes(int32_t width, int32_t height) { return make_layout(0, width, height, 0, 0).image_bytes; }
 
@@ -391,7 +406,10 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
     // sorts while the host waits, instead of idling until the host has enqueued the next launch.
     // Should the range need more passes than guessed, the sort is run again below.
     const uint32_t seq = ++hb->seq == 0 ? ++hb->seq : hb->seq;
-    LSR_TRY(launch_publish_counters((P + kPreThreads - 1) / kPreThreads, pp.partial, counters, hb->slot, seq, stream),
+    const uint32_t fwd_flags = ((a->flags & LSR_FWD_ZERO_GRAD_RECORDS) ? kFwdZeroedRecords : 0u) |
+                               ((a->out_loss && s->include_feature && a->language_feature) ? kFwdFusedLoss : 0u);
+    LSR_TRY(launch_publish_counters((P + kPreThreads - 1) / kPreThreads, pp.partial, counters, hb->slot, seq,
+                                    fwd_flags, stream),
             "publish counters");
     const int guess = hb->depth_passes > 0 ? hb->depth_passes : 4;
     // MSD path: the bucket sort also emits the super-tile entries (into geometry arrays of fixed
@@ -510,6 +528,19 @@ int32_t lsr_backward(const lsr_settings* s, const lsr_backward_args* a, lsr_allo
     char* geom = static_cast<char*>(a->geom_buffer);
     char* image = static_cast<char*>(a->image_buffer);
     char* binning = static_cast<char*>(a->binning_buffer);
+    if (debug && (a->flags & LSR_BWD_RECORDS_ZEROED || a->dL_dloss)) {
+        // what the forward prepared (counters[kCntFwdFlags]; the render backward clears the records
+        // bit, so a second backward cannot reuse accumulated records)
+        uint32_t ff = 0;
+        LSR_TRY(hipMemcpyAsync(&ff, image + L.counters + 4 * kCntFwdFlags, 4, hipMemcpyDeviceToHost, stream),
+                "read forward flags");
+        LSR_TRY(hipStreamSynchronize(stream), "read forward flags");
+        if ((a->flags & LSR_BWD_RECORDS_ZEROED) && !(ff & kFwdZeroedRecords))
+            return fail(LSR_ERR_INVALID, "lsr_backward: LSR_BWD_RECORDS_ZEROED, but the forward did not clear the "
+                                         "records (LSR_FWD_ZERO_GRAD_RECORDS) or they were used by a backward");
+        if (a->dL_dloss && !(ff & kFwdFusedLoss))
+            return fail(LSR_ERR_INVALID, "lsr_backward: dL_dloss, but the forward did not fuse the loss");
+    }
     // the render backward's 5-value form (no geometry, no colour gradient) keeps 20-B records; the
     // first backward of a forward that cleared them (LSR_FWD_ZERO_GRAD_RECORDS) uses them directly
     const bool compact = !geometry && !a->dL_dout_color;
@@ -543,6 +574,7 @@ int32_t lsr_backward(const lsr_settings* s, const lsr_backward_args* a, lsr_allo
     rp.dL_dloss = a->dL_dloss;
     rp.loss_code = reinterpret_cast<uint8_t*>(image + L.loss_code);
     rp.grad = grad;
+    rp.fwd_flags = reinterpret_cast<uint32_t*>(image + L.counters) + kCntFwdFlags;
     rp.geo = geometry ? 1 : 0;
     if (a->num_rendered > 0) LSR_TRY(launch_render_backward(rp, L.tiles, stream), "render backward");
     if (!geometry) {
@@ -761,17 +793,45 @@ int32_t lsr_adam_step(int64_t n, float* param, const float* grad, float* exp_avg
         return fail(LSR_ERR_INVALID, "lsr_adam_step: invalid argument");
     hipStream_t stream = reinterpret_cast<hipStream_t>(stream_ptr);
     const bool debug = false;
-    // torch/optim/adam.py _single_tensor_adam: Python-float scalars, cast where they meet tensors
-    const double bc1 = 1.0 - pow(beta1, (double)step);
-    const double bc2 = 1.0 - pow(beta2, (double)step);
-    AdamScalars a;
-    a.w1 = (float)(1.0 - beta1);
-    a.beta2 = (float)beta2;
-    a.w2 = (float)(1.0 - beta2);
-    a.inv_bc2_sqrt = 1.0f / (float)sqrt(bc2);
-    a.eps = (float)eps;
-    a.neg_step_size = (float)(-(lr / bc1));
+    const AdamScalars a = adam_scalars(lr, beta1, beta2, eps, step);
     LSR_TRY(launch_adam(n, param, grad, exp_avg, exp_avg_sq, a, stream), "adam");
+    return LSR_OK;
+}
+
+int32_t lsr_adam_multi(int32_t count, const lsr_adam_tensor* tensors, float grad_scale, void* stream_ptr)
+{
+    if (count < 0 || (count > 0 && !tensors)) return fail(LSR_ERR_INVALID, "lsr_adam_multi: invalid argument");
+    hipStream_t stream = reinterpret_cast<hipStream_t>(stream_ptr);
+    const bool debug = false;
+    for (int32_t k0 = 0; k0 < count; k0 += kAdamMaxTensors) {
+        AdamTable tab{};
+        for (int32_t k = k0; k < count && k < k0 + kAdamMaxTensors; k++) {
+            const lsr_adam_tensor& t = tensors[k];
+            if (t.n < 0 || (t.n > 0 && (!t.param || !t.grad || !t.exp_avg || !t.exp_avg_sq)) || t.step < 1)
+                return fail(LSR_ERR_INVALID, "lsr_adam_multi: invalid tensor entry");
+            if (t.n == 0) continue;
+            AdamSegment& g = tab.seg[tab.count++];
+            g.param = t.param;
+            g.grad = t.grad;
+            g.m = t.exp_avg;
+            g.v = t.exp_avg_sq;
+            g.n = t.n;
+            g.a = adam_scalars(t.lr, t.beta1, t.beta2, t.eps, t.step);
+        }
+        LSR_TRY(launch_adam_multi(tab, grad_scale, stream), "adam");
+    }
+    return LSR_OK;
+}
+
+int32_t lsr_densification_stats(int32_t P, const int32_t* radii, const float* dL_dmeans2D, float* max_radii2D,
+                                float* xyz_gradient_accum, float* denom, void* stream_ptr)
+{
+    if (P < 0 || (P > 0 && (!radii || !dL_dmeans2D)))
+        return fail(LSR_ERR_INVALID, "lsr_densification_stats: invalid argument");
+    hipStream_t stream = reinterpret_cast<hipStream_t>(stream_ptr);
+    const bool debug = false;
+    LSR_TRY(launch_densification_stats(P, radii, dL_dmeans2D, max_radii2D, xyz_gradient_accum, denom, stream),
+            "densification stats");
     return LSR_OK;
 }
 

@@ -227,7 +227,8 @@ constexpr int kPublishThreads = 1024;
 
 __global__ __launch_bounds__(kPublishThreads) void k_publish_counters(int nb, const uint4* __restrict__ partial,
                                                                       uint32_t* __restrict__ counters,
-                                                                      uint64_t* host_slots, uint32_t seq)
+                                                                      uint64_t* host_slots, uint32_t seq,
+                                                                      uint32_t fwd_flags)
 {
     constexpr int kWaves = kPublishThreads / 64;
     __shared__ uint32_t red[4][kWaves];
@@ -251,7 +252,7 @@ __global__ __launch_bounds__(kPublishThreads) void k_publish_counters(int nb, co
     }
     for (int i = threadIdx.x; i < kCntWords; i += kPublishThreads)
         if (i != kCntRendered && i != kCntSuper && i != kCntKeyMin && i != kCntKeyMax && i != kCntError)
-            counters[i] = 0u;
+            counters[i] = i == kCntFwdFlags ? fwd_flags : 0u;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         t += __shfl_xor(t, o, 64);
@@ -287,10 +288,10 @@ __global__ __launch_bounds__(kPublishThreads) void k_publish_counters(int nb, co
 }
 
 hipError_t launch_publish_counters(int nb, const uint4* partial, uint32_t* counters, uint64_t* host_slots,
-                                   uint32_t seq, hipStream_t s)
+                                   uint32_t seq, uint32_t fwd_flags, hipStream_t s)
 {
     hipLaunchKernelGGL(k_publish_counters, dim3(1), dim3(kPublishThreads), 0, s, nb, partial, counters, host_slots,
-                       seq);
+                       seq, fwd_flags);
     return hipGetLastError();
 }
 

@@ -15,6 +15,16 @@ namespace lsr {
 constexpr int kTile = 16;              // BLOCK_X = BLOCK_Y = 16
 constexpr int kTilePixels = kTile * kTile;
 
+// Four floats of a caller's tensor at a dword-aligned address.  A contiguous torch view may start at
+// any float (and a 180-B _features_rest row at a 4-B boundary), so the type tells the compiler the
+// real alignment; gfx950's global_load_dwordx4 needs only dword alignment, so it is still one load.
+typedef float lsr_f4u __attribute__((ext_vector_type(4), aligned(4)));
+__device__ __forceinline__ float4 load_f4u(const void* ptr)
+{
+    const lsr_f4u v = *reinterpret_cast<const lsr_f4u*>(ptr);
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+
 // SH constants, utils/sh_utils.py:26-45
 constexpr float SH_C0 = 0.28209479177387814f;
 constexpr float SH_C1 = 0.4886025119029199f;

@@ -14,11 +14,15 @@ namespace lsr {
 enum Counter : int {
     kCntRendered = 1,
     kCntError = 2,
+    kCntFwdFlags = 3,    // what the forward prepared for its backward: kFwdZeroedRecords | kFwdFusedLoss
     kCntSuper = 4,       // super-tile entries E (binning)
     kCntKeyMin = 5,      // smallest visible depth key (float bits)
     kCntKeyMax = 6,      // largest visible depth key
     kCntSlots = 16
 };
+constexpr uint32_t kFwdZeroedRecords = 1u;  // the language step's gradient records cleared (the render
+                                            // backward clears this bit: only its first use is valid)
+constexpr uint32_t kFwdFusedLoss = 2u;      // loss codes written (dL_dloss is valid)
 // longest-first tile schedule (lsr_render.hip): tiles per work class, forward and backward,
 // right after the counters so one memset clears both
 constexpr int kWorkClasses = 64;
@@ -214,6 +218,7 @@ struct RenderParams {
     // backward
     const float *dL_dcolor, *dL_dlang;
     float* grad;
+    uint32_t* fwd_flags;  // counters[kCntFwdFlags] of the forward (its records bit is cleared)
     // fused language-feature loss (null: off).  forward: gt (3 x HW), mask (HW bool bytes) -> codes,
     // per-workgroup partials, out_loss; backward: dL_dloss (device scalar) with the forward's codes
     const float* loss_gt;
@@ -287,6 +292,22 @@ struct AdamScalars {
 };
 hipError_t launch_adam(int64_t n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
                        const AdamScalars& a, hipStream_t s);
+constexpr int kAdamMaxTensors = 16;
+struct AdamSegment {
+    float* param;
+    const float* grad;
+    float *m, *v;
+    int64_t n, block0;
+    AdamScalars a;
+    int vec;
+};
+struct AdamTable {
+    int count;
+    AdamSegment seg[kAdamMaxTensors];
+};
+hipError_t launch_adam_multi(AdamTable& tab, float grad_scale, hipStream_t s);
+hipError_t launch_densification_stats(int P, const int* radii, const float* dmeans2D, float* max_radii, float* accum,
+                                      float* denom, hipStream_t s);
 
 // out[i] = sum(in[0..i)); region: scan_region_words(n) zeroed words (single-pass look-back scan)
 hipError_t scan_exclusive_u32(const uint32_t* in, uint32_t* out, int n, uint32_t* region, uint32_t* fault,
@@ -294,7 +315,7 @@ hipError_t scan_exclusive_u32(const uint32_t* in, uint32_t* out, int n, uint32_t
 // reduces the preprocess block partials into counters and publishes counters[0..7], each with seq,
 // to the host slots (8 x u64 pinned)
 hipError_t launch_publish_counters(int nb, const uint4* partial, uint32_t* counters, uint64_t* host_slots,
-                                   uint32_t seq, hipStream_t s);
+                                   uint32_t seq, uint32_t fwd_flags, hipStream_t s);
 size_t knn_scratch_bytes(int64_t N);
 hipError_t launch_knn_mean_dist3(int64_t N, const float* pts, float* out, void* scratch, uint32_t* stall,
                                  hipStream_t s);

@@ -24,6 +24,90 @@ __device__ __forceinline__ void adam_one(float& p, float g, float& m, float& v, 
     p = p + a.neg_step_size * m / denom;
 }
 
+// A table of tensors stepped by ONE launch (lsr_adam_multi): RGB mode's six parameter groups
+// (scene/gaussian_model.py:219-226) -- each with its own lr, step count and moments, i.e. torch's
+// per-parameter state -- in one pass, their gradients typically the slices of one all-reduced bucket
+// (langsplat_amd.distributed.GradBucket).  grad_scale multiplies every gradient first (the 1 / N of
+// an averaging all-reduce done as a SUM; 1: none).
+__global__ __launch_bounds__(256) void k_adam_multi(AdamTable tab, float grad_scale)
+{
+    int s = 0;
+    while (s + 1 < tab.count && (int64_t)blockIdx.x >= tab.seg[s + 1].block0) s++;
+    const AdamSegment& g = tab.seg[s];
+    const int64_t first = ((int64_t)blockIdx.x - g.block0) * 256 + threadIdx.x;
+    const bool scale = grad_scale != 1.0f;
+    if (g.vec) {
+        const int64_t i = first;
+        if (4 * i + 3 < g.n) {
+            float4 p = reinterpret_cast<float4*>(g.param)[i], m = reinterpret_cast<float4*>(g.m)[i],
+                   v = reinterpret_cast<float4*>(g.v)[i];
+            float4 gr = reinterpret_cast<const float4*>(g.grad)[i];
+            if (scale) gr = make_float4(gr.x * grad_scale, gr.y * grad_scale, gr.z * grad_scale, gr.w * grad_scale);
+            adam_one(p.x, gr.x, m.x, v.x, g.a);
+            adam_one(p.y, gr.y, m.y, v.y, g.a);
+            adam_one(p.z, gr.z, m.z, v.z, g.a);
+            adam_one(p.w, gr.w, m.w, v.w, g.a);
+            reinterpret_cast<float4*>(g.param)[i] = p;
+            reinterpret_cast<float4*>(g.m)[i] = m;
+            reinterpret_cast<float4*>(g.v)[i] = v;
+        } else {
+            for (int64_t k = 4 * i; k < g.n; k++) {
+                const float gr = scale ? g.grad[k] * grad_scale : g.grad[k];
+                adam_one(g.param[k], gr, g.m[k], g.v[k], g.a);
+            }
+        }
+        return;
+    }
+    if (first < g.n) {
+        const float gr = scale ? g.grad[first] * grad_scale : g.grad[first];
+        adam_one(g.param[first], gr, g.m[first], g.v[first], g.a);
+    }
+}
+
+hipError_t launch_adam_multi(AdamTable& tab, float grad_scale, hipStream_t s)
+{
+    int64_t blocks = 0;
+    auto al = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+    for (int k = 0; k < tab.count; k++) {
+        AdamSegment& g = tab.seg[k];
+        g.vec = al(g.param) && al(g.grad) && al(g.m) && al(g.v);
+        g.block0 = blocks;
+        const int64_t work = g.vec ? (g.n + 3) / 4 : g.n;
+        blocks += (work + 255) / 256;
+    }
+    if (blocks == 0) return hipSuccess;
+    if (blocks > 0x7FFFFFFF) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_adam_multi, dim3((unsigned)blocks), dim3(256), 0, s, tab, grad_scale);
+    return hipGetLastError();
+}
+
+// Densification statistics of one view (train.py:125-126: max_radii2D[vis] = max(max_radii2D[vis],
+// radii[vis]) and add_densification_stats, scene/gaussian_model.py:480-482: xyz_gradient_accum[vis]
+// += ||viewspace.grad[vis, :2]||, denom[vis] += 1), vis = radii > 0, in one pass.
+__global__ __launch_bounds__(256) void k_densification_stats(int P, const int* __restrict__ radii,
+                                                             const float* __restrict__ dmeans2D,
+                                                             float* __restrict__ max_radii, float* __restrict__ accum,
+                                                             float* __restrict__ denom)
+{
+    const int i = (int)(blockIdx.x * 256 + threadIdx.x);
+    if (i >= P) return;
+    const int r = radii[i];
+    if (!(r > 0)) return;
+    const float gx = dmeans2D[3 * (size_t)i], gy = dmeans2D[3 * (size_t)i + 1];
+    if (max_radii) max_radii[i] = fmaxf(max_radii[i], (float)r);
+    if (accum) accum[i] = accum[i] + sqrtf(__builtin_fmaf(gy, gy, gx * gx));
+    if (denom) denom[i] = denom[i] + 1.0f;
+}
+
+hipError_t launch_densification_stats(int P, const int* radii, const float* dmeans2D, float* max_radii, float* accum,
+                                      float* denom, hipStream_t s)
+{
+    if (P <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_densification_stats, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, P, radii, dmeans2D,
+                       max_radii, accum, denom);
+    return hipGetLastError();
+}
+
 __global__ __launch_bounds__(256) void k_adam(int64_t n, float* __restrict__ param, const float* __restrict__ grad,
                                               float* __restrict__ exp_avg, float* __restrict__ exp_avg_sq,
                                               AdamScalars a, int vec)

@@ -209,7 +209,7 @@ __global__ __launch_bounds__(kPreThreads) __attribute__((amdgpu_waves_per_eu(
         px = at(p.means, o3)[0];
         py = at(p.means, o3)[1];
         pz = at(p.means, o3)[2];
-        q = *reinterpret_cast<const float4*>(at(p.rots, ic * 16u));
+        q = load_f4u(at(p.rots, ic * 16u));
         sx = at(p.scales, o3)[0];
         sy = at(p.scales, o3)[1];
         sz = at(p.scales, o3)[2];
@@ -223,7 +223,7 @@ __global__ __launch_bounds__(kPreThreads) __attribute__((amdgpu_waves_per_eu(
         const char* row = reinterpret_cast<const char*>(p.shs_rest) + ic * 180u;
 #pragma unroll
         for (int k = 0; k < 11; k++) {
-            const float4 v = *reinterpret_cast<const float4*>(row + 16 * k);
+            const float4 v = load_f4u(row + 16 * k);
             rr[4 * k] = v.x;
             rr[4 * k + 1] = v.y;
             rr[4 * k + 2] = v.z;
@@ -246,7 +246,7 @@ __global__ __launch_bounds__(kPreThreads) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
             for (int k = 0; k < 6; k++) cov[k] = p.cov_pre[6 * (size_t)i + k];
         } else {
-            q = *reinterpret_cast<const float4*>(at(p.rots, o4));
+            q = load_f4u(at(p.rots, o4));
             sx = at(p.scales, o3)[0];
             sy = at(p.scales, o3)[1];
             sz = at(p.scales, o3)[2];
@@ -605,7 +605,7 @@ __device__ __forceinline__ void load_bwd_in(const PreprocessBwdParams& p, int i,
 #pragma unroll
         for (int k = 0; k < 6; k++) in.cov[k] = p.cov_pre[6 * (size_t)i + k];
     } else {
-        in.q = *reinterpret_cast<const float4*>(p.rots + 4 * (size_t)i);
+        in.q = load_f4u(p.rots + 4 * (size_t)i);
         in.sc[0] = p.scales[i3];
         in.sc[1] = p.scales[i3 + 1];
         in.sc[2] = p.scales[i3 + 2];

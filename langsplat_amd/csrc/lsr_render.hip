@@ -1010,6 +1010,9 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
     __shared__ uint32_t s_gid[k5 ? kThreads : 1];  // the language step's flush: the batch's Gaussian ids
 
     const uint64_t t_start = kStats ? wall_clock64() : 0;
+    // the forward's cleared records are used by this backward only (include/lsr.h): one store, no
+    // reader in this launch
+    if (p.fwd_flags && blockIdx.x == 0 && threadIdx.x == 0) *p.fwd_flags &= ~kFwdZeroedRecords;
     int tile = (int)blockIdx.x;
     if (p.sched_counts) {  // tiles without contributors are not scheduled: nothing to do
         const int T = p.gx * p.gy;

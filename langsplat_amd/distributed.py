@@ -33,37 +33,54 @@ class GradBucket:
     """The trainable parameters' gradients as ONE all-reduce buffer.
 
     Several parameters (RGB mode: six groups): a flat fp32 buffer whose slices ARE the .grad
-    tensors.  Call after the parameters exist and before the first backward, and keep it by using
-    optimizer.zero_grad(set_to_none=False) (a None .grad would detach the parameter from the
-    bucket); `zero()` clears the whole bucket in one memset.
+    tensors.  Call after the parameters exist and before the first backward; `zero()` clears the
+    whole bucket in one memset (optimizer.zero_grad(set_to_none=False) keeps the aliasing; after a
+    set_to_none the next all_reduce re-attaches: a fresh .grad is copied into its slice, a missing one
+    reads as zeros).
 
     One parameter (LangSplat's language-feature step, scene/gaussian_model.py:203-217): `direct`
     mode, no buffer of its own.  The .grad tensor autograd leaves (with zero_grad(set_to_none=True)
-    it is the rasterizer backward's own output, handed over without a copy) is contiguous and is
-    reduced in place -- no per-step memset of a bucket and no accumulate-add into it.
+    it is the rasterizer backward's own output, handed over without a copy) is reduced in place --
+    no per-step memset of a bucket and no accumulate-add into it.  A rank whose parameter got no
+    gradient this step reduces zeros, so every rank always joins the collective.
+
+    densify_points = P > 0 (RGB mode, train.py:122-126): the bucket also carries the view's
+    densification statistics, 2 P floats after the gradients -- per Gaussian ||dL/dmeans2D[:, :2]||
+    and the visibility count of this rank's view (stage_densification) -- so the SAME collective
+    sums them over the ranks' views, as the reference would accumulate them over that many
+    iterations; the MAX of the radii is one more collective over max_radii2D.
+    apply_densification then adds the sums into xyz_gradient_accum / denom.
     """
 
-    def __init__(self, params: Iterable[torch.nn.Parameter]):
+    def __init__(self, params: Iterable[torch.nn.Parameter], densify_points: int = 0):
         self.params: List[torch.Tensor] = [p for p in params if p.requires_grad]
         if not self.params:
             raise ValueError("GradBucket: no trainable parameters")
         for p in self.params:
             if p.dtype != torch.float32:
                 raise TypeError("GradBucket expects fp32 parameters")
-        self.direct = len(self.params) == 1
+        self.densify_points = int(densify_points)
+        self.direct = len(self.params) == 1 and self.densify_points == 0
         self.flat = None
         self.views = []
+        self.stats_norm = self.stats_count = None
+        self._divided_by = 1     # what the last all_reduce divided the bucket by (N when averaged)
+        self._max_radii = None   # max_radii2D staged for the MAX collective
         if self.direct:
             return
         dev = self.params[0].device
         total = sum(p.numel() for p in self.params)
-        self.flat = torch.zeros((total,), dtype=torch.float32, device=dev)
+        self.flat = torch.zeros((total + 2 * self.densify_points,), dtype=torch.float32, device=dev)
         off = 0
         for p in self.params:
             v = self.flat[off:off + p.numel()].view_as(p)
             p.grad = v
             self.views.append(v)
             off += p.numel()
+        if self.densify_points:
+            P = self.densify_points
+            self.stats_norm = self.flat[off:off + P]
+            self.stats_count = self.flat[off + P:off + 2 * P]
 
     @property
     def nbytes(self) -> int:
@@ -74,6 +91,26 @@ class GradBucket:
             g = self.params[0].grad
             return g is not None and g.is_contiguous()
         return all(p.grad is not None and p.grad.data_ptr() == v.data_ptr() for p, v in zip(self.params, self.views))
+
+    def _attach(self):
+        """Make every .grad reducible without raising (a rank that raised here would leave the others
+        waiting inside the collective)."""
+        if self.direct:
+            p = self.params[0]
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+            elif not p.grad.is_contiguous():
+                p.grad = p.grad.contiguous()
+            return
+        for p, v in zip(self.params, self.views):
+            g = p.grad
+            if g is not None and g.data_ptr() == v.data_ptr():
+                continue
+            if g is None:
+                v.zero_()
+            else:
+                v.copy_(g)
+            p.grad = v
 
     def zero(self):
         if self.direct:
@@ -86,19 +123,50 @@ class GradBucket:
         """The tensor the collective reduces (the flat bucket, or the one parameter's .grad)."""
         return self.params[0].grad if self.direct else self.flat
 
+    def stage_densification(self, radii: torch.Tensor, viewspace_grad: torch.Tensor, max_radii2D: torch.Tensor):
+        """This rank's view into the bucket's statistics slots (which zero() clears) and into
+        max_radii2D (train.py:125-126 for one view).  On a GPU one kernel
+        (include/lsr.h lsr_densification_stats); gloo tests on CPU run the reference's torch ops."""
+        if not self.densify_points:
+            raise RuntimeError("GradBucket: built without densify_points")
+        if radii.is_cuda:
+            from . import _native
+            _native.densification_stats(radii, viewspace_grad, max_radii2D, self.stats_norm, self.stats_count)
+        else:
+            vis = radii > 0
+            max_radii2D[vis] = torch.max(max_radii2D[vis], radii[vis].to(max_radii2D.dtype))
+            self.stats_norm[vis] += torch.norm(viewspace_grad[vis, :2], dim=-1)
+            self.stats_count[vis] += 1
+        self._max_radii = max_radii2D
+
+    def apply_densification(self, xyz_gradient_accum: torch.Tensor, denom: torch.Tensor):
+        """xyz_gradient_accum += the ranks' summed norms; denom += their summed visibility counts
+        (exact: the counts are integers, recovered from an averaged bucket by rounding)."""
+        n = self._divided_by
+        if n == 1:
+            xyz_gradient_accum.view(-1).add_(self.stats_norm)
+            denom.view(-1).add_(self.stats_count)
+        else:
+            xyz_gradient_accum.view(-1).add_(self.stats_norm * n)
+            denom.view(-1).add_(torch.round(self.stats_count * n))
+
     def all_reduce(self, average: bool = True, group=None):
-        """SUM over ranks (then / world_size when average) -- the one collective of a step."""
+        """SUM over ranks (then / world_size when average) -- the one collective of a step (and, with
+        staged densification statistics, the MAX of max_radii2D)."""
         if not (dist.is_available() and dist.is_initialized()):
+            self._divided_by = 1
             return
-        if not self.attached():
-            raise RuntimeError("GradBucket: no gradient to reduce -- the parameter's .grad is missing or not "
-                               "contiguous (direct mode), or no longer aliases the bucket (use "
-                               "zero_grad(set_to_none=False) with several parameters)")
+        self._attach()
         buf = self.buffer()
+        world = dist.get_world_size(group)
         if average and dist.get_backend(group) == "nccl":
             # RCCL's ncclAvg: the division is part of the collective (no separate scaling kernel)
             dist.all_reduce(buf, op=dist.ReduceOp.AVG, group=group)
-            return
-        dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
-        if average:
-            buf.mul_(1.0 / dist.get_world_size(group))
+        else:
+            dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
+            if average:
+                buf.mul_(1.0 / world)
+        self._divided_by = world if average else 1
+        if self._max_radii is not None:
+            dist.all_reduce(self._max_radii, op=dist.ReduceOp.MAX, group=group)
+            self._max_radii = None

@@ -4,9 +4,12 @@ Drop-in for the `torch.optim.Adam(l, lr=0.0, eps=1e-15)` of scene/gaussian_model
 :203-217 in language-feature mode).  Same param_groups ("lr", "betas", "eps", "name" ...), same
 per-parameter state keys ("step", "exp_avg", "exp_avg_sq") -- so update_learning_rate
 (:231-241) and the densification code that rewrites optimizer state (:326-420) work unchanged --
-but each parameter is updated by ONE HIP kernel (liblsr.so lsr_adam_step: one HBM pass over
-param / grad / moments) instead of torch's multi-tensor kernels.  amsgrad, weight decay and
-maximize are not used by LangSplat and are not offered.
+but every parameter of every group is updated by ONE HIP launch (liblsr.so lsr_adam_multi: one
+HBM pass over param / grad / moments per tensor, each tensor with its own group's lr and its own
+step count) instead of torch's multi-tensor kernels.  In RGB mode the six gradients are the
+slices of the one all-reduced bucket (langsplat_amd.distributed.GradBucket), and a SUM all-reduce's
+1 / N is applied inside that same pass (step(grad_scale=...)).  amsgrad, weight decay and maximize
+are not used by LangSplat and are not offered.
 """
 from __future__ import annotations
 
@@ -24,12 +27,15 @@ class Adam(torch.optim.Optimizer):
         super().__init__(params, dict(lr=lr, betas=tuple(betas), eps=eps))
 
     @torch.no_grad()
-    def step(self, closure=None):
+    def step(self, closure=None, grad_scale: float = 1.0):
+        """One Adam step of every parameter with a gradient; grad_scale multiplies the gradients
+        first (1 / N after a SUM all-reduce of N views' gradients; 1.0: as torch.optim.Adam)."""
         loss = None
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
-        lib = _native.load()
+        entries, keep = [], []
+        device = None
         for group in self.param_groups:
             beta1, beta2 = group["betas"]
             for p in group["params"]:
@@ -40,6 +46,9 @@ class Adam(torch.optim.Optimizer):
                                        "ROCm GPU device (there is no CPU path)")
                 if p.grad.is_sparse:
                     raise RuntimeError("langsplat_amd.optim.Adam does not support sparse gradients")
+                if device is not None and p.device != device:
+                    raise RuntimeError("langsplat_amd.optim.Adam: all parameters must be on one device")
+                device = p.device
                 grad = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
                 state = self.state[p]
                 if len(state) == 0:
@@ -47,11 +56,14 @@ class Adam(torch.optim.Optimizer):
                     state["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     state["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                 state["step"] += 1
-                step = int(state["step"].item())
-                with _native._on_device(p.device):
-                    _native._check(lib.lsr_adam_step(
-                        p.numel(), ctypes.c_void_p(p.data_ptr()), ctypes.c_void_p(grad.data_ptr()),
-                        ctypes.c_void_p(state["exp_avg"].data_ptr()), ctypes.c_void_p(state["exp_avg_sq"].data_ptr()),
-                        float(group["lr"]), float(beta1), float(beta2), float(group["eps"]), step,
-                        _native._stream(p.device)), "lsr_adam_step")
+                entries.append(_native.LsrAdamTensor(
+                    p.numel(), p.data_ptr(), grad.data_ptr(), state["exp_avg"].data_ptr(),
+                    state["exp_avg_sq"].data_ptr(), float(group["lr"]), float(beta1), float(beta2),
+                    float(group["eps"]), int(state["step"].item())))
+                keep.append(grad)  # a contiguous copy lives until the launch is enqueued (stream order)
+        if entries:
+            table = (_native.LsrAdamTensor * len(entries))(*entries)
+            with _native._on_device(device):
+                _native._check(_native.load().lsr_adam_multi(len(entries), table, float(grad_scale),
+                                                             _native._stream(device)), "lsr_adam_multi")
         return loss

@@ -53,13 +53,15 @@ def _worker(rank, world, port, out_dir):
         opac.grad.add_(go)
         bucket.all_reduce(average=True)
         np.save(os.path.join(out_dir, f"lang_avg_{rank}.npy"), lang.grad.numpy())
-        # a detached .grad is reported instead of silently reducing a stale buffer
+        # zero_grad(set_to_none=True) detaches the .grad tensors from the bucket: the next all_reduce
+        # re-attaches them (a fresh .grad is copied into its slice, a missing one reduces as zeros), so
+        # no rank raises while the others wait inside the collective
+        bucket.zero()
         lang.grad = None
-        try:
-            bucket.all_reduce()
-            raise AssertionError("expected RuntimeError")
-        except RuntimeError:
-            pass
+        opac.grad = go.clone()  # a fresh tensor, as autograd leaves after set_to_none
+        bucket.all_reduce(average=False)
+        assert bucket.attached() and not lang.grad.any()
+        np.save(os.path.join(out_dir, f"reattach_{rank}.npy"), opac.grad.numpy())
         # one trainable parameter (the language-feature step): direct mode reduces the .grad
         # autograd left (zero_grad(set_to_none=True): a fresh tensor each step) in place
         lang1 = torch.nn.Parameter(torch.zeros((150, 3)))
@@ -68,12 +70,10 @@ def _worker(rank, world, port, out_dir):
         lang1.grad = gl.clone()
         direct.all_reduce(average=False)
         np.save(os.path.join(out_dir, f"direct_{rank}.npy"), lang1.grad.numpy())
-        lang1.grad = None  # set_to_none: nothing to reduce is an error, not a silent no-op
-        try:
-            direct.all_reduce()
-            raise AssertionError("expected RuntimeError")
-        except RuntimeError:
-            pass
+        # a rank whose parameter got no gradient this step joins with zeros (rank 0 here)
+        lang1.grad = None if rank == 0 else gl.clone()
+        direct.all_reduce(average=False)
+        np.save(os.path.join(out_dir, f"direct_none_{rank}.npy"), lang1.grad.numpy())
     finally:
         dist.destroy_process_group()
 
@@ -89,6 +89,9 @@ def test_allreduced_bucket_equals_sum_of_view_gradients(tmp_path, world):
         np.testing.assert_allclose(np.load(tmp_path / f"opac_{r}.npy"), ref_o, rtol=1e-5, atol=1e-8)
         np.testing.assert_allclose(np.load(tmp_path / f"lang_avg_{r}.npy"), ref_l / world, rtol=1e-5, atol=1e-8)
         np.testing.assert_allclose(np.load(tmp_path / f"direct_{r}.npy"), ref_l, rtol=1e-5, atol=1e-8)
+        np.testing.assert_allclose(np.load(tmp_path / f"reattach_{r}.npy"), ref_o, rtol=1e-5, atol=1e-8)
+        ref_none = sum(_view_grads(v, world)[0] for v in range(1, world)).numpy()
+        np.testing.assert_allclose(np.load(tmp_path / f"direct_none_{r}.npy"), ref_none, rtol=1e-5, atol=1e-8)
     # the ranks agree bit for bit (one collective, same result everywhere; float sums in ring order)
     for r in range(1, world):
         assert np.array_equal(np.load(tmp_path / f"lang_{r}.npy"), np.load(tmp_path / "lang_0.npy"))
@@ -99,3 +102,62 @@ def test_bucket_requires_trainable_fp32():
         GradBucket([torch.nn.Parameter(torch.zeros(3), requires_grad=False)])
     with pytest.raises(TypeError):
         GradBucket([torch.nn.Parameter(torch.zeros(3, dtype=torch.float64))])
+
+
+def _view_stats(view, n_views):
+    """One view's radii and dL/dmeans2D (oracle) of the shared densification scene."""
+    from oracle import oracle
+    from tests.scenes import grad_seed, scene
+    st, inp = scene(P=200, W=48, H=40, seed=1, view=view, n_views=n_views, scale_range=(0.05, 0.25))
+    run = oracle.forward(st, **inp)
+    gc, gl = grad_seed(40, 48, seed=20 + view)
+    g = run.backward(gc, gl)
+    return torch.tensor(run.radii), torch.tensor(g["means2D"])
+
+
+def _densify_worker(rank, world, port, out_dir, average):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        P = 200
+        xyz = torch.nn.Parameter(torch.zeros((P, 3)))
+        opac = torch.nn.Parameter(torch.zeros((P, 1)))
+        bucket = GradBucket([xyz, opac], densify_points=P)
+        accum, denom = torch.full((P, 1), 0.25), torch.full((P, 1), 2.0)   # earlier iterations' sums
+        max_radii = torch.full((P,), 3.0)
+        for step in range(2):  # the statistics of two steps accumulate; the bucket is zeroed between
+            bucket.zero()
+            radii, dm2 = _view_stats(rank + world * step, 2 * world)
+            xyz.grad.add_(dm2)
+            bucket.stage_densification(radii, dm2, max_radii)
+            bucket.all_reduce(average=average)
+            bucket.apply_densification(accum, denom)
+        np.save(os.path.join(out_dir, f"accum_{rank}.npy"), accum.numpy())
+        np.save(os.path.join(out_dir, f"denom_{rank}.npy"), denom.numpy())
+        np.save(os.path.join(out_dir, f"maxr_{rank}.npy"), max_radii.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,average", [(2, True), (3, True), (3, False)])
+def test_densification_statistics_sum_over_views(tmp_path, world, average):
+    """RGB-mode densification statistics (train.py:125-126, scene/gaussian_model.py:480-482) over
+    view-sharded ranks equal the reference's accumulation over the same views done one after
+    another: SUM of ||dL/dmeans2D[:, :2]|| and of the visibility counts, MAX of the radii."""
+    P = 200
+    port = _free_port()
+    mp.spawn(_densify_worker, args=(world, port, str(tmp_path), average), nprocs=world, join=True)
+    accum, denom = torch.full((P, 1), 0.25, dtype=torch.float64), torch.full((P, 1), 2.0, dtype=torch.float64)
+    max_radii = torch.full((P,), 3.0, dtype=torch.float64)
+    for v in range(2 * world):  # the reference: one view per iteration
+        radii, dm2 = _view_stats(v, 2 * world)
+        vis = radii > 0
+        max_radii[vis] = torch.max(max_radii[vis], radii[vis].double())
+        accum[vis] += torch.norm(dm2[vis, :2].double(), dim=-1, keepdim=True)
+        denom[vis] += 1
+    for r in range(world):
+        np.testing.assert_allclose(np.load(tmp_path / f"accum_{r}.npy"), accum.numpy(), rtol=1e-5, atol=1e-9)
+        np.testing.assert_array_equal(np.load(tmp_path / f"denom_{r}.npy"), denom.numpy().astype(np.float32))
+        np.testing.assert_array_equal(np.load(tmp_path / f"maxr_{r}.npy"), max_radii.numpy().astype(np.float32))
+    assert denom.max() > 2.0 + world  # the views overlap: some Gaussians counted by several ranks

@@ -108,3 +108,58 @@ def test_adam_through_densification_surgery():
         sm, sr = mine.state[a], ref.state[b]
         for x, y in ((a.detach(), b.detach()), (sm["exp_avg"], sr["exp_avg"]), (sm["exp_avg_sq"], sr["exp_avg_sq"])):
             torch.testing.assert_close(x, y, rtol=2e-6, atol=1e-6 * float(y.abs().max()))
+
+
+def test_adam_one_launch_over_bucket_slices_with_grad_scale():
+    """RGB mode's step: the six gradients are slices of one GradBucket (offsets not 16-B aligned:
+    the element-wise path beside the float4 one) and a SUM all-reduce's 1 / N is applied inside the
+    Adam pass (step(grad_scale=...)); equal to torch.optim.Adam on the scaled gradients."""
+    from langsplat_amd.distributed import GradBucket
+    g = torch.Generator().manual_seed(6)
+    P = 1001
+    shapes = {"xyz": (3,), "f_dc": (1, 3), "f_rest": (15, 3), "opacity": (1,), "scaling": (3,), "rotation": (4,)}
+    lrs = {"xyz": 1.6e-4, "f_dc": 2.5e-3, "f_rest": 1.25e-4, "opacity": 0.05, "scaling": 5e-3, "rotation": 1e-3}
+    init = {k: torch.randn((P,) + s, generator=g) for k, s in shapes.items()}
+    mp = {k: torch.nn.Parameter(v.clone().to(DEV)) for k, v in init.items()}
+    rp = {k: torch.nn.Parameter(v.clone().to(DEV)) for k, v in init.items()}
+    bucket = GradBucket(list(mp.values()))
+    mine = Adam([{"params": [mp[k]], "lr": lrs[k], "name": k} for k in shapes], lr=0.0, eps=1e-15)
+    ref = torch.optim.Adam([{"params": [rp[k]], "lr": lrs[k], "name": k} for k in shapes], lr=0.0, eps=1e-15,
+                           foreach=False)
+    scale = 1.0 / 3.0
+    for it in range(4):
+        bucket.zero()
+        for k in shapes:
+            grad = torch.randn((P,) + shapes[k], generator=g).to(DEV)
+            mp[k].grad.add_(grad)  # autograd accumulates into the bucket slice
+            rp[k].grad = grad * scale
+        assert bucket.attached()
+        mine.step(grad_scale=scale)
+        ref.step()
+    for k in shapes:
+        sm, sr = mine.state[mp[k]], ref.state[rp[k]]
+        for x, y in ((mp[k].detach(), rp[k].detach()), (sm["exp_avg"], sr["exp_avg"]),
+                     (sm["exp_avg_sq"], sr["exp_avg_sq"])):
+            torch.testing.assert_close(x, y, rtol=2e-6, atol=1e-6 * float(y.abs().max()))
+
+
+def test_densification_stats_kernel_matches_reference_ops():
+    """lsr_densification_stats == train.py:125-126 + scene/gaussian_model.py:480-482 as torch ops."""
+    from langsplat_amd import _native
+    g = torch.Generator().manual_seed(7)
+    P = 5003
+    radii = torch.randint(-1, 40, (P,), generator=g, dtype=torch.int32).clamp_min(0).to(DEV)
+    dm2 = torch.randn((P, 3), generator=g).to(DEV)
+    max_r = (torch.rand((P,), generator=g) * 30).to(DEV)
+    accum = torch.rand((P, 1), generator=g).to(DEV)
+    denom = torch.randint(0, 5, (P, 1), generator=g).float().to(DEV)
+    ref = [max_r.clone(), accum.clone(), denom.clone()]
+    vis = radii > 0
+    ref[0][vis] = torch.max(ref[0][vis], radii[vis])
+    ref[1][vis] += torch.norm(dm2[vis, :2], dim=-1, keepdim=True)
+    ref[2][vis] += 1
+    _native.densification_stats(radii, dm2, max_r, accum, denom)
+    torch.testing.assert_close(max_r, ref[0], rtol=0, atol=0)
+    torch.testing.assert_close(accum, ref[1], rtol=1e-6, atol=0)
+    torch.testing.assert_close(denom, ref[2], rtol=0, atol=0)
+    assert vis.any() and (~vis).any()

@@ -407,3 +407,45 @@ def test_binning_buffer_grows_between_views():
         run, std, ind, out = check_forward_exact(st, inp)
         runs.append(run.num_rendered)
     assert runs[1] > 1.2 * runs[0]  # beyond the 12.5 % headroom of the first view's size
+
+
+def test_forward_requests_the_sizes_the_abi_reports():
+    """lsr_geom_bytes / lsr_image_bytes are exactly what lsr_forward requests, and the binning
+    request stays within lsr_binning_bytes (include/lsr.h), so a C caller can size its buffers."""
+    lib = _native.load()
+    for (P, W, H) in ((3000, 160, 120), (2000, 1920, 1080)):
+        st, inp = scene(P=P, W=W, H=H, seed=3, scale_range=(0.03, 0.2))
+        std, ind, out = native_forward(st, inp)
+        nr, color, lang, radii, geom, binning, image = out
+        assert geom.numel() == lib.lsr_geom_bytes(P, W, H)
+        assert image.numel() == lib.lsr_image_bytes(W, H)
+        assert 0 < binning.numel() <= lib.lsr_binning_bytes(W, H, nr) * 1.125 + 256
+
+
+def test_debug_backward_rejects_flags_its_forward_did_not_prepare():
+    """With settings.debug the backward checks what the forward recorded (include/lsr.h): records
+    claimed cleared by a forward that did not clear them, records reused by a second backward, and
+    a loss gradient for a forward without the fused loss all fail instead of reading stale data."""
+    st, inp = scene(P=500, W=64, H=48, seed=2, scale_range=(0.03, 0.2))
+    st = st._replace(debug=True)
+    std, ind = to_device(st, inp, DEV)
+    args = (ind["means3D"], ind["shs"], None, ind["language_feature_precomp"], ind["opacities"], ind["scales"],
+            ind["rotations"], None)
+
+    def bwd(out, flags=0, grad_loss=None):
+        nr, color, lang, radii, geom, binning, image = out
+        return _native.rasterize_gaussians_backward(
+            std, ind["means3D"], ind["shs"], None, ind["language_feature_precomp"], ind["scales"],
+            ind["rotations"], None, radii, None, torch.ones_like(lang), nr, geom, binning, image, geometry=False,
+            flags=flags, grad_loss=grad_loss)
+    plain = _native.rasterize_gaussians(std, *args)
+    with pytest.raises(RuntimeError, match="did not clear"):
+        bwd(plain, flags=_native.BWD_RECORDS_ZEROED)
+    with pytest.raises(RuntimeError, match="did not fuse"):
+        bwd(plain, grad_loss=torch.ones((), device=DEV))
+    zeroed = _native.rasterize_gaussians(std, *args, flags=_native.FWD_ZERO_GRAD_RECORDS)
+    g1 = bwd(zeroed, flags=_native.BWD_RECORDS_ZEROED)["language_feature_precomp"].clone()
+    with pytest.raises(RuntimeError, match="did not clear"):
+        bwd(zeroed, flags=_native.BWD_RECORDS_ZEROED)
+    g2 = bwd(zeroed)["language_feature_precomp"]
+    assert_grad_close("second backward", g2.cpu().numpy(), g1.cpu().numpy())

@@ -31,18 +31,20 @@ def test_library_loads_and_exports_every_declared_symbol():
     for name in _declared_functions():
         assert hasattr(lib, name), name
         assert name in _native.SIGNATURES, f"ctypes binding misses {name}"
-    assert lib.lsr_abi_version() == _native.ABI_VERSION == 6
+    assert lib.lsr_abi_version() == _native.ABI_VERSION == 7
 
 
 def test_sizes_and_layout_are_consistent():
     lib = _native.load()
     P, W, H, R = 1000, 100, 70, 12345
     lay = _native.state_layout(P, W, H, R)
-    assert lay["record"] % 16 == 0 and lay["record"] + 48 * P <= lib.lsr_geom_bytes(P)
+    assert lay["record"] % 16 == 0 and lay["record"] + 48 * P <= lib.lsr_geom_bytes(P, W, H)
     assert lay["n_contrib"] + 4 * W * H <= lib.lsr_image_bytes(W, H)
     assert lay["point_list"] + 4 * R <= lib.lsr_binning_bytes(W, H, R)
     assert lib.lsr_backward_bytes(P) == 64 * P
-    assert lib.lsr_geom_bytes(2 * P) > lib.lsr_geom_bytes(P)
+    assert lib.lsr_geom_bytes(2 * P, W, H) > lib.lsr_geom_bytes(P, W, H)
+    # the geometry buffer carries one fused-loss word per tile: it grows with the image
+    assert lib.lsr_geom_bytes(P, 1920, 1080) > lib.lsr_geom_bytes(P, W, H)
 
 
 def test_invalid_arguments_report_errors_without_gpu():
