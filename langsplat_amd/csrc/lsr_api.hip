@@ -491,6 +491,8 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
         rp.loss_code = reinterpret_cast<uint8_t*>(image + L.loss_code);
         rp.loss_words = reinterpret_cast<uint64_t*>(geom + L.loss_words);
         rp.out_loss = a->out_loss;
+        rp.spin_limit = stall_spin_limit();
+        rp.stall = &hb->stall;
     }
     LSR_TRY(launch_render_forward(rp, L.tiles, stream), "render forward");
     hm.mark();

@@ -227,6 +227,8 @@ struct RenderParams {
     double* loss_partial;     // P == 0 (k_loss_background): one double per workgroup
     uint64_t* loss_words;     // render forward: words and tickets of loss_block_publish (zeroed)
     float* out_loss;
+    uint32_t spin_limit;      // loss_block_publish's poll bound (stall_spin_limit())
+    uint32_t* stall;          // its stall flag (the calling thread's pinned host word)
     const float* dL_dloss;
 };
 

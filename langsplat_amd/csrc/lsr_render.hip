@@ -258,13 +258,16 @@ __device__ __forceinline__ void fwd_pixel_blend(FwdPixel& q, float al, uint32_t 
 // grad * (1 / (3 HW)) * sign(d_c) * m without reading the images again.
 __device__ __forceinline__ uint32_t sign_code(float d) { return d > 0.0f ? 1u : (d < 0.0f ? 2u : 0u); }
 
+template <bool kCode = true>
 __device__ __forceinline__ float loss_pixel(const RenderParams& p, size_t pix, size_t HW, float f0, float f1, float f2)
 {
     const float m = p.loss_mask[pix] ? 1.0f : 0.0f;
     const float d0 = f0 * m - p.loss_gt[pix] * m;
     const float d1 = f1 * m - p.loss_gt[HW + pix] * m;
     const float d2 = f2 * m - p.loss_gt[2 * HW + pix] * m;
-    p.loss_code[pix] = (uint8_t)(sign_code(d0) | (sign_code(d1) << 2) | (sign_code(d2) << 4) | (m != 0.0f ? 64u : 0u));
+    if (kCode)
+        p.loss_code[pix] =
+            (uint8_t)(sign_code(d0) | (sign_code(d1) << 2) | (sign_code(d2) << 4) | (m != 0.0f ? 64u : 0u));
     return fabsf(d0) + fabsf(d1) + fabsf(d2);
 }
 
@@ -291,25 +294,90 @@ __device__ __forceinline__ void loss_block_partial(const RenderParams& p, float 
     if (threadIdx.x == 0) p.loss_partial[blockIdx.x] = t;
 }
 
+// The language feature of one pixel composited by a scalar front-to-back walk over the whole tile
+// list, reading the records from global memory: the oracle's render_pixel with the main walk's
+// cutoff test (power < cut rejects exactly what alpha < 1/255 would), so the same operations and the
+// same values as the kernel's packed two-entry walk.
+__device__ void composite_lang_pixel(const RenderParams& p, uint2 range, float pfx, float pfy, float& f0, float& f1,
+                                     float& f2)
+{
+    float T = 1.0f;
+    f0 = f1 = f2 = 0.0f;
+    for (uint32_t k = range.x; k < range.y; k++) {
+        const uint32_t g = p.point_list[k];
+        const float4 a = p.record[3 * (size_t)g], b = p.record[3 * (size_t)g + 1], c = p.record[3 * (size_t)g + 2];
+        const float dx = a.x - pfx, dy = a.y - pfy;
+        const float hx = -0.5f * a.z, hz = -0.5f * b.x;
+        const float pw = fma_(dx, fma_(-a.w, dy, hx * dx), (hz * dy) * dy);
+        if (pw > 0.0f || pw < power_cutoff(b.y)) continue;
+        const float al = fminf(0.99f, b.y * expf_exact_render(pw));
+        if (al < 1.0f / 255.0f) continue;
+        const float test_T = T * (1.0f - al);
+        if (test_T < 0.0001f) break;
+        const float w = al * T;
+        f0 = fma_(c.y, w, f0);
+        f1 = fma_(c.z, w, f1);
+        f2 = fma_(c.w, w, f2);
+        T = test_T;
+    }
+}
+
+// This thread's part of the loss share forward workgroup b publishes (b uniform): the same pixels
+// and per-pixel operations as b's own (its tile, or its strided run of empty tiles), computed from
+// the inputs, not from b's outputs.
+__device__ float loss_share_part(const RenderParams& p, int b)
+{
+    const int T = p.gx * p.gy;
+    const size_t HW = (size_t)p.W * p.H;
+    int tile = b;
+    if (p.sched_counts) tile = scheduled_tile(b, p.sched_counts + kCntFwdClass, p.sched_lists, T);
+    float part = 0.0f;
+    if (tile < 0) {  // render_empty_tiles(p, b - listed, T - listed)
+        const int listed = -1 - tile, j = b - listed, M = T - listed;
+        for (int u = j; u < T; u += M) {
+            const uint2 r = p.ranges[u];
+            if (r.x != r.y) continue;
+            int px, py;
+            pixel_map(u % p.gx, u / p.gx, (int)threadIdx.x, px, py);
+            if (px < p.W && py < p.H) part += loss_pixel<false>(p, (size_t)py * p.W + px, HW, 0.0f, 0.0f, 0.0f);
+        }
+        return part;
+    }
+    int px, py;
+    pixel_map(tile % p.gx, tile / p.gx, (int)threadIdx.x, px, py);
+    if (!(px < p.W && py < p.H)) return 0.0f;
+    float f0, f1, f2;
+    composite_lang_pixel(p, p.ranges[tile], (float)px, (float)py, f0, f1, f2);
+    return loss_pixel<false>(p, (size_t)py * p.W + px, HW, f0, f1, f2);
+}
+
+__device__ __forceinline__ void loss_word_store(const RenderParams& p, int b, double t)
+{
+    __hip_atomic_store(&p.loss_words[b], (1ull << 32) | __float_as_uint((float)t), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Render forward: each workgroup publishes its share as ONE 64-bit word {1, float} (agent-scope
 // store, coherent across the XCDs' L2s; no atomic, so no workgroup waits for a round trip before it
 // retires).  The LAST workgroup of the grid -- dispatched after every other one, so all of them are
 // resident or done and none depends on it -- waits for every word and adds them in workgroup order
 // (deterministic) into Ll1: no second launch.  The words start at 0 (cleared by preprocess).
+// Bounded wait: a word still absent after p.spin_limit polls is computed by this workgroup from the
+// inputs (loss_share_part: the same value workgroup b publishes, stored the same way) and the stall
+// is flagged (lsr_debug_scan_stalls); spin_limit 0 takes that path for every word not yet there.
 __device__ __forceinline__ void loss_block_publish(const RenderParams& p, float part)
 {
     __shared__ double s_fw[kTilePixels / 64];
     const double t = loss_block_sum(part);
     const int nb = (int)gridDim.x;
-    if (threadIdx.x == 0)
-        __hip_atomic_store(&p.loss_words[blockIdx.x], (1ull << 32) | __float_as_uint((float)t), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) loss_word_store(p, (int)blockIdx.x, t);
     if ((int)blockIdx.x != nb - 1) return;
     // thread i adds the run [i per, (i + 1) per) in order (threads in order = workgroups in order)
     const int per = (nb + kTilePixels - 1) / kTilePixels;
     const int i0 = (int)threadIdx.x * per, e = min(nb, i0 + per);
     double v = 0.0;
     constexpr int kBatch = 16;  // loads in flight per round trip
+    bool miss = false;
     for (int i = i0; i < e; i += kBatch) {
         uint64_t w[kBatch];
 #pragma unroll
@@ -318,12 +386,38 @@ __device__ __forceinline__ void loss_block_publish(const RenderParams& p, float 
                              : (1ull << 32);
 #pragma unroll
         for (int k = 0; k < kBatch; k++) {
-            while ((w[k] >> 32) == 0ull) {
+            for (uint32_t spins = 0; (w[k] >> 32) == 0ull && spins < p.spin_limit; spins++) {
                 __builtin_amdgcn_s_sleep(2);
                 w[k] = __hip_atomic_load(&p.loss_words[i + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
+            miss = miss || (w[k] >> 32) == 0ull;
             v += (double)__uint_as_float((uint32_t)w[k]);  // padding words add +0
         }
+    }
+    if (__syncthreads_or(miss)) {
+        // a word did not come within the bound: compute the missing words one at a time (the smallest
+        // missing index over the workgroup, then the next), then sum every word again in order
+        __shared__ int s_b;
+        for (;;) {
+            int mine = 0x7FFFFFFF;
+            for (int i = i0; i < e && mine == 0x7FFFFFFF; i++)
+                if ((__hip_atomic_load(&p.loss_words[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 32) == 0ull)
+                    mine = i;
+            if (threadIdx.x == 0) s_b = 0x7FFFFFFF;
+            __syncthreads();
+            if (mine != 0x7FFFFFFF) atomicMin(&s_b, mine);
+            __syncthreads();
+            const int bm = s_b;  // uniform
+            if (bm == 0x7FFFFFFF) break;
+            const double tb = loss_block_sum(loss_share_part(p, bm));
+            if (threadIdx.x == 0) loss_word_store(p, bm, tb);
+            __syncthreads();  // the store before the next scan (one workgroup: program order)
+        }
+        v = 0.0;
+        for (int i = i0; i < e; i++)
+            v += (double)__uint_as_float(
+                (uint32_t)__hip_atomic_load(&p.loss_words[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        if (threadIdx.x == 0) note_stall(p.stall);
     }
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {  // in-order prefix within the wave: lane 63 holds lanes 0..63 in order
@@ -368,8 +462,11 @@ __device__ float render_empty_tiles(const RenderParams& p, int j, int M)
     return part;
 }
 
+// 7 waves per SIMD (<= 72 VGPRs): the fused-loss variant's rare bounded-wait fallback
+// (loss_block_publish) would otherwise raise its register count to 83 (6 waves); with the bound the
+// compiler spills three values, stored once per workgroup and reloaded on that path only.
 template <bool kStats, bool kFeat, bool kLoss>
-__global__ __launch_bounds__(kTilePixels) void k_render_forward(RenderParams p)
+__global__ __launch_bounds__(kTilePixels, 7) void k_render_forward(RenderParams p)
 {
     const uint64_t t_start = kStats ? wall_clock64() : 0;
     constexpr int kThreads = kTilePixels;

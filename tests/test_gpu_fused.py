@@ -279,3 +279,31 @@ def test_second_backward_clears_its_own_records(fused_loss, monkeypatch):
     g2 = m._language_feature.grad.detach().clone()
     assert g1.abs().sum() > 0
     assert_grad_close("second backward", g2.cpu().numpy(), g1.cpu().numpy())
+
+
+def test_fused_loss_wait_fallback_is_exact(monkeypatch):
+    """The fused loss's last workgroup waits for every workgroup's word at most spin_limit polls
+    (ADVICE r02); spin limit 0 sends every word not yet published through the fallback, which
+    computes it from the inputs (the same pixels and operations as its workgroup: the oracle's
+    compositing loop): the loss, the image and the gradients are bit-identical, and the stall is
+    reported (lsr_debug_scan_stalls)."""
+    lib = _native.load()
+    W, H = 96, 64
+    g = make_gaussians(1500, seed=10, scale_range=(0.03, 0.2))
+    cam = make_cameras(1, W, H, device=DEV)[0]
+    gen = torch.Generator().manual_seed(W)
+    gt = torch.nn.functional.normalize(torch.randn((3, H, W), generator=gen), dim=0).to(DEV)
+    mask = (torch.rand((1, H, W), generator=gen) < 0.8).to(DEV)
+    l0, img0, g0 = _language_step(g, cam, gt, mask, True, monkeypatch)
+    torch.cuda.synchronize()
+    lib.lsr_debug_scan_stalls()  # clear
+    old = lib.lsr_debug_set_spin_limit(0)
+    try:
+        l1, img1, g1 = _language_step(g, cam, gt, mask, True, monkeypatch)
+        torch.cuda.synchronize()
+        assert lib.lsr_debug_scan_stalls() == 1
+    finally:
+        lib.lsr_debug_set_spin_limit(old)
+    assert torch.equal(l0, l1) and torch.equal(img0, img1)
+    for k in g0:
+        assert_grad_close(k, g1[k], g0[k])
