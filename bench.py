@@ -38,6 +38,7 @@ sys.path.insert(0, ROOT)
 
 from langsplat_amd import _native  # noqa: E402
 from langsplat_amd.distributed import GradBucket, init_from_env  # noqa: E402
+from langsplat_amd.graph import GraphedStep  # noqa: E402
 from langsplat_amd.optim import Adam as AmdAdam  # noqa: E402
 from langsplat_amd.render import render  # noqa: E402
 from langsplat_amd.synthetic import CONFIGS, activated_inputs, make_cameras, make_gaussians  # noqa: E402
@@ -233,9 +234,6 @@ def survey_step_bytes(P, R, HW, M, geometry):
     return P * b_g + R * 148 + HW * 64
 
 
-# the timed loop records the dominant kernel's events on every LIVE_EVENT_EVERY-th step
-LIVE_EVENT_EVERY = 5
-
 # the stage that dominates the step (measured: profiles/r02_summary.json); timed live in the bench
 DOMINANT_STAGE = "render backward"
 
@@ -399,40 +397,21 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-
-    # timed region: HIP events around the dominant kernel only (its live average feeds the
-    # roofline), so event bookkeeping does not sit on the host's critical path of every stage; and
-    # only on every 5th step (each event pair stalls the stream for ~2 x 4 us: DESIGN.md section 5)
-    live = os.environ.get("LSR_BENCH_LIVE_EVENTS", "1") != "0"  # 0: measurement of the events' own cost
-    _native.profile_enable(live, stages=[DOMINANT_STAGE], every=LIVE_EVENT_EVERY)
     # the collector stays off inside the timed loops (as timeit does): a collection of the steps'
     # autograd garbage would land on the host's critical path of one step
     gc.collect()
     gc.disable()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
+
+    # eager passes first (the captured graph then owns the parameters' .grad tensors):
+    # (1) the dominant kernel's average launch time, HIP events around it on its stream (every step)
+    _native.profile_enable(True, stages=[DOMINANT_STAGE], every=1)
+    for _ in range(min(args.steps, 20)):
         step()
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
     _native.profile_enable(False)
     dom = _native.profile_report().get(DOMINANT_STAGE, {"avg_ms": float("nan")})
-    # the same steps with train.py:108's loss.item() after each (a device-to-host sync per step: the
-    # host cannot run ahead into the next step), reported beside `value` as ms_per_step_with_sync
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    ts = time.perf_counter()
-    for _ in range(args.steps):
-        step().item()
-    torch.cuda.synchronize()
-    elapsed_sync = time.perf_counter() - ts
-    # the same step with every geometry gradient computed although no parameter needs one (what the
-    # reference extension does; LSR_ALL_GRADS=1): reported beside, never as `value`
+    # (2) the same step with every geometry gradient computed although no parameter needs one (what
+    # the reference extension does; LSR_ALL_GRADS=1): reported beside, never as `value`
     _native.FORCE_GEOMETRY_GRADS = True
     for _ in range(2):
         step()
@@ -444,8 +423,72 @@ def main():
         step()
     torch.cuda.synchronize()
     elapsed_all = time.perf_counter() - t1
-    gc.enable()
     _native.FORCE_GEOMETRY_GRADS = os.environ.get("LSR_ALL_GRADS", "0") == "1"
+    # (3) the eager step itself (the host enqueues every launch, one wait per forward)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    te = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    elapsed_eager = time.perf_counter() - te
+    # (4) stage breakdown: every stage profiled
+    prof_steps = min(args.steps, 10)
+    _native.profile_enable(True)
+    for _ in range(prof_steps):
+        step()
+    torch.cuda.synchronize()
+    _native.profile_enable(False)
+    prof = _native.profile_report()
+
+    # the timed step: render + loss + backward captured once into a HIP graph (langsplat_amd.graph;
+    # the rasterizer in capacity mode, no host wait), replayed, then [N > 1: the all-reduce] and Adam
+    run = step
+    graphed = fused and os.environ.get("LSR_GRAPH", "1") != "0"
+    if graphed:
+        def fwd_bwd():
+            loss = render(cam, model, Pipe, bg, Opt, language_target=(gt, mask))["language_l1"]
+            loss.backward()
+            return loss
+        gstep = GraphedStep(fwd_bwd, model.trainable())
+        gstep.capture()
+
+        def run():
+            loss = gstep.replay()
+            if bucket is not None:
+                bucket.all_reduce(average=True)
+            optim.step()
+            return loss
+        for _ in range(3):
+            run()
+        torch.cuda.synchronize()
+        if not gstep.check():
+            run()
+            torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if graphed and not gstep.check():
+        raise RuntimeError("a captured view exceeded its capacities during the timed steps")
+    # the same steps with train.py:108's loss.item() after each (a device-to-host sync per step: the
+    # host cannot run ahead into the next step), reported beside `value` as ms_per_step_with_sync
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ts = time.perf_counter()
+    for _ in range(args.steps):
+        run().item()
+    torch.cuda.synchronize()
+    elapsed_sync = time.perf_counter() - ts
+    gc.enable()
     # the RGB stage's step on the same scene and view (all six groups trainable, L1 + SSIM, densification
     # statistics): reported beside, never as `value`
     rgb_ms = None
@@ -464,14 +507,6 @@ def main():
         torch.cuda.synchronize()
         rgb_ms = 1000.0 * (time.perf_counter() - t2) / rgb_steps
         del rgb
-    # stage breakdown: a separate, untimed pass with every stage profiled
-    prof_steps = min(args.steps, 10)
-    _native.profile_enable(True)
-    for _ in range(prof_steps):
-        step()
-    torch.cuda.synchronize()
-    _native.profile_enable(False)
-    prof = _native.profile_report()
 
     t = torch.tensor([elapsed, float(blends)], dtype=torch.float64, device=dev)
     if world > 1:
@@ -552,6 +587,8 @@ def main():
                                 "as needed: means2D + language feature (geometry frozen, "
                                 "scene/gaussian_model.py:203-217)"},
         "ms_per_step_with_sync": round(1000.0 * elapsed_sync / args.steps, 4),
+        "ms_per_step_eager": round(1000.0 * elapsed_eager / args.steps, 4),
+        "step_form": "HIP graph replay (render + loss + backward) + Adam" if graphed else "eager",
         "ms_per_step_all_gradients": round(1000.0 * elapsed_all / args.steps, 4),
         "ms_per_step_rgb": None if rgb_ms is None else round(rgb_ms, 4),
         "raster_ms_per_step": round(raster_ms, 4),

@@ -22,7 +22,9 @@
  *   - Matrices are the reference's row-vector matrices stored row-major, exactly the memory of
  *     Camera.world_view_transform / full_proj_transform (scene/cameras.py:54-56).
  *   - Work is enqueued on `stream` (a hipStream_t; NULL = legacy default stream).  lsr_forward
- *     performs ONE stream synchronisation to learn num_rendered (as upstream does).
+ *     waits once for the device to learn num_rendered (as upstream does) -- except in capacity mode
+ *     (lsr_forward_args.capacity_rendered > 0), which sizes everything from caller capacities and
+ *     never waits, so that a whole train step can be captured into a HIP graph.
  *   - Scratch is owned by the caller and requested through `alloc` (upstream's resizable
  *     geometry/binning/image buffers).  The three forward buffers must be kept alive, unchanged,
  *     and passed back to lsr_backward.
@@ -40,7 +42,7 @@
 extern "C" {
 #endif
 
-#define LSR_ABI_VERSION 7
+#define LSR_ABI_VERSION 8
 
 enum lsr_status {
     LSR_OK = 0,
@@ -135,6 +137,19 @@ typedef struct lsr_forward_args {
     const float* loss_target;        /* 3 x H x W, or NULL */
     const uint8_t* loss_mask;        /* H x W bool bytes (scene/cameras.py:72 seg != -1), or NULL */
     float* out_loss;                 /* one float (device), or NULL */
+    /* Capacity mode (graph capture): capacity_rendered > 0 bounds the tile instances and
+     * capacity_entries (> 0) the super-tile entries of this view; the buffers and launch grids are
+     * sized from them, the device reads the true counts, and the call enqueues its work without
+     * waiting for the device.  *num_rendered then returns capacity_rendered (the value lsr_backward
+     * needs).  A view that exceeds either capacity is not rasterized (background image, zero
+     * gradients) and sets *overflow (device int32, written by every capacity-mode forward: 1 or 0);
+     * the caller re-runs it with larger capacities.  capacity_rendered == 0: the host reads the
+     * counts after the preprocess (one wait) and sizes exactly. */
+    int64_t capacity_rendered;
+    int64_t capacity_entries;
+    int32_t* overflow;               /* device int32 or NULL */
+    int64_t* out_num_entries;        /* HOST pointer or NULL: the super-tile entry count (not in
+                                        capacity mode), the capacity_entries a later call needs */
 } lsr_forward_args;
 
 /* Inputs/outputs of _C.rasterize_gaussians_backward.  Every non-NULL output is fully written

@@ -22,7 +22,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LSR_LIB") or os.path.join(_HERE, "liblsr.so")
 
 LSR_BUF_GEOM, LSR_BUF_BINNING, LSR_BUF_IMAGE, LSR_BUF_BACKWARD = 0, 1, 2, 3
-ABI_VERSION = 7
+ABI_VERSION = 8
 # lsr_raw_flags (include/lsr.h): inputs are GaussianModel's raw parameters
 RAW_OPACITY, RAW_SCALES, RAW_ROTATIONS, RAW_LANGUAGE = 1, 2, 4, 8
 FWD_ZERO_GRAD_RECORDS = 1  # lsr_forward_flags
@@ -54,7 +54,8 @@ class LsrForwardArgs(ctypes.Structure):
         (n, _vp) for n in ("means3D", "shs", "colors_precomp", "language_feature", "opacities", "scales",
                            "rotations", "cov3D_precomp", "out_color", "out_language_feature", "radii")
     ] + [("raw", ctypes.c_int32), ("flags", ctypes.c_int32), ("shs_rest", _vp), ("visible", _vp),
-         ("loss_target", _vp), ("loss_mask", _vp), ("out_loss", _vp)]
+         ("loss_target", _vp), ("loss_mask", _vp), ("out_loss", _vp), ("capacity_rendered", ctypes.c_int64),
+         ("capacity_entries", ctypes.c_int64), ("overflow", _vp), ("out_num_entries", ctypes.POINTER(ctypes.c_int64))]
 
 
 class LsrBackwardArgs(ctypes.Structure):
@@ -229,6 +230,40 @@ class _on_device:
             self.ctx.__exit__(*exc)
 
 
+class capacity:
+    """Within the block, the rasterizer forwards of this thread run in capacity mode (include/lsr.h
+    lsr_forward_args.capacity_*): buffers and launch grids sized from `rendered` tile instances and
+    `entries` super-tile entries, no wait for the device -- what a HIP graph capture of the step needs
+    (langsplat_amd.graph).  `overflow`: a () int32 device tensor each forward sets to 1 when its view
+    exceeds a capacity (it is then not rasterized) or 0."""
+
+    _tls = threading.local()
+
+    def __init__(self, rendered: int, entries: int, overflow: torch.Tensor):
+        if rendered <= 0 or entries <= 0:
+            raise ValueError("capacity: both capacities must be positive")
+        if overflow.dtype != torch.int32 or overflow.numel() != 1:
+            raise ValueError("capacity: overflow must be a one-element int32 tensor")
+        self.rendered, self.entries, self.overflow = int(rendered), int(entries), overflow
+
+    @staticmethod
+    def active():
+        return getattr(capacity._tls, "cur", None)
+
+    def __enter__(self):
+        self._prev = capacity.active()
+        capacity._tls.cur = self
+        return self
+
+    def __exit__(self, *exc):
+        capacity._tls.cur = self._prev
+
+
+# (P, W, H) -> (tile instances, super-tile entries) of this thread's last forward outside capacity mode
+# (the capacities a later capture needs)
+LAST_COUNTS: Dict[tuple, tuple] = {}
+
+
 _SETTINGS_CACHE: Dict[int, tuple] = {}
 
 
@@ -341,11 +376,21 @@ def rasterize_gaussians(rs, means3D, shs, colors_precomp, language_feature, opac
         a.loss_target = _ptr(loss_target)
         a.loss_mask = _ptr(loss_mask)
         a.out_loss = _ptr(out_loss)
+    cap = capacity.active()
+    entries = ctypes.c_int64(0)
+    if cap is not None:
+        a.capacity_rendered = cap.rendered
+        a.capacity_entries = cap.entries
+        a.overflow = _ptr(cap.overflow)
+    else:
+        a.out_num_entries = ctypes.pointer(entries)
     alloc = _Allocator(device)
     nr = ctypes.c_int64(0)
     with _on_device(device), alloc:
         _check(lib.lsr_forward(ctypes.byref(s), ctypes.byref(a), _ALLOC_CB, None, _stream(device), ctypes.byref(nr)),
                "lsr_forward")
+    if cap is None:
+        LAST_COUNTS[(P, W, H)] = (int(nr.value), int(entries.value))
     return (int(nr.value), color, lang, radii, alloc.get(LSR_BUF_GEOM), alloc.get(LSR_BUF_BINNING),
             alloc.get(LSR_BUF_IMAGE))
 

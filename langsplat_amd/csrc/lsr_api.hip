@@ -9,6 +9,7 @@
 #include <string.h>
 #include <time.h>
 
+#include <algorithm>
 #include <map>
 #include <mutex>
 #include <string>
@@ -255,6 +256,46 @@ static AdamScalars adam_scalars(double lr, double beta1, double beta2, double ep
     return a;
 }
 
+// The render forward of lsr_forward (both modes), after the binning.
+static int32_t render_forward_and_finish(const lsr_settings* s, const lsr_forward_args* a, const Layout& L, char* geom,
+                                         char* image, char* binning, HostBlock* hb, hipStream_t stream, bool debug)
+{
+    const int P = a->P, W = s->image_width, H = s->image_height;
+    (void)P;
+    RenderParams rp{};
+    rp.W = W;
+    rp.H = H;
+    rp.gx = L.gx;
+    rp.gy = L.gy;
+    rp.include_feature = (s->include_feature && a->language_feature) ? 1 : 0;
+    rp.ranges = reinterpret_cast<const uint2*>(image + L.ranges);
+    rp.point_list = reinterpret_cast<const uint32_t*>(binning + L.point_list);
+    rp.cover = reinterpret_cast<uint8_t*>(binning + L.cover);
+    rp.record = reinterpret_cast<const float4*>(geom + L.record);
+    rp.bg = s->bg;
+    rp.final_T = reinterpret_cast<float*>(image + L.final_T);
+    rp.n_contrib = reinterpret_cast<uint32_t*>(image + L.n_contrib);
+    rp.sched_counts = reinterpret_cast<uint32_t*>(image + L.counters);
+    rp.sched_lists = reinterpret_cast<uint32_t*>(image + L.tile_lists);
+    rp.out_color = a->out_color;
+    rp.out_lang = a->out_language_feature;
+    if (a->flags & LSR_FWD_ZERO_GRAD_RECORDS) {
+        rp.zero_records = reinterpret_cast<float4*>(geom + L.grad_records);
+        rp.zero_records_n4 = ((int64_t)P * kGradStrideLang + 3) / 4;
+    }
+    if (a->out_loss && rp.include_feature) {
+        rp.loss_gt = a->loss_target;
+        rp.loss_mask = a->loss_mask;
+        rp.loss_code = reinterpret_cast<uint8_t*>(image + L.loss_code);
+        rp.loss_words = reinterpret_cast<uint64_t*>(geom + L.loss_words);
+        rp.out_loss = a->out_loss;
+        rp.spin_limit = stall_spin_limit();
+        rp.stall = &hb->stall;
+    }
+    LSR_TRY(launch_render_forward(rp, L.tiles, stream), "render forward");
+    return LSR_OK;
+}
+
 extern "C" {
 
 int32_t lsr_abi_version(void) { return LSR_ABI_VERSION; }
@@ -316,6 +357,11 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
     if (a->flags & ~LSR_FWD_ZERO_GRAD_RECORDS) return fail(LSR_ERR_INVALID, "lsr_forward: unknown flag");
     if (a->shs_rest && (!a->shs || a->M < 2))
         return fail(LSR_ERR_INVALID, "lsr_forward: shs_rest needs shs (features_dc) and M >= 2");
+    if (a->capacity_rendered < 0 || (a->capacity_rendered > 0 && a->capacity_entries <= 0) ||
+        a->capacity_rendered > 0xFFFFFFFFll || a->capacity_entries > 0xFFFFFFFFll)
+        return fail(LSR_ERR_INVALID, "lsr_forward: capacity mode needs capacity_rendered > 0 and capacity_entries > 0 "
+                                     "(both < 2^32)");
+    if (a->out_num_entries) *a->out_num_entries = 0;
     if (a->out_loss && (!s->include_feature || (P > 0 && !a->language_feature) || !a->loss_target || !a->loss_mask))
         return fail(LSR_ERR_INVALID, "lsr_forward: the fused loss needs include_feature, language_feature, "
                                      "loss_target and loss_mask");
@@ -405,11 +451,33 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
     // any pass count >= the needed one gives the same order (the extra digits are all 0), so the GPU
     // sorts while the host waits, instead of idling until the host has enqueued the next launch.
     // Should the range need more passes than guessed, the sort is run again below.
-    const uint32_t seq = ++hb->seq == 0 ? ++hb->seq : hb->seq;
     const uint32_t fwd_flags = ((a->flags & LSR_FWD_ZERO_GRAD_RECORDS) ? kFwdZeroedRecords : 0u) |
                                ((a->out_loss && s->include_feature && a->language_feature) ? kFwdFusedLoss : 0u);
+    if (a->capacity_rendered > 0) {
+        // Capacity mode: nothing waits for the device.  The counters stay on the device, the binning's
+        // grids and buffers come from the capacities and its kernels read the true counts; a view over
+        // capacity sets counters[kCntOverflow] (and *overflow) and is not binned.
+        const int64_t R_cap = a->capacity_rendered;
+        const bool fused = !depth_order_uses_pass_count(P);
+        const int64_t E_cap = fused ? std::min<int64_t>(a->capacity_entries, L.fused_cap) : a->capacity_entries;
+        LSR_TRY(launch_publish_counters((P + kPreThreads - 1) / kPreThreads, pp.partial, counters, nullptr, 0,
+                                        fwd_flags, (uint32_t)R_cap, (uint32_t)E_cap, a->overflow, stream),
+                "publish counters");
+        // LSD order (large P): all four passes (the key range is not read on the host)
+        LSR_TRY(launch_depth_order(P, 4, L, geom, counters, &hb->stall, stream, debug, fused, (uint32_t)E_cap),
+                "depth order");
+        L = make_layout(P, W, H, R_cap, E_cap);
+        char* binning = static_cast<char*>(alloc(user, LSR_BUF_BINNING, L.binning_bytes));
+        if (!binning) return fail(LSR_ERR_ALLOC, "lsr_forward: binning buffer allocation failed");
+        LSR_TRY(launch_binning(P, R_cap, L, geom, image, binning, &hb->stall, stream, debug, fused,
+                               DevCount{counters + kCntSuper, counters + kCntOverflow}),
+                "binning");
+        *num_rendered = R_cap;
+        return render_forward_and_finish(s, a, L, geom, image, binning, hb, stream, debug);
+    }
+    const uint32_t seq = ++hb->seq == 0 ? ++hb->seq : hb->seq;
     LSR_TRY(launch_publish_counters((P + kPreThreads - 1) / kPreThreads, pp.partial, counters, hb->slot, seq,
-                                    fwd_flags, stream),
+                                    fwd_flags, 0u, 0u, nullptr, stream),
             "publish counters");
     const int guess = hb->depth_passes > 0 ? hb->depth_passes : 4;
     // MSD path: the bucket sort also emits the super-tile entries (into geometry arrays of fixed
@@ -434,6 +502,7 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
         return fail(LSR_ERR_PREFILTERED, "lsr_forward: prefiltered=True but a Gaussian is outside the frustum");
     const int64_t R = host_cnt[kCntRendered];
     *num_rendered = R;
+    if (a->out_num_entries) *a->out_num_entries = (int64_t)host_cnt[kCntSuper];
     if (R > 0) {
         // sort only the bits the visible keys span (key - min <= max - min)
         const uint32_t span = host_cnt[kCntKeyMax] - host_cnt[kCntKeyMin];
@@ -464,39 +533,9 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
     hb->binning_hint = L.binning_bytes + L.binning_bytes / 8;  // 12.5 % headroom for the next view
     LSR_TRY(launch_binning(P, R, L, geom, image, binning, &hb->stall, stream, debug, emitted), "binning");
     hm.mark();
-    RenderParams rp{};
-    rp.W = W;
-    rp.H = H;
-    rp.gx = L.gx;
-    rp.gy = L.gy;
-    rp.include_feature = (s->include_feature && a->language_feature) ? 1 : 0;
-    rp.ranges = reinterpret_cast<const uint2*>(image + L.ranges);
-    rp.point_list = reinterpret_cast<const uint32_t*>(binning + L.point_list);
-    rp.cover = reinterpret_cast<uint8_t*>(binning + L.cover);
-    rp.record = reinterpret_cast<const float4*>(geom + L.record);
-    rp.bg = s->bg;
-    rp.final_T = reinterpret_cast<float*>(image + L.final_T);
-    rp.n_contrib = reinterpret_cast<uint32_t*>(image + L.n_contrib);
-    rp.sched_counts = reinterpret_cast<uint32_t*>(image + L.counters);
-    rp.sched_lists = reinterpret_cast<uint32_t*>(image + L.tile_lists);
-    rp.out_color = a->out_color;
-    rp.out_lang = a->out_language_feature;
-    if (a->flags & LSR_FWD_ZERO_GRAD_RECORDS) {
-        rp.zero_records = reinterpret_cast<float4*>(geom + L.grad_records);
-        rp.zero_records_n4 = ((int64_t)P * kGradStrideLang + 3) / 4;
-    }
-    if (a->out_loss && rp.include_feature) {
-        rp.loss_gt = a->loss_target;
-        rp.loss_mask = a->loss_mask;
-        rp.loss_code = reinterpret_cast<uint8_t*>(image + L.loss_code);
-        rp.loss_words = reinterpret_cast<uint64_t*>(geom + L.loss_words);
-        rp.out_loss = a->out_loss;
-        rp.spin_limit = stall_spin_limit();
-        rp.stall = &hb->stall;
-    }
-    LSR_TRY(launch_render_forward(rp, L.tiles, stream), "render forward");
+    const int32_t rc = render_forward_and_finish(s, a, L, geom, image, binning, hb, stream, debug);
     hm.mark();
-    return LSR_OK;
+    return rc;
 }
 
 int32_t lsr_backward(const lsr_settings* s, const lsr_backward_args* a, lsr_alloc_fn alloc, void* user,

@@ -228,7 +228,8 @@ constexpr int kPublishThreads = 1024;
 __global__ __launch_bounds__(kPublishThreads) void k_publish_counters(int nb, const uint4* __restrict__ partial,
                                                                       uint32_t* __restrict__ counters,
                                                                       uint64_t* host_slots, uint32_t seq,
-                                                                      uint32_t fwd_flags)
+                                                                      uint32_t fwd_flags, uint32_t r_cap, uint32_t e_cap,
+                                                                      int32_t* overflow)
 {
     constexpr int kWaves = kPublishThreads / 64;
     __shared__ uint32_t red[4][kWaves];
@@ -280,6 +281,12 @@ __global__ __launch_bounds__(kPublishThreads) void k_publish_counters(int nb, co
     counters[kCntKeyMin] = red[2][0];
     counters[kCntKeyMax] = red[3][0] & 0x7FFFFFFFu;
     counters[kCntError] = red[3][0] >> 31;
+    if (r_cap) {  // capacity mode: nothing goes to the host; the binning reads the counts here
+        const uint32_t ovf = (red[0][0] > r_cap || red[1][0] > e_cap) ? 1u : 0u;
+        counters[kCntOverflow] = ovf;
+        if (overflow) *overflow = (int32_t)ovf;
+        return;
+    }
     // each value travels with the sequence number in one 64-bit store (single-copy atomic): the
     // host waits for all 8 slots to carry `seq`, so no release fence (L2 write-back) is needed
     for (int i = 0; i < 8; i++)
@@ -288,10 +295,11 @@ __global__ __launch_bounds__(kPublishThreads) void k_publish_counters(int nb, co
 }
 
 hipError_t launch_publish_counters(int nb, const uint4* partial, uint32_t* counters, uint64_t* host_slots,
-                                   uint32_t seq, uint32_t fwd_flags, hipStream_t s)
+                                   uint32_t seq, uint32_t fwd_flags, uint32_t r_cap, uint32_t e_cap,
+                                   int32_t* overflow, hipStream_t s)
 {
     hipLaunchKernelGGL(k_publish_counters, dim3(1), dim3(kPublishThreads), 0, s, nb, partial, counters, host_slots,
-                       seq, fwd_flags);
+                       seq, fwd_flags, r_cap, e_cap, overflow);
     return hipGetLastError();
 }
 
@@ -393,11 +401,13 @@ template <int kItems>
 __global__ __launch_bounds__(kRadixThreads) void k_radix_hist(const uint32_t* __restrict__ keys, int n, int shift,
                                                               int nbits, uint32_t* __restrict__ hist, int nblk,
                                                               const uint32_t* __restrict__ kxf, int remap, int msd,
-                                                              ZeroList zero)
+                                                              ZeroList zero, DevCount dc)
 {
     constexpr int kWaves = kRadixThreads / 64;
     __shared__ uint32_t wcnt[kWaves][256];
     zero_words_strided(zero);
+    if (dc.abort && *dc.abort) return;
+    if (dc.n) n = min(n, (int)*dc.n);
     if (msd) msd_digit(kxf, shift, nbits);
     const int blk = xcd_tile(nblk, remap);
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
@@ -442,8 +452,10 @@ template <int kItems, bool kCarry = false>
 __global__ __launch_bounds__(kRadixThreads) void k_radix_scatter(
     const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in, int n, int shift, int nbits,
     const uint32_t* __restrict__ hist, int nblk, uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
-    const uint32_t* __restrict__ kxf, ScatterTail tail, int remap, int msd)
+    const uint32_t* __restrict__ kxf, ScatterTail tail, int remap, int msd, DevCount dc)
 {
+    if (dc.abort && *dc.abort) return;
+    if (dc.n) n = min(n, (int)*dc.n);
     if (msd) msd_digit(kxf, shift, nbits);
     const int blk = xcd_tile(nblk, remap);
     constexpr int kTile = kRadixThreads * kItems;
@@ -575,7 +587,7 @@ static hipError_t radix_sort(const uint32_t* k0, const uint32_t* v0, int n, int 
                              uint32_t* scan_regions, size_t region_words, uint32_t* stall, hipStream_t s, bool debug,
                              int* passes_out,
                              const uint32_t* kxf = nullptr, ScatterTail last = ScatterTail{nullptr, nullptr, nullptr},
-                             ZeroList zero = ZeroList{})
+                             ZeroList zero = ZeroList{}, DevCount dc = DevCount{nullptr, nullptr})
 {
     const bool small = radix_small(n);
     const int tile = kRadixThreads * (small ? 4 : 16);
@@ -597,10 +609,10 @@ static hipError_t radix_sort(const uint32_t* k0, const uint32_t* v0, int n, int 
         const ZeroList z = pass == 0 ? zero : ZeroList{};
         if (small)
             hipLaunchKernelGGL(k_radix_hist<4>, dim3(nblk), dim3(kRadixThreads), 0, s, kin, n, shift, nbits, hist, nblk,
-                               pass == 0 ? kxf : nullptr, remap, 0, z);
+                               pass == 0 ? kxf : nullptr, remap, 0, z, dc);
         else
             hipLaunchKernelGGL(k_radix_hist<16>, dim3(nblk), dim3(kRadixThreads), 0, s, kin, n, shift, nbits, hist,
-                               nblk, pass == 0 ? kxf : nullptr, remap, 0, z);
+                               nblk, pass == 0 ? kxf : nullptr, remap, 0, z, dc);
         if ((e = post(debug, s)) != hipSuccess) return e;
         if ((e = scan_exclusive(hist, hist_scan, (1 << nbits) * nblk, scan_regions + pass * region_words, nullptr,
                                 stall, s, debug)) != hipSuccess)
@@ -608,10 +620,10 @@ static hipError_t radix_sort(const uint32_t* k0, const uint32_t* v0, int n, int 
         const ScatterTail tail = pass == passes - 1 ? last : ScatterTail{nullptr, nullptr, nullptr};
         if (small)
             hipLaunchKernelGGL(k_radix_scatter<4>, dim3(nblk), dim3(kRadixThreads), 0, s, kin, vin, n, shift, nbits,
-                               hist_scan, nblk, kout, vout, pass == 0 ? kxf : nullptr, tail, remap, 0);
+                               hist_scan, nblk, kout, vout, pass == 0 ? kxf : nullptr, tail, remap, 0, dc);
         else
             hipLaunchKernelGGL(k_radix_scatter<16>, dim3(nblk), dim3(kRadixThreads), 0, s, kin, vin, n, shift, nbits,
-                               hist_scan, nblk, kout, vout, pass == 0 ? kxf : nullptr, tail, remap, 0);
+                               hist_scan, nblk, kout, vout, pass == 0 ? kxf : nullptr, tail, remap, 0, dc);
         if ((e = post(debug, s)) != hipSuccess) return e;
         kin = kout;
         vin = vout;
@@ -1211,7 +1223,7 @@ bool fused_emit_enabled()
 }
 
 hipError_t launch_depth_order(int P, int passes, const Layout& L, char* geom, uint32_t* counters, uint32_t* stall,
-                              hipStream_t s, bool debug, bool fused_emit)
+                              hipStream_t s, bool debug, bool fused_emit, uint32_t emit_cap)
 {
     if (P == 0) return hipSuccess;
     uint32_t* hist = reinterpret_cast<uint32_t*>(geom + L.radix_hist);
@@ -1242,10 +1254,10 @@ hipError_t launch_depth_order(int P, int passes, const Layout& L, char* geom, ui
         const int nblk = (P + kRadixThreads * (small ? 4 : 16) - 1) / (kRadixThreads * (small ? 4 : 16));
         if (small)
             hipLaunchKernelGGL(k_radix_hist<4>, dim3(nblk), dim3(kRadixThreads), 0, s, keys, P, 0, 8, hist, nblk, kxf,
-                               remap, 1, ZeroList{});
+                               remap, 1, ZeroList{}, DevCount{nullptr, nullptr});
         else
             hipLaunchKernelGGL(k_radix_hist<16>, dim3(nblk), dim3(kRadixThreads), 0, s, keys, P, 0, 8, hist, nblk, kxf,
-                               remap, 1, ZeroList{});
+                               remap, 1, ZeroList{}, DevCount{nullptr, nullptr});
         if ((e = post(debug, s)) != hipSuccess) return e;
         if ((e = scan_exclusive(hist, hist_scan, 256 * nblk, regions, nullptr, stall, s, debug)) != hipSuccess)
             return e;
@@ -1253,10 +1265,12 @@ hipError_t launch_depth_order(int P, int passes, const Layout& L, char* geom, ui
         const ScatterTail carry{tail.rect, tail.rect_ranked, nullptr};
         if (small)
             hipLaunchKernelGGL((k_radix_scatter<4, true>), dim3(nblk), dim3(kRadixThreads), 0, s, keys,
-                               (const uint32_t*)nullptr, P, 0, 8, hist_scan, nblk, kb, vb, kxf, carry, remap, 1);
+                               (const uint32_t*)nullptr, P, 0, 8, hist_scan, nblk, kb, vb, kxf, carry, remap, 1,
+                               DevCount{nullptr, nullptr});
         else
             hipLaunchKernelGGL((k_radix_scatter<16, true>), dim3(nblk), dim3(kRadixThreads), 0, s, keys,
-                               (const uint32_t*)nullptr, P, 0, 8, hist_scan, nblk, kb, vb, kxf, carry, remap, 1);
+                               (const uint32_t*)nullptr, P, 0, 8, hist_scan, nblk, kb, vb, kxf, carry, remap, 1,
+                               DevCount{nullptr, nullptr});
         if ((e = post(debug, s)) != hipSuccess) return e;
         // bucket-local offsets into super_offset, bucket totals for k_emit_super (no P-long scan);
         // with fused emission also the super-tile entries themselves
@@ -1264,7 +1278,7 @@ hipError_t launch_depth_order(int P, int passes, const Layout& L, char* geom, ui
         if (fused_emit) {
             em.keys = reinterpret_cast<uint32_t*>(geom + L.fused_keys);
             em.vals = reinterpret_cast<uint32_t*>(geom + L.fused_vals);
-            em.cap = (uint32_t)L.fused_cap;
+            em.cap = emit_cap > 0 && emit_cap < (uint32_t)L.fused_cap ? emit_cap : (uint32_t)L.fused_cap;
             em.status = reinterpret_cast<uint64_t*>(geom + L.bucket_status);
             em.sgx = L.sgx;
             em.stall = stall;
@@ -1306,7 +1320,7 @@ __global__ __launch_bounds__(256) void k_emit_super(int P, int sgx, const uint32
                                                     uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
                                                     uint32_t* __restrict__ z0, int n0, uint32_t* __restrict__ z1,
                                                     int n1, uint32_t* __restrict__ z2, int n2,
-                                                    uint32_t* __restrict__ z3, int n3, MsdOffsets msd)
+                                                    uint32_t* __restrict__ z3, int n3, MsdOffsets msd, DevCount dc)
 {
     __shared__ uint32_t s_start[256], s_base[256], s_wsum[4];
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1341,6 +1355,7 @@ __global__ __launch_bounds__(256) void k_emit_super(int P, int sgx, const uint32
     for (int w = r; w < n1; w += stride) z1[w] = 0u;
     for (int w = r; w < n2; w += stride) z2[w] = 0u;
     for (int w = r; w < n3; w += stride) z3[w] = 0u;
+    if (dc.abort && *dc.abort) return;    // capacity mode, view over capacity: nothing is binned
     if (r >= P || rc.x == rc.y) return;  // past the ranks, or culled (empty rectangle)
     int sx0, sy0, sx1, sy1;
     super_rect(rc, sx0, sy0, sx1, sy1);
@@ -1363,8 +1378,10 @@ __global__ __launch_bounds__(256) void k_emit_super(int P, int sgx, const uint32
 
 // [start, end) of every super-tile in the sorted entries (the low 16 key bits)
 __global__ __launch_bounds__(256) void k_super_ranges(int64_t E, const uint32_t* __restrict__ keys,
-                                                      uint2* __restrict__ ranges)
+                                                      uint2* __restrict__ ranges, DevCount dc)
 {
+    if (dc.abort && *dc.abort) return;
+    if (dc.n) E = min(E, (int64_t)*dc.n);
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= E) return;
     const uint32_t t = keys[k] & 0xFFFFu;
@@ -1383,8 +1400,9 @@ __global__ __launch_bounds__(kScanThreads) void k_seg_setup(int S, int sgx, int 
                                                             const uint2* __restrict__ sranges,
                                                             uint32_t* __restrict__ seg_base,
                                                             uint32_t* __restrict__ col_prefix,
-                                                            uint32_t* __restrict__ row_prefix)
+                                                            uint32_t* __restrict__ row_prefix, DevCount dc)
 {
+    if (dc.abort && *dc.abort) return;
     __shared__ uint32_t wsum[kScanThreads / 64];
     extern __shared__ uint32_t row_total[];  // per super-row: tiles-weighted segment count of one tile row
     uint32_t carry = 0;
@@ -1480,8 +1498,10 @@ __global__ __launch_bounds__(256) void k_bin_count(int S, int sgx, int gx, int g
                                                    const uint2* __restrict__ sranges,
                                                    const uint32_t* __restrict__ col_prefix,
                                                    const uint32_t* __restrict__ row_prefix,
-                                                   const uint32_t* __restrict__ keys, uint32_t* __restrict__ table)
+                                                   const uint32_t* __restrict__ keys, uint32_t* __restrict__ table,
+                                                   DevCount dc)
 {
+    if (dc.abort && *dc.abort) return;
     __shared__ uint32_t cnt[64];
     int s, seg;
     if (!block_segment(S, seg_base, &s, &seg)) return;
@@ -1526,8 +1546,11 @@ __global__ __launch_bounds__(256) void k_bin_count_fused(int S, int sgx, int sgy
                                                          int64_t E, const uint32_t* __restrict__ hist,
                                                          uint2* __restrict__ g_sranges, uint32_t* __restrict__ g_seg_base,
                                                          uint32_t* __restrict__ g_colpre, uint32_t* __restrict__ g_rowpre,
-                                                         const uint32_t* __restrict__ keys, uint32_t* __restrict__ table)
+                                                         const uint32_t* __restrict__ keys, uint32_t* __restrict__ table,
+                                                         DevCount dc)
 {
+    if (dc.abort && *dc.abort) return;
+    if (dc.n) E = min(E, (int64_t)*dc.n);
     __shared__ uint2 sr[kFusedSupers];
     __shared__ uint32_t sbase[kFusedSupers + 1];
     __shared__ uint32_t scol[kFusedSupers];
@@ -1632,8 +1655,9 @@ __global__ __launch_bounds__(256) void k_bin_emit(int S, int sgx, int gx, int gy
                                                   const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals,
                                                   const uint32_t* __restrict__ table, uint32_t* __restrict__ point_list,
                                                   uint2* __restrict__ ranges, uint32_t* __restrict__ sched_counts,
-                                                  uint32_t* __restrict__ sched_lists)
+                                                  uint32_t* __restrict__ sched_lists, DevCount dc)
 {
+    if (dc.abort && *dc.abort) return;
     __shared__ uint64_t colw[4][64];
     __shared__ uint32_t pre[4][64];    // per wave: rank base of tile l inside the batch's staging
     __shared__ uint32_t cursor[64];    // global position of tile l's next instance
@@ -1740,7 +1764,7 @@ static MsdOffsets msd_offsets(int P, const Layout& L, char* geom, char* image)
 }
 
 hipError_t launch_binning(int P, int64_t R, const Layout& L, char* geom, char* image, char* binning, uint32_t* stall,
-                          hipStream_t s, bool debug, bool emitted)
+                          hipStream_t s, bool debug, bool emitted, DevCount dc)
 {
     uint2* ranges = reinterpret_cast<uint2*>(image + L.ranges);
     if (R == 0) return hipMemsetAsync(ranges, 0, 8 * (size_t)L.tiles, s);
@@ -1773,14 +1797,14 @@ hipError_t launch_binning(int P, int64_t R, const Layout& L, char* geom, char* i
                            reinterpret_cast<const uint32_t*>(geom + L.super_offset),
                            reinterpret_cast<const uint2*>(geom + L.rect_ranked), kA, vA, zero.p[0], zero.n[0],
                            zero.p[1], zero.n[1], zero.p[2], zero.n[2], zero.p[3], zero.n[3],
-                           msd_offsets(P, L, geom, image));
+                           msd_offsets(P, L, geom, image), dc);
         if ((e = post(debug, s)) != hipSuccess) return e;
     }
     int passes = 0;
     uint32_t* bin_hist_scan = reinterpret_cast<uint32_t*>(binning + L.bin_radix_hist_scan);
     e = radix_sort(k0, v0, (int)E, L.super_bits, kA, vA, kB, vB, reinterpret_cast<uint32_t*>(binning + L.bin_radix_hist),
                    bin_hist_scan, regions, L.scan_region_bin, stall, s, debug, &passes, nullptr,
-                   ScatterTail{nullptr, nullptr, nullptr}, emitted ? zero : ZeroList{});
+                   ScatterTail{nullptr, nullptr, nullptr}, emitted ? zero : ZeroList{}, dc);
     if (e != hipSuccess) return e;
     const uint32_t* skeys = (passes & 1) ? kB : kA;
     const uint32_t* svals = (passes & 1) ? vB : vA;
@@ -1792,17 +1816,17 @@ hipError_t launch_binning(int P, int64_t R, const Layout& L, char* geom, char* i
         const int nblk = (int)((E + tile - 1) / tile);
         hipLaunchKernelGGL(k_bin_count_fused, dim3(grid), dim3(256), 0, s, L.supers, L.sgx, L.sgy, L.gx, L.gy, nblk,
                            1 << L.super_bits, E, (const uint32_t*)bin_hist_scan, sranges,
-                           seg_base, colpre, rowpre, skeys, table);
+                           seg_base, colpre, rowpre, skeys, table, dc);
         if ((e = post(debug, s)) != hipSuccess) return e;
     } else {
-        hipLaunchKernelGGL(k_super_ranges, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, s, E, skeys, sranges);
+        hipLaunchKernelGGL(k_super_ranges, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, s, E, skeys, sranges, dc);
         if ((e = post(debug, s)) != hipSuccess) return e;
         hipLaunchKernelGGL(k_seg_setup, dim3(1), dim3(kScanThreads), 4 * (size_t)L.sgy, s, L.supers, L.sgx, L.sgy,
-                           L.gx, L.gy, (const uint2*)sranges, seg_base, colpre, rowpre);
+                           L.gx, L.gy, (const uint2*)sranges, seg_base, colpre, rowpre, dc);
         if ((e = post(debug, s)) != hipSuccess) return e;
         hipLaunchKernelGGL(k_bin_count, dim3(grid), dim3(256), 0, s, L.supers, L.sgx, L.gx, L.gy,
                            (const uint32_t*)seg_base, (const uint2*)sranges, (const uint32_t*)colpre,
-                           (const uint32_t*)rowpre, skeys, table);
+                           (const uint32_t*)rowpre, skeys, table, dc);
         if ((e = post(debug, s)) != hipSuccess) return e;
     }
     uint32_t* table_scan = reinterpret_cast<uint32_t*>(binning + L.seg_table_scan);
@@ -1813,7 +1837,7 @@ hipError_t launch_binning(int P, int64_t R, const Layout& L, char* geom, char* i
                        (const uint2*)sranges, (const uint32_t*)colpre, (const uint32_t*)rowpre, skeys, svals,
                        (const uint32_t*)table_scan, pl, ranges,
                        reinterpret_cast<uint32_t*>(image + L.counters) + kCntFwdClass,
-                       reinterpret_cast<uint32_t*>(image + L.tile_lists));
+                       reinterpret_cast<uint32_t*>(image + L.tile_lists), dc);
     return post(debug, s);
 }
 

@@ -18,6 +18,7 @@ enum Counter : int {
     kCntSuper = 4,       // super-tile entries E (binning)
     kCntKeyMin = 5,      // smallest visible depth key (float bits)
     kCntKeyMax = 6,      // largest visible depth key
+    kCntOverflow = 7,    // capacity mode: the view exceeds the caller's capacities (nothing is binned)
     kCntSlots = 16
 };
 constexpr uint32_t kFwdZeroedRecords = 1u;  // the language step's gradient records cleared (the render
@@ -244,8 +245,9 @@ hipError_t launch_mark_visible(int P, const float* means, const float* view, con
 // super-tile entry offsets in that order
 // fused_emit (MSD path only): the bucket sort also writes the super-tile entries into L.fused_keys /
 // fused_vals when they fit (E <= L.fused_cap), so k_emit_super is not launched
+// emit_cap > 0: the fused emission writes at most that many entries (capacity mode), else L.fused_cap
 hipError_t launch_depth_order(int P, int passes, const Layout& L, char* geom, uint32_t* counters, uint32_t* stall,
-                              hipStream_t s, bool debug, bool fused_emit = false);
+                              hipStream_t s, bool debug, bool fused_emit = false, uint32_t emit_cap = 0);
 // false: the depth order reads its pass count on the device (MSD pass + per-bucket LDS sort) and
 // ignores `passes`; true (large P): LSD passes, `passes` must cover the visible key range
 bool depth_order_uses_pass_count(int P);
@@ -253,8 +255,16 @@ bool depth_order_uses_pass_count(int P);
 bool fused_emit_enabled();
 // super-tile lists, per-(tile, segment) counts, scanned bases -> point_list and tile ranges.
 // emitted: the depth order's bucket sort already wrote the E entries into L.fused_keys / fused_vals.
+// Device-read counts for launches sized from capacities: n = min(n, *n) when n is set; a set *abort
+// (counters[kCntOverflow]) makes the kernel skip its work (after the clearing the binning's first
+// launch does).  Both null: the host's counts.
+struct DevCount {
+    const uint32_t* n;
+    const uint32_t* abort;
+};
+// capacity mode: dc = {counters + kCntSuper, counters + kCntOverflow}, R / L from the capacities
 hipError_t launch_binning(int P, int64_t R, const Layout& L, char* geom, char* image, char* binning, uint32_t* stall,
-                          hipStream_t s, bool debug, bool emitted = false);
+                          hipStream_t s, bool debug, bool emitted = false, DevCount dc = DevCount{nullptr, nullptr});
 
 // Look-back stall handling (k_scan, k_masked_l1_forward).  A single-pass look-back polls at most
 // stall_spin_limit() times for a predecessor's value; past that it computes the value itself from
@@ -316,8 +326,10 @@ hipError_t scan_exclusive_u32(const uint32_t* in, uint32_t* out, int n, uint32_t
                               hipStream_t s);
 // reduces the preprocess block partials into counters and publishes counters[0..7], each with seq,
 // to the host slots (8 x u64 pinned)
+// capacity mode (r_cap > 0): no host slots; counters[kCntOverflow] (and *overflow) = R > r_cap || E > e_cap
 hipError_t launch_publish_counters(int nb, const uint4* partial, uint32_t* counters, uint64_t* host_slots,
-                                   uint32_t seq, uint32_t fwd_flags, hipStream_t s);
+                                   uint32_t seq, uint32_t fwd_flags, uint32_t r_cap, uint32_t e_cap,
+                                   int32_t* overflow, hipStream_t s);
 size_t knn_scratch_bytes(int64_t N);
 hipError_t launch_knn_mean_dist3(int64_t N, const float* pts, float* out, void* scratch, uint32_t* stall,
                                  hipStream_t s);

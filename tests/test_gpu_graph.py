@@ -1,0 +1,142 @@
+"""Capacity mode (include/lsr.h lsr_forward_args.capacity_*) and the captured train step
+(langsplat_amd.graph.GraphedStep).
+
+Capacity mode sizes the binning from caller capacities and never waits for the device: its outputs
+must be bit-identical to the eager forward's (images, radii, per-tile ranges and order, final T,
+contributor counts), its backward identical too, and a view over capacity must be flagged and left
+un-rasterized (background, no out-of-bounds writes).  The captured step must reproduce the eager
+language step (train.py:92-104) loss and gradients on every replay.
+"""
+import numpy as np
+import pytest
+import torch
+
+from langsplat_amd import _native
+from langsplat_amd.graph import GraphedStep
+from langsplat_amd.render import render
+from langsplat_amd.synthetic import make_cameras, make_gaussians
+from tests.scenes import grad_seed, scene, to_device
+from tests.test_gpu_fused import _Model, _Opt, _Pipe
+from tests.test_gpu_parity import assert_grad_close, state
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _forward(st, ind, cap=None, flags=0):
+    args = (ind["means3D"], ind["shs"], None, ind["language_feature_precomp"], ind["opacities"], ind["scales"],
+            ind["rotations"], None)
+    if cap is None:
+        out = _native.rasterize_gaussians(st, *args, flags=flags)
+    else:
+        with cap:
+            out = _native.rasterize_gaussians(st, *args, flags=flags)
+    torch.cuda.synchronize()
+    return out
+
+
+@pytest.mark.parametrize("P,W,H", [(3000, 160, 120), (20000, 640, 360)])
+def test_capacity_mode_matches_eager(P, W, H):
+    st, inp = scene(P=P, W=W, H=H, seed=4, scale_range=(0.02, 0.15))
+    std, ind = to_device(st, inp, DEV)
+    eager = _forward(std, ind)
+    R, E = _native.LAST_COUNTS[(P, W, H)]
+    assert R == eager[0] and E > 0
+    ovf = torch.full((), 7, dtype=torch.int32, device=DEV)
+    capd = _forward(std, ind, _native.capacity(R + 100, E + 10, ovf))
+    assert int(ovf.item()) == 0
+    assert capd[0] == R + 100  # the layout key lsr_backward needs
+    for a, b in zip(eager[1:4], capd[1:4]):
+        assert torch.equal(a, b)
+    se, sc = state(eager, P, W, H), state(capd, P, W, H)
+    np.testing.assert_array_equal(se["ranges"], sc["ranges"])
+    np.testing.assert_array_equal(se["final_T"], sc["final_T"])
+    np.testing.assert_array_equal(se["n_contrib"], sc["n_contrib"])
+    np.testing.assert_array_equal(se["point_list"], sc["point_list"][:R])
+    # exact capacities fit too
+    capx = _forward(std, ind, _native.capacity(R, E, ovf))
+    assert int(ovf.item()) == 0 and torch.equal(capx[1], eager[1])
+    # the backward over the capacity-mode state
+    gc, gl = grad_seed(H, W, seed=5)
+    bw = lambda out: _native.rasterize_gaussians_backward(  # noqa: E731
+        std, ind["means3D"], ind["shs"], None, ind["language_feature_precomp"], ind["scales"], ind["rotations"], None,
+        out[3], gc.to(DEV), gl.to(DEV), out[0], out[4], out[5], out[6])
+    ge, gcap = bw(eager), bw(capd)
+    for k in ("means2D", "opacities", "means3D", "language_feature_precomp", "shs", "scales", "rotations"):
+        assert_grad_close(k, gcap[k].cpu().numpy(), ge[k].cpu().numpy())
+
+
+@pytest.mark.parametrize("short", ["rendered", "entries"])
+def test_capacity_overflow_is_flagged_and_safe(short):
+    """A view over capacity: flagged, background image, zero contributors -- and the next forward
+    with room is exact again (nothing was written out of bounds)."""
+    P, W, H = 4000, 128, 96
+    st, inp = scene(P=P, W=W, H=H, seed=6, scale_range=(0.03, 0.2), bg=(0.25, 0.5, 0.75))
+    std, ind = to_device(st, inp, DEV)
+    eager = _forward(std, ind)
+    R, E = _native.LAST_COUNTS[(P, W, H)]
+    ovf = torch.zeros((), dtype=torch.int32, device=DEV)
+    cap = _native.capacity(R // 2, E, ovf) if short == "rendered" else _native.capacity(R, E // 2, ovf)
+    out = _forward(std, ind, cap)
+    assert int(ovf.item()) == 1
+    bg = torch.tensor([0.25, 0.5, 0.75], device=DEV).view(3, 1, 1).expand(3, H, W)
+    assert torch.equal(out[1], bg) and not out[2].any()
+    assert not state(out, P, W, H)["n_contrib"].any()
+    ok = _forward(std, ind, _native.capacity(R, E, ovf))
+    assert int(ovf.item()) == 0 and torch.equal(ok[1], eager[1]) and torch.equal(ok[2], eager[2])
+
+
+def _language_setup(W=160, H=120, P=6000):
+    g = make_gaussians(P, seed=17, scale_range=(0.02, 0.15))
+    cam = make_cameras(1, W, H, device=DEV)[0]
+    gen = torch.Generator().manual_seed(3)
+    gt = torch.nn.functional.normalize(torch.randn((3, H, W), generator=gen), dim=0).to(DEV)
+    mask = (torch.rand((1, H, W), generator=gen) < 0.9).to(DEV)
+    m = _Model(g, DEV)
+    for n in ("xyz", "features_dc", "features_rest", "scaling", "rotation", "opacity"):
+        getattr(m, "_" + n).requires_grad_(False)
+    bg = torch.zeros(3, device=DEV)
+
+    def step():
+        loss = render(cam, m, _Pipe, bg, _Opt, language_target=(gt, mask))["language_l1"]
+        loss.backward()
+        return loss
+    return m, step
+
+
+def test_graphed_language_step_matches_eager(monkeypatch):
+    monkeypatch.setenv("LANGSPLAT_AMD_FUSED", "1")
+    m, step = _language_setup()
+    m._language_feature.grad = None
+    loss0 = step().detach().clone()
+    g0 = m._language_feature.grad.detach().clone()
+    gs = GraphedStep(step, [m._language_feature])
+    for it in range(3):
+        loss = gs.replay()
+        torch.cuda.synchronize()
+        assert gs.check()
+        torch.testing.assert_close(loss, loss0, rtol=0, atol=0)
+        assert_grad_close(f"replay {it}", m._language_feature.grad.cpu().numpy(), g0.cpu().numpy())
+    assert gs.captures == 1
+
+
+def test_graphed_step_recaptures_on_overflow(monkeypatch):
+    """Capacities from the warm-up view; the parameters then change so that the view needs more
+    tile instances than captured: check() reports it once and re-captures; the next replay fits and
+    matches the eager step."""
+    monkeypatch.setenv("LANGSPLAT_AMD_FUSED", "1")
+    m, step = _language_setup(P=3000)
+    gs = GraphedStep(step, [m._language_feature], headroom=1.0)
+    gs.capture()
+    gs.rendered_at_capture = gs.rendered
+    with torch.no_grad():
+        m._scaling.add_(0.7)  # twice the size: many more tile instances
+    gs.replay()
+    assert not gs.check() and gs.captures == 2 and gs.rendered > gs.rendered_at_capture
+    loss = gs.replay().detach().clone()
+    assert gs.check()
+    g1 = m._language_feature.grad.detach().clone()
+    m._language_feature.grad = None
+    loss_e = step()
+    torch.testing.assert_close(loss, loss_e.detach(), rtol=0, atol=0)
+    assert_grad_close("after recapture", g1.cpu().numpy(), m._language_feature.grad.cpu().numpy())
