@@ -451,14 +451,16 @@ def main():
             loss = render(cam, model, Pipe, bg, Opt, language_target=(gt, mask))["language_l1"]
             loss.backward()
             return loss
-        gstep = GraphedStep(fwd_bwd, model.trainable())
+        # N = 1: Adam inside the graph too (its step count advanced on the device); N > 1: the
+        # all-reduce and Adam after each replay
+        gstep = GraphedStep(fwd_bwd, model.trainable(), optimizer=optim if bucket is None else None)
         gstep.capture()
 
         def run():
             loss = gstep.replay()
             if bucket is not None:
                 bucket.all_reduce(average=True)
-            optim.step()
+                optim.step()
             return loss
         for _ in range(3):
             run()
@@ -588,7 +590,8 @@ def main():
                                 "scene/gaussian_model.py:203-217)"},
         "ms_per_step_with_sync": round(1000.0 * elapsed_sync / args.steps, 4),
         "ms_per_step_eager": round(1000.0 * elapsed_eager / args.steps, 4),
-        "step_form": "HIP graph replay (render + loss + backward) + Adam" if graphed else "eager",
+        "step_form": ("HIP graph replay (render + loss + backward + Adam)" if world == 1 else
+                      "HIP graph replay (render + loss + backward), RCCL all-reduce, Adam") if graphed else "eager",
         "ms_per_step_all_gradients": round(1000.0 * elapsed_all / args.steps, 4),
         "ms_per_step_rgb": None if rgb_ms is None else round(rgb_ms, 4),
         "raster_ms_per_step": round(raster_ms, 4),

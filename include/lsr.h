@@ -329,7 +329,11 @@ int32_t lsr_adam_step(int64_t n, float* param, const float* grad, float* exp_avg
 /* The same step for several tensors in ONE launch (RGB mode's six parameter groups,
  * scene/gaussian_model.py:219-226, each with its own lr, betas, eps and step count, i.e. torch's
  * per-parameter state).  Every gradient is multiplied by grad_scale first (e.g. the 1 / N of a
- * gradient all-reduced as a SUM over N ranks; 1 = none). */
+ * gradient all-reduced as a SUM over N ranks; 1 = none).
+ * step_dev (device int64, with ticket: a device uint32 that is 0) replaces the tensors' step fields
+ * for a step replayed from a HIP graph: the launch uses step *step_dev + 1 for every tensor and
+ * stores it back (the launch's last workgroup), so each replay advances the count on the device;
+ * at most 16 tensors then.  NULL: the host's step counts. */
 typedef struct lsr_adam_tensor {
     int64_t n;
     float* param;
@@ -339,7 +343,8 @@ typedef struct lsr_adam_tensor {
     double lr, beta1, beta2, eps;
     int64_t step;                /* 1-based, after this update */
 } lsr_adam_tensor;
-int32_t lsr_adam_multi(int32_t count, const lsr_adam_tensor* tensors, float grad_scale, void* stream);
+int32_t lsr_adam_multi(int32_t count, const lsr_adam_tensor* tensors, float grad_scale, int64_t* step_dev,
+                       uint32_t* ticket, void* stream);
 
 /* Densification statistics of one rendered view, one pass (train.py:125-126 with
  * GaussianModel.add_densification_stats, scene/gaussian_model.py:480-482), for Gaussians with

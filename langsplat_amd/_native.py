@@ -104,7 +104,8 @@ SIGNATURES = {
     "lsr_mark_visible": (ctypes.c_int32, [ctypes.c_int32, _vp, _vp, _vp, _vp, _vp]),
     "lsr_adam_step": (ctypes.c_int32, [ctypes.c_int64, _vp, _vp, _vp, _vp, ctypes.c_double, ctypes.c_double,
                                        ctypes.c_double, ctypes.c_double, ctypes.c_int64, _vp]),
-    "lsr_adam_multi": (ctypes.c_int32, [ctypes.c_int32, ctypes.POINTER(LsrAdamTensor), ctypes.c_float, _vp]),
+    "lsr_adam_multi": (ctypes.c_int32, [ctypes.c_int32, ctypes.POINTER(LsrAdamTensor), ctypes.c_float, _vp, _vp,
+                                        _vp]),
     "lsr_densification_stats": (ctypes.c_int32, [ctypes.c_int32, _vp, _vp, _vp, _vp, _vp, _vp]),
     "lsr_dist_cuda2": (ctypes.c_int32, [ctypes.c_int64, _vp, _vp, ALLOC_FN, _vp, _vp]),
     "lsr_masked_l1_scratch_bytes": (ctypes.c_size_t, [ctypes.c_int32, ctypes.c_int64]),

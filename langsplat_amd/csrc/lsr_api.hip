@@ -839,26 +839,33 @@ int32_t lsr_adam_step(int64_t n, float* param, const float* grad, float* exp_avg
     return LSR_OK;
 }
 
-int32_t lsr_adam_multi(int32_t count, const lsr_adam_tensor* tensors, float grad_scale, void* stream_ptr)
+int32_t lsr_adam_multi(int32_t count, const lsr_adam_tensor* tensors, float grad_scale, int64_t* step_dev,
+                       uint32_t* ticket, void* stream_ptr)
 {
     if (count < 0 || (count > 0 && !tensors)) return fail(LSR_ERR_INVALID, "lsr_adam_multi: invalid argument");
+    if ((step_dev != nullptr) != (ticket != nullptr) || (step_dev && count > kAdamMaxTensors))
+        return fail(LSR_ERR_INVALID, "lsr_adam_multi: step_dev needs a ticket and at most 16 tensors");
     hipStream_t stream = reinterpret_cast<hipStream_t>(stream_ptr);
     const bool debug = false;
     for (int32_t k0 = 0; k0 < count; k0 += kAdamMaxTensors) {
         AdamTable tab{};
         for (int32_t k = k0; k < count && k < k0 + kAdamMaxTensors; k++) {
             const lsr_adam_tensor& t = tensors[k];
-            if (t.n < 0 || (t.n > 0 && (!t.param || !t.grad || !t.exp_avg || !t.exp_avg_sq)) || t.step < 1)
+            if (t.n < 0 || (t.n > 0 && (!t.param || !t.grad || !t.exp_avg || !t.exp_avg_sq)) ||
+                (t.step < 1 && !step_dev))
                 return fail(LSR_ERR_INVALID, "lsr_adam_multi: invalid tensor entry");
             if (t.n == 0) continue;
+            tab.hyper[tab.count] = AdamHyper{t.lr, t.beta1, t.beta2, t.eps};
             AdamSegment& g = tab.seg[tab.count++];
             g.param = t.param;
             g.grad = t.grad;
             g.m = t.exp_avg;
             g.v = t.exp_avg_sq;
             g.n = t.n;
-            g.a = adam_scalars(t.lr, t.beta1, t.beta2, t.eps, t.step);
+            g.a = adam_scalars(t.lr, t.beta1, t.beta2, t.eps, t.step < 1 ? 1 : t.step);
         }
+        tab.step_dev = step_dev;
+        tab.ticket = ticket;
         LSR_TRY(launch_adam_multi(tab, grad_scale, stream), "adam");
     }
     return LSR_OK;

@@ -313,9 +313,15 @@ struct AdamSegment {
     AdamScalars a;
     int vec;
 };
+struct AdamHyper {
+    double lr, beta1, beta2, eps;
+};
 struct AdamTable {
     int count;
     AdamSegment seg[kAdamMaxTensors];
+    AdamHyper hyper[kAdamMaxTensors];  // used with step_dev: the scalars are formed on the device
+    int64_t* step_dev;                 // null: the host's step counts (seg[].a)
+    uint32_t* ticket;                  // zero at launch (the last workgroup resets it)
 };
 hipError_t launch_adam_multi(AdamTable& tab, float grad_scale, hipStream_t s);
 hipError_t launch_densification_stats(int P, const int* radii, const float* dmeans2D, float* max_radii, float* accum,

@@ -29,11 +29,8 @@ __device__ __forceinline__ void adam_one(float& p, float g, float& m, float& v, 
 // per-parameter state -- in one pass, their gradients typically the slices of one all-reduced bucket
 // (langsplat_amd.distributed.GradBucket).  grad_scale multiplies every gradient first (the 1 / N of
 // an averaging all-reduce done as a SUM; 1: none).
-__global__ __launch_bounds__(256) void k_adam_multi(AdamTable tab, float grad_scale)
+__device__ __forceinline__ void adam_segment(const AdamSegment& g, float grad_scale)
 {
-    int s = 0;
-    while (s + 1 < tab.count && (int64_t)blockIdx.x >= tab.seg[s + 1].block0) s++;
-    const AdamSegment& g = tab.seg[s];
     const int64_t first = ((int64_t)blockIdx.x - g.block0) * 256 + threadIdx.x;
     const bool scale = grad_scale != 1.0f;
     if (g.vec) {
@@ -61,6 +58,47 @@ __global__ __launch_bounds__(256) void k_adam_multi(AdamTable tab, float grad_sc
     if (first < g.n) {
         const float gr = scale ? g.grad[first] * grad_scale : g.grad[first];
         adam_one(g.param[first], gr, g.m[first], g.v[first], g.a);
+    }
+}
+
+// Device step count (tab.step_dev, for a step replayed from a HIP graph): every workgroup computes
+// the bias corrections of step *step_dev + 1 (torch's formulas, in double), and the workgroup that
+// finishes last -- the last ticket -- stores that step and resets the ticket, after every workgroup
+// has read the old value.
+__device__ __forceinline__ AdamScalars adam_scalars_dev(const AdamHyper& h, int64_t step)
+{
+    const double bc1 = 1.0 - pow(h.beta1, (double)step);
+    const double bc2 = 1.0 - pow(h.beta2, (double)step);
+    AdamScalars a;
+    a.w1 = (float)(1.0 - h.beta1);
+    a.beta2 = (float)h.beta2;
+    a.w2 = (float)(1.0 - h.beta2);
+    a.inv_bc2_sqrt = 1.0f / (float)sqrt(bc2);
+    a.eps = (float)h.eps;
+    a.neg_step_size = (float)(-(h.lr / bc1));
+    return a;
+}
+
+__global__ __launch_bounds__(256) void k_adam_multi(AdamTable tab, float grad_scale)
+{
+    int s = 0;
+    while (s + 1 < tab.count && (int64_t)blockIdx.x >= tab.seg[s + 1].block0) s++;
+    AdamSegment g = tab.seg[s];
+    int64_t dstep = 0;
+    if (tab.step_dev) {
+        dstep = *tab.step_dev + 1;
+        g.a = adam_scalars_dev(tab.hyper[s], dstep);
+    }
+    adam_segment(g, grad_scale);
+    if (tab.step_dev) {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __threadfence();
+            if (atomicAdd(tab.ticket, 1u) == gridDim.x - 1) {
+                *tab.step_dev = dstep;
+                *tab.ticket = 0u;
+            }
+        }
     }
 }
 

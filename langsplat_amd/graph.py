@@ -12,8 +12,10 @@ true counts.  A view over capacity is flagged in `overflow` (not rasterized); `c
 (a device-to-host sync: call it where the loop syncs anyway, e.g. with train.py:108's loss.item())
 and, when set, re-captures with larger capacities.
 
-The optimizer step stays outside the graph (it runs after each replay, on the gradients the graph
-wrote into the parameters' .grad tensors, which the graph owns: do not set them to None).
+With `optimizer` (langsplat_amd.optim.Adam) its step is captured too, after the backward: its step
+count then advances on the device at every replay (sync() copies it back into the optimizer state).
+Without, the optimizer runs after each replay on the gradients the graph wrote into the parameters'
+.grad tensors.  Either way the graph owns those .grad tensors: do not set them to None.
 """
 from __future__ import annotations
 
@@ -26,10 +28,11 @@ from . import _native
 
 class GraphedStep:
     def __init__(self, step_fn: Callable[[], torch.Tensor], params: Iterable[torch.Tensor], headroom: float = 1.125,
-                 warmup: int = 2):
+                 warmup: int = 2, optimizer=None):
         """step_fn: runs render + loss + loss.backward() and returns the loss; params: the tensors
-        whose .grad the step produces (the trainable parameters)."""
+        whose .grad the step produces (the trainable parameters); optimizer: stepped inside the graph."""
         self.step_fn = step_fn
+        self.optimizer = optimizer
         self.params = [p for p in params]
         self.headroom = float(headroom)
         self.warmup = int(warmup)
@@ -50,7 +53,7 @@ class GraphedStep:
             for _ in range(self.warmup):
                 for p in self.params:
                     p.grad = None
-                self.step_fn()
+                self._body()
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
         if not _native.LAST_COUNTS:
@@ -64,12 +67,25 @@ class GraphedStep:
         self._measure(min_rendered, min_entries)
         for p in self.params:
             p.grad = None  # the captured backward assigns fresh .grad tensors (no accumulate)
+        if self.optimizer is not None:
+            self.optimizer.prepare_capture()
         self.graph = torch.cuda.CUDAGraph()
         with _native.capacity(self.rendered, self.entries, self.overflow):
             with torch.cuda.graph(self.graph):
-                self.static_loss = self.step_fn()
+                self.static_loss = self._body()
         self.captures += 1
         return self
+
+    def _body(self):
+        loss = self.step_fn()
+        if self.optimizer is not None:
+            self.optimizer.step()
+        return loss
+
+    def sync(self):
+        """The optimizer state's step counts from the device (a device-to-host copy)."""
+        if self.optimizer is not None:
+            self.optimizer.sync_steps()
 
     def replay(self) -> torch.Tensor:
         if self.graph is None:
@@ -82,5 +98,8 @@ class GraphedStep:
         not rasterized) re-capture with twice the capacities and return False: run the step again."""
         if int(self.overflow.item()) == 0:
             return True
+        # the over-capacity replay was not rasterized, but its optimizer step ran (on zero gradients
+        # of that view); the re-capture measures the view again
+        self.sync()
         self.capture(2 * self.rendered, 2 * self.entries)
         return False

@@ -10,6 +10,10 @@ step count) instead of torch's multi-tensor kernels.  In RGB mode the six gradie
 slices of the one all-reduced bucket (langsplat_amd.distributed.GradBucket), and a SUM all-reduce's
 1 / N is applied inside that same pass (step(grad_scale=...)).  amsgrad, weight decay and maximize
 are not used by LangSplat and are not offered.
+
+Inside a HIP graph capture (langsplat_amd.graph.GraphedStep) the step count lives on the device:
+prepare_capture() copies it there before the capture, every replay of the captured launch advances
+it (include/lsr.h lsr_adam_multi step_dev), and sync_steps() copies it back into state["step"].
 """
 from __future__ import annotations
 
@@ -25,6 +29,36 @@ class Adam(torch.optim.Optimizer):
         if lr < 0.0 or eps < 0.0 or not (0.0 <= betas[0] < 1.0 and 0.0 <= betas[1] < 1.0):
             raise ValueError(f"invalid Adam hyper-parameters lr={lr} betas={betas} eps={eps}")
         super().__init__(params, dict(lr=lr, betas=tuple(betas), eps=eps))
+        self._step_dev = None  # graph capture: (int64 step count, uint32 ticket) on the device
+
+    def _params_with_grad(self):
+        return [p for g in self.param_groups for p in g["params"] if p.grad is not None]
+
+    @torch.no_grad()
+    def prepare_capture(self):
+        """Before a graph capture of step(): the step count (equal for every parameter, as one
+        optimizer steps them together) goes to the device, where the captured launch advances it."""
+        ps = [p for g in self.param_groups for p in g["params"]]
+        steps = {int(self.state[p]["step"].item()) for p in ps if len(self.state[p])}
+        if len(steps) > 1:
+            raise RuntimeError("langsplat_amd.optim.Adam: a captured step needs equal step counts")
+        missing = [p for p in ps if len(self.state[p]) == 0]
+        if missing:
+            raise RuntimeError("langsplat_amd.optim.Adam: run one eager step before capturing")
+        dev = ps[0].device
+        self._step_dev = (torch.full((1,), steps.pop() if steps else 0, dtype=torch.int64, device=dev),
+                          torch.zeros((1,), dtype=torch.int32, device=dev))
+
+    @torch.no_grad()
+    def sync_steps(self):
+        """state["step"] of every parameter from the device count (a device-to-host copy)."""
+        if self._step_dev is None:
+            return
+        n = float(self._step_dev[0].item())
+        for g in self.param_groups:
+            for p in g["params"]:
+                if len(self.state[p]):
+                    self.state[p]["step"] = torch.tensor(n)
 
     @torch.no_grad()
     def step(self, closure=None, grad_scale: float = 1.0):
@@ -34,6 +68,9 @@ class Adam(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        capturing = torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+        if capturing and self._step_dev is None:
+            raise RuntimeError("langsplat_amd.optim.Adam: call prepare_capture() before capturing step()")
         entries, keep = [], []
         device = None
         for group in self.param_groups:
@@ -55,15 +92,19 @@ class Adam(torch.optim.Optimizer):
                     state["step"] = torch.tensor(0.0)
                     state["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     state["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-                state["step"] += 1
+                if not capturing:
+                    state["step"] += 1
                 entries.append(_native.LsrAdamTensor(
                     p.numel(), p.data_ptr(), grad.data_ptr(), state["exp_avg"].data_ptr(),
                     state["exp_avg_sq"].data_ptr(), float(group["lr"]), float(beta1), float(beta2),
-                    float(group["eps"]), int(state["step"].item())))
+                    float(group["eps"]), 0 if capturing else int(state["step"].item())))
                 keep.append(grad)  # a contiguous copy lives until the launch is enqueued (stream order)
         if entries:
             table = (_native.LsrAdamTensor * len(entries))(*entries)
+            sd = tk = None
+            if capturing:
+                sd, tk = (ctypes.c_void_p(t.data_ptr()) for t in self._step_dev)
             with _native._on_device(device):
-                _native._check(_native.load().lsr_adam_multi(len(entries), table, float(grad_scale),
+                _native._check(_native.load().lsr_adam_multi(len(entries), table, float(grad_scale), sd, tk,
                                                              _native._stream(device)), "lsr_adam_multi")
         return loss

@@ -140,3 +140,34 @@ def test_graphed_step_recaptures_on_overflow(monkeypatch):
     loss_e = step()
     torch.testing.assert_close(loss, loss_e.detach(), rtol=0, atol=0)
     assert_grad_close("after recapture", g1.cpu().numpy(), m._language_feature.grad.cpu().numpy())
+
+
+def test_graphed_step_with_adam_matches_eager_steps(monkeypatch):
+    """Adam captured with the step (its step count on the device): K replays give the parameters and
+    moments of K eager steps (to float rounding), and sync() brings the step count back to the host."""
+    from langsplat_amd.optim import Adam
+    monkeypatch.setenv("LANGSPLAT_AMD_FUSED", "1")
+    runs = {}
+    for mode in ("eager", "graph"):
+        m, step = _language_setup(P=4000)
+        opt = Adam([{"params": [m._language_feature], "lr": 0.01, "name": "language_feature"}], lr=0.0, eps=1e-15)
+        if mode == "eager":
+            for _ in range(2 + 5):  # GraphedStep's two warm-up steps + five replays
+                m._language_feature.grad = None
+                step()
+                opt.step()
+        else:
+            gs = GraphedStep(step, [m._language_feature], optimizer=opt)
+            for _ in range(5):
+                gs.replay()
+            assert gs.check()
+            gs.sync()
+        torch.cuda.synchronize()
+        st = opt.state[m._language_feature]
+        runs[mode] = (m._language_feature.detach().clone(), st["exp_avg"].clone(), st["exp_avg_sq"].clone(),
+                      int(st["step"].item()))
+    (pe, me, ve, se), (pg, mg, vg, sg) = runs["eager"], runs["graph"]
+    assert se == sg == 7
+    torch.testing.assert_close(pg, pe, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(mg, me, rtol=1e-4, atol=1e-9)
+    torch.testing.assert_close(vg, ve, rtol=1e-4, atol=1e-12)

@@ -1,0 +1,83 @@
+"""Kernel timeline of the bench's language step, eager or as a captured graph (measurement aid):
+
+    rocprofv3 --kernel-trace --output-format csv -d gpurun_out/st_graph -o t -- python3 tools/step_trace.py graph
+    python3 tools/step_trace.py --summary gpurun_out/st_graph/t_kernel_trace.csv
+
+The summary prints, per step (one preprocess launch to the next), the span, the summed kernel time
+and the idle gaps between consecutive kernels, so graph replay and eager launches can be compared.
+"""
+import csv
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def run(mode, steps=30):
+    import torch
+    import bench
+    from langsplat_amd.graph import GraphedStep
+    from langsplat_amd.synthetic import CONFIGS, make_cameras, make_gaussians
+    c = CONFIGS["C3"]
+    P, W, H = c["P"], c["width"], c["height"]
+    dev = torch.device("cuda", 0)
+    params = make_gaussians(P, seed=0).to(dev)
+    model = bench.Model(params, include_feature=True)
+    cam = make_cameras(1, W, H, device=dev)[0]
+    bg = torch.zeros(3, device=dev)
+    gen = torch.Generator().manual_seed(100)
+    gt = torch.nn.functional.normalize(torch.randn((3, H, W), generator=gen), dim=0).to(dev)
+    mask = (torch.rand((1, H, W), generator=gen) < 0.9).to(dev)
+    optim = bench.AmdAdam([{"params": [model._language_feature], "lr": 0.0025}], lr=0.0, eps=1e-15)
+
+    def fwd_bwd():
+        loss = bench.render(cam, model, bench.Pipe, bg, bench.Opt, language_target=(gt, mask))["language_l1"]
+        loss.backward()
+        return loss
+
+    if mode == "graph":
+        g = GraphedStep(fwd_bwd, [model._language_feature]).capture()
+
+        def step():
+            g.replay()
+            optim.step()
+    else:
+        def step():
+            fwd_bwd()
+            optim.step()
+            optim.zero_grad(set_to_none=True)
+    for _ in range(10):
+        step()
+    torch.cuda.synchronize()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+
+
+def summary(path):
+    rows = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in csv.DictReader(open(path))))
+    starts = [i for i, r in enumerate(rows) if "k_preprocess<" in r[2]]
+    out = []
+    for a, b in zip(starts[-21:-1], starts[-20:]):
+        seg = rows[a:b]
+        span = seg[-1][1] - seg[0][0]
+        busy = sum(e - s for s, e, _ in seg)
+        gaps = [(seg[i + 1][0] - seg[i][1], seg[i][2][:40], seg[i + 1][2][:40]) for i in range(len(seg) - 1)]
+        out.append((span, busy, gaps))
+    n = len(out)
+    print(f"{n} steps: span {sum(o[0] for o in out) / n / 1e3:.1f} us, kernels {sum(o[1] for o in out) / n / 1e3:.1f} us, "
+          f"kernels per step {len(out[0][2]) + 1}")
+    gsum = {}
+    for o in out:
+        for i, (g, x, y) in enumerate(o[2]):
+            gsum.setdefault(i, [0, x, y])[0] += g
+    for i, (g, x, y) in sorted(gsum.items()):
+        print(f"  gap {g / n / 1e3:7.2f} us  after {x}  before {y}")
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "--summary":
+        summary(sys.argv[2])
+    else:
+        run(sys.argv[1])
