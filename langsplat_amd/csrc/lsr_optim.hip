@@ -90,14 +90,14 @@ __global__ __launch_bounds__(256) void k_adam_multi(AdamTable tab, float grad_sc
         g.a = adam_scalars_dev(tab.hyper[s], dstep);
     }
     adam_segment(g, grad_scale);
-    if (tab.step_dev) {
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            __threadfence();
-            if (atomicAdd(tab.ticket, 1u) == gridDim.x - 1) {
-                *tab.step_dev = dstep;
-                *tab.ticket = 0u;
-            }
+    if (!tab.step_dev) return;
+    __syncthreads();  // every wave of the workgroup has consumed its read of *step_dev
+    if (threadIdx.x == 0) {
+        // no fence: the reads were consumed (they formed the scalars above) before the ticket; the
+        // stores reach the next launch at the kernel boundary
+        if (__hip_atomic_fetch_add(tab.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
+            *tab.step_dev = dstep;
+            *tab.ticket = 0u;
         }
     }
 }
