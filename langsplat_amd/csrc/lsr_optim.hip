@@ -10,9 +10,13 @@
 //     denom      = sqrt(exp_avg_sq) * (1 / sqrt(bias_correction2)) + eps
 //     param      = param + (-lr / bias_correction1) * exp_avg / denom
 // The step-dependent scalars are computed on the host in double, as torch does.
+#include <algorithm>
+
 #include "lsr_internal.h"
 
 namespace lsr {
+
+constexpr int64_t kAdamDevBlocks = 512;  // device-step launches: 2 per CU
 
 __device__ __forceinline__ void adam_one(float& p, float g, float& m, float& v, const AdamScalars& a)
 {
@@ -29,9 +33,9 @@ __device__ __forceinline__ void adam_one(float& p, float g, float& m, float& v, 
 // per-parameter state -- in one pass, their gradients typically the slices of one all-reduced bucket
 // (langsplat_amd.distributed.GradBucket).  grad_scale multiplies every gradient first (the 1 / N of
 // an averaging all-reduce done as a SUM; 1: none).
-__device__ __forceinline__ void adam_segment(const AdamSegment& g, float grad_scale)
+__device__ __forceinline__ void adam_segment(const AdamSegment& g, int64_t chunk, float grad_scale)
 {
-    const int64_t first = ((int64_t)blockIdx.x - g.block0) * 256 + threadIdx.x;
+    const int64_t first = (chunk - g.block0) * 256 + threadIdx.x;
     const bool scale = grad_scale != 1.0f;
     if (g.vec) {
         const int64_t i = first;
@@ -79,17 +83,18 @@ __device__ __forceinline__ AdamScalars adam_scalars_dev(const AdamHyper& h, int6
     return a;
 }
 
-__global__ __launch_bounds__(256) void k_adam_multi(AdamTable tab, float grad_scale)
+// Workgroups take 256-thread chunks grid-stride (chunk -> tensor through block0); with a device step
+// the grid is small (kAdamDevBlocks), so few tickets meet on the one counter.
+__global__ __launch_bounds__(256) void k_adam_multi(AdamTable tab, int64_t chunks, float grad_scale)
 {
-    int s = 0;
-    while (s + 1 < tab.count && (int64_t)blockIdx.x >= tab.seg[s + 1].block0) s++;
-    AdamSegment g = tab.seg[s];
-    int64_t dstep = 0;
-    if (tab.step_dev) {
-        dstep = *tab.step_dev + 1;
-        g.a = adam_scalars_dev(tab.hyper[s], dstep);
+    const int64_t dstep = tab.step_dev ? *tab.step_dev + 1 : 0;
+    for (int64_t c = blockIdx.x; c < chunks; c += gridDim.x) {
+        int s = 0;
+        while (s + 1 < tab.count && c >= tab.seg[s + 1].block0) s++;
+        AdamSegment g = tab.seg[s];
+        if (tab.step_dev) g.a = adam_scalars_dev(tab.hyper[s], dstep);
+        adam_segment(g, c, grad_scale);
     }
-    adam_segment(g, grad_scale);
     if (!tab.step_dev) return;
     __syncthreads();  // every wave of the workgroup has consumed its read of *step_dev
     if (threadIdx.x == 0) {
@@ -114,8 +119,8 @@ hipError_t launch_adam_multi(AdamTable& tab, float grad_scale, hipStream_t s)
         blocks += (work + 255) / 256;
     }
     if (blocks == 0) return hipSuccess;
-    if (blocks > 0x7FFFFFFF) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_adam_multi, dim3((unsigned)blocks), dim3(256), 0, s, tab, grad_scale);
+    const int64_t grid = tab.step_dev ? std::min<int64_t>(blocks, kAdamDevBlocks) : std::min<int64_t>(blocks, 1 << 20);
+    hipLaunchKernelGGL(k_adam_multi, dim3((unsigned)grid), dim3(256), 0, s, tab, blocks, grad_scale);
     return hipGetLastError();
 }
 
