@@ -460,11 +460,14 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
         const int64_t R_cap = a->capacity_rendered;
         const bool fused = !depth_order_uses_pass_count(P);
         const int64_t E_cap = fused ? std::min<int64_t>(a->capacity_entries, L.fused_cap) : a->capacity_entries;
+        // LSD order (large P): the passes this thread's last eager forward needed (its key range is
+        // not read on the host here; a view that needs more is flagged as over capacity)
+        const int passes = fused ? 0 : (hb->depth_passes > 0 ? hb->depth_passes : 4);
         LSR_TRY(launch_publish_counters((P + kPreThreads - 1) / kPreThreads, pp.partial, counters, nullptr, 0,
-                                        fwd_flags, (uint32_t)R_cap, (uint32_t)E_cap, a->overflow, stream),
+                                        fwd_flags, (uint32_t)R_cap, (uint32_t)E_cap, a->overflow, passes, stream),
                 "publish counters");
-        // LSD order (large P): all four passes (the key range is not read on the host)
-        LSR_TRY(launch_depth_order(P, 4, L, geom, counters, &hb->stall, stream, debug, fused, (uint32_t)E_cap),
+        LSR_TRY(launch_depth_order(P, fused ? 4 : passes, L, geom, counters, &hb->stall, stream, debug, fused,
+                                   (uint32_t)E_cap),
                 "depth order");
         L = make_layout(P, W, H, R_cap, E_cap);
         char* binning = static_cast<char*>(alloc(user, LSR_BUF_BINNING, L.binning_bytes));
@@ -477,7 +480,7 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
     }
     const uint32_t seq = ++hb->seq == 0 ? ++hb->seq : hb->seq;
     LSR_TRY(launch_publish_counters((P + kPreThreads - 1) / kPreThreads, pp.partial, counters, hb->slot, seq,
-                                    fwd_flags, 0u, 0u, nullptr, stream),
+                                    fwd_flags, 0u, 0u, nullptr, 0, stream),
             "publish counters");
     const int guess = hb->depth_passes > 0 ? hb->depth_passes : 4;
     // MSD path: the bucket sort also emits the super-tile entries (into geometry arrays of fixed

@@ -229,7 +229,7 @@ __global__ __launch_bounds__(kPublishThreads) void k_publish_counters(int nb, co
                                                                       uint32_t* __restrict__ counters,
                                                                       uint64_t* host_slots, uint32_t seq,
                                                                       uint32_t fwd_flags, uint32_t r_cap, uint32_t e_cap,
-                                                                      int32_t* overflow)
+                                                                      int32_t* overflow, int depth_passes)
 {
     constexpr int kWaves = kPublishThreads / 64;
     __shared__ uint32_t red[4][kWaves];
@@ -282,7 +282,13 @@ __global__ __launch_bounds__(kPublishThreads) void k_publish_counters(int nb, co
     counters[kCntKeyMax] = red[3][0] & 0x7FFFFFFFu;
     counters[kCntError] = red[3][0] >> 31;
     if (r_cap) {  // capacity mode: nothing goes to the host; the binning reads the counts here
-        const uint32_t ovf = (red[0][0] > r_cap || red[1][0] > e_cap) ? 1u : 0u;
+        // LSD depth order (depth_passes > 0): the passes the visible key range needs (as the host
+        // computes them in the eager forward) must not exceed the ones enqueued
+        const uint32_t span = (red[3][0] & 0x7FFFFFFFu) - red[2][0];
+        const int bits = span ? 32 - __clz(span) : 0;
+        const int need = red[0][0] == 0 ? 0 : (bits <= 8 ? 1 : (bits + 7) / 8);
+        const uint32_t ovf = (red[0][0] > r_cap || red[1][0] > e_cap || (depth_passes > 0 && need > depth_passes))
+            ? 1u : 0u;
         counters[kCntOverflow] = ovf;
         if (overflow) *overflow = (int32_t)ovf;
         return;
@@ -296,10 +302,10 @@ __global__ __launch_bounds__(kPublishThreads) void k_publish_counters(int nb, co
 
 hipError_t launch_publish_counters(int nb, const uint4* partial, uint32_t* counters, uint64_t* host_slots,
                                    uint32_t seq, uint32_t fwd_flags, uint32_t r_cap, uint32_t e_cap,
-                                   int32_t* overflow, hipStream_t s)
+                                   int32_t* overflow, int depth_passes, hipStream_t s)
 {
     hipLaunchKernelGGL(k_publish_counters, dim3(1), dim3(kPublishThreads), 0, s, nb, partial, counters, host_slots,
-                       seq, fwd_flags, r_cap, e_cap, overflow);
+                       seq, fwd_flags, r_cap, e_cap, overflow, depth_passes);
     return hipGetLastError();
 }
 

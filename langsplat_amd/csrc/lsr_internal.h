@@ -333,9 +333,10 @@ hipError_t scan_exclusive_u32(const uint32_t* in, uint32_t* out, int n, uint32_t
 // reduces the preprocess block partials into counters and publishes counters[0..7], each with seq,
 // to the host slots (8 x u64 pinned)
 // capacity mode (r_cap > 0): no host slots; counters[kCntOverflow] (and *overflow) = R > r_cap || E > e_cap
+// || the LSD depth order needs more than depth_passes passes (depth_passes 0: not checked)
 hipError_t launch_publish_counters(int nb, const uint4* partial, uint32_t* counters, uint64_t* host_slots,
                                    uint32_t seq, uint32_t fwd_flags, uint32_t r_cap, uint32_t e_cap,
-                                   int32_t* overflow, hipStream_t s);
+                                   int32_t* overflow, int depth_passes, hipStream_t s);
 size_t knn_scratch_bytes(int64_t N);
 hipError_t launch_knn_mean_dist3(int64_t N, const float* pts, float* out, void* scratch, uint32_t* stall,
                                  hipStream_t s);

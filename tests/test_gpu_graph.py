@@ -171,3 +171,45 @@ def test_graphed_step_with_adam_matches_eager_steps(monkeypatch):
     torch.testing.assert_close(pg, pe, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(mg, me, rtol=1e-4, atol=1e-9)
     torch.testing.assert_close(vg, ve, rtol=1e-4, atol=1e-12)
+
+
+def _depth_scene(P, W, H, wide, seed):
+    """Gaussians in front of camera 0 (view depth = z + 4) over a wide (0.3..80) or narrow depth range."""
+    import math
+    g = torch.Generator().manual_seed(seed)
+    if wide:
+        d = torch.exp(torch.rand(P, generator=g) * (math.log(80.0) - math.log(0.3)) + math.log(0.3))
+    else:
+        d = 4.0 + torch.rand(P, generator=g) * 1e-3
+    u, v = torch.rand(P, generator=g) * 2 - 1, torch.rand(P, generator=g) * 2 - 1
+    means = torch.stack([u * d * 0.4, v * d * 0.3, d - 4.0], 1)
+    from tests.scenes import settings_for
+    st = settings_for(make_cameras(1, W, H)[0], sh_degree=3)
+    inp = dict(means3D=means, opacities=torch.rand((P, 1), generator=g) * 0.6 + 0.05,
+               shs=torch.randn((P, 16, 3), generator=g) * 0.2,
+               language_feature_precomp=torch.nn.functional.normalize(torch.randn((P, 3), generator=g)),
+               scales=torch.full((P, 3), 0.02) * d[:, None] / 4.0,
+               rotations=torch.nn.functional.normalize(torch.randn((P, 4), generator=g)))
+    return to_device(st, inp, DEV)
+
+
+def test_capacity_mode_lsd_depth_order(monkeypatch):
+    """The LSD depth order (P > 2M, forced here by LSR_DEPTH_LSD=1) in capacity mode uses the pass
+    count of the thread's last eager forward: exact when it suffices, flagged when the view's key range
+    needs more passes, exact again after an eager forward of that view."""
+    monkeypatch.setenv("LSR_DEPTH_LSD", "1")
+    P, W, H = 3000, 96, 64
+    narrow = _depth_scene(P, W, H, False, 41)
+    wide = _depth_scene(P, W, H, True, 42)
+    e_wide = _forward(*wide)
+    Rw, Ew = _native.LAST_COUNTS[(P, W, H)]
+    ovf = torch.zeros((), dtype=torch.int32, device=DEV)
+    c_wide = _forward(*wide, cap=_native.capacity(Rw, Ew, ovf))
+    assert int(ovf.item()) == 0 and torch.equal(c_wide[1], e_wide[1])
+    np.testing.assert_array_equal(state(c_wide, P, W, H)["point_list"][:Rw], state(e_wide, P, W, H)["point_list"])
+    _forward(*narrow)  # the thread's last eager view now needs fewer passes
+    c2 = _forward(*wide, cap=_native.capacity(Rw, Ew, ovf))
+    assert int(ovf.item()) == 1 and not c2[2].any()
+    _forward(*wide)
+    c3 = _forward(*wide, cap=_native.capacity(Rw, Ew, ovf))
+    assert int(ovf.item()) == 0 and torch.equal(c3[1], e_wide[1])
