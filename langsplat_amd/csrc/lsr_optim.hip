@@ -10,6 +10,8 @@
 //     denom      = sqrt(exp_avg_sq) * (1 / sqrt(bias_correction2)) + eps
 //     param      = param + (-lr / bias_correction1) * exp_avg / denom
 // The step-dependent scalars are computed on the host in double, as torch does.
+#include <stdlib.h>
+
 #include <algorithm>
 
 #include "lsr_internal.h"
@@ -85,9 +87,15 @@ __device__ __forceinline__ AdamScalars adam_scalars_dev(const AdamHyper& h, int6
 
 // Workgroups take 256-thread chunks grid-stride (chunk -> tensor through block0); with a device step
 // the grid is small (kAdamDevBlocks), so few tickets meet on the one counter.
+__global__ void k_adam_advance(int64_t* step_dev)
+{
+    if (threadIdx.x == 0) *step_dev += 1;
+}
+
 __global__ __launch_bounds__(256) void k_adam_multi(AdamTable tab, int64_t chunks, float grad_scale)
 {
-    const int64_t dstep = tab.step_dev ? *tab.step_dev + 1 : 0;
+    // ticket null with a device step: k_adam_advance already advanced it
+    const int64_t dstep = tab.step_dev ? *tab.step_dev + (tab.ticket ? 1 : 0) : 0;
     for (int64_t c = blockIdx.x; c < chunks; c += gridDim.x) {
         int s = 0;
         while (s + 1 < tab.count && c >= tab.seg[s + 1].block0) s++;
@@ -95,7 +103,7 @@ __global__ __launch_bounds__(256) void k_adam_multi(AdamTable tab, int64_t chunk
         if (tab.step_dev) g.a = adam_scalars_dev(tab.hyper[s], dstep);
         adam_segment(g, c, grad_scale);
     }
-    if (!tab.step_dev) return;
+    if (!tab.step_dev || !tab.ticket) return;
     __syncthreads();  // every wave of the workgroup has consumed its read of *step_dev
     if (threadIdx.x == 0) {
         // no fence: the reads were consumed (they formed the scalars above) before the ticket; the
@@ -119,7 +127,22 @@ hipError_t launch_adam_multi(AdamTable& tab, float grad_scale, hipStream_t s)
         blocks += (work + 255) / 256;
     }
     if (blocks == 0) return hipSuccess;
-    const int64_t grid = tab.step_dev ? std::min<int64_t>(blocks, kAdamDevBlocks) : std::min<int64_t>(blocks, 1 << 20);
+    static const int64_t dev_blocks = [] {  // LSR_ADAM_DEV_BLOCKS: measurement knob
+        const char* e = getenv("LSR_ADAM_DEV_BLOCKS");
+        return e ? (int64_t)atoll(e) : kAdamDevBlocks;
+    }();
+    static const bool advance = [] {  // LSR_ADAM_ADVANCE=1: a one-thread kernel advances the step first
+        const char* e = getenv("LSR_ADAM_ADVANCE");
+        return e && e[0] == '1';
+    }();
+    if (tab.step_dev && advance) {
+        hipLaunchKernelGGL(k_adam_advance, dim3(1), dim3(64), 0, s, tab.step_dev);
+        tab.ticket = nullptr;
+        const int64_t grid = std::min<int64_t>(blocks, 1 << 20);
+        hipLaunchKernelGGL(k_adam_multi, dim3((unsigned)grid), dim3(256), 0, s, tab, blocks, grad_scale);
+        return hipGetLastError();
+    }
+    const int64_t grid = tab.step_dev ? std::min<int64_t>(blocks, dev_blocks) : std::min<int64_t>(blocks, 1 << 20);
     hipLaunchKernelGGL(k_adam_multi, dim3((unsigned)grid), dim3(256), 0, s, tab, blocks, grad_scale);
     return hipGetLastError();
 }

@@ -1,14 +1,10 @@
 #!/usr/bin/env bash
-# Same-box A/B of an environment knob on the bench (run on the GPU box from the repo root):
-#   tools/ab_env.sh VAR "valA valB" [rounds]  -> gpurun_out/ab_<VAR>_<val>_<round>.log
-set -euo pipefail
-var=$1
-vals=$2
-rounds=${3:-2}
-mkdir -p gpurun_out
-for r in $(seq 1 "$rounds"); do
-    for v in $vals; do
-        tag=$(basename "$v")
-        env "$var=$v" timeout -k 10 120 python bench.py --no-cpu-baseline > "gpurun_out/ab_${var}_${tag}_${r}.log" 2>&1
-    done
+# Same-box A/B of runtime environment variants on the bench step (measurement aid):
+#   bash tools/ab_env.sh "VAR=1" "VAR=0 OTHER=2" ...   (each variant twice; prints ms_per_step, eager)
+set -e
+for v in "$@"; do
+  for rep in 1 2; do
+    env $v LSR_BENCH_RGB=0 timeout -k 10 200 python bench.py --no-cpu-baseline --steps 100 > gpurun_out/ab_env.log 2>&1
+    echo "$v | $(tail -1 gpurun_out/ab_env.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d["ms_per_step_eager"], d["ms_per_step_with_sync"])')"
+  done
 done

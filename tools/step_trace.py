@@ -37,11 +37,10 @@ def run(mode, steps=30):
         return loss
 
     if mode == "graph":
-        g = GraphedStep(fwd_bwd, [model._language_feature]).capture()
+        g = GraphedStep(fwd_bwd, [model._language_feature], optimizer=optim).capture()
 
         def step():
             g.replay()
-            optim.step()
     else:
         def step():
             fwd_bwd()
@@ -53,6 +52,14 @@ def run(mode, steps=30):
     for _ in range(steps):
         step()
     torch.cuda.synchronize()
+
+
+def per_kernel(path):
+    import collections
+    acc = collections.defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        acc[r["Kernel_Name"][:60]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    return {k: (len(v), sum(v[-20:]) / len(v[-20:])) for k, v in acc.items()}
 
 
 def summary(path):
@@ -79,5 +86,9 @@ def summary(path):
 if __name__ == "__main__":
     if sys.argv[1] == "--summary":
         summary(sys.argv[2])
+    elif sys.argv[1] == "--compare":  # per-kernel average (last 20 launches) of two traces
+        a, b = per_kernel(sys.argv[2]), per_kernel(sys.argv[3])
+        for k in sorted(set(a) | set(b), key=lambda k: -max(a.get(k, (0, 0))[1], b.get(k, (0, 0))[1])):
+            print(f"{a.get(k, (0, 0))[1]:8.1f} {b.get(k, (0, 0))[1]:8.1f}  {k}")
     else:
         run(sys.argv[1])
