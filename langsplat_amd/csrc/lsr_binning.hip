@@ -1441,51 +1441,49 @@ __global__ __launch_bounds__(kScanThreads) void k_seg_setup(int S, int sgx, int 
     }
 }
 
-// block -> (super-tile, segment) through seg_base; false for the grid's spare blocks
-__device__ __forceinline__ bool block_segment(int S, const uint32_t* __restrict__ seg_base, int* s_out, int* seg_out)
-{
-    __shared__ int sh[2];
-    if (threadIdx.x == 0) {
-        const uint32_t b = blockIdx.x;
-        int s = -1, seg = 0;
-        if (b < seg_base[S]) {
-            int lo = 0, hi = S - 1;  // last s with seg_base[s] <= b
-            while (lo < hi) {
-                const int mid = (lo + hi + 1) >> 1;
-                if (seg_base[mid] <= b) lo = mid;
-                else hi = mid - 1;
-            }
-            s = lo;
-            seg = (int)(b - seg_base[lo]);
-        }
-        sh[0] = s;
-        sh[1] = seg;
-    }
-    __syncthreads();
-    *s_out = sh[0];
-    *seg_out = sh[1];
-    return sh[0] >= 0;
-}
-
+// This workgroup's (super-tile, segment) and its context; false for the grid's spare blocks.  Every
+// thread tests its share of the S intervals [seg_base[s], seg_base[s + 1]) and loads the
+// interval's super-tile range and column prefix alongside: one memory round trip on every
+// workgroup's critical path (a binary search by one thread, then the context loads, were ~13
+// dependent loads).
 struct SegmentCtx {
     int s, seg, ox, oy;
     uint32_t e0, e1, nseg, colpre;
 };
 
-__device__ __forceinline__ SegmentCtx segment_ctx(int s, int seg, int sgx, const uint2* __restrict__ sranges,
-                                                  const uint32_t* __restrict__ col_prefix)
+__device__ __forceinline__ bool block_segment_ctx(int S, int sgx, const uint32_t* __restrict__ seg_base,
+                                                  const uint2* __restrict__ sranges,
+                                                  const uint32_t* __restrict__ col_prefix, SegmentCtx* out)
 {
-    SegmentCtx c;
-    c.s = s;
-    c.seg = seg;
-    c.ox = (s % sgx) * kSuper;
-    c.oy = (s / sgx) * kSuper;
-    const uint2 r = sranges[s];
-    c.e0 = r.x + (uint32_t)seg * kSegEntries;
+    __shared__ uint32_t sh[5];
+    const uint32_t b = blockIdx.x;
+    if (threadIdx.x == 0) sh[0] = 0xFFFFFFFFu;
+    __syncthreads();
+    for (int s = threadIdx.x; s < S; s += blockDim.x) {
+        const uint32_t lo = seg_base[s], hi = seg_base[s + 1];
+        const uint2 r = sranges[s];
+        const uint32_t cp = col_prefix[s];
+        if (lo <= b && b < hi) {
+            sh[0] = (uint32_t)s;
+            sh[1] = b - lo;
+            sh[2] = r.x;
+            sh[3] = r.y;
+            sh[4] = cp;
+        }
+    }
+    __syncthreads();
+    if (sh[0] == 0xFFFFFFFFu) return false;
+    SegmentCtx& c = *out;
+    c.s = (int)sh[0];
+    c.seg = (int)sh[1];
+    c.ox = (c.s % sgx) * kSuper;
+    c.oy = (c.s / sgx) * kSuper;
+    const uint2 r = make_uint2(sh[2], sh[3]);
+    c.e0 = r.x + (uint32_t)c.seg * kSegEntries;
     c.e1 = min(r.y, c.e0 + (uint32_t)kSegEntries);
     c.nseg = super_segments(r);
-    c.colpre = col_prefix[s];
-    return c;
+    c.colpre = sh[4];
+    return true;
 }
 
 // count-table slot of (local tile l, segment 0) of the super-tile, -1 outside the image;
@@ -1509,9 +1507,9 @@ __global__ __launch_bounds__(256) void k_bin_count(int S, int sgx, int gx, int g
 {
     if (dc.abort && *dc.abort) return;
     __shared__ uint32_t cnt[64];
-    int s, seg;
-    if (!block_segment(S, seg_base, &s, &seg)) return;
-    const SegmentCtx c = segment_ctx(s, seg, sgx, sranges, col_prefix);
+    SegmentCtx c;
+    if (!block_segment_ctx(S, sgx, seg_base, sranges, col_prefix, &c)) return;
+    const int seg = c.seg;
     if (threadIdx.x < 64) cnt[threadIdx.x] = 0;
     __syncthreads();
     uint32_t mine = 0;  // lane l: entries of this wave covering local tile l
@@ -1671,9 +1669,9 @@ __global__ __launch_bounds__(256) void k_bin_emit(int S, int sgx, int gx, int gy
     __shared__ uint32_t stage_g[kStage];
     __shared__ uint8_t stage_t[kStage];
     __shared__ uint32_t sg[4][64];     // the batch's Gaussian ids, entry order
-    int s, seg;
-    if (!block_segment(S, seg_base, &s, &seg)) return;
-    const SegmentCtx c = segment_ctx(s, seg, sgx, sranges, col_prefix);
+    SegmentCtx c;
+    if (!block_segment_ctx(S, sgx, seg_base, sranges, col_prefix, &c)) return;
+    const int seg = c.seg;
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
     // both batches' entries loaded up front (a segment is at most kSegEntries = 2 x 256 entries):
     // one memory round trip instead of one per batch

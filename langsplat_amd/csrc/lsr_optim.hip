@@ -67,10 +67,12 @@ __device__ __forceinline__ void adam_segment(const AdamSegment& g, int64_t chunk
     }
 }
 
-// Device step count (tab.step_dev, for a step replayed from a HIP graph): every workgroup computes
-// the bias corrections of step *step_dev + 1 (torch's formulas, in double), and the workgroup that
-// finishes last -- the last ticket -- stores that step and resets the ticket, after every workgroup
-// has read the old value.
+// Device step count (tab.step_dev, for a step replayed from a HIP graph): a one-thread kernel
+// advances *step_dev first, then every workgroup computes the bias corrections of that step
+// (torch's formulas, in double).  Measured on the graph-replayed C3 step (tools/ab_env.sh): 5 us
+// faster than the alternative kept behind LSR_ADAM_ADVANCE=0, where the workgroup that finishes
+// last (the last ticket) stores step + 1 and resets the ticket (same-address atomics from a small
+// grid, and a long tail).
 __device__ __forceinline__ AdamScalars adam_scalars_dev(const AdamHyper& h, int64_t step)
 {
     const double bc1 = 1.0 - pow(h.beta1, (double)step);
@@ -85,7 +87,7 @@ __device__ __forceinline__ AdamScalars adam_scalars_dev(const AdamHyper& h, int6
     return a;
 }
 
-// Workgroups take 256-thread chunks grid-stride (chunk -> tensor through block0); with a device step
+// Workgroups take 256-thread chunks grid-stride (chunk -> tensor through block0); with the ticket
 // the grid is small (kAdamDevBlocks), so few tickets meet on the one counter.
 __global__ void k_adam_advance(int64_t* step_dev)
 {
@@ -131,9 +133,9 @@ hipError_t launch_adam_multi(AdamTable& tab, float grad_scale, hipStream_t s)
         const char* e = getenv("LSR_ADAM_DEV_BLOCKS");
         return e ? (int64_t)atoll(e) : kAdamDevBlocks;
     }();
-    static const bool advance = [] {  // LSR_ADAM_ADVANCE=1: a one-thread kernel advances the step first
+    static const bool advance = [] {  // LSR_ADAM_ADVANCE=0: the ticket form (measurement knob)
         const char* e = getenv("LSR_ADAM_ADVANCE");
-        return e && e[0] == '1';
+        return !(e && e[0] == '0');
     }();
     if (tab.step_dev && advance) {
         hipLaunchKernelGGL(k_adam_advance, dim3(1), dim3(64), 0, s, tab.step_dev);

@@ -1036,19 +1036,22 @@ __device__ __forceinline__ void bwd_walk_entry(BwdPixel& q, const BwdEntry& E, i
     bool h = kk < (int)q.last && pw <= 0.0f && pw >= B.z;
     if (__ballot(h) == 0ull) return;  // wave-uniform skip
     // hardware exp (a few ulp): gradients need 1e-4.  Only the 1/255 skip decision must equal the
-    // forward's, so alphas within 1e-6 of it use the exact exp.
+    // forward's, so alphas within 1e-6 of it use the exact exp: two compares bracket that band
+    // (alpha = min(0.99, og) equals og = o G there), and the band's lanes take the exact exp.
     float G = __expf(pw);
     float og = B.y * G;
-    float al = fminf(0.99f, og);
-    const bool near = fabsf(al - 1.0f / 255.0f) < 1e-6f;
-    if (__ballot(near) != 0ull) {  // wave-uniform: keeps the exact exp off the hot path
-        if (near) {
+    bool hit = og >= 1.0f / 255.0f + 1e-6f;
+    // two ballots of plain compares (a ballot of their combination is materialised per lane); in
+    // the rare band branch every lane short of `hit` takes the exact exp (below the band it only
+    // confirms the miss)
+    if ((__ballot(og > 1.0f / 255.0f - 1e-6f) & ~__ballot(hit)) != 0ull) {  // wave-uniform
+        if (!hit) {
             G = expf_exact_render(pw);  // the forward's exp (pw >= cutoff > -6 here)
             og = B.y * G;
-            al = fminf(0.99f, og);
+            hit = og >= 1.0f / 255.0f;
         }
     }
-    h = h && al >= 1.0f / 255.0f;
+    h = h && hit;
     if (kStats) {
         const int nh = __popcll(__ballot(h));
         if (lane == 0) {
@@ -1060,7 +1063,9 @@ __device__ __forceinline__ void bwd_walk_entry(BwdPixel& q, const BwdEntry& E, i
             atomicAdd(&s_stat[8 + nh], 1u);
         }
     }
-    if (!h) al = G = og = 0.0f;
+    og = h ? og : 0.0f;
+    if (kGeo) G = h ? G : 0.0f;
+    const float al = __builtin_amdgcn_fmed3f(og, 0.0f, 0.99f);  // min(0.99, og) (og >= 0), no canonicalise
     float3 C = make_float3(0.f, 0.f, 0.f), F = make_float3(0.f, 0.f, 0.f);
     if (kColor) {
         C = make_float3(E.C.x, E.C.y, E.C.z);
