@@ -458,9 +458,12 @@ template <int kItems, bool kCarry = false>
 __global__ __launch_bounds__(kRadixThreads) void k_radix_scatter(
     const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in, int n, int shift, int nbits,
     const uint32_t* __restrict__ hist, int nblk, uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
-    const uint32_t* __restrict__ kxf, ScatterTail tail, int remap, int msd, DevCount dc)
+    const uint32_t* __restrict__ kxf, ScatterTail tail, int remap, int msd, DevCount dc, int hstride = 0,
+    int hrows = 256, ZeroList zero = ZeroList{})
 {
+    zero_words_strided(zero);
     if (dc.abort && *dc.abort) return;
+    if (hstride == 0) hstride = nblk;  // histogram rows of nblk blocks (the hist kernel's layout)
     if (dc.n) n = min(n, (int)*dc.n);
     if (msd) msd_digit(kxf, shift, nbits);
     const int blk = xcd_tile(nblk, remap);
@@ -477,7 +480,7 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_scatter(
     const uint32_t mask = (1u << nbits) - 1u;
 #pragma unroll
     for (int w = 0; w < kWaves; w++) wcnt[w][t] = 0;
-    gbase[t] = t <= (int)mask ? hist[t * nblk + blk] : 0u;
+    gbase[t] = t <= (int)mask && t < hrows ? hist[t * hstride + blk] : 0u;
     const int tile0 = blk * kTile;
     const int base = tile0 + wave * 64 * kItems;
     uint32_t key[kItems], val[kItems], rank[kItems];
@@ -870,9 +873,19 @@ struct BucketEmit {
     const uint32_t* depth_key;  // stall fallback: the entries of all Gaussians in lower buckets
     const uint2* rect;
     int P;
+    // the super-tile pass's [super-tile][block] histogram (null: not counted here), blocks of
+    // kSuperHistBlock entry positions, row stride hstride; zero at launch (the MSD histogram
+    // launch clears it)
+    uint32_t* shist;
+    int hstride;
+    int supers;
 };
+static_assert(kSuperHistBlock == 4 * kRadixThreads, "super-tile pass blocks: k_radix_scatter<4> tiles");
 
-__device__ __forceinline__ void emit_entries(const BucketEmit& em, uint32_t o, uint32_t g, uint2 rc)
+// Writes Gaussian g's entries from position o and counts them into the super-tile histogram:
+// hl (LDS, [super-tile][block - b0], nbl blocks) or, without it, straight into em.shist.
+__device__ __forceinline__ void emit_entries(const BucketEmit& em, uint32_t o, uint32_t g, uint2 rc,
+                                             uint32_t* hl = nullptr, uint32_t b0 = 0, int nbl = 0)
 {
     if (rc.x == rc.y) return;  // culled: no entries
     int sx0, sy0, sx1, sy1;
@@ -881,6 +894,12 @@ __device__ __forceinline__ void emit_entries(const BucketEmit& em, uint32_t o, u
         for (int x = sx0; x < sx1; x++) {
             em.keys[o] = entry_key(rc, x, y, em.sgx);
             em.vals[o] = g;
+            const int sid = y * em.sgx + x;
+            const uint32_t blk = o / kSuperHistBlock;
+            if (hl)
+                atomicAdd(&hl[sid * nbl + (int)(blk - b0)], 1u);
+            else if (em.shist)
+                atomicAdd(&em.shist[(size_t)sid * em.hstride + blk], 1u);
             o++;
         }
 }
@@ -1142,10 +1161,27 @@ void k_depth_bucket_sort(
         publish_bucket_total(em, d, tot);
         const uint32_t ebase = bucket_entry_base(em, d, kxf, L.wsum);
         if ((uint64_t)ebase + tot > (uint64_t)em.cap) return;  // over capacity: the host re-runs unfused
+        // the bucket's entries [ebase, ebase + tot) meet nbl blocks of the super-tile pass: their
+        // [super-tile][block] counts in LDS (the free buffer S), then one atomic per non-zero count
+        // (blocks at the bucket's ends are shared with its neighbours)
+        const uint32_t b0 = ebase / kSuperHistBlock;
+        const int nbl = tot ? (int)((ebase + tot - 1) / kSuperHistBlock - b0) + 1 : 0;
+        uint32_t* hl = em.shist && tot && nbl * em.supers <= kBucketCap ? S : nullptr;
+        if (hl) {
+            for (int i = t; i < nbl * em.supers; i += kBucketThreads) hl[i] = 0u;
+            __syncthreads();
+        }
 #pragma unroll
         for (int r = 0; r < kBucketRounds; r++) {
             const int i = t + r * kBucketThreads;
-            if (i < nb) emit_entries(em, ebase + X[i], id[r], rc[r]);
+            if (i < nb) emit_entries(em, ebase + X[i], id[r], rc[r], hl, b0, nbl);
+        }
+        if (hl) {
+            __syncthreads();
+            for (int i = t; i < nbl * em.supers; i += kBucketThreads) {
+                const uint32_t v = hl[i];
+                if (v) atomicAdd(&em.shist[(size_t)(i / nbl) * em.hstride + b0 + (uint32_t)(i % nbl)], v);
+            }
         }
         return;
     }
@@ -1258,12 +1294,19 @@ hipError_t launch_depth_order(int P, int passes, const Layout& L, char* geom, ui
         }();
         const bool small = radix_small(P);
         const int nblk = (P + kRadixThreads * (small ? 4 : 16) - 1) / (kRadixThreads * (small ? 4 : 16));
+        // the super-tile histogram the bucket sort counts into, and its scan's status words
+        const bool shist_on = fused_emit && L.super_hist_words > 0;
+        const ZeroList zmsd = shist_on
+            ? ZeroList{{reinterpret_cast<uint32_t*>(geom + L.super_hist), reinterpret_cast<uint32_t*>(geom + L.super_hist_status),
+                        nullptr, nullptr},
+                       {(int)L.super_hist_words, (int)L.super_hist_status_words, 0, 0}}
+            : ZeroList{};
         if (small)
             hipLaunchKernelGGL(k_radix_hist<4>, dim3(nblk), dim3(kRadixThreads), 0, s, keys, P, 0, 8, hist, nblk, kxf,
-                               remap, 1, ZeroList{}, DevCount{nullptr, nullptr});
+                               remap, 1, zmsd, DevCount{nullptr, nullptr});
         else
             hipLaunchKernelGGL(k_radix_hist<16>, dim3(nblk), dim3(kRadixThreads), 0, s, keys, P, 0, 8, hist, nblk, kxf,
-                               remap, 1, ZeroList{}, DevCount{nullptr, nullptr});
+                               remap, 1, zmsd, DevCount{nullptr, nullptr});
         if ((e = post(debug, s)) != hipSuccess) return e;
         if ((e = scan_exclusive(hist, hist_scan, 256 * nblk, regions, nullptr, stall, s, debug)) != hipSuccess)
             return e;
@@ -1292,6 +1335,9 @@ hipError_t launch_depth_order(int P, int passes, const Layout& L, char* geom, ui
             em.depth_key = keys;
             em.rect = tail.rect;
             em.P = P;
+            em.shist = shist_on ? reinterpret_cast<uint32_t*>(geom + L.super_hist) : nullptr;
+            em.hstride = L.super_hist_stride;
+            em.supers = L.supers;
         }
         hipLaunchKernelGGL(k_depth_bucket_sort, dim3(256), dim3(kBucketThreads), kBucketLdsBytes, s, P, kb, vb,
                            (const uint32_t*)hist_scan, nblk, kxf, tail.rect, va, tail.rect_ranked, off,
@@ -1456,19 +1502,51 @@ __device__ __forceinline__ bool block_segment_ctx(int S, int sgx, const uint32_t
                                                   const uint32_t* __restrict__ col_prefix, SegmentCtx* out)
 {
     __shared__ uint32_t sh[5];
-    const uint32_t b = blockIdx.x;
+    // XCD-aware segment order (xcd_tile): consecutive segments of a super-tile write adjacent runs of
+    // the same tile lists, so they are given to workgroups of one XCD, whose L2 then assembles the
+    // shared point_list lines (instead of 8 L2s each writing back partial lines).  Over the segments
+    // that exist (seg_base[S], read in the same round trip as the lookup), not the grid, whose
+    // capacity-mode size exceeds them.
+    const uint32_t nseg_all = seg_base[S];
+    constexpr int kMaxPer = 4;  // intervals per thread, loaded before the block index is known
+    uint32_t lo[kMaxPer], hi[kMaxPer], cp[kMaxPer];
+    uint2 rr[kMaxPer];
+#pragma unroll
+    for (int k = 0; k < kMaxPer; k++) {
+        const int s = threadIdx.x + k * blockDim.x;
+        if (s < S) {
+            lo[k] = seg_base[s];
+            hi[k] = seg_base[s + 1];
+            rr[k] = sranges[s];
+            cp[k] = col_prefix[s];
+        }
+    }
     if (threadIdx.x == 0) sh[0] = 0xFFFFFFFFu;
     __syncthreads();
-    for (int s = threadIdx.x; s < S; s += blockDim.x) {
-        const uint32_t lo = seg_base[s], hi = seg_base[s + 1];
-        const uint2 r = sranges[s];
-        const uint32_t cp = col_prefix[s];
-        if (lo <= b && b < hi) {
+    if (blockIdx.x >= nseg_all) return false;  // block-uniform
+    const int i = (int)blockIdx.x, n = (int)nseg_all;
+    const int x = i & 7, q = n >> 3, r = n & 7;  // as xcd_tile: XCD x takes [x q + min(x, r), ...)
+    const uint32_t b = (uint32_t)(x * q + min(x, r) + (i >> 3));
+#pragma unroll
+    for (int k = 0; k < kMaxPer; k++) {
+        const int s = threadIdx.x + k * blockDim.x;
+        if (s < S && lo[k] <= b && b < hi[k]) {
             sh[0] = (uint32_t)s;
-            sh[1] = b - lo;
-            sh[2] = r.x;
-            sh[3] = r.y;
-            sh[4] = cp;
+            sh[1] = b - lo[k];
+            sh[2] = rr[k].x;
+            sh[3] = rr[k].y;
+            sh[4] = cp[k];
+        }
+    }
+    for (int s = threadIdx.x + kMaxPer * blockDim.x; s < S; s += blockDim.x) {  // beyond 1024 super-tiles
+        const uint32_t l = seg_base[s], h = seg_base[s + 1];
+        if (l <= b && b < h) {
+            const uint2 rs = sranges[s];
+            sh[0] = (uint32_t)s;
+            sh[1] = b - l;
+            sh[2] = rs.x;
+            sh[3] = rs.y;
+            sh[4] = col_prefix[s];
         }
     }
     __syncthreads();
@@ -1478,10 +1556,10 @@ __device__ __forceinline__ bool block_segment_ctx(int S, int sgx, const uint32_t
     c.seg = (int)sh[1];
     c.ox = (c.s % sgx) * kSuper;
     c.oy = (c.s / sgx) * kSuper;
-    const uint2 r = make_uint2(sh[2], sh[3]);
-    c.e0 = r.x + (uint32_t)c.seg * kSegEntries;
-    c.e1 = min(r.y, c.e0 + (uint32_t)kSegEntries);
-    c.nseg = super_segments(r);
+    const uint2 rg = make_uint2(sh[2], sh[3]);
+    c.e0 = rg.x + (uint32_t)c.seg * kSegEntries;
+    c.e1 = min(rg.y, c.e0 + (uint32_t)kSegEntries);
+    c.nseg = super_segments(rg);
     c.colpre = sh[4];
     return true;
 }
@@ -1600,7 +1678,11 @@ __global__ __launch_bounds__(256) void k_bin_count_fused(int S, int sgx, int sgy
     __syncthreads();
     // this workgroup's (super-tile, segment): the s with sbase[s] <= b < sbase[s + 1]
     {
-        const uint32_t b = blockIdx.x;
+        // XCD-aware segment order, as k_bin_emit (block_segment_ctx): adjacent count-table words
+        // are written by one XCD
+        const int i = (int)blockIdx.x, n = (int)sbase[S];
+        const int x = i & 7, q = n >> 3, r = n & 7;
+        const uint32_t b = i < n ? (uint32_t)(x * q + min(x, r) + (i >> 3)) : (uint32_t)i;
         if (t < S && sbase[t] <= b && b < sbase[t + 1]) {
             sh[0] = t;
             sh[1] = (int)(b - sbase[t]);
@@ -1806,21 +1888,47 @@ hipError_t launch_binning(int P, int64_t R, const Layout& L, char* geom, char* i
     }
     int passes = 0;
     uint32_t* bin_hist_scan = reinterpret_cast<uint32_t*>(binning + L.bin_radix_hist_scan);
-    e = radix_sort(k0, v0, (int)E, L.super_bits, kA, vA, kB, vB, reinterpret_cast<uint32_t*>(binning + L.bin_radix_hist),
-                   bin_hist_scan, regions, L.scan_region_bin, stall, s, debug, &passes, nullptr,
-                   ScatterTail{nullptr, nullptr, nullptr}, emitted ? zero : ZeroList{}, dc);
-    if (e != hipSuccess) return e;
+    int hist_stride = 0, hist_rows = 1 << L.super_bits;  // of the scanned histogram count_fused reads
+    if (emitted && L.super_hist_words > 0) {
+        // the bucket sort counted the super-tile pass's [super-tile][block] histogram as it emitted
+        // (blocks of kSuperHistBlock entries): no histogram launch; the scatter clears the tables
+        // the later kernels need cleared
+        bin_hist_scan = reinterpret_cast<uint32_t*>(geom + L.super_hist_scan);
+        if ((e = scan_exclusive(reinterpret_cast<const uint32_t*>(geom + L.super_hist), bin_hist_scan,
+                                (int)L.super_hist_words, reinterpret_cast<uint32_t*>(geom + L.super_hist_status),
+                                nullptr, stall, s, debug)) != hipSuccess)
+            return e;
+        static const int remap = [] {
+            const char* v = getenv("LSR_XCD_REMAP");
+            return v && v[0] == '0' ? 0 : 1;
+        }();
+        const int nblk = (int)((E + kSuperHistBlock - 1) / kSuperHistBlock);
+        hipLaunchKernelGGL((k_radix_scatter<4, false>), dim3(nblk), dim3(kRadixThreads), 0, s, k0, v0, (int)E, 0,
+                           L.super_bits, (const uint32_t*)bin_hist_scan, nblk, kB, vB, (const uint32_t*)nullptr,
+                           ScatterTail{nullptr, nullptr, nullptr}, remap, 0, dc, L.super_hist_stride, L.supers, zero);
+        if ((e = post(debug, s)) != hipSuccess) return e;
+        passes = 1;
+        hist_stride = L.super_hist_stride;
+        hist_rows = L.supers;
+    } else {
+        e = radix_sort(k0, v0, (int)E, L.super_bits, kA, vA, kB, vB, reinterpret_cast<uint32_t*>(binning + L.bin_radix_hist),
+                       bin_hist_scan, regions, L.scan_region_bin, stall, s, debug, &passes, nullptr,
+                       ScatterTail{nullptr, nullptr, nullptr}, emitted ? zero : ZeroList{}, dc);
+        if (e != hipSuccess) return e;
+        if (passes == 1) {
+            const int tile = kRadixThreads * (radix_small(E) ? 4 : 16);
+            hist_stride = (int)((E + tile - 1) / tile);
+        }
+    }
     const uint32_t* skeys = (passes & 1) ? kB : kA;
     const uint32_t* svals = (passes & 1) ? vB : vA;
     const unsigned grid = (unsigned)L.seg_blocks;
     if (passes == 1 && L.supers <= kFusedSupers) {
-        // one pass: the scanned histogram of that pass holds the super-tile ranges (radix_sort's
-        // layout: [digit][block], nblk blocks of its tile size, 1 << super_bits digits)
-        const int tile = kRadixThreads * (radix_small(E) ? 4 : 16);
-        const int nblk = (int)((E + tile - 1) / tile);
-        hipLaunchKernelGGL(k_bin_count_fused, dim3(grid), dim3(256), 0, s, L.supers, L.sgx, L.sgy, L.gx, L.gy, nblk,
-                           1 << L.super_bits, E, (const uint32_t*)bin_hist_scan, sranges,
-                           seg_base, colpre, rowpre, skeys, table, dc);
+        // one pass: the scanned histogram of that pass holds the super-tile ranges (layout
+        // [digit][block], hist_stride blocks per digit row, hist_rows rows)
+        hipLaunchKernelGGL(k_bin_count_fused, dim3(grid), dim3(256), 0, s, L.supers, L.sgx, L.sgy, L.gx, L.gy,
+                           hist_stride, hist_rows, E, (const uint32_t*)bin_hist_scan, sranges, seg_base, colpre, rowpre,
+                           skeys, table, dc);
         if ((e = post(debug, s)) != hipSuccess) return e;
     } else {
         hipLaunchKernelGGL(k_super_ranges, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, s, E, skeys, sranges, dc);

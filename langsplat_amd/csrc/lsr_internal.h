@@ -43,6 +43,7 @@ constexpr int kSegEntries = 512;   // super-tile list entries per binning workgr
 constexpr int kGradStride = 16;                          // floats per Gaussian grad record
 constexpr int kGradStrideLang = 5;  // without geometry gradients: {dxy, dlang}, packed 20-B records
 constexpr int kFusedEntries = 3;    // capacity of the fused super-tile emission, entries per Gaussian
+constexpr int kSuperHistBlock = 1024;  // entries per block of the super-tile pass (k_radix_scatter<4>)
 
 size_t radix_hist_words(int64_t n);   // per-block digit histograms for n keys
 size_t scan_region_words(int64_t n);  // look-back status + ticket of one scan of n words
@@ -60,6 +61,12 @@ struct Layout {
                               // + the bucket ticket, inside the range preprocess clears
     size_t fused_keys, fused_vals;  // the super-tile entries the bucket sort emits (fused_cap each)
     int64_t fused_cap;
+    // with fused emission and <= 256 super-tiles: the super-tile radix pass's [super-tile][block]
+    // histogram (blocks of kSuperHistBlock entries, row stride super_hist_stride), counted by the
+    // bucket sort as it emits; its scan and that scan's status words
+    size_t super_hist, super_hist_scan, super_hist_status;
+    size_t super_hist_words, super_hist_status_words;
+    int super_hist_stride;
     size_t grad_records;      // P x kGradStrideLang floats: the language step's gradient records (cleared
                               // by the render forward under LSR_FWD_ZERO_GRAD_RECORDS)
     size_t geom_bytes;
@@ -110,6 +117,17 @@ inline Layout make_layout(int P, int W, int H, int64_t R, int64_t E)
     L.rect_ranked = take(8 * p);
     L.grad_records = take(4 * kGradStrideLang * p + 16);  // + padding: cleared as whole float4s
     L.bucket_totals = take(4 * 256);
+    {
+        const int gx = (W + kTile - 1) / kTile, gy = (H + kTile - 1) / kTile;
+        const int supers = ((gx + kSuper - 1) / kSuper) * ((gy + kSuper - 1) / kSuper);
+        const int64_t cap = (int64_t)kFusedEntries * (int64_t)p;
+        L.super_hist_stride = (int)((cap + kSuperHistBlock - 1) / kSuperHistBlock);
+        L.super_hist_words = supers <= 256 ? (size_t)supers * (size_t)L.super_hist_stride : 0;
+        L.super_hist_status_words = L.super_hist_words ? scan_region_words((int64_t)L.super_hist_words) : 0;
+        L.super_hist = take(4 * L.super_hist_words);
+        L.super_hist_scan = take(4 * L.super_hist_words);
+        L.super_hist_status = take(4 * L.super_hist_status_words);
+    }
     // E is ~1.5 per visible Gaussian at 1080p; a view with more than kFusedEntries per Gaussian
     // falls back to k_emit_super after the host wait
     L.fused_cap = (int64_t)kFusedEntries * (int64_t)p;

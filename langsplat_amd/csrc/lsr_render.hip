@@ -1128,7 +1128,6 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
     int px, py;
     pixel_map(tx, ty, t, px, py);
     const float pfx = (float)px, pfy = (float)py;
-    const float tx0 = (float)(tx * kTile), ty0 = (float)(ty * kTile);
     const size_t HW = (size_t)p.W * p.H;
     const uint32_t start = p.ranges[tile].x;
 
