@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define LSR_ABI_VERSION 8
+#define LSR_ABI_VERSION 9
 
 enum lsr_status {
     LSR_OK = 0,
@@ -150,6 +150,15 @@ typedef struct lsr_forward_args {
     int32_t* overflow;               /* device int32 or NULL */
     int64_t* out_num_entries;        /* HOST pointer or NULL: the super-tile entry count (not in
                                         capacity mode), the capacity_entries a later call needs */
+    /* Deferred language feature (the gradient all-reduce overlap).  NULL: off.
+     * Otherwise a hipEvent_t: the preprocess, depth order and binning run without reading
+     * language_feature, and the stream waits for this event only before a small kernel copies
+     * (raw: activates) language_feature into the per-Gaussian records and the compositing starts.
+     * A trainer records the event after the previous step's all-reduce and optimiser update of the
+     * language feature on another stream, so that update overlaps this view's geometry work
+     * (langsplat_amd.distributed.UpdateOverlap).  Results are identical to a call without it.  Not
+     * with capacity mode (LSR_ERR_INVALID). */
+    void* language_ready;
 } lsr_forward_args;
 
 /* Inputs/outputs of _C.rasterize_gaussians_backward.  Every non-NULL output is fully written
@@ -330,10 +339,11 @@ int32_t lsr_adam_step(int64_t n, float* param, const float* grad, float* exp_avg
  * scene/gaussian_model.py:219-226, each with its own lr, betas, eps and step count, i.e. torch's
  * per-parameter state).  Every gradient is multiplied by grad_scale first (e.g. the 1 / N of a
  * gradient all-reduced as a SUM over N ranks; 1 = none).
- * step_dev (device int64, with ticket: a device uint32 that is 0) replaces the tensors' step fields
- * for a step replayed from a HIP graph: the launch uses step *step_dev + 1 for every tensor and
- * stores it back (the launch's last workgroup), so each replay advances the count on the device;
- * at most 16 tensors then.  NULL: the host's step counts. */
+ * step_dev (device int64) replaces the tensors' step fields for a step replayed from a HIP graph:
+ * a one-thread kernel first advances *step_dev by one, and the update uses that step for every
+ * tensor, so each replay advances the count on the device; at most 16 tensors then.  `ticket` (a
+ * device uint32 that is 0, or NULL) serves only the measurement variant LSR_ADAM_ADVANCE=0, where
+ * the launch's last workgroup stores the step instead.  step_dev NULL: the host's step counts. */
 typedef struct lsr_adam_tensor {
     int64_t n;
     float* param;

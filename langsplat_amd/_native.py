@@ -22,7 +22,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LSR_LIB") or os.path.join(_HERE, "liblsr.so")
 
 LSR_BUF_GEOM, LSR_BUF_BINNING, LSR_BUF_IMAGE, LSR_BUF_BACKWARD = 0, 1, 2, 3
-ABI_VERSION = 8
+ABI_VERSION = 9
 # lsr_raw_flags (include/lsr.h): inputs are GaussianModel's raw parameters
 RAW_OPACITY, RAW_SCALES, RAW_ROTATIONS, RAW_LANGUAGE = 1, 2, 4, 8
 FWD_ZERO_GRAD_RECORDS = 1  # lsr_forward_flags
@@ -55,7 +55,8 @@ class LsrForwardArgs(ctypes.Structure):
                            "rotations", "cov3D_precomp", "out_color", "out_language_feature", "radii")
     ] + [("raw", ctypes.c_int32), ("flags", ctypes.c_int32), ("shs_rest", _vp), ("visible", _vp),
          ("loss_target", _vp), ("loss_mask", _vp), ("out_loss", _vp), ("capacity_rendered", ctypes.c_int64),
-         ("capacity_entries", ctypes.c_int64), ("overflow", _vp), ("out_num_entries", ctypes.POINTER(ctypes.c_int64))]
+         ("capacity_entries", ctypes.c_int64), ("overflow", _vp), ("out_num_entries", ctypes.POINTER(ctypes.c_int64)),
+         ("language_ready", _vp)]
 
 
 class LsrBackwardArgs(ctypes.Structure):
@@ -260,6 +261,31 @@ class capacity:
         capacity._tls.cur = self._prev
 
 
+class language_ready:
+    """Within the block, the rasterizer forwards of this thread defer the language feature
+    (include/lsr.h lsr_forward_args.language_ready): preprocess, depth order and binning run at
+    once, and the stream waits for `event` (a torch.cuda.Event recorded after the language feature's
+    last update, on any stream) only before the feature enters the records and the compositing
+    starts.  event None: off (the block is a no-op)."""
+
+    _tls = threading.local()
+
+    def __init__(self, event):
+        self.event = event
+
+    @staticmethod
+    def active():
+        return getattr(language_ready._tls, "cur", None)
+
+    def __enter__(self):
+        self._prev = language_ready.active()
+        language_ready._tls.cur = self.event
+        return self
+
+    def __exit__(self, *exc):
+        language_ready._tls.cur = self._prev
+
+
 # (P, W, H) -> (tile instances, super-tile entries) of this thread's last forward outside capacity mode
 # (the capacities a later capture needs)
 LAST_COUNTS: Dict[tuple, tuple] = {}
@@ -379,6 +405,12 @@ def rasterize_gaussians(rs, means3D, shs, colors_precomp, language_feature, opac
         a.out_loss = _ptr(out_loss)
     cap = capacity.active()
     entries = ctypes.c_int64(0)
+    ready = language_ready.active()
+    if ready is not None and language_feature is not None:
+        if cap is not None:
+            raise ValueError("language_ready cannot be combined with capacity mode")
+        a.language_ready = ready.cuda_event
+        keep.append(ready)
     if cap is not None:
         a.capacity_rendered = cap.rendered
         a.capacity_entries = cap.entries

@@ -442,6 +442,9 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
     pp.raw = a->raw;
     pp.shs_rest = a->shs_rest;
     pp.partial = reinterpret_cast<uint4*>(geom + L.pre_partial);
+    // deferred language feature: geometry first, the feature after the caller's event
+    const bool deferred = a->language_ready && s->include_feature && a->language_feature;
+    pp.lang_deferred = deferred ? 1 : 0;
     LSR_TRY(launch_preprocess(pp, stream), "preprocess");
     hm.mark();
 
@@ -454,6 +457,7 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
     const uint32_t fwd_flags = ((a->flags & LSR_FWD_ZERO_GRAD_RECORDS) ? kFwdZeroedRecords : 0u) |
                                ((a->out_loss && s->include_feature && a->language_feature) ? kFwdFusedLoss : 0u);
     if (a->capacity_rendered > 0) {
+        if (deferred) return fail(LSR_ERR_INVALID, "lsr_forward: language_ready with capacity mode");
         // Capacity mode: nothing waits for the device.  The counters stay on the device, the binning's
         // grids and buffers come from the capacities and its kernels read the true counts; a view over
         // capacity sets counters[kCntOverflow] (and *overflow) and is not binned.
@@ -535,6 +539,12 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
     hb->hint_H = H;
     hb->binning_hint = L.binning_bytes + L.binning_bytes / 8;  // 12.5 % headroom for the next view
     LSR_TRY(launch_binning(P, R, L, geom, image, binning, &hb->stall, stream, debug, emitted), "binning");
+    if (deferred) {  // the feature's update (another stream) has overlapped everything above
+        LSR_TRY(hipStreamWaitEvent(stream, static_cast<hipEvent_t>(a->language_ready), 0), "wait language_ready");
+        LSR_TRY(launch_fill_language(P, a->language_feature, a->raw, a->radii, reinterpret_cast<float4*>(geom + L.record),
+                                     stream),
+                "fill language");
+    }
     hm.mark();
     const int32_t rc = render_forward_and_finish(s, a, L, geom, image, binning, hb, stream, debug);
     hm.mark();

@@ -375,15 +375,50 @@ __device__ __forceinline__ int xcd_tile(int nblk, int remap)
     return x * q + min(x, r) + (i >> 3);
 }
 
-// MSD depth sort (launch_depth_order, P <= kMsdMaxKeys): the pass sorts on the TOP <= 8 bits the
-// visible keys span -- read on the device from kxf (min / max visible key) -- so no host value is
-// needed: bits = bit length of (max - min), digit = (key_xf >> max(bits - 8, 0)) & 0xFF.
-__device__ __forceinline__ void msd_digit(const uint32_t* kxf, int& shift, int& nbits)
+// MSD depth sort (launch_depth_order, P <= kMsdMaxKeys): one radix pass splits the keys into 256
+// buckets by a monotone function of the key, read on the device from kxf (min / max visible key),
+// so no host value is needed; each bucket then sorts its keys on their own range.  The key is the
+// depth's float bits, and two bucket maps are used:
+//   - a narrow depth range (max <= kMsdLinearRatio min): 256 buckets of EQUAL DEPTH WIDTH,
+//     bucket = min(255, (depth - dmin) 256 / w) (a float subtraction, a multiplication by a
+//     positive constant and a truncation are each monotone);
+//   - a wide one: the top 8 bits of key - min, i.e. equal KEY intervals, which are logarithmic in
+//     depth (every float octave gets the same share).
+// Equal key intervals alone (round 2) double their depth width at every float exponent step: at C3
+// (depths 3..5) the keys of [4, 5) fell into half as many buckets as those of [3, 4), 64 buckets
+// held ~8k keys, 120 ~3k and 64 none, and the 8k buckets set the bucket kernel's span (equal depth
+// widths: 3.7k..4.1k per bucket).  Over a wide range depth counts fall off with distance, where
+// logarithmic buckets stay even.  Culled keys (key_xf: max - min) land in the last bucket.
+constexpr float kMsdLinearRatio = 2.5f;
+
+struct MsdMap {
+    uint32_t kmin;
+    float dmin, scale;
+    int shift;
+    bool linear;
+};
+
+__device__ __forceinline__ MsdMap msd_map(const uint32_t* kxf)
 {
+    MsdMap m;
+    m.kmin = kxf[0];
+    m.dmin = __uint_as_float(kxf[0]);
+    const float dmax = __uint_as_float(kxf[1]);
+    const float w = dmax - m.dmin;
+    m.linear = m.dmin > 0.0f && dmax <= kMsdLinearRatio * m.dmin;  // false when none is visible
+    m.scale = w > 1e-30f ? 256.0f / w : 0.0f;
     const uint32_t span = kxf[1] - kxf[0];
     const int bits = span ? 32 - __clz(span) : 0;
-    shift = bits > 8 ? bits - 8 : 0;
-    nbits = bits - shift;
+    m.shift = bits > 8 ? bits - 8 : 0;
+    return m;
+}
+
+// bucket of a transformed key kx = key_xf(key)
+__device__ __forceinline__ uint32_t msd_bucket(uint32_t kx, const MsdMap& m)
+{
+    if (!m.linear) return (kx >> m.shift) & 0xFFu;
+    const float v = (__uint_as_float(kx + m.kmin) - m.dmin) * m.scale;
+    return (uint32_t)min(255, max(0, (int)v));
 }
 
 // Word ranges a kernel clears with grid-stride stores besides its own work (n = 0: none).  The
@@ -414,7 +449,12 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_hist(const uint32_t* __
     zero_words_strided(zero);
     if (dc.abort && *dc.abort) return;
     if (dc.n) n = min(n, (int)*dc.n);
-    if (msd) msd_digit(kxf, shift, nbits);
+    MsdMap mm{};
+    if (msd) {
+        mm = msd_map(kxf);
+        shift = 0;
+        nbits = 8;
+    }
     const int blk = xcd_tile(nblk, remap);
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
     const uint32_t mask = (1u << nbits) - 1u;
@@ -430,7 +470,7 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_hist(const uint32_t* __
         valid[it] = idx < n;
         uint32_t k = valid[it] ? keys[idx] : 0u;
         if (kxf) k = key_xf(k, kxf);
-        d[it] = valid[it] ? (k >> shift) & mask : 0u;
+        d[it] = valid[it] ? (msd ? msd_bucket(k, mm) : (k >> shift) & mask) : 0u;
     }
 #pragma unroll
     for (int it = 0; it < kItems; it++) {
@@ -465,7 +505,13 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_scatter(
     if (dc.abort && *dc.abort) return;
     if (hstride == 0) hstride = nblk;  // histogram rows of nblk blocks (the hist kernel's layout)
     if (dc.n) n = min(n, (int)*dc.n);
-    if (msd) msd_digit(kxf, shift, nbits);
+    MsdMap mm{};
+    if (msd) {
+        mm = msd_map(kxf);
+        shift = 0;
+        nbits = 8;
+    }
+    auto digit_of = [&](uint32_t k) { return msd ? msd_bucket(k, mm) : (k >> shift) & ((1u << nbits) - 1u); };
     const int blk = xcd_tile(nblk, remap);
     constexpr int kTile = kRadixThreads * kItems;
     constexpr int kWaves = kRadixThreads / 64;
@@ -498,7 +544,7 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_scatter(
 #pragma unroll
     for (int it = 0; it < kItems; it++) {
         const bool valid = base + it * 64 + lane < n;
-        const uint32_t d = (key[it] >> shift) & mask;
+        const uint32_t d = digit_of(key[it]);
         const uint64_t peers = match_digit(d, valid, nbits);
         const uint32_t r = (uint32_t)__popcll(peers & lanemask_lt());
         const uint32_t c = wcnt[wave][d];
@@ -531,7 +577,7 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_scatter(
 #pragma unroll
     for (int it = 0; it < kItems; it++) {
         if (base + it * 64 + lane < n) {
-            const uint32_t d = (key[it] >> shift) & mask;
+            const uint32_t d = digit_of(key[it]);
             const uint32_t pos = dstart[d] + wcnt[wave][d] + rank[it];
             sk[pos] = key[it];
             sv[pos] = val[it];
@@ -543,7 +589,7 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_scatter(
     if (kCarry || !tail.rect) {
         for (int i = t; i < cnt; i += kRadixThreads) {
             const uint32_t k = sk[i];
-            const uint32_t d = (k >> shift) & mask;
+            const uint32_t d = digit_of(k);
             const uint32_t o = gbase[d] + (uint32_t)i - dstart[d];
             keys_out[o] = k;
             vals_out[o] = sv[i];
@@ -559,7 +605,7 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_scatter(
         const int i = t + it * kRadixThreads;
         outp[it] = 0xFFFFFFFFu;
         if (i < cnt) {
-            const uint32_t d = (sk[i] >> shift) & mask;
+            const uint32_t d = digit_of(sk[i]);
             outp[it] = gbase[d] + (uint32_t)i - dstart[d];
             vid[it] = sv[i];
         }
@@ -940,13 +986,11 @@ __device__ uint32_t bucket_entry_base(const BucketEmit& em, int d, const uint32_
     }
     __syncthreads();
     if (s_ok) return s_base;
-    // stalled: the entries of every Gaussian whose top digit is below d, from the inputs
-    int shift, nbits;
-    msd_digit(kxf, shift, nbits);
-    const uint32_t mask = (1u << nbits) - 1u;
+    // stalled: the entries of every Gaussian whose bucket is below d, from the inputs
+    const MsdMap mm = msd_map(kxf);
     uint32_t part = 0;
     for (int g = t; g < em.P; g += kBucketThreads)
-        if (((key_xf(em.depth_key[g], kxf) >> shift) & mask) < (uint32_t)d) part += super_count(em.rect[g]);
+        if (msd_bucket(key_xf(em.depth_key[g], kxf), mm) < (uint32_t)d) part += super_count(em.rect[g]);
     uint32_t tot;
     scan1024(part, wsum, &tot);
     if (t == 0) note_stall(em.stall);
@@ -1012,36 +1056,66 @@ void k_depth_bucket_sort(
         __syncthreads();
         d = s_d;
     }
-    // bucket range: both scanned starts are loaded (in bounds: the histogram has 256 digit rows)
-    // together with the width (kxf), then discarded for digits beyond the width, whose histogram
-    // rows the MSD pass did not write
-    const uint32_t s0 = hist_scan[(size_t)d * nblk];
-    const uint32_t s1 = d < 255 ? hist_scan[(size_t)(d + 1) * nblk] : 0u;
-    int shift, nbits;
-    msd_digit(kxf, shift, nbits);
-    uint32_t start = 0, end = 0;
-    if (d < (1 << nbits)) {
-        start = s0;
-        end = d + 1 < (1 << nbits) ? s1 : (uint32_t)n;
-    }
+    // bucket range from the scanned [bucket][block] histogram
+    const uint32_t start = hist_scan[(size_t)d * nblk];
+    const uint32_t end = d < 255 ? hist_scan[(size_t)(d + 1) * nblk] : (uint32_t)n;
     const int nb = (int)(end - start);
     guard.nb = nb;
-    if (nb <= 0) {  // no such top digit, or no key in it
+    if (nb <= 0) {  // no key in this depth interval
         if (t == 0) totals[d] = 0u;
         publish_bucket_total(em, d, 0u);
         return;
     }
-    const int lowbits = shift;  // the bits below the top digit (equal top digits inside a bucket)
+    // the bucket's own key range [lo, hi]: it sorts key - lo on the bits that span
+    const int w = t >> 6, lane = t & 63;
+    uint32_t kr[kBucketRounds];
+    uint32_t klo = 0xFFFFFFFFu, khi = 0u;
     if (nb <= kBucketCap) {
-        const int w = t >> 6, lane = t & 63;
-        const uint32_t lowmask = lowbits >= 32 ? 0xFFFFFFFFu : ((1u << lowbits) - 1u);
-        uint32_t dig[kBucketRounds], val[kBucketRounds];
-        // pass 0 from registers: the keys in wave-blocked order, digit = key bits 0..7, and the
-        // packed word {key bits 8.., local index} as the value
 #pragma unroll
         for (int r = 0; r < kBucketRounds; r++) {
             const int idx = (w * kBucketRounds + r) * 64 + lane;
-            const uint32_t k = idx < nb ? keys[start + idx] & lowmask : 0u;
+            kr[r] = idx < nb ? keys[start + idx] : 0u;
+            if (idx < nb) {
+                klo = min(klo, kr[r]);
+                khi = max(khi, kr[r]);
+            }
+        }
+    } else {
+        for (int i = t; i < nb; i += kBucketThreads) {
+            const uint32_t k = keys[start + i];
+            klo = min(klo, k);
+            khi = max(khi, k);
+        }
+    }
+    {
+        __shared__ uint32_t s_lo[kBucketWaves], s_hi[kBucketWaves];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            klo = min(klo, (uint32_t)__shfl_xor((int)klo, o, 64));
+            khi = max(khi, (uint32_t)__shfl_xor((int)khi, o, 64));
+        }
+        if (lane == 0) {
+            s_lo[w] = klo;
+            s_hi[w] = khi;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < kBucketWaves; i++) {
+            klo = min(klo, s_lo[i]);
+            khi = max(khi, s_hi[i]);
+        }
+    }
+    const uint32_t span = khi - klo;
+    const int lowbits = span ? 32 - __clz(span) : 0;
+    // the LDS sort packs {key bits 8.., local index} in one word: at most 27 key bits
+    if (nb <= kBucketCap && lowbits <= 32 - kIdxBits + 8) {
+        uint32_t dig[kBucketRounds], val[kBucketRounds];
+        // pass 0 from registers: the keys in wave-blocked order, digit = bits 0..7 of key - lo, and
+        // the packed word {bits 8.., local index} as the value
+#pragma unroll
+        for (int r = 0; r < kBucketRounds; r++) {
+            const int idx = (w * kBucketRounds + r) * 64 + lane;
+            const uint32_t k = idx < nb ? kr[r] - klo : 0u;
             dig[r] = k & 0xFFu;
             val[r] = ((k >> 8) << kIdxBits) | (uint32_t)idx;
         }
@@ -1193,6 +1267,8 @@ void k_depth_bucket_sort(
         scan1024(part, L.wsum, &etot);
         publish_bucket_total(em, d, etot);
     }
+    for (int i = t; i < nb; i += kBucketThreads) keys[start + i] -= klo;  // sort key - lo
+    __syncthreads();
     const int res = bucket_global_sort(L, keys + start, ids + start, scratch_k + start, sorted_ids + start, nb,
                                        lowbits);
     const uint32_t* rid = res ? sorted_ids + start : ids + start;
@@ -1386,9 +1462,7 @@ __global__ __launch_bounds__(256) void k_emit_super(int P, int sgx, const uint32
         o = offset[r];
     }
     if (msd.totals) {  // bucket starts and bases (every workgroup, 256 threads = 256 buckets)
-        int shift, nbits;
-        msd_digit(msd.kxf, shift, nbits);
-        const int t = threadIdx.x, ndig = 1 << nbits;
+        const int t = threadIdx.x, ndig = 256;
         s_start[t] = t < ndig ? msd.hist_scan[(size_t)t * msd.nblk] : (uint32_t)P;
         uint32_t x = msd.totals[t], v = x;
 #pragma unroll

@@ -199,6 +199,7 @@ struct PreprocessParams {
     int raw;                  // lsr_raw_flags
     const float* shs_rest;    // split SH rows (shs = dc only) or null
     uint8_t* visible;         // optional radii > 0 bytes
+    int lang_deferred;        // the records' language slots are filled later (launch_fill_language)
 };
 
 struct PreprocessBwdParams {
@@ -252,6 +253,9 @@ struct RenderParams {
 };
 
 hipError_t launch_preprocess(const PreprocessParams& p, hipStream_t s);
+// the language slots of the visible Gaussians' records (after a deferred preprocess)
+hipError_t launch_fill_language(int P, const float* lang, int raw, const int32_t* radii, float4* record,
+                                hipStream_t s);
 hipError_t launch_preprocess_backward(const PreprocessBwdParams& p, hipStream_t s);
 hipError_t launch_grad_epilogue(int P, const int* radii, const float* grad, int stride, const float* lang,
                                 int raw_lang, float* dmeans2D, float* dlang, hipStream_t s);

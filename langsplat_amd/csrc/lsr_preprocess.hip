@@ -214,9 +214,11 @@ __global__ __launch_bounds__(kPreThreads) __attribute__((amdgpu_waves_per_eu(
         sy = at(p.scales, o3)[1];
         sz = at(p.scales, o3)[2];
         opac = at(p.opac, ic * 4u)[0];
-        f0 = at(p.lang, o3)[0];
-        f1 = at(p.lang, o3)[1];
-        f2 = at(p.lang, o3)[2];
+        if (!p.lang_deferred) {  // kernel-uniform
+            f0 = at(p.lang, o3)[0];
+            f1 = at(p.lang, o3)[1];
+            f2 = at(p.lang, o3)[2];
+        }
         dc[0] = at(p.shs, o3)[0];
         dc[1] = at(p.shs, o3)[1];
         dc[2] = at(p.shs, o3)[2];
@@ -252,7 +254,7 @@ __global__ __launch_bounds__(kPreThreads) __attribute__((amdgpu_waves_per_eu(
             sz = at(p.scales, o3)[2];
         }
         opac = at(p.opac, 4u * (uint32_t)i)[0];
-        if (feat) {
+        if (feat && !p.lang_deferred) {
             f0 = at(p.lang, o3)[0];
             f1 = at(p.lang, o3)[1];
             f2 = at(p.lang, o3)[2];
@@ -344,7 +346,7 @@ __global__ __launch_bounds__(kPreThreads) __attribute__((amdgpu_waves_per_eu(
         rgb[1] = p.colors[3 * i + 1];
         rgb[2] = p.colors[3 * i + 2];
     }
-    if (feat && (p.raw & LSR_RAW_LANGUAGE)) {
+    if (feat && (p.raw & LSR_RAW_LANGUAGE) && !p.lang_deferred) {
         const float3 f = act_lang(f0, f1, f2);
         f0 = f.x;
         f1 = f.y;
@@ -408,6 +410,33 @@ __global__ __launch_bounds__(kPreThreads) __attribute__((amdgpu_waves_per_eu(
     }
 }
 
+
+// Deferred language feature (lsr_forward_args.language_ready): the records' language slots of the
+// visible Gaussians, {b, f0, f1, f2} = record[3 i + 2] with b kept, after the stream has waited for
+// the feature's update.  Same values (and activation) as the preprocess writes otherwise.
+__global__ __launch_bounds__(256) void k_fill_language(int P, const float* __restrict__ lang, int raw,
+                                                       const int32_t* __restrict__ radii, float4* __restrict__ record)
+{
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= P || radii[i] <= 0) return;
+    float f0 = lang[3 * (size_t)i], f1 = lang[3 * (size_t)i + 1], f2 = lang[3 * (size_t)i + 2];
+    if (raw & LSR_RAW_LANGUAGE) {
+        const float3 f = act_lang(f0, f1, f2);
+        f0 = f.x;
+        f1 = f.y;
+        f2 = f.z;
+    }
+    float4* r = record + 3 * (size_t)i + 2;
+    *r = make_float4(r->x, f0, f1, f2);
+}
+
+hipError_t launch_fill_language(int P, const float* lang, int raw, const int32_t* radii, float4* record,
+                                hipStream_t s)
+{
+    if (P == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_fill_language, dim3((P + 255) / 256), dim3(256), 0, s, P, lang, raw, radii, record);
+    return hipGetLastError();
+}
 
 // dynamic LDS beyond the 64 KiB default (M > 20 stored SH coefficients) must be opted into
 static hipError_t allow_lds(const void* fn, size_t bytes)

@@ -170,3 +170,48 @@ class GradBucket:
         if self._max_radii is not None:
             dist.all_reduce(self._max_radii, op=dist.ReduceOp.MAX, group=group)
             self._max_radii = None
+
+
+class UpdateOverlap:
+    """The language step's gradient all-reduce and optimiser update on a side stream, overlapped with
+    the next view's geometry work (SURVEY.md §8e cost model; VERDICT r02 missing item 5).
+
+    In LangSplat's language step (scene/gaussian_model.py:203-217) every geometry parameter is frozen,
+    so the next view's preprocess, depth order and binning -- ~200 us at C3 -- do not depend on the
+    update of the language feature.  `update()` enqueues the all-reduce of the step's gradient
+    (GradBucket, RCCL on the side stream) and `optimizer.step()` behind the main stream's backward,
+    then drops the .grad tensors (zero_grad(set_to_none=True), train.py:138); `forward()` is the
+    context for the next render(): its rasterizer forward runs the geometry stages at once and waits
+    for the update only before the feature enters the records (include/lsr.h
+    lsr_forward_args.language_ready).  Results are identical to the serial step; only the order of
+    independent work changes.  `synchronize()` makes the current stream wait for the last update
+    (before reading the parameters elsewhere, e.g. a checkpoint)."""
+
+    def __init__(self, bucket: "GradBucket", optimizer, device=None):
+        self.bucket = bucket
+        self.optimizer = optimizer
+        self.side = torch.cuda.Stream(device)
+        self.ready = None
+
+    def forward(self):
+        from . import _native
+        return _native.language_ready(self.ready)
+
+    def update(self, average: bool = True):
+        done = torch.cuda.Event()
+        done.record()
+        self.side.wait_event(done)
+        with torch.cuda.stream(self.side):
+            for p in self.bucket.params:
+                if p.grad is not None:
+                    p.grad.record_stream(self.side)  # freed by zero_grad below, still read on the side
+            self.bucket.all_reduce(average=average)
+            self.optimizer.step()
+            ev = torch.cuda.Event()
+            ev.record(self.side)
+        self.optimizer.zero_grad(set_to_none=True)
+        self.ready = ev
+
+    def synchronize(self):
+        if self.ready is not None:
+            torch.cuda.current_stream().wait_event(self.ready)
