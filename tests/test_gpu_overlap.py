@@ -12,7 +12,7 @@ from langsplat_amd.distributed import GradBucket, UpdateOverlap
 from langsplat_amd.optim import Adam
 from tests.scenes import grad_seed, scene, to_device
 from tests.test_gpu_graph import _language_setup
-from tests.test_gpu_parity import state
+from tests.test_gpu_parity import assert_grad_close, state
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -58,7 +58,8 @@ def test_deferred_language_forward_is_identical(raw):
         gc.to(DEV), gl.to(DEV), o[0], o[4], o[5], o[6], raw=raw)
     ga, gb = bw(out), bw(ref)
     for k in ("means2D", "language_feature_precomp", "opacities", "means3D"):
-        assert torch.equal(ga[k], gb[k]), k
+        # the backward's per-Gaussian float atomics land in any order: two runs agree to rounding
+        assert_grad_close(k, ga[k].cpu().numpy(), gb[k].cpu().numpy())
 
 
 def test_deferred_language_rejected_in_capacity_mode():
@@ -75,7 +76,9 @@ def test_deferred_language_rejected_in_capacity_mode():
 
 def test_update_overlap_matches_serial_steps(monkeypatch):
     """Five language steps with UpdateOverlap (update on a side stream, the next forward deferring the
-    feature) leave the parameters and Adam moments bit-identical to five serial steps."""
+    feature) leave the parameters, Adam moments and losses of five serial steps (to the rounding of
+    the backward's float atomics, whose order varies between any two runs: the first loss is
+    identical)."""
     monkeypatch.setenv("LANGSPLAT_AMD_FUSED", "1")
     runs = {}
     for mode in ("serial", "overlap"):
@@ -98,5 +101,9 @@ def test_update_overlap_matches_serial_steps(monkeypatch):
         st = opt.state[m._language_feature]
         runs[mode] = (m._language_feature.detach().clone(), st["exp_avg"].clone(), st["exp_avg_sq"].clone(),
                       torch.stack(losses))
-    for a, b in zip(runs["serial"], runs["overlap"]):
-        assert torch.equal(a, b)
+    (ps, ms, vs, ls), (po, mo, vo, lo) = runs["serial"], runs["overlap"]
+    assert torch.equal(ls[0], lo[0])
+    torch.testing.assert_close(lo, ls, rtol=1e-5, atol=0)
+    torch.testing.assert_close(po, ps, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(mo, ms, rtol=1e-4, atol=1e-9)
+    torch.testing.assert_close(vo, vs, rtol=1e-4, atol=1e-12)

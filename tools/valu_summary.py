@@ -5,8 +5,9 @@ tools/pmc_lds.sh (measurement aid) -> profiles/<tag>_valu.json.
         --lds gpurun_out/<tag>_lds/pmc_counter_collection.csv --out profiles/<tag>_valu.json
 
 valu_per_cu_cycle = SQ_INSTS_VALU / 256 CUs / (GRBM_GUI_ACTIVE / 8 XCDs): wave64 VALU instructions
-issued per CU per cycle; a CU issues at most one (4 SIMDs x one wave64 VALU instruction per 4
-cycles), so this is the VALU-issue fraction of the kernel's span.  lds_utilisation =
+issued per CU per cycle.  The CU's issue peak is ~2 (4 SIMDs x one wave64 VALU instruction per 2
+cycles; tools/valu_peak.hip measures 1.85 for independent v_fma_f32 at 8 waves per SIMD,
+profiles/r03_valu_peak.txt), so the VALU-issue fraction of the kernel's span is this / 2.  lds_utilisation =
 SQ_LDS_IDX_ACTIVE / 256 CUs / (GRBM_GUI_ACTIVE / 8).
 """
 import argparse
