@@ -1,8 +1,9 @@
 """The gradient all-reduce / optimiser overlap of the language step (VERDICT r02 missing
 item 5): the rasterizer forward with a deferred language feature (include/lsr.h
 lsr_forward_args.language_ready) and langsplat_amd.distributed.UpdateOverlap, which runs the update
-on a side stream while the next view's geometry stages run.  Both only reorder independent work, so
-the results must be bit-identical to the serial step."""
+on a side stream while the next view's geometry stages run.  Both only reorder independent work: the
+forward is bit-identical to the serial one, and what follows a backward agrees to the rounding of its
+float atomics (whose order varies between any two runs)."""
 import numpy as np
 import pytest
 import torch
