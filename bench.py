@@ -37,9 +37,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from langsplat_amd import _native  # noqa: E402
-from langsplat_amd.distributed import GradBucket, UpdateOverlap, init_from_env  # noqa: E402
+from langsplat_amd.distributed import GradBucket, init_from_env  # noqa: E402
 from langsplat_amd.graph import GraphedStep  # noqa: E402
 from langsplat_amd.optim import Adam as AmdAdam  # noqa: E402
+from langsplat_amd.pipeline import PipelinedGraphStep, ViewPipeline  # noqa: E402
 from langsplat_amd.render import render  # noqa: E402
 from langsplat_amd.synthetic import CONFIGS, activated_inputs, make_cameras, make_gaussians  # noqa: E402
 
@@ -442,6 +443,36 @@ def main():
     _native.profile_enable(False)
     prof = _native.profile_report()
 
+    # (5) the pipelined form (langsplat_amd.pipeline.ViewPipeline): consecutive steps on two alternating
+    # streams, each forward deferring the language feature until the previous update has landed, so the
+    # next view's geometry stages run beside this view's backward, [all-reduce] and Adam.  Eager launches.
+    elapsed_pipe = float("inf")
+    if fused and os.environ.get("LSR_PIPELINE", "1") != "0":
+        pipe = ViewPipeline(optim, bucket=bucket)
+        optim.zero_grad(set_to_none=True)
+
+        def run_pipe():
+            with pipe.step():
+                loss = render(cam, model, Pipe, bg, Opt, language_target=(gt, mask))["language_l1"]
+                loss.backward()
+                pipe.update()
+            return loss
+        for _ in range(3):
+            run_pipe()
+        pipe.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        tp = time.perf_counter()
+        for _ in range(args.steps):
+            run_pipe()
+        pipe.synchronize()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed_pipe = time.perf_counter() - tp
+        del pipe
+
     # the timed step: render + loss + backward captured once into a HIP graph (langsplat_amd.graph;
     # the rasterizer in capacity mode, no host wait), replayed, then [N > 1: the all-reduce] and Adam
     run = step
@@ -490,33 +521,29 @@ def main():
         run().item()
     torch.cuda.synchronize()
     elapsed_sync = time.perf_counter() - ts
-    # N > 1: the same step with the all-reduce and Adam on a side stream, overlapped with the next
-    # view's geometry work (distributed.UpdateOverlap; the rasterizer defers the language feature,
-    # include/lsr.h language_ready).  Eager launches (the wait on the update sits inside the forward);
-    # `value` is the faster of the two full-step forms, the other is reported beside.
-    elapsed_ov = float("inf")
-    if world > 1 and fused and os.environ.get("LSR_OVERLAP", "1") != "0":
-        ov = UpdateOverlap(bucket, optim)
-        optim.zero_grad(set_to_none=True)  # the graph's static .grad tensors stay with the graph
-
-        def run_ov():
-            with ov.forward():
-                loss = render(cam, model, Pipe, bg, Opt, language_target=(gt, mask))["language_l1"]
-            loss.backward()
-            ov.update()
-            return loss
-        for _ in range(3):
-            run_ov()
-        ov.synchronize()
-        dist.barrier()
+    # (6) N = 1: the pipelined order captured into HIP graphs (langsplat_amd.pipeline.PipelinedGraphStep):
+    # each replay is one full step -- this view's backward and Adam beside the next view's geometry
+    # stages, then the next view's compositing and loss -- with no host work inside
+    elapsed_pg = float("inf")
+    if world == 1 and graphed and os.environ.get("LSR_PIPELINE", "1") != "0":
+        pg = PipelinedGraphStep(lambda: render(cam, model, Pipe, bg, Opt, language_target=(gt, mask))["language_l1"],
+                                model.trainable(), optim)
+        pg.capture()
+        for _ in range(4):
+            pg.replay()
         torch.cuda.synchronize()
-        to = time.perf_counter()
+        if not pg.check():
+            for _ in range(2):
+                pg.replay()
+            torch.cuda.synchronize()
+        tq = time.perf_counter()
         for _ in range(args.steps):
-            run_ov()
-        ov.synchronize()
+            pg.replay()
         torch.cuda.synchronize()
-        dist.barrier()
-        elapsed_ov = time.perf_counter() - to
+        elapsed_pg = time.perf_counter() - tq
+        if not pg.check():
+            raise RuntimeError("a pipelined view exceeded its capacities during the timed steps")
+        del pg
     gc.enable()
     # the RGB stage's step on the same scene and view (all six groups trainable, L1 + SSIM, densification
     # statistics): reported beside, never as `value`
@@ -537,21 +564,22 @@ def main():
         rgb_ms = 1000.0 * (time.perf_counter() - t2) / rgb_steps
         del rgb
 
-    t = torch.tensor([elapsed, min(elapsed_ov, 1e30), float(blends)], dtype=torch.float64, device=dev)
-    ov_max = None
+    # `value`: the fastest of the full-step forms timed above (each does the whole step's work; the
+    # others are reported beside it)
+    forms = {"graph" if graphed else "eager": elapsed, "eager": elapsed_eager, "pipelined": elapsed_pipe,
+             "pipelined_graph": elapsed_pg}
+    names = sorted(forms)
+    t = torch.tensor([min(forms[n], 1e30) for n in names] + [float(blends)], dtype=torch.float64, device=dev)
     if world > 1:
-        tmax = t[:2].clone()
+        tmax = t[:-1].clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        tsum = t[2:].clone()
+        tsum = t[-1:].clone()
         dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
-        elapsed_max, blends_all = float(tmax[0].item()), float(tsum.item())
-        ov_max = float(tmax[1].item()) if elapsed_ov != float("inf") else None
+        times, blends_all = dict(zip(names, tmax.tolist())), float(tsum.item())
     else:
-        elapsed_max, blends_all = elapsed, float(blends)
-    serial_ms = 1000.0 * elapsed_max / args.steps
-    overlapped = ov_max is not None and ov_max < elapsed_max
-    if overlapped:
-        elapsed_max = ov_max
+        times, blends_all = dict(zip(names, t[:-1].tolist())), float(blends)
+    best = min(names, key=lambda n: times[n])
+    elapsed_max = times[best]
 
     if rank != 0:
         dist.barrier()
@@ -623,12 +651,15 @@ def main():
                                 "scene/gaussian_model.py:203-217)"},
         "ms_per_step_with_sync": round(1000.0 * elapsed_sync / args.steps, 4),
         "ms_per_step_eager": round(1000.0 * elapsed_eager / args.steps, 4),
-        "step_form": ("eager, RCCL all-reduce + Adam on a side stream overlapped with the next view's geometry"
-                      if overlapped else
-                      ("HIP graph replay (render + loss + backward + Adam)" if world == 1 else
-                       "HIP graph replay (render + loss + backward), RCCL all-reduce, Adam") if graphed else "eager"),
-        "ms_per_step_overlap": None if ov_max is None else round(1000.0 * ov_max / args.steps, 4),
-        "ms_per_step_serial_update": serial_ms if world > 1 else None,
+        "step_form": {"graph": ("HIP graph replay (render + loss + backward + Adam)" if world == 1 else
+                                "HIP graph replay (render + loss + backward), RCCL all-reduce, Adam"),
+                      "eager": "eager launches, one stream",
+                      "pipelined": "eager launches, consecutive views on two streams (the next view's geometry "
+                                   "beside this view's backward" + (", RCCL all-reduce" if world > 1 else "")
+                                   + " and Adam)",
+                      "pipelined_graph": "HIP graph replays of the pipelined step (this view's backward + Adam "
+                                         "beside the next view's geometry, then its compositing + loss)"}[best],
+        "ms_per_step_forms": {n: (round(1000.0 * v / args.steps, 4) if v < 1e29 else None) for n, v in times.items()},
         "ms_per_step_all_gradients": round(1000.0 * elapsed_all / args.steps, 4),
         "ms_per_step_rgb": None if rgb_ms is None else round(rgb_ms, 4),
         "raster_ms_per_step": round(raster_ms, 4),

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define LSR_ABI_VERSION 9
+#define LSR_ABI_VERSION 10
 
 enum lsr_status {
     LSR_OK = 0,
@@ -339,11 +339,13 @@ int32_t lsr_adam_step(int64_t n, float* param, const float* grad, float* exp_avg
  * scene/gaussian_model.py:219-226, each with its own lr, betas, eps and step count, i.e. torch's
  * per-parameter state).  Every gradient is multiplied by grad_scale first (e.g. the 1 / N of a
  * gradient all-reduced as a SUM over N ranks; 1 = none).
- * step_dev (device int64) replaces the tensors' step fields for a step replayed from a HIP graph:
- * a one-thread kernel first advances *step_dev by one, and the update uses that step for every
- * tensor, so each replay advances the count on the device; at most 16 tensors then.  `ticket` (a
+ * step_dev (device int64[LSR_ADAM_STEP_WORDS], ABI 10) replaces the tensors' step fields for a step
+ * replayed from a HIP graph: step_dev[0] is the step count; a one-wave kernel first advances it by
+ * one and writes that step's bias-corrected scalars of every tensor into the words after it, which
+ * the update reads, so each replay advances the count on the device; at most 16 tensors then.  `ticket` (a
  * device uint32 that is 0, or NULL) serves only the measurement variant LSR_ADAM_ADVANCE=0, where
  * the launch's last workgroup stores the step instead.  step_dev NULL: the host's step counts. */
+#define LSR_ADAM_STEP_WORDS 49 /* the count + 16 tensors' scalars (24 B each) */
 typedef struct lsr_adam_tensor {
     int64_t n;
     float* param;

@@ -22,7 +22,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LSR_LIB") or os.path.join(_HERE, "liblsr.so")
 
 LSR_BUF_GEOM, LSR_BUF_BINNING, LSR_BUF_IMAGE, LSR_BUF_BACKWARD = 0, 1, 2, 3
-ABI_VERSION = 9
+ABI_VERSION = 10
+ADAM_STEP_WORDS = 49  # include/lsr.h LSR_ADAM_STEP_WORDS
 # lsr_raw_flags (include/lsr.h): inputs are GaussianModel's raw parameters
 RAW_OPACITY, RAW_SCALES, RAW_ROTATIONS, RAW_LANGUAGE = 1, 2, 4, 8
 FWD_ZERO_GRAD_RECORDS = 1  # lsr_forward_flags
@@ -200,7 +201,10 @@ def _alloc_cb(user, which, nbytes):
     if a is None:
         return None
     try:
-        t = torch.empty((max(int(nbytes), 1),), dtype=torch.uint8, device=a.device)
+        n = max(int(nbytes), 1)
+        st = static_buffers.active()
+        t = st.tensor(("scratch", int(which)), (n,), torch.uint8, a.device, at_least=True) if st is not None \
+            else torch.empty((n,), dtype=torch.uint8, device=a.device)
     except Exception:  # noqa: BLE001 -- reported to C as NULL -> LSR_ERR_ALLOC
         return None
     a.buffers[int(which)] = t
@@ -286,6 +290,52 @@ class language_ready:
         language_ready._tls.cur = self._prev
 
 
+class static_buffers:
+    """Within the block, the rasterizer forwards of this thread put their scratch buffers and output
+    tensors into this object's persistent tensors instead of fresh allocations: the same addresses at
+    every forward.  A pipelined graph step (langsplat_amd.pipeline.PipelinedGraphStep) captures a
+    backward that reads what a forward captured in ANOTHER graph writes, so both must name the same
+    memory.  Tensors are (re)allocated only when a request does not fit (never during a capture)."""
+
+    _tls = threading.local()
+
+    def __init__(self):
+        self.tensors: Dict[tuple, torch.Tensor] = {}
+
+    @staticmethod
+    def active():
+        return getattr(static_buffers._tls, "cur", None)
+
+    def tensor(self, key, shape, dtype, device, at_least=False):
+        """The persistent tensor `key` of `shape` (at_least: a 1-D tensor of at least shape[0] elements,
+        a view of its first shape[0])."""
+        t = self.tensors.get(key)
+        fits = t is not None and t.dtype == dtype and t.device == torch.device(device) and (
+            t.numel() >= shape[0] if at_least else tuple(t.shape) == tuple(shape))
+        if not fits:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError(f"static_buffers: {key} {tuple(shape)} does not fit during a capture")
+            t = torch.empty(shape, dtype=dtype, device=device)
+            self.tensors[key] = t
+        return t[:shape[0]] if at_least else t
+
+    def __enter__(self):
+        self._prev = static_buffers.active()
+        static_buffers._tls.cur = self
+        return self
+
+    def __exit__(self, *exc):
+        static_buffers._tls.cur = self._prev
+
+
+def output_tensor(key, shape, dtype, device) -> torch.Tensor:
+    """An output tensor of the rasterizer forward: the active static_buffers' persistent one, else new."""
+    st = static_buffers.active()
+    if st is None:
+        return torch.empty(shape, dtype=dtype, device=device)
+    return st.tensor(("out", key), shape, dtype, device)
+
+
 # (P, W, H) -> (tile instances, super-tile entries) of this thread's last forward outside capacity mode
 # (the capacities a later capture needs)
 LAST_COUNTS: Dict[tuple, tuple] = {}
@@ -367,9 +417,9 @@ def rasterize_gaussians(rs, means3D, shs, colors_precomp, language_feature, opac
     H, W = int(rs.image_height), int(rs.image_width)
     keep: list = []
     s = make_settings(rs, keep)
-    color = torch.empty((3, H, W), dtype=torch.float32, device=device)
-    lang = torch.empty((3, H, W), dtype=torch.float32, device=device)
-    radii = torch.empty((P,), dtype=torch.int32, device=device)  # preprocess writes every entry
+    color = output_tensor("color", (3, H, W), torch.float32, device)
+    lang = output_tensor("language", (3, H, W), torch.float32, device)
+    radii = output_tensor("radii", (P,), torch.int32, device)  # preprocess writes every entry
     a = LsrForwardArgs()
     a.P = P
     a.M = int(shs.shape[1]) if shs is not None and shs.numel() > 0 else 0
@@ -407,8 +457,6 @@ def rasterize_gaussians(rs, means3D, shs, colors_precomp, language_feature, opac
     entries = ctypes.c_int64(0)
     ready = language_ready.active()
     if ready is not None and language_feature is not None:
-        if cap is not None:
-            raise ValueError("language_ready cannot be combined with capacity mode")
         a.language_ready = ready.cuda_event
         keep.append(ready)
     if cap is not None:

@@ -334,6 +334,18 @@ int32_t lsr_state_layout_of(int32_t P, int32_t width, int32_t height, int64_t nu
     return LSR_OK;
 }
 
+// The deferred language feature (lsr_forward_args.language_ready): the feature's update (another
+// stream) has overlapped everything enqueued so far; the stream waits for it, then the visible
+// Gaussians' records receive the feature.  Inside a graph capture the event is one recorded in the
+// same capture (a join of the two branches).
+static hipError_t wait_and_fill_language(const lsr_forward_args* a, const Layout& L, char* geom, hipStream_t stream)
+{
+    hipError_t e = hipStreamWaitEvent(stream, static_cast<hipEvent_t>(a->language_ready), 0);
+    if (e != hipSuccess) return e;
+    return launch_fill_language(a->P, a->language_feature, a->raw, a->radii, reinterpret_cast<float4*>(geom + L.record),
+                                stream);
+}
+
 int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_fn alloc, void* user,
                     void* stream_ptr, int64_t* num_rendered)
 {
@@ -457,7 +469,6 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
     const uint32_t fwd_flags = ((a->flags & LSR_FWD_ZERO_GRAD_RECORDS) ? kFwdZeroedRecords : 0u) |
                                ((a->out_loss && s->include_feature && a->language_feature) ? kFwdFusedLoss : 0u);
     if (a->capacity_rendered > 0) {
-        if (deferred) return fail(LSR_ERR_INVALID, "lsr_forward: language_ready with capacity mode");
         // Capacity mode: nothing waits for the device.  The counters stay on the device, the binning's
         // grids and buffers come from the capacities and its kernels read the true counts; a view over
         // capacity sets counters[kCntOverflow] (and *overflow) and is not binned.
@@ -480,6 +491,7 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
                                DevCount{counters + kCntSuper, counters + kCntOverflow}),
                 "binning");
         *num_rendered = R_cap;
+        if (deferred) LSR_TRY(wait_and_fill_language(a, L, geom, stream), "fill language");
         return render_forward_and_finish(s, a, L, geom, image, binning, hb, stream, debug);
     }
     const uint32_t seq = ++hb->seq == 0 ? ++hb->seq : hb->seq;
@@ -539,12 +551,7 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
     hb->hint_H = H;
     hb->binning_hint = L.binning_bytes + L.binning_bytes / 8;  // 12.5 % headroom for the next view
     LSR_TRY(launch_binning(P, R, L, geom, image, binning, &hb->stall, stream, debug, emitted), "binning");
-    if (deferred) {  // the feature's update (another stream) has overlapped everything above
-        LSR_TRY(hipStreamWaitEvent(stream, static_cast<hipEvent_t>(a->language_ready), 0), "wait language_ready");
-        LSR_TRY(launch_fill_language(P, a->language_feature, a->raw, a->radii, reinterpret_cast<float4*>(geom + L.record),
-                                     stream),
-                "fill language");
-    }
+    if (deferred) LSR_TRY(wait_and_fill_language(a, L, geom, stream), "fill language");
     hm.mark();
     const int32_t rc = render_forward_and_finish(s, a, L, geom, image, binning, hb, stream, debug);
     hm.mark();

@@ -67,9 +67,10 @@ __device__ __forceinline__ void adam_segment(const AdamSegment& g, int64_t chunk
     }
 }
 
-// Device step count (tab.step_dev, for a step replayed from a HIP graph): a one-thread kernel
-// advances *step_dev first, then every workgroup computes the bias corrections of that step
-// (torch's formulas, in double).  Measured on the graph-replayed C3 step (tools/ab_env.sh): 5 us
+// Device step count (tab.step_dev, for a step replayed from a HIP graph): a one-wave kernel
+// advances *step_dev first and forms every tensor's bias-corrected scalars of that step once (torch's
+// formulas, in double); the update's workgroups read them.  (Round 3's first form had every
+// workgroup evaluate the double pow()s itself: 18.5 us against 15.4 us eager in the graph's trace.)  Measured on the graph-replayed C3 step (tools/ab_env.sh): 5 us
 // faster than the alternative kept behind LSR_ADAM_ADVANCE=0, where the workgroup that finishes
 // last (the last ticket) stores step + 1 and resets the ticket (same-address atomics from a small
 // grid, and a long tail).
@@ -87,22 +88,32 @@ __device__ __forceinline__ AdamScalars adam_scalars_dev(const AdamHyper& h, int6
     return a;
 }
 
-// Workgroups take 256-thread chunks grid-stride (chunk -> tensor through block0); with the ticket
-// the grid is small (kAdamDevBlocks), so few tickets meet on the one counter.
-__global__ void k_adam_advance(int64_t* step_dev)
+// One wave: every lane reads the step count before lane 0 stores it advanced, and lane k < count
+// forms tensor k's scalars of the new step (torch's formulas, in double) into the words after the
+// count -- once per step instead of once per workgroup of the update.
+__global__ void k_adam_advance(int64_t* step_dev, AdamTable tab)
 {
-    if (threadIdx.x == 0) *step_dev += 1;
+    const int64_t step = *step_dev + 1;
+    const int k = (int)threadIdx.x;
+    if (k < tab.count) reinterpret_cast<AdamScalars*>(step_dev + 1)[k] = adam_scalars_dev(tab.hyper[k], step);
+    if (k == 0) *step_dev = step;
 }
 
+// Workgroups take 256-thread chunks grid-stride (chunk -> tensor through block0); with the ticket
+// the grid is small (kAdamDevBlocks), so few tickets meet on the one counter.
 __global__ __launch_bounds__(256) void k_adam_multi(AdamTable tab, int64_t chunks, float grad_scale)
 {
-    // ticket null with a device step: k_adam_advance already advanced it
-    const int64_t dstep = tab.step_dev ? *tab.step_dev + (tab.ticket ? 1 : 0) : 0;
+    // device step: k_adam_advance formed the scalars (ticket null), or every workgroup forms them
+    // from the count (the ticket form)
+    const int64_t dstep = tab.step_dev && tab.ticket ? *tab.step_dev + 1 : 0;
+    const AdamScalars* dev_scalars = tab.step_dev && !tab.ticket
+        ? reinterpret_cast<const AdamScalars*>(tab.step_dev + 1) : nullptr;
     for (int64_t c = blockIdx.x; c < chunks; c += gridDim.x) {
         int s = 0;
         while (s + 1 < tab.count && c >= tab.seg[s + 1].block0) s++;
         AdamSegment g = tab.seg[s];
-        if (tab.step_dev) g.a = adam_scalars_dev(tab.hyper[s], dstep);
+        if (dev_scalars) g.a = dev_scalars[s];
+        else if (tab.step_dev) g.a = adam_scalars_dev(tab.hyper[s], dstep);
         adam_segment(g, c, grad_scale);
     }
     if (!tab.step_dev || !tab.ticket) return;
@@ -138,8 +149,8 @@ hipError_t launch_adam_multi(AdamTable& tab, float grad_scale, hipStream_t s)
         return !(e && e[0] == '0');
     }();
     if (tab.step_dev && advance) {
-        hipLaunchKernelGGL(k_adam_advance, dim3(1), dim3(64), 0, s, tab.step_dev);
         tab.ticket = nullptr;
+        hipLaunchKernelGGL(k_adam_advance, dim3(1), dim3(64), 0, s, tab.step_dev, tab);
         const int64_t grid = std::min<int64_t>(blocks, 1 << 20);
         hipLaunchKernelGGL(k_adam_multi, dim3((unsigned)grid), dim3(256), 0, s, tab, blocks, grad_scale);
         return hipGetLastError();

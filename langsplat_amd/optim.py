@@ -29,7 +29,7 @@ class Adam(torch.optim.Optimizer):
         if lr < 0.0 or eps < 0.0 or not (0.0 <= betas[0] < 1.0 and 0.0 <= betas[1] < 1.0):
             raise ValueError(f"invalid Adam hyper-parameters lr={lr} betas={betas} eps={eps}")
         super().__init__(params, dict(lr=lr, betas=tuple(betas), eps=eps))
-        self._step_dev = None  # graph capture: (int64 step count, uint32 ticket) on the device
+        self._step_dev = None  # graph capture: (int64 step count + the step's scalars, uint32 ticket) on the device
 
     def _params_with_grad(self):
         return [p for g in self.param_groups for p in g["params"] if p.grad is not None]
@@ -46,15 +46,16 @@ class Adam(torch.optim.Optimizer):
         if missing:
             raise RuntimeError("langsplat_amd.optim.Adam: run one eager step before capturing")
         dev = ps[0].device
-        self._step_dev = (torch.full((1,), steps.pop() if steps else 0, dtype=torch.int64, device=dev),
-                          torch.zeros((1,), dtype=torch.int32, device=dev))
+        count = torch.zeros((_native.ADAM_STEP_WORDS,), dtype=torch.int64, device=dev)
+        count[0] = steps.pop() if steps else 0
+        self._step_dev = (count, torch.zeros((1,), dtype=torch.int32, device=dev))
 
     @torch.no_grad()
     def sync_steps(self):
         """state["step"] of every parameter from the device count (a device-to-host copy)."""
         if self._step_dev is None:
             return
-        n = float(self._step_dev[0].item())
+        n = float(self._step_dev[0][0].item())
         for g in self.param_groups:
             for p in g["params"]:
                 if len(self.state[p]):

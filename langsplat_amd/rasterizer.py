@@ -184,12 +184,12 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
         rest = _f32(features_rest) if features_rest is not None and features_rest.numel() > 0 else None
         m3, dc, ln, op, sc, ro = (_f32(means3D), _f32(features_dc), _f32(lang) if use_lang else None,
                                   _f32(opacity_raw), _f32(scaling_raw), _f32(rotation_raw))
-        visible = torch.empty((P,), dtype=torch.bool, device=m3.device)  # radii > 0, written by preprocess
+        visible = _native.output_tensor("visible", (P,), torch.bool, m3.device)  # radii > 0, written by preprocess
         fuse_loss = loss_target is not None
         if fuse_loss and not raster_settings.include_feature:
             raise ValueError("the fused language loss needs include_feature=True")
         # without the fused loss this output is never handed to the caller (no fill kernel)
-        loss = torch.empty((), dtype=torch.float32, device=m3.device)
+        loss = _native.output_tensor("loss", (), torch.float32, m3.device)
         # a backward will follow: let the compositing kernel clear its gradient records
         flags = _native.FWD_ZERO_GRAD_RECORDS if any(ctx.needs_input_grad) else 0
         ctx.records_zeroed = flags != 0

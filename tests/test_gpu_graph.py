@@ -97,10 +97,14 @@ def _language_setup(W=160, H=120, P=6000):
         getattr(m, "_" + n).requires_grad_(False)
     bg = torch.zeros(3, device=DEV)
 
+    def forward():
+        return render(cam, m, _Pipe, bg, _Opt, language_target=(gt, mask))["language_l1"]
+
     def step():
-        loss = render(cam, m, _Pipe, bg, _Opt, language_target=(gt, mask))["language_l1"]
+        loss = forward()
         loss.backward()
         return loss
+    step.forward = forward
     return m, step
 
 

@@ -63,16 +63,28 @@ def test_deferred_language_forward_is_identical(raw):
         assert_grad_close(k, ga[k].cpu().numpy(), gb[k].cpu().numpy())
 
 
-def test_deferred_language_rejected_in_capacity_mode():
-    st, inp = scene(P=500, W=64, H=48, seed=2)
+def test_deferred_language_in_capacity_mode_is_identical():
+    """Capacity mode (a graph capture's forward) with the deferred feature (PipelinedGraphStep's
+    forward): the same images and state as the eager forward that had the feature from the start."""
+    P, W, H = 3000, 96, 64
+    st, inp = scene(P=P, W=W, H=H, seed=2, scale_range=(0.03, 0.2))
     std, ind = to_device(st, inp, DEV)
+    args = (ind["means3D"], ind["shs"], None, ind["language_feature_precomp"], ind["opacities"], ind["scales"],
+            ind["rotations"], None)
+    ref = _native.rasterize_gaussians(std, *args)
+    R, E = _native.LAST_COUNTS[(P, W, H)]
     ev = torch.cuda.Event()
     ev.record()
     ovf = torch.zeros((), dtype=torch.int32, device=DEV)
-    with pytest.raises(ValueError):
-        with _native.capacity(10000, 10000, ovf), _native.language_ready(ev):
-            _native.rasterize_gaussians(std, ind["means3D"], ind["shs"], None, ind["language_feature_precomp"],
-                                        ind["opacities"], ind["scales"], ind["rotations"], None)
+    with _native.capacity(R + 100, E + 100, ovf), _native.language_ready(ev):
+        out = _native.rasterize_gaussians(std, *args)
+    torch.cuda.synchronize()
+    assert int(ovf.item()) == 0
+    for a, b in zip(out[1:4], ref[1:4]):
+        assert torch.equal(a, b)
+    sa, sb = state(out, P, W, H), state(ref, P, W, H)
+    for k in ("n_contrib", "final_T"):
+        np.testing.assert_array_equal(sa[k], sb[k])
 
 
 def test_update_overlap_matches_serial_steps(monkeypatch):

@@ -31,7 +31,13 @@ def test_library_loads_and_exports_every_declared_symbol():
     for name in _declared_functions():
         assert hasattr(lib, name), name
         assert name in _native.SIGNATURES, f"ctypes binding misses {name}"
-    assert lib.lsr_abi_version() == _native.ABI_VERSION == 9
+    assert lib.lsr_abi_version() == _native.ABI_VERSION == 10
+
+
+def test_header_constants_match_the_python_side():
+    hdr = open(os.path.join(ROOT, "include", "lsr.h")).read()
+    assert int(re.search(r"#define LSR_ABI_VERSION (\d+)", hdr).group(1)) == _native.ABI_VERSION
+    assert int(re.search(r"#define LSR_ADAM_STEP_WORDS (\d+)", hdr).group(1)) == _native.ADAM_STEP_WORDS
 
 
 def test_sizes_and_layout_are_consistent():

@@ -41,6 +41,17 @@ def run(mode, steps=30):
 
         def step():
             g.replay()
+    elif mode == "pgraph":  # the pipelined step (langsplat_amd.pipeline.PipelinedGraphStep)
+        from langsplat_amd.pipeline import PipelinedGraphStep
+        fwd_bwd()
+        optim.step()
+        optim.zero_grad(set_to_none=True)
+        pg = PipelinedGraphStep(lambda: bench.render(cam, model, bench.Pipe, bg, bench.Opt,
+                                                     language_target=(gt, mask))["language_l1"],
+                                [model._language_feature], optim).capture()
+
+        def step():
+            pg.replay()
     else:
         def step():
             fwd_bwd()
@@ -83,9 +94,23 @@ def summary(path):
         print(f"  gap {g / n / 1e3:7.2f} us  after {x}  before {y}")
 
 
+def timeline(path, anchor="k_render_forward<"):
+    """Kernels of the last few steps, each with its start and end relative to the step's anchor
+    kernel's start (pipelined steps overlap, so kernels are listed by start time)."""
+    rows = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in csv.DictReader(open(path))))
+    starts = [i for i, r in enumerate(rows) if anchor in r[2]]
+    a, b = starts[-3], starts[-2]
+    t0 = rows[a][0]
+    print(f"step span (anchor to anchor): {(rows[b][0] - t0) / 1e3:.1f} us")
+    for s, e, n in rows[a - 12:b + 1]:
+        print(f"  {(s - t0) / 1e3:8.1f} {(e - t0) / 1e3:8.1f} {(e - s) / 1e3:7.1f}  {n[:70]}")
+
+
 if __name__ == "__main__":
     if sys.argv[1] == "--summary":
         summary(sys.argv[2])
+    elif sys.argv[1] == "--timeline":
+        timeline(sys.argv[2])
     elif sys.argv[1] == "--compare":  # per-kernel average (last 20 launches) of two traces
         a, b = per_kernel(sys.argv[2]), per_kernel(sys.argv[3])
         for k in sorted(set(a) | set(b), key=lambda k: -max(a.get(k, (0, 0))[1], b.get(k, (0, 0))[1])):
