@@ -119,31 +119,35 @@ class OptRGB:
     lambda_dssim = 0.2
 
 
-def _ssim_window(window_size, channel, device):
-    """utils/loss_utils.py:24-33: the 11 x 11 Gaussian window (sigma 1.5), one per channel."""
+def _ssim_taps(window_size, channels, device):
+    """utils/loss_utils.py:24-33's 11 x 11 window (sigma 1.5) is the outer product g g^T of the 1-D
+    Gaussian g: returned as its two separable factors, one per channel."""
     x = torch.arange(window_size, dtype=torch.float64) - window_size // 2
     g = torch.exp(-x * x / (2 * 1.5 ** 2))
-    g = (g / g.sum()).float().unsqueeze(1)
-    w = g.mm(g.t()).unsqueeze(0).unsqueeze(0)
-    return w.expand(channel, 1, window_size, window_size).contiguous().to(device)
+    g = (g / g.sum()).float()
+    return (g.view(1, 1, window_size, 1).expand(channels, 1, window_size, 1).contiguous().to(device),
+            g.view(1, 1, 1, window_size).expand(channels, 1, 1, window_size).contiguous().to(device))
 
 
 def ssim(img1, img2, window_size=11):
     """utils/loss_utils.py:35-63 (size_average=True) as torch ops: the RGB stage's loss consumer of
-    the rasterizer output (outside the hot path; MIOpen convolutions here)."""
+    the rasterizer output (outside the hot path).  The five windowed means
+    (mu1, mu2, E[x1^2], E[x2^2], E[x1 x2]) are one separable pass over 15 stacked channels (an 11 x 1
+    then a 1 x 11 depthwise convolution, zero padded as the 11 x 11 one: the same sums, a different
+    rounding order) instead of five 11 x 11 depthwise convolutions."""
     F = torch.nn.functional
-    channel = img1.size(-3)
-    w = _ssim_window(window_size, channel, img1.device).type_as(img1)
+    c = img1.size(-3)
     pad = window_size // 2
-    mu1 = F.conv2d(img1, w, padding=pad, groups=channel)
-    mu2 = F.conv2d(img2, w, padding=pad, groups=channel)
+    x = torch.cat([img1, img2, img1 * img1, img2 * img2, img1 * img2], dim=-3).unsqueeze(0)
+    gv, gh = _ssim_taps(window_size, 5 * c, img1.device)
+    m = F.conv2d(F.conv2d(x, gv.type_as(x), padding=(pad, 0), groups=5 * c), gh.type_as(x), padding=(0, pad),
+                 groups=5 * c)[0]
+    mu1, mu2, e11, e22, e12 = m.split(c, dim=-3)
     mu1_sq, mu2_sq, mu1_mu2 = mu1.pow(2), mu2.pow(2), mu1 * mu2
-    s1 = F.conv2d(img1 * img1, w, padding=pad, groups=channel) - mu1_sq
-    s2 = F.conv2d(img2 * img2, w, padding=pad, groups=channel) - mu2_sq
-    s12 = F.conv2d(img1 * img2, w, padding=pad, groups=channel) - mu1_mu2
+    s1, s2, s12 = e11 - mu1_sq, e22 - mu2_sq, e12 - mu1_mu2
     C1, C2 = 0.01 ** 2, 0.03 ** 2
-    m = ((2 * mu1_mu2 + C1) * (2 * s12 + C2)) / ((mu1_sq + mu2_sq + C1) * (s1 + s2 + C2))
-    return m.mean()
+    r = ((2 * mu1_mu2 + C1) * (2 * s12 + C2)) / ((mu1_sq + mu2_sq + C1) * (s1 + s2 + C2))
+    return r.mean()
 
 
 class RGBStep:

@@ -85,7 +85,10 @@ enum lsr_raw_flags {
  * LSR_FWD_ZERO_GRAD_RECORDS, and lsr_backward_args.dL_dloss only for a forward that fused the loss
  * (out_loss set): the forward records both in its image buffer, and with settings.debug the
  * backward checks them and fails with LSR_ERR_INVALID instead of reading stale records or codes. */
-enum lsr_forward_flags { LSR_FWD_ZERO_GRAD_RECORDS = 1 };
+/* LSR_FWD_READY_EXTERNAL: the wait on language_ready is enqueued with hipEventWaitExternal, so that
+ * inside a HIP graph capture it becomes an external event-wait node (the event is recorded by
+ * ANOTHER graph, with hipEventRecordExternal: langsplat_amd.pipeline.PipelinedGraphStep). */
+enum lsr_forward_flags { LSR_FWD_ZERO_GRAD_RECORDS = 1, LSR_FWD_READY_EXTERNAL = 2 };
 enum lsr_backward_flags { LSR_BWD_RECORDS_ZEROED = 1 };
 
 /* GaussianRasterizationSettings (gaussian_renderer/__init__.py:37-51), device-pointer form. */
@@ -156,8 +159,9 @@ typedef struct lsr_forward_args {
      * (raw: activates) language_feature into the per-Gaussian records and the compositing starts.
      * A trainer records the event after the previous step's all-reduce and optimiser update of the
      * language feature on another stream, so that update overlaps this view's geometry work
-     * (langsplat_amd.distributed.UpdateOverlap).  Results are identical to a call without it.  Not
-     * with capacity mode (LSR_ERR_INVALID). */
+     * (langsplat_amd.distributed.UpdateOverlap, langsplat_amd.pipeline).  Results are identical to a
+     * call without it.  In capacity mode (a graph capture) the event is one recorded in the same
+     * capture, or, with LSR_FWD_READY_EXTERNAL, one another graph records as an external event. */
     void* language_ready;
 } lsr_forward_args;
 

@@ -27,6 +27,7 @@ ADAM_STEP_WORDS = 49  # include/lsr.h LSR_ADAM_STEP_WORDS
 # lsr_raw_flags (include/lsr.h): inputs are GaussianModel's raw parameters
 RAW_OPACITY, RAW_SCALES, RAW_ROTATIONS, RAW_LANGUAGE = 1, 2, 4, 8
 FWD_ZERO_GRAD_RECORDS = 1  # lsr_forward_flags
+FWD_READY_EXTERNAL = 2
 BWD_RECORDS_ZEROED = 1     # lsr_backward_flags
 _vp = ctypes.c_void_p
 
@@ -265,17 +266,30 @@ class capacity:
         capacity._tls.cur = self._prev
 
 
+class _ExternalEvent:
+    """A torch.cuda.Event marked as recorded by another graph (language_ready(..., external=True))."""
+
+    def __init__(self, event):
+        self.event = event
+
+    @property
+    def cuda_event(self):
+        return self.event.cuda_event
+
+
 class language_ready:
     """Within the block, the rasterizer forwards of this thread defer the language feature
     (include/lsr.h lsr_forward_args.language_ready): preprocess, depth order and binning run at
     once, and the stream waits for `event` (a torch.cuda.Event recorded after the language feature's
     last update, on any stream) only before the feature enters the records and the compositing
-    starts.  event None: off (the block is a no-op)."""
+    starts.  event None: off (the block is a no-op).  external: the event is recorded by another
+    HIP graph (hipEventRecordExternal) and the wait is captured as an external event-wait node
+    (include/lsr.h LSR_FWD_READY_EXTERNAL)."""
 
     _tls = threading.local()
 
-    def __init__(self, event):
-        self.event = event
+    def __init__(self, event, external: bool = False):
+        self.event = event if event is None or not external else _ExternalEvent(event)
 
     @staticmethod
     def active():
@@ -458,6 +472,8 @@ def rasterize_gaussians(rs, means3D, shs, colors_precomp, language_feature, opac
     ready = language_ready.active()
     if ready is not None and language_feature is not None:
         a.language_ready = ready.cuda_event
+        if isinstance(ready, _ExternalEvent):
+            a.flags |= FWD_READY_EXTERNAL
         keep.append(ready)
     if cap is not None:
         a.capacity_rendered = cap.rendered

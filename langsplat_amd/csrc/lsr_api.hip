@@ -277,6 +277,9 @@ static int32_t render_forward_and_finish(const lsr_settings* s, const lsr_forwar
     rp.n_contrib = reinterpret_cast<uint32_t*>(image + L.n_contrib);
     rp.sched_counts = reinterpret_cast<uint32_t*>(image + L.counters);
     rp.sched_lists = reinterpret_cast<uint32_t*>(image + L.tile_lists);
+    rp.split_pool = reinterpret_cast<float*>(image + L.split_pool);
+    rp.split_desc = reinterpret_cast<uint4*>(image + L.split_desc);
+    rp.split_cap = L.split_cap;
     rp.out_color = a->out_color;
     rp.out_lang = a->out_language_feature;
     if (a->flags & LSR_FWD_ZERO_GRAD_RECORDS) {
@@ -337,10 +340,12 @@ int32_t lsr_state_layout_of(int32_t P, int32_t width, int32_t height, int64_t nu
 // The deferred language feature (lsr_forward_args.language_ready): the feature's update (another
 // stream) has overlapped everything enqueued so far; the stream waits for it, then the visible
 // Gaussians' records receive the feature.  Inside a graph capture the event is one recorded in the
-// same capture (a join of the two branches).
+// same capture (a join of the two branches), or with LSR_FWD_READY_EXTERNAL one another graph records
+// (an external event-wait node).
 static hipError_t wait_and_fill_language(const lsr_forward_args* a, const Layout& L, char* geom, hipStream_t stream)
 {
-    hipError_t e = hipStreamWaitEvent(stream, static_cast<hipEvent_t>(a->language_ready), 0);
+    hipError_t e = hipStreamWaitEvent(stream, static_cast<hipEvent_t>(a->language_ready),
+                                      (a->flags & LSR_FWD_READY_EXTERNAL) ? hipEventWaitExternal : 0);
     if (e != hipSuccess) return e;
     return launch_fill_language(a->P, a->language_feature, a->raw, a->radii, reinterpret_cast<float4*>(geom + L.record),
                                 stream);
@@ -366,7 +371,8 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
         return fail(LSR_ERR_INVALID, "lsr_forward: settings tensors missing");
     if (a->raw & ~(LSR_RAW_OPACITY | LSR_RAW_SCALES | LSR_RAW_ROTATIONS | LSR_RAW_LANGUAGE))
         return fail(LSR_ERR_INVALID, "lsr_forward: unknown raw flag");
-    if (a->flags & ~LSR_FWD_ZERO_GRAD_RECORDS) return fail(LSR_ERR_INVALID, "lsr_forward: unknown flag");
+    if (a->flags & ~(LSR_FWD_ZERO_GRAD_RECORDS | LSR_FWD_READY_EXTERNAL))
+        return fail(LSR_ERR_INVALID, "lsr_forward: unknown flag");
     if (a->shs_rest && (!a->shs || a->M < 2))
         return fail(LSR_ERR_INVALID, "lsr_forward: shs_rest needs shs (features_dc) and M >= 2");
     if (a->capacity_rendered < 0 || (a->capacity_rendered > 0 && a->capacity_entries <= 0) ||
@@ -630,6 +636,9 @@ int32_t lsr_backward(const lsr_settings* s, const lsr_backward_args* a, lsr_allo
     rp.n_contrib = reinterpret_cast<uint32_t*>(image + L.n_contrib);
     rp.sched_counts = reinterpret_cast<uint32_t*>(image + L.counters);
     rp.sched_lists = reinterpret_cast<uint32_t*>(image + L.tile_lists);
+    rp.split_pool = reinterpret_cast<float*>(image + L.split_pool);
+    rp.split_desc = reinterpret_cast<uint4*>(image + L.split_desc);
+    rp.split_cap = L.split_cap;
     rp.dL_dcolor = a->dL_dout_color;
     rp.dL_dlang = a->dL_dout_language_feature;
     rp.dL_dloss = a->dL_dloss;

@@ -426,8 +426,10 @@ __global__ __launch_bounds__(256) void k_fill_language(int P, const float* __res
         f1 = f.y;
         f2 = f.z;
     }
-    float4* r = record + 3 * (size_t)i + 2;
-    *r = make_float4(r->x, f0, f1, f2);
+    // the three slots only (a dword and a dwordx2 store): no read of the record's colour word b
+    float* r = reinterpret_cast<float*>(record + 3 * (size_t)i + 2);
+    r[1] = f0;
+    *reinterpret_cast<float2*>(r + 2) = make_float2(f1, f2);
 }
 
 hipError_t launch_fill_language(int P, const float* lang, int raw, const int32_t* radii, float4* record,

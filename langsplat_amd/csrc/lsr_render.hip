@@ -479,6 +479,9 @@ __global__ __launch_bounds__(kTilePixels, 7) void k_render_forward(RenderParams 
     // second entry of a pair without testing i + 1 < n (its result is discarded then)
     __shared__ uint16_t sL[kThreads / 64][kThreads + 1];
     __shared__ uint32_t s_last;
+    // split replay: [0] boundaries recorded (a prefix of 256, 512, 768), [j] the slot of boundary j,
+    // [kSplitMax + 1] the slot thread 0 took for the current batch (broadcast)
+    __shared__ uint32_t s_split[kSplitMax + 2];
 
     const int T = p.gx * p.gy;
     if (p.zero_records) {  // the backward's gradient records: stores beside the VALU-bound walk
@@ -509,7 +512,10 @@ __global__ __launch_bounds__(kTilePixels, 7) void k_render_forward(RenderParams 
     const uint2 range = p.ranges[tile];
     const uint32_t start = range.x, end = range.y;
     const bool inside = px < p.W && py < p.H;
-    if (t == 0) s_last = 0;
+    if (t == 0) {
+        s_last = 0;
+        s_split[0] = 0;
+    }
 
     FwdPixel q{inside ? 1.0f : -1.0f, make_f2(0.f, 0.f), make_f2(0.f, 0.f), make_f2(0.f, 0.f), 0u, 0u};
     PhaseTicks ph;
@@ -525,6 +531,36 @@ __global__ __launch_bounds__(kTilePixels, 7) void k_render_forward(RenderParams 
             break;
         }
         if (kStats) ph.batches++;
+        if (p.split_pool && base != start && base - start <= (uint32_t)(kSplitMax * kThreads)) {
+            // split replay: every pixel's state before list entry 256 j, while some pixel composites
+            // (a slot per boundary from the grid-wide counter; the recorded boundaries stay a prefix)
+            const uint32_t j = (base - start) / kThreads;
+            if (t == 0) {
+                uint32_t slot = 0xFFFFFFFFu;
+                if (s_split[0] == j - 1u) {
+                    slot = atomicAdd(p.sched_counts + kCntSplit, 1u);
+                    if (slot < p.split_cap) {
+                        s_split[j] = slot;
+                        s_split[0] = j;
+                    } else {
+                        slot = 0xFFFFFFFFu;
+                    }
+                }
+                s_split[kSplitMax + 1] = slot;
+            }
+            __syncthreads();
+            const uint32_t slot = s_split[kSplitMax + 1];
+            if (slot != 0xFFFFFFFFu) {
+                float* st = p.split_pool + (size_t)slot * (kSplitVals * kThreads) + t;
+                st[0] = q.T;
+                st[kThreads] = q.C01.x;
+                st[2 * kThreads] = q.C01.y;
+                st[3 * kThreads] = q.C2F0.x;
+                st[4 * kThreads] = q.C2F0.y;
+                st[5 * kThreads] = q.F12.x;
+                st[6 * kThreads] = q.F12.y;
+            }
+        }
         const uint32_t idx = base + t;
         if (idx < end) {
             const uint32_t g = g_next;
@@ -589,8 +625,33 @@ __global__ __launch_bounds__(kTilePixels, 7) void k_render_forward(RenderParams 
     __syncthreads();
     if (lane == 0) atomicMax(&s_last, wl);
     __syncthreads();
-    if (t == 0 && p.sched_counts && s_last > 0)
-        schedule_tile(p.sched_counts + kCntBwdClass, p.sched_lists + (size_t)kWorkClasses * T, T, tile, s_last);
+    // the backward's work items: the tile's replay [0, s_last) cut at the recorded boundaries below
+    // s_last (split replay), each appended to the class of its length
+    const uint32_t maxl = s_last;
+    const uint32_t nsplit = p.split_pool && maxl > 0 ? min(s_split[0], (maxl - 1u) / (uint32_t)kThreads) : 0u;
+    if (t == 0 && p.sched_counts && maxl > 0) {
+        uint32_t* bwd_lists = p.sched_lists + (size_t)kWorkClasses * T;
+        if (p.split_pool) p.split_desc[tile] = make_uint4(nsplit, s_split[1], s_split[2], s_split[3]);
+        for (uint32_t k = 0; k <= nsplit; k++) {
+            const uint32_t lo = k * (uint32_t)kThreads, hi = k < nsplit ? lo + (uint32_t)kThreads : maxl;
+            schedule_tile(p.sched_counts + kCntBwdClass, bwd_lists, kSplitItems * T, kSplitItems * tile + (int)k,
+                          hi - lo);
+        }
+    }
+    // the recorded sums become the colour / feature composited BEHIND each boundary, normalised by
+    // the transmittance there -- the backward's running `acc` at that point: (C_final - C_front) / T_b
+    for (uint32_t j = 1; j <= nsplit; j++) {
+        float* st = p.split_pool + (size_t)s_split[j] * (kSplitVals * kThreads) + t;
+        const float Tb = st[0];
+        if (!(Tb > 0.0f)) continue;  // done before the boundary: the backward does not read it
+        const float inv = 1.0f / Tb;
+        st[kThreads] = (q.C01.x - st[kThreads]) * inv;
+        st[2 * kThreads] = (q.C01.y - st[2 * kThreads]) * inv;
+        st[3 * kThreads] = (q.C2F0.x - st[3 * kThreads]) * inv;
+        st[4 * kThreads] = (q.C2F0.y - st[4 * kThreads]) * inv;
+        st[5 * kThreads] = (q.F12.x - st[5 * kThreads]) * inv;
+        st[6 * kThreads] = (q.F12.y - st[6 * kThreads]) * inv;
+    }
     if (kStats) {
         if (!ph.stopped && ph.batches) ph.lap(ph.walk);  // the last batch's walk
         timeline_put(0, t_start, tile, ph);
@@ -712,6 +773,17 @@ static size_t backward_pad()
     return v;
 }
 
+// LSR_SPLIT=0: no split replay (the forward records no boundary state, the backward replays each
+// tile as one work item; measurement aid)
+static bool split_replay()
+{
+    static const bool v = [] {
+        const char* e = getenv("LSR_SPLIT");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+
 // LSR_ORDER=0 launches the tiles in tile order (measurement aid)
 static bool scheduled()
 {
@@ -727,6 +799,7 @@ hipError_t launch_render_forward(const RenderParams& pin, int tiles, hipStream_t
     if (tiles == 0) return hipSuccess;
     RenderParams p = pin;
     if (!scheduled()) p.sched_counts = p.sched_lists = nullptr;
+    if (!p.sched_counts || !split_replay()) p.split_pool = nullptr;
     p.prio = p.sched_counts ? prio_levels() : 0;
     const bool feat = p.include_feature != 0;
     const bool loss = feat && p.loss_words != nullptr;  // one word per workgroup: the full grid
@@ -1116,11 +1189,15 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
     // reader in this launch
     if (p.fwd_flags && blockIdx.x == 0 && threadIdx.x == 0) *p.fwd_flags &= ~kFwdZeroedRecords;
     int tile = (int)blockIdx.x;
+    uint32_t chunk = 0;  // split replay: this workgroup replays list entries [256 chunk, ...) of the tile
     if (p.sched_counts) {  // tiles without contributors are not scheduled: nothing to do
         const int T = p.gx * p.gy;
-        tile = scheduled_tile((int)blockIdx.x, p.sched_counts + kCntBwdClass,
-                              p.sched_lists + (size_t)kWorkClasses * T, T);
-        if (tile < 0) return;
+        const int item = scheduled_tile((int)blockIdx.x, p.sched_counts + kCntBwdClass,
+                                        p.sched_lists + (size_t)kWorkClasses * T, kSplitItems * T);
+        if (item < 0) return;
+        const int it = __builtin_amdgcn_readfirstlane(item);  // uniform: scalar registers
+        tile = it / kSplitItems;
+        chunk = (uint32_t)(it % kSplitItems);
     }
     launch_priority((int)blockIdx.x, p.prio);
     const int tx = tile % p.gx, ty = tile / p.gx;
@@ -1133,6 +1210,31 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
 
     BwdPixel q;
     bwd_pixel_init<kFeat, kColor>(q, p, px < p.W && py < p.H, (size_t)py * p.W + px, HW);
+    // split replay: a chunk that ends at a recorded boundary hi = 256 (chunk + 1) starts the pixels
+    // that composite past hi from the forward's state there (T and the normalised sums behind it);
+    // pixels whose last contributor lies inside the chunk start from T_final as usual, and pixels
+    // that end before it have nothing here (every entry >= their count is skipped)
+    const uint32_t lo = chunk * (uint32_t)kThreads;
+    if (p.split_pool && p.sched_counts) {
+        const uint4 desc = p.split_desc[tile];
+        const uint32_t hi = lo + (uint32_t)kThreads;
+        if (chunk < desc.x && q.last > hi) {
+            const uint32_t slot = chunk == 0 ? desc.y : (chunk == 1 ? desc.z : desc.w);
+            const float* st = p.split_pool + (size_t)slot * (kSplitVals * kThreads) + t;
+            q.T = st[0];
+            if (kColor) {
+                q.acc0 = st[kThreads];
+                q.acc1 = st[2 * kThreads];
+                q.acc2 = st[3 * kThreads];
+            }
+            if (kFeat) {
+                q.accF0 = st[4 * kThreads];
+                q.accF1 = st[5 * kThreads];
+                q.accF2 = st[6 * kThreads];
+            }
+            q.last = hi;
+        }
+    }
     uint32_t wmax = q.last;
 
     if (kStats) {
@@ -1149,11 +1251,11 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
     const int vidx = k5 ? scatter_index5(lane) : scatter_index(lane);
     float* const sGl = sG + gslot<kColor, k5>(vidx);  // this lane's value slot in the tile sums
 
-    for (int done_cnt = 0; done_cnt < maxl; done_cnt += kThreads) {
+    for (int done_cnt = 0; done_cnt < maxl - (int)lo; done_cnt += kThreads) {
         __syncthreads();
         const int kload = maxl - 1 - (done_cnt + t);
         uint32_t cover = 0;
-        if (kload >= 0) {
+        if (kload >= (int)lo) {
             const uint32_t g = p.point_list[start + (uint32_t)kload];
             if (k5) s_gid[t] = g;
             const float4 a = p.record[3 * (size_t)g];
@@ -1180,7 +1282,7 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
         sM[t] = (uint8_t)cover;
         for (int i = t; i < kThreads * kGS; i += kThreads) sG[i] = 0.f;
         __syncthreads();
-        const int cnt = min(kThreads, maxl - done_cnt);
+        const int cnt = min(kThreads, maxl - (int)lo - done_cnt);
         // the wave walks the set bits of a ballot over the cover masks (no list, no barrier)
         uint32_t nw = 0;  // kStats
         for (int r = 0; r < cnt; r += 64) {
@@ -1262,6 +1364,8 @@ hipError_t launch_render_backward(const RenderParams& pin, int tiles, hipStream_
     const bool feat = p.include_feature != 0;
     const bool color = p.dL_dcolor != nullptr;  // null: the colour image does not reach the loss
     const int variant = (feat ? 1 : 0) | (color ? 2 : 0) | (p.geo ? 4 : 0);
+    if (!p.sched_counts || !split_replay()) p.split_pool = nullptr;
+    if (p.split_pool) tiles += (int)p.split_cap;  // the items: a tile's chunks beyond its first
     if (render_stats_on()) tiles = debug_grid(tiles);
 #define LSR_BWD(S, V)                                                                                         \
     hipLaunchKernelGGL((k_render_backward<S, (V & 1) != 0, (V & 2) != 0, (V & 4) != 0>), dim3(tiles), \

@@ -93,7 +93,9 @@ def test_pipelined_graph_matches_serial_steps(monkeypatch):
             torch.cuda.synchronize()
             losses.append(g.static_loss[0].clone())  # the prologue's view
             for _ in range(K):
-                losses.append(g.replay().clone())
+                loss = g.replay()
+                g.synchronize()  # the loss is written on the pipeline's forward stream
+                losses.append(loss.clone())
             torch.cuda.synchronize()
             assert g.check() and g.captures == 1
             g.sync()
