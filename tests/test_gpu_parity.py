@@ -280,6 +280,23 @@ def test_full_size_oracle_parity(cfg):
     check_backward(st, inp, run, out, seed=3, outliers=1e-5)
 
 
+def test_full_size_oracle_parity_C5():
+    """BASELINE.json configs[4]'s scene (3M Gaussians, 1920x1080, camera 0): above 2M Gaussians the
+    depth order takes the LSD passes, checked here at full size against the oracle -- forward
+    bit-exact (images, radii, tile ranges, per-tile order, final T, contributor counts) and every
+    gradient within the tolerance of test_full_size_oracle_parity."""
+    c = CONFIGS["C5"]
+    g = make_gaussians(c["P"], seed=0)
+    cam = make_cameras(1, c["width"], c["height"])[0]
+    st = settings_for(cam, sh_degree=3)
+    with torch.no_grad():
+        inp = {k: v.contiguous() for k, v in activated_inputs(g).items()}
+    run = oracle.forward(st, **inp)
+    assert run.blends > 0
+    run, std, ind, out = check_forward_exact(st, inp, run)
+    check_backward(st, inp, run, out, seed=3, outliers=1e-5)
+
+
 @pytest.mark.parametrize("cfg", ["C2", "C3", "C5"])
 def test_full_size_properties(cfg):
     """BASELINE.json full sizes: per-tile lists sorted by (depth, id), instance accounting, and the
@@ -449,3 +466,17 @@ def test_debug_backward_rejects_flags_its_forward_did_not_prepare():
         bwd(zeroed, flags=_native.BWD_RECORDS_ZEROED)
     g2 = bwd(zeroed)["language_feature_precomp"]
     assert_grad_close("second backward", g2.cpu().numpy(), g1.cpu().numpy())
+
+
+@pytest.mark.parametrize("include_feature", [True, False])
+def test_split_replay_dense_tiles(include_feature):
+    """Split replay (lsr_render.hip): a dense scene whose tiles composite past list entries 256, 512
+    and 768, so the forward records boundary states (counters[8] counts the slots) and the backward
+    replays those tiles as independent chunks started from them -- forward still bit-exact, every
+    gradient within the parity tolerance of the oracle's unsplit replay."""
+    st, inp = scene(P=40000, W=96, H=80, seed=21, scale_range=(0.02, 0.12), include_feature=include_feature)
+    run, std, ind, out = check_forward_exact(st, inp)
+    s = state(out, 40000, 96, 80)
+    assert int(s["counters"][8]) > 0, "no split-replay boundary was recorded"
+    assert int(s["n_contrib"].max()) > 768
+    check_backward(st, inp, run, out, seed=11)
