@@ -272,6 +272,12 @@ int32_t lsr_profile_select(const char* stages);
  * call): a timed run samples its dominant kernel's duration at a fraction of the events' cost. */
 int32_t lsr_profile_sample(int32_t every);
 
+/* hipEventRecordWithFlags(event, stream, hipEventRecordExternal) through this library's HIP runtime
+ * (the one the rasterizer's streams and events belong to): inside a stream capture, an external
+ * event-record node -- the update another graph's forward waits for with LSR_FWD_READY_EXTERNAL
+ * (langsplat_amd.pipeline.PipelinedGraphStep). */
+int32_t lsr_event_record_external(void* event, void* stream);
+
 /* _C.mark_visible: visible[i] = 1 iff Gaussian i passes the near-plane frustum test. */
 int32_t lsr_mark_visible(int32_t P, const float* means3D, const float* viewmatrix,
                          const float* projmatrix, uint8_t* visible, void* stream);

@@ -105,6 +105,7 @@ SIGNATURES = {
     "lsr_backward": (ctypes.c_int32, [ctypes.POINTER(LsrSettings), ctypes.POINTER(LsrBackwardArgs), ALLOC_FN, _vp,
                                       _vp]),
     "lsr_mark_visible": (ctypes.c_int32, [ctypes.c_int32, _vp, _vp, _vp, _vp, _vp]),
+    "lsr_event_record_external": (ctypes.c_int32, [_vp, _vp]),
     "lsr_adam_step": (ctypes.c_int32, [ctypes.c_int64, _vp, _vp, _vp, _vp, ctypes.c_double, ctypes.c_double,
                                        ctypes.c_double, ctypes.c_double, ctypes.c_int64, _vp]),
     "lsr_adam_multi": (ctypes.c_int32, [ctypes.c_int32, ctypes.POINTER(LsrAdamTensor), ctypes.c_float, _vp, _vp,
@@ -678,3 +679,10 @@ def debug_render_timeline(kernel, n):
         out.append({"start": r[0], "end": r[1], "tile": r[2] if r[2] < 2 ** 31 else r[2] - 2 ** 32, "slot": r[3],
                     "load": r[4], "compact": r[5], "walk": r[6], "batches": r[7]})
     return out
+
+
+def event_record_external(event, stream):
+    """Records torch.cuda.Event `event` on torch.cuda.Stream `stream` as an external event
+    (include/lsr.h lsr_event_record_external): inside a capture, an external event-record node."""
+    _check(load().lsr_event_record_external(ctypes.c_void_p(event.cuda_event), ctypes.c_void_p(stream.cuda_stream)),
+           "lsr_event_record_external")

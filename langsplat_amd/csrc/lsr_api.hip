@@ -351,6 +351,15 @@ static hipError_t wait_and_fill_language(const lsr_forward_args* a, const Layout
                                 stream);
 }
 
+int32_t lsr_event_record_external(void* event, void* stream)
+{
+    if (!event) return fail(LSR_ERR_INVALID, "lsr_event_record_external: null event");
+    const hipError_t e = hipEventRecordWithFlags(static_cast<hipEvent_t>(event), static_cast<hipStream_t>(stream),
+                                                 hipEventRecordExternal);
+    if (e != hipSuccess) return fail(LSR_ERR_HIP, "lsr_event_record_external", e);
+    return LSR_OK;
+}
+
 int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_fn alloc, void* user,
                     void* stream_ptr, int64_t* num_rendered)
 {

@@ -413,30 +413,51 @@ __global__ __launch_bounds__(kPreThreads) __attribute__((amdgpu_waves_per_eu(
 
 // Deferred language feature (lsr_forward_args.language_ready): the records' language slots of the
 // visible Gaussians, {b, f0, f1, f2} = record[3 i + 2] with b kept, after the stream has waited for
-// the feature's update.  Same values (and activation) as the preprocess writes otherwise.
-__global__ __launch_bounds__(256) void k_fill_language(int P, const float* __restrict__ lang, int raw,
-                                                       const int32_t* __restrict__ radii, float4* __restrict__ record)
+// the feature's update.  Same values (and activation) as the preprocess writes otherwise.  Four
+// Gaussians per thread: their 48 feature bytes and 16 radius bytes are whole dwordx4 loads (a wave
+// reads 3 KB + 1 KB contiguous); each record gets its three slots only (a dword and a dwordx2 store,
+// no read of the colour word b).  On the pipelined step's critical path.
+__device__ __forceinline__ void fill_one(float4* record, size_t i, float f0, float f1, float f2, int raw)
 {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= P || radii[i] <= 0) return;
-    float f0 = lang[3 * (size_t)i], f1 = lang[3 * (size_t)i + 1], f2 = lang[3 * (size_t)i + 2];
     if (raw & LSR_RAW_LANGUAGE) {
         const float3 f = act_lang(f0, f1, f2);
         f0 = f.x;
         f1 = f.y;
         f2 = f.z;
     }
-    // the three slots only (a dword and a dwordx2 store): no read of the record's colour word b
-    float* r = reinterpret_cast<float*>(record + 3 * (size_t)i + 2);
+    float* r = reinterpret_cast<float*>(record + 3 * i + 2);
     r[1] = f0;
     *reinterpret_cast<float2*>(r + 2) = make_float2(f1, f2);
+}
+
+__global__ __launch_bounds__(256) void k_fill_language(int P, const float* __restrict__ lang, int raw,
+                                                       const int32_t* __restrict__ radii, float4* __restrict__ record)
+{
+    const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;  // Gaussians 4 q .. 4 q + 3
+    const int64_t i0 = 4 * q;
+    if (i0 >= P) return;
+    const bool vec = i0 + 3 < P && ((reinterpret_cast<uintptr_t>(lang) | reinterpret_cast<uintptr_t>(radii)) & 15) == 0;
+    if (vec) {
+        const int4 r = reinterpret_cast<const int4*>(radii)[q];
+        const float4* l4 = reinterpret_cast<const float4*>(lang) + 3 * q;
+        const float4 a = l4[0], b = l4[1], c = l4[2];  // {f0 f1 f2 | f0} {f1 f2 | f0 f1} {f2 | f0 f1 f2}
+        if (r.x > 0) fill_one(record, (size_t)i0, a.x, a.y, a.z, raw);
+        if (r.y > 0) fill_one(record, (size_t)i0 + 1, a.w, b.x, b.y, raw);
+        if (r.z > 0) fill_one(record, (size_t)i0 + 2, b.z, b.w, c.x, raw);
+        if (r.w > 0) fill_one(record, (size_t)i0 + 3, c.y, c.z, c.w, raw);
+        return;
+    }
+    for (int64_t i = i0; i < P && i < i0 + 4; i++)
+        if (radii[i] > 0) fill_one(record, (size_t)i, lang[3 * i], lang[3 * i + 1], lang[3 * i + 2], raw);
 }
 
 hipError_t launch_fill_language(int P, const float* lang, int raw, const int32_t* radii, float4* record,
                                 hipStream_t s)
 {
     if (P == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_fill_language, dim3((P + 255) / 256), dim3(256), 0, s, P, lang, raw, radii, record);
+    const int64_t threads = ((int64_t)P + 3) / 4;
+    hipLaunchKernelGGL(k_fill_language, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, P, lang, raw, radii,
+                       record);
     return hipGetLastError();
 }
 

@@ -32,7 +32,6 @@ stay bound to the previous step's stream.
 from __future__ import annotations
 
 import contextlib
-import ctypes
 
 import torch
 
@@ -89,28 +88,6 @@ class ViewPipeline:
         cur = torch.cuda.current_stream()
         for s in self.streams:
             cur.wait_stream(s)
-
-
-def _record_external(event, stream):
-    """hipEventRecordWithFlags(event, stream, hipEventRecordExternal): inside a capture, an external
-    event-record node another graph's external wait node waits on (torch exposes no such record)."""
-    lib = _hip_runtime()
-    err = lib.hipEventRecordWithFlags(ctypes.c_void_p(event.cuda_event), ctypes.c_void_p(stream.cuda_stream),
-                                      ctypes.c_uint(1))
-    if err != 0:
-        raise RuntimeError(f"hipEventRecordWithFlags failed ({err})")
-
-
-_HIP = None
-
-
-def _hip_runtime():
-    global _HIP
-    if _HIP is None:
-        _HIP = ctypes.CDLL("libamdhip64.so")  # the runtime torch already loaded (same soname)
-        _HIP.hipEventRecordWithFlags.restype = ctypes.c_int
-        _HIP.hipEventRecordWithFlags.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint]
-    return _HIP
 
 
 class PipelinedGraphStep:
@@ -193,7 +170,7 @@ class PipelinedGraphStep:
             loss.backward()
             B.wait_stream(A)
             self.optimizer.step()
-            _record_external(self.ev_update, B)
+            _native.event_record_external(self.ev_update, B)
         self.g_bwd[s] = g
 
     def _capture_forward(self, s, cap):
