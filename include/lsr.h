@@ -85,10 +85,7 @@ enum lsr_raw_flags {
  * LSR_FWD_ZERO_GRAD_RECORDS, and lsr_backward_args.dL_dloss only for a forward that fused the loss
  * (out_loss set): the forward records both in its image buffer, and with settings.debug the
  * backward checks them and fails with LSR_ERR_INVALID instead of reading stale records or codes. */
-/* LSR_FWD_READY_EXTERNAL: the wait on language_ready is enqueued with hipEventWaitExternal, so that
- * inside a HIP graph capture it becomes an external event-wait node (the event is recorded by
- * ANOTHER graph, with hipEventRecordExternal: langsplat_amd.pipeline.PipelinedGraphStep). */
-enum lsr_forward_flags { LSR_FWD_ZERO_GRAD_RECORDS = 1, LSR_FWD_READY_EXTERNAL = 2 };
+enum lsr_forward_flags { LSR_FWD_ZERO_GRAD_RECORDS = 1 };
 enum lsr_backward_flags { LSR_BWD_RECORDS_ZEROED = 1 };
 
 /* GaussianRasterizationSettings (gaussian_renderer/__init__.py:37-51), device-pointer form. */
@@ -161,7 +158,7 @@ typedef struct lsr_forward_args {
      * language feature on another stream, so that update overlaps this view's geometry work
      * (langsplat_amd.distributed.UpdateOverlap, langsplat_amd.pipeline).  Results are identical to a
      * call without it.  In capacity mode (a graph capture) the event is one recorded in the same
-     * capture, or, with LSR_FWD_READY_EXTERNAL, one another graph records as an external event. */
+     * capture (a join of two branches). */
     void* language_ready;
 } lsr_forward_args;
 
@@ -271,12 +268,6 @@ int32_t lsr_profile_select(const char* stages);
 /* Records the events on every `every`-th launch of a selected stage only (default 1; reset by each
  * call): a timed run samples its dominant kernel's duration at a fraction of the events' cost. */
 int32_t lsr_profile_sample(int32_t every);
-
-/* hipEventRecordWithFlags(event, stream, hipEventRecordExternal) through this library's HIP runtime
- * (the one the rasterizer's streams and events belong to): inside a stream capture, an external
- * event-record node -- the update another graph's forward waits for with LSR_FWD_READY_EXTERNAL
- * (langsplat_amd.pipeline.PipelinedGraphStep). */
-int32_t lsr_event_record_external(void* event, void* stream);
 
 /* _C.mark_visible: visible[i] = 1 iff Gaussian i passes the near-plane frustum test. */
 int32_t lsr_mark_visible(int32_t P, const float* means3D, const float* viewmatrix,

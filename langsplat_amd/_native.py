@@ -27,7 +27,6 @@ ADAM_STEP_WORDS = 49  # include/lsr.h LSR_ADAM_STEP_WORDS
 # lsr_raw_flags (include/lsr.h): inputs are GaussianModel's raw parameters
 RAW_OPACITY, RAW_SCALES, RAW_ROTATIONS, RAW_LANGUAGE = 1, 2, 4, 8
 FWD_ZERO_GRAD_RECORDS = 1  # lsr_forward_flags
-FWD_READY_EXTERNAL = 2
 BWD_RECORDS_ZEROED = 1     # lsr_backward_flags
 _vp = ctypes.c_void_p
 
@@ -105,7 +104,6 @@ SIGNATURES = {
     "lsr_backward": (ctypes.c_int32, [ctypes.POINTER(LsrSettings), ctypes.POINTER(LsrBackwardArgs), ALLOC_FN, _vp,
                                       _vp]),
     "lsr_mark_visible": (ctypes.c_int32, [ctypes.c_int32, _vp, _vp, _vp, _vp, _vp]),
-    "lsr_event_record_external": (ctypes.c_int32, [_vp, _vp]),
     "lsr_adam_step": (ctypes.c_int32, [ctypes.c_int64, _vp, _vp, _vp, _vp, ctypes.c_double, ctypes.c_double,
                                        ctypes.c_double, ctypes.c_double, ctypes.c_int64, _vp]),
     "lsr_adam_multi": (ctypes.c_int32, [ctypes.c_int32, ctypes.POINTER(LsrAdamTensor), ctypes.c_float, _vp, _vp,
@@ -267,30 +265,17 @@ class capacity:
         capacity._tls.cur = self._prev
 
 
-class _ExternalEvent:
-    """A torch.cuda.Event marked as recorded by another graph (language_ready(..., external=True))."""
-
-    def __init__(self, event):
-        self.event = event
-
-    @property
-    def cuda_event(self):
-        return self.event.cuda_event
-
-
 class language_ready:
     """Within the block, the rasterizer forwards of this thread defer the language feature
     (include/lsr.h lsr_forward_args.language_ready): preprocess, depth order and binning run at
     once, and the stream waits for `event` (a torch.cuda.Event recorded after the language feature's
     last update, on any stream) only before the feature enters the records and the compositing
-    starts.  event None: off (the block is a no-op).  external: the event is recorded by another
-    HIP graph (hipEventRecordExternal) and the wait is captured as an external event-wait node
-    (include/lsr.h LSR_FWD_READY_EXTERNAL)."""
+    starts.  event None: off (the block is a no-op)."""
 
     _tls = threading.local()
 
-    def __init__(self, event, external: bool = False):
-        self.event = event if event is None or not external else _ExternalEvent(event)
+    def __init__(self, event):
+        self.event = event
 
     @staticmethod
     def active():
@@ -473,8 +458,6 @@ def rasterize_gaussians(rs, means3D, shs, colors_precomp, language_feature, opac
     ready = language_ready.active()
     if ready is not None and language_feature is not None:
         a.language_ready = ready.cuda_event
-        if isinstance(ready, _ExternalEvent):
-            a.flags |= FWD_READY_EXTERNAL
         keep.append(ready)
     if cap is not None:
         a.capacity_rendered = cap.rendered
@@ -680,9 +663,3 @@ def debug_render_timeline(kernel, n):
                     "load": r[4], "compact": r[5], "walk": r[6], "batches": r[7]})
     return out
 
-
-def event_record_external(event, stream):
-    """Records torch.cuda.Event `event` on torch.cuda.Stream `stream` as an external event
-    (include/lsr.h lsr_event_record_external): inside a capture, an external event-record node."""
-    _check(load().lsr_event_record_external(ctypes.c_void_p(event.cuda_event), ctypes.c_void_p(stream.cuda_stream)),
-           "lsr_event_record_external")

@@ -340,24 +340,13 @@ int32_t lsr_state_layout_of(int32_t P, int32_t width, int32_t height, int64_t nu
 // The deferred language feature (lsr_forward_args.language_ready): the feature's update (another
 // stream) has overlapped everything enqueued so far; the stream waits for it, then the visible
 // Gaussians' records receive the feature.  Inside a graph capture the event is one recorded in the
-// same capture (a join of the two branches), or with LSR_FWD_READY_EXTERNAL one another graph records
-// (an external event-wait node).
+// same capture (a join of the two branches).
 static hipError_t wait_and_fill_language(const lsr_forward_args* a, const Layout& L, char* geom, hipStream_t stream)
 {
-    hipError_t e = hipStreamWaitEvent(stream, static_cast<hipEvent_t>(a->language_ready),
-                                      (a->flags & LSR_FWD_READY_EXTERNAL) ? hipEventWaitExternal : 0);
+    hipError_t e = hipStreamWaitEvent(stream, static_cast<hipEvent_t>(a->language_ready), 0);
     if (e != hipSuccess) return e;
     return launch_fill_language(a->P, a->language_feature, a->raw, a->radii, reinterpret_cast<float4*>(geom + L.record),
                                 stream);
-}
-
-int32_t lsr_event_record_external(void* event, void* stream)
-{
-    if (!event) return fail(LSR_ERR_INVALID, "lsr_event_record_external: null event");
-    const hipError_t e = hipEventRecordWithFlags(static_cast<hipEvent_t>(event), static_cast<hipStream_t>(stream),
-                                                 hipEventRecordExternal);
-    if (e != hipSuccess) return fail(LSR_ERR_HIP, "lsr_event_record_external", e);
-    return LSR_OK;
 }
 
 int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_fn alloc, void* user,
@@ -380,8 +369,7 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
         return fail(LSR_ERR_INVALID, "lsr_forward: settings tensors missing");
     if (a->raw & ~(LSR_RAW_OPACITY | LSR_RAW_SCALES | LSR_RAW_ROTATIONS | LSR_RAW_LANGUAGE))
         return fail(LSR_ERR_INVALID, "lsr_forward: unknown raw flag");
-    if (a->flags & ~(LSR_FWD_ZERO_GRAD_RECORDS | LSR_FWD_READY_EXTERNAL))
-        return fail(LSR_ERR_INVALID, "lsr_forward: unknown flag");
+    if (a->flags & ~LSR_FWD_ZERO_GRAD_RECORDS) return fail(LSR_ERR_INVALID, "lsr_forward: unknown flag");
     if (a->shs_rest && (!a->shs || a->M < 2))
         return fail(LSR_ERR_INVALID, "lsr_forward: shs_rest needs shs (features_dc) and M >= 2");
     if (a->capacity_rendered < 0 || (a->capacity_rendered > 0 && a->capacity_entries <= 0) ||

@@ -91,32 +91,31 @@ class ViewPipeline:
 
 
 class PipelinedGraphStep:
-    """ViewPipeline's order replayed from HIP graphs: every step is one full language step -- view k's
-    backward and Adam on one stream, view k+1's forward on the other, its compositing waiting for the
-    update -- with no host work between the kernels (langsplat_amd.graph.GraphedStep is the
-    unpipelined form).
+    """ViewPipeline's order captured into HIP graphs: every replay is one full language step --
+    view k's backward and Adam on one branch, view k+1's geometry stages on the other, joined before
+    view k+1's compositing -- with no host work between the kernels (langsplat_amd.graph.GraphedStep
+    is the unpipelined form).
 
-    The HIP runtime launches one graph's kernels on one queue in capture order, so two branches of a
-    single captured graph barely overlap (measured: DESIGN.md §5b).  Here each step is two graph
-    launches on two streams: G_bwd (backward + Adam, ending in an external event record of the update)
-    and G_fwd (the whole forward of the next view; the rasterizer's wait for the update is an external
-    event-wait node, include/lsr.h LSR_FWD_READY_EXTERNAL, so the geometry stages run at once).  A
-    backward reads what the previous step's forward wrote, so forwards alternate between two static
-    buffer sets (_native.static_buffers: the same addresses at every forward): per set s a forward
-    graph G_fwd[s] and a backward graph G_bwd[s].  Host events order the launches: G_bwd[s] after
-    G_fwd[s]; G_fwd[s] after the previous G_bwd[s] (its buffers' last reader).  The rasterizer runs
-    in capacity mode (capacities from eager warm-up views, with headroom; a view over capacity is
-    flagged, check() re-captures).  N = 1: the optimizer is captured (its step count advances on the
-    device); a collective is not captured.
+    The HIP runtime launches a graph's kernels on one queue in capture order, so the two branches
+    overlap only where independent kernels meet (measured); the eager ViewPipeline
+    overlaps more when the host keeps ahead.  (Two graphs on two streams joined by external event
+    nodes would overlap fully, but this runtime refuses hipEventRecordExternal in a capture and
+    crashes on an external wait.)
+
+    A replay's backward reads what the PREVIOUS replay's forward wrote, so the forwards alternate
+    between two static buffer sets (_native.static_buffers: the same addresses at every forward) and
+    two graphs, G1 (backward of set 0, forward into set 1) and G0 (the reverse), replayed in turn.
+    The rasterizer runs in capacity mode (capacities from eager warm-up views, with headroom; a view
+    over capacity is flagged, check() re-captures).  N = 1: the optimizer is captured (its step count
+    advances on the device); a collective is not captured.
 
         g = PipelinedGraphStep(lambda: render(...)["language_l1"], [gaussians._language_feature], optimizer)
         for it in range(iterations):
-            loss = g.replay()   # the loss of the view this step composited (its backward: next step)
-        g.synchronize(); g.check(); g.sync()
+            loss = g.replay()   # the loss of the view this replay composited (its backward: next replay)
+        g.check(); g.sync()
 
     forward_fn() runs render() + the loss and returns the loss (no backward).  The graphs own the
-    parameters' .grad tensors.  A returned loss is written on the pipeline's forward stream: read it
-    after synchronize() (or with .item() after torch.cuda.synchronize())."""
+    parameters' .grad tensors."""
 
     def __init__(self, forward_fn, params, optimizer, headroom: float = 1.125, warmup: int = 2):
         self.forward_fn = forward_fn
@@ -126,15 +125,11 @@ class PipelinedGraphStep:
         self.warmup = int(warmup)
         dev = self.params[0].device
         self.sets = (_native.static_buffers(), _native.static_buffers())
-        self.fwd_stream, self.bwd_stream = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+        self.streams = (torch.cuda.Stream(dev), torch.cuda.Stream(dev))
         self.overflow = torch.zeros((), dtype=torch.int32, device=dev)
-        self.g_fwd = [None, None]
-        self.g_bwd = [None, None]
+        self.graphs = [None, None]
         self.static_loss = [None, None]
-        self.ev_fwd = [torch.cuda.Event(), torch.cuda.Event()]
-        self.ev_bwd = [torch.cuda.Event(), torch.cuda.Event()]
-        self.ev_update = torch.cuda.Event()
-        self.next = 0  # the set whose backward the next step runs
+        self.next = 1
         self.captures = 0
         self.rendered = self.entries = 0
 
@@ -156,94 +151,71 @@ class PipelinedGraphStep:
         self.rendered = max(int(r * self.headroom) + 1024, int(min_rendered))
         self.entries = max(int(e * self.headroom) + 1024, int(min_entries))
 
-    def _capture_backward(self, s, loss):
-        """G_bwd[s]: the backward of set s's forward (autograd runs it on the forward stream, forked
-        into this capture) + the optimizer step, then the update's external event record."""
-        A, B = self.fwd_stream, self.bwd_stream
-        for p in self.params:
-            p.grad = None  # the captured backward assigns its own .grad (no accumulate)
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=B):
-            fork = torch.cuda.Event()
-            fork.record(B)
-            A.wait_event(fork)
-            loss.backward()
-            B.wait_stream(A)
-            self.optimizer.step()
-            _native.event_record_external(self.ev_update, B)
-        self.g_bwd[s] = g
-
-    def _capture_forward(self, s, cap):
-        """G_fwd[s]: the next view's forward into set s, its compositing behind the update."""
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=self.fwd_stream):
-            with cap, self.sets[s], _native.language_ready(self.ev_update, external=True):
-                loss = self.forward_fn()
-        self.g_fwd[s] = g
-        self.static_loss[s] = loss.detach()  # the set's static loss tensor
-        return loss
-
     def capture(self, min_rendered: int = 0, min_entries: int = 0):
         self._measure(min_rendered, min_entries)
-        self.g_fwd, self.g_bwd = [None, None], [None, None]
+        self.graphs = [None, None]
+        self.static_loss = [None, None]
         self.optimizer.prepare_capture()
         cap = _native.capacity(self.rendered, self.entries, self.overflow)
-        A, B = self.fwd_stream, self.bwd_stream
         cur = torch.cuda.current_stream()
-        A.wait_stream(cur)
-        B.wait_stream(cur)
+        for s in self.streams:
+            s.wait_stream(cur)
         # eager forwards allocate both sets at their capacity sizes (no allocation may happen during a
-        # capture); set 0's is the prologue, whose backward the first step runs
-        with torch.cuda.stream(A):
-            for s in (1, 0):
-                with cap, self.sets[s]:
+        # capture); set 0's is the prologue: the first replay (G1) runs its backward
+        for parity in (1, 0):
+            with torch.cuda.stream(self.streams[parity]), cap, self.sets[parity]:
+                prev = self.forward_fn()
+        pool = torch.cuda.graph_pool_handle()
+        for parity in (1, 0):
+            bwd_s, fwd_s = self.streams[1 - parity], self.streams[parity]
+            for p in self.params:
+                p.grad = None  # the captured backward assigns its own .grad (no accumulate)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=pool, stream=bwd_s):
+                fork = torch.cuda.Event()
+                fork.record(bwd_s)
+                fwd_s.wait_event(fork)
+                prev.backward()       # on bwd_s: autograd runs it on its forward's stream
+                prev = None           # release the autograd graph (and its AccumulateGrad nodes)
+                self.optimizer.step()
+                ready = torch.cuda.Event()
+                ready.record(bwd_s)
+                with torch.cuda.stream(fwd_s), cap, self.sets[parity], _native.language_ready(ready):
                     loss = self.forward_fn()
-        self.static_loss[0] = loss.detach()
-        self.ev_update.record(B)  # creates the event
-        torch.cuda.synchronize()
-        self._capture_backward(0, loss)   # backward of the prologue (set 0)
-        loss = None
-        loss = self._capture_forward(1, cap)
-        self._capture_backward(1, loss)
-        loss = None
-        self._capture_forward(0, cap)     # its autograd graph is not needed: G_bwd[0] holds the kernels
-        self.ev_fwd[0].record(A)          # the prologue's forward: the first backward waits for it
-        self.next = 0
+                bwd_s.wait_stream(fwd_s)
+            self.graphs[parity] = g
+            self.static_loss[parity] = loss.detach()  # the set's static loss tensor
+            prev = loss
+            loss = None
+        # G0's forward (set 0) is never backwarded by Python: the graphs hold the kernels it captured
+        # (replays change the views' data in place, e.g. a camera's matrices copied into the tensors
+        # the captured settings point at; the graphs' launches stay the same)
+        del prev
+        cur.wait_stream(self.streams[0])
+        cur.wait_stream(self.streams[1])
+        self.next = 1
         self.captures += 1
         return self
 
     def replay(self) -> torch.Tensor:
-        if self.g_fwd[0] is None:
+        if self.graphs[0] is None:
             self.capture()
-        s = self.next
-        n = 1 - s
-        A, B = self.fwd_stream, self.bwd_stream
-        B.wait_event(self.ev_fwd[s])          # set s's forward has run
-        with torch.cuda.stream(B):
-            self.g_bwd[s].replay()            # its backward + Adam (records the update)
-        self.ev_bwd[s].record(B)
-        A.wait_event(self.ev_bwd[n])          # set n's last reader (the previous step's backward)
-        with torch.cuda.stream(A):
-            self.g_fwd[n].replay()            # the next view into set n, compositing behind the update
-        self.ev_fwd[n].record(A)
-        self.next = n
-        return self.static_loss[n]
+        k = self.next
+        self.graphs[k].replay()
+        self.next = 1 - k
+        return self.static_loss[k]
 
     def synchronize(self):
-        """The caller's current stream waits for every step enqueued so far."""
-        cur = torch.cuda.current_stream()
-        cur.wait_stream(self.fwd_stream)
-        cur.wait_stream(self.bwd_stream)
+        """A replay runs on the caller's current stream (its branches join before it ends): nothing
+        to wait for beyond stream order."""
 
     def sync(self):
         """The optimizer state's step counts from the device (a device-to-host copy)."""
-        self.synchronize()
         self.optimizer.sync_steps()
 
     def check(self) -> bool:
         """True if every replay's view fitted its capacities.  Otherwise re-capture with twice the
         capacities (the over-capacity views were not rasterized) and return False."""
-        self.synchronize()
         if int(self.overflow.item()) == 0:
             return True
         self.sync()
