@@ -279,7 +279,6 @@ static int32_t render_forward_and_finish(const lsr_settings* s, const lsr_forwar
     rp.sched_lists = reinterpret_cast<uint32_t*>(image + L.tile_lists);
     rp.split_pool = reinterpret_cast<float*>(image + L.split_pool);
     rp.split_desc = reinterpret_cast<uint4*>(image + L.split_desc);
-    rp.split_cap = L.split_cap;
     rp.out_color = a->out_color;
     rp.out_lang = a->out_language_feature;
     if (a->flags & LSR_FWD_ZERO_GRAD_RECORDS) {
@@ -635,7 +634,6 @@ int32_t lsr_backward(const lsr_settings* s, const lsr_backward_args* a, lsr_allo
     rp.sched_lists = reinterpret_cast<uint32_t*>(image + L.tile_lists);
     rp.split_pool = reinterpret_cast<float*>(image + L.split_pool);
     rp.split_desc = reinterpret_cast<uint4*>(image + L.split_desc);
-    rp.split_cap = L.split_cap;
     rp.dL_dcolor = a->dL_dout_color;
     rp.dL_dlang = a->dL_dout_language_feature;
     rp.dL_dloss = a->dL_dloss;

@@ -19,7 +19,6 @@ enum Counter : int {
     kCntKeyMin = 5,      // smallest visible depth key (float bits)
     kCntKeyMax = 6,      // largest visible depth key
     kCntOverflow = 7,    // capacity mode: the view exceeds the caller's capacities (nothing is binned)
-    kCntSplit = 8,       // render forward: replay-boundary state slots taken (split replay)
     kCntSlots = 16
 };
 constexpr uint32_t kFwdZeroedRecords = 1u;  // the language step's gradient records cleared (the render
@@ -33,7 +32,8 @@ constexpr int kCntBwdClass = kCntSlots + kWorkClasses;
 constexpr int kCntWords = kCntSlots + 2 * kWorkClasses;
 
 // Split replay (lsr_render.hip): the render forward records each pixel's state (T and the colour /
-// feature sums) before list entries 256, 512, 768 of a tile it is still compositing, so the backward
+// feature sums) before list entries 256, 512, 768 of a tile it is still compositing (in the tile's
+// own kSplitMax slots), so the backward
 // can replay a long tile as up to kSplitItems independent work items of <= 256 entries each
 // (the last one: the rest) instead of one long serial chain.
 constexpr int kSplitMax = 3;                // recorded boundaries per tile
@@ -81,8 +81,7 @@ struct Layout {
     size_t geom_bytes;
     // image (per pixel / tile)
     size_t counters, ranges, final_T, n_contrib, tile_lists, loss_partial, loss_code;
-    size_t split_desc, split_pool;  // per tile {boundaries, slots}; slots x kSplitVals x 256 floats
-    uint32_t split_cap;             // state slots (one per tile)
+    size_t split_desc, split_pool;  // per tile {boundaries, -}; per tile kSplitMax x kSplitVals x 256 floats
     size_t image_bytes;
     // binning (point_list per tile instance, the rest per super-tile entry / segment)
     size_t point_list, cover, super_keys, super_vals, alt_keys, alt_vals, bin_radix_hist, bin_radix_hist_scan;
@@ -167,9 +166,8 @@ inline Layout make_layout(int P, int W, int H, int64_t R, int64_t E)
     L.tile_lists = take(4 * kWorkClasses * T * (1 + kSplitItems));
     L.loss_partial = take(8 * T);                    // fused loss, P == 0: one double per workgroup
     L.loss_code = take(HW > 0 ? HW : 1);             // fused loss: per-pixel sign / mask code
-    L.split_cap = (uint32_t)T;
     L.split_desc = take(16 * T);
-    L.split_pool = take(4 * (size_t)kSplitVals * kTilePixels * T);
+    L.split_pool = take(4 * (size_t)kSplitMax * kSplitVals * kTilePixels * T);
     L.image_bytes = o;
 
     o = 0;
@@ -247,10 +245,10 @@ struct RenderParams {
     // sched_lists[kWorkClasses * tiles + c * kSplitItems * tiles]); null: launch order
     uint32_t* sched_counts;
     uint32_t* sched_lists;
-    // split replay (scheduled launches only; null: off): per-pixel state slots, per-tile descriptors
+    // split replay (scheduled launches only; null: off): per tile kSplitMax per-pixel state slots and
+    // a descriptor {boundaries recorded below the replay length, -, -, -}
     float* split_pool;
     uint4* split_desc;
-    uint32_t split_cap;
     int prio;  // wave priority by launch position (longest tiles highest), 0: off
     int geo;   // backward: the conic / opacity partials are needed (geometry gradients)
     float4* zero_records;  // forward: clear these zero_records_n4 float4s (grid-stride), or null

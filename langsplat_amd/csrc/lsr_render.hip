@@ -479,9 +479,6 @@ __global__ __launch_bounds__(kTilePixels, 7) void k_render_forward(RenderParams 
     // second entry of a pair without testing i + 1 < n (its result is discarded then)
     __shared__ uint16_t sL[kThreads / 64][kThreads + 1];
     __shared__ uint32_t s_last;
-    // split replay: [0] boundaries recorded (a prefix of 256, 512, 768), [j] the slot of boundary j,
-    // [kSplitMax + 1] the slot thread 0 took for the current batch (broadcast)
-    __shared__ uint32_t s_split[kSplitMax + 2];
 
     const int T = p.gx * p.gy;
     if (p.zero_records) {  // the backward's gradient records: stores beside the VALU-bound walk
@@ -512,10 +509,8 @@ __global__ __launch_bounds__(kTilePixels, 7) void k_render_forward(RenderParams 
     const uint2 range = p.ranges[tile];
     const uint32_t start = range.x, end = range.y;
     const bool inside = px < p.W && py < p.H;
-    if (t == 0) {
-        s_last = 0;
-        s_split[0] = 0;
-    }
+    if (t == 0) s_last = 0;
+    uint32_t nrec = 0;  // split replay: boundaries recorded (256, 512, ... up to kSplitMax; uniform)
 
     FwdPixel q{inside ? 1.0f : -1.0f, make_f2(0.f, 0.f), make_f2(0.f, 0.f), make_f2(0.f, 0.f), 0u, 0u};
     PhaseTicks ph;
@@ -532,26 +527,12 @@ __global__ __launch_bounds__(kTilePixels, 7) void k_render_forward(RenderParams 
         }
         if (kStats) ph.batches++;
         if (p.split_pool && base != start && base - start <= (uint32_t)(kSplitMax * kThreads)) {
-            // split replay: every pixel's state before list entry 256 j, while some pixel composites
-            // (a slot per boundary from the grid-wide counter; the recorded boundaries stay a prefix)
-            const uint32_t j = (base - start) / kThreads;
-            if (t == 0) {
-                uint32_t slot = 0xFFFFFFFFu;
-                if (s_split[0] == j - 1u) {
-                    slot = atomicAdd(p.sched_counts + kCntSplit, 1u);
-                    if (slot < p.split_cap) {
-                        s_split[j] = slot;
-                        s_split[0] = j;
-                    } else {
-                        slot = 0xFFFFFFFFu;
-                    }
-                }
-                s_split[kSplitMax + 1] = slot;
-            }
-            __syncthreads();
-            const uint32_t slot = s_split[kSplitMax + 1];
-            if (slot != 0xFFFFFFFFu) {
-                float* st = p.split_pool + (size_t)slot * (kSplitVals * kThreads) + t;
+            // split replay: every pixel's state before list entry 256 j while some pixel composites,
+            // in the tile's own slot j - 1 (no allocation: a grid-wide counter cost ~40 us of
+            // contended cross-XCD atomics)
+            // (a pixel already done is never started from here: its last contributor lies before)
+            if (q.T > 0.0f) {
+                float* st = p.split_pool + ((size_t)tile * kSplitMax + nrec) * (kSplitVals * kThreads) + t;
                 st[0] = q.T;
                 st[kThreads] = q.C01.x;
                 st[2 * kThreads] = q.C01.y;
@@ -560,6 +541,7 @@ __global__ __launch_bounds__(kTilePixels, 7) void k_render_forward(RenderParams 
                 st[5 * kThreads] = q.F12.x;
                 st[6 * kThreads] = q.F12.y;
             }
+            nrec++;
         }
         const uint32_t idx = base + t;
         if (idx < end) {
@@ -628,10 +610,10 @@ __global__ __launch_bounds__(kTilePixels, 7) void k_render_forward(RenderParams 
     // the backward's work items: the tile's replay [0, s_last) cut at the recorded boundaries below
     // s_last (split replay), each appended to the class of its length
     const uint32_t maxl = s_last;
-    const uint32_t nsplit = p.split_pool && maxl > 0 ? min(s_split[0], (maxl - 1u) / (uint32_t)kThreads) : 0u;
+    const uint32_t nsplit = p.split_pool && maxl > 0 ? min(nrec, (maxl - 1u) / (uint32_t)kThreads) : 0u;
     if (t == 0 && p.sched_counts && maxl > 0) {
         uint32_t* bwd_lists = p.sched_lists + (size_t)kWorkClasses * T;
-        if (p.split_pool) p.split_desc[tile] = make_uint4(nsplit, s_split[1], s_split[2], s_split[3]);
+        if (p.split_pool) p.split_desc[tile] = make_uint4(nsplit, 0u, 0u, 0u);
         for (uint32_t k = 0; k <= nsplit; k++) {
             const uint32_t lo = k * (uint32_t)kThreads, hi = k < nsplit ? lo + (uint32_t)kThreads : maxl;
             schedule_tile(p.sched_counts + kCntBwdClass, bwd_lists, kSplitItems * T, kSplitItems * tile + (int)k,
@@ -639,18 +621,27 @@ __global__ __launch_bounds__(kTilePixels, 7) void k_render_forward(RenderParams 
         }
     }
     // the recorded sums become the colour / feature composited BEHIND each boundary, normalised by
-    // the transmittance there -- the backward's running `acc` at that point: (C_final - C_front) / T_b
-    for (uint32_t j = 1; j <= nsplit; j++) {
-        float* st = p.split_pool + (size_t)s_split[j] * (kSplitVals * kThreads) + t;
-        const float Tb = st[0];
-        if (!(Tb > 0.0f)) continue;  // done before the boundary: the backward does not read it
-        const float inv = 1.0f / Tb;
-        st[kThreads] = (q.C01.x - st[kThreads]) * inv;
-        st[2 * kThreads] = (q.C01.y - st[2 * kThreads]) * inv;
-        st[3 * kThreads] = (q.C2F0.x - st[3 * kThreads]) * inv;
-        st[4 * kThreads] = (q.C2F0.y - st[4 * kThreads]) * inv;
-        st[5 * kThreads] = (q.F12.x - st[5 * kThreads]) * inv;
-        st[6 * kThreads] = (q.F12.y - st[6 * kThreads]) * inv;
+    // the transmittance there -- the backward's running `acc` at that point: (C_final - C_front) / T_b.
+    // Every slot's loads are issued before any is used: one memory round trip on the tile's
+    // critical path, not two per boundary.
+    // Only slots the backward reads: boundary 256 (j + 1) of a pixel whose last contributor lies past it
+    // (it was compositing there, so the forward stored its state).
+    if (nsplit > 0) {
+        float* st0 = p.split_pool + (size_t)tile * kSplitMax * (kSplitVals * kThreads) + t;
+        auto used = [&](int j) { return (uint32_t)j < nsplit && qlast > (uint32_t)(kThreads * (j + 1)); };
+        float v[kSplitMax][kSplitVals];
+#pragma unroll
+        for (int j = 0; j < kSplitMax; j++)
+#pragma unroll
+            for (int c = 0; c < kSplitVals; c++) v[j][c] = used(j) ? st0[(j * kSplitVals + c) * kThreads] : 1.0f;
+        const float cf[kSplitVals - 1] = {q.C01.x, q.C01.y, q.C2F0.x, q.C2F0.y, q.F12.x, q.F12.y};
+#pragma unroll
+        for (int j = 0; j < kSplitMax; j++) {
+            if (!used(j)) continue;
+            const float inv = 1.0f / v[j][0];
+#pragma unroll
+            for (int c = 1; c < kSplitVals; c++) st0[(j * kSplitVals + c) * kThreads] = (cf[c - 1] - v[j][c]) * inv;
+        }
     }
     if (kStats) {
         if (!ph.stopped && ph.batches) ph.lap(ph.walk);  // the last batch's walk
@@ -1219,8 +1210,7 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
         const uint4 desc = p.split_desc[tile];
         const uint32_t hi = lo + (uint32_t)kThreads;
         if (chunk < desc.x && q.last > hi) {
-            const uint32_t slot = chunk == 0 ? desc.y : (chunk == 1 ? desc.z : desc.w);
-            const float* st = p.split_pool + (size_t)slot * (kSplitVals * kThreads) + t;
+            const float* st = p.split_pool + ((size_t)tile * kSplitMax + chunk) * (kSplitVals * kThreads) + t;
             q.T = st[0];
             if (kColor) {
                 q.acc0 = st[kThreads];
@@ -1365,7 +1355,7 @@ hipError_t launch_render_backward(const RenderParams& pin, int tiles, hipStream_
     const bool color = p.dL_dcolor != nullptr;  // null: the colour image does not reach the loss
     const int variant = (feat ? 1 : 0) | (color ? 2 : 0) | (p.geo ? 4 : 0);
     if (!p.sched_counts || !split_replay()) p.split_pool = nullptr;
-    if (p.split_pool) tiles += (int)p.split_cap;  // the items: a tile's chunks beyond its first
+    if (p.split_pool) tiles *= kSplitItems;  // the items: up to kSplitItems chunks per tile
     if (render_stats_on()) tiles = debug_grid(tiles);
 #define LSR_BWD(S, V)                                                                                         \
     hipLaunchKernelGGL((k_render_backward<S, (V & 1) != 0, (V & 2) != 0, (V & 4) != 0>), dim3(tiles), \
