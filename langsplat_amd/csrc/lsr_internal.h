@@ -38,7 +38,8 @@ constexpr int kCntWords = kCntSlots + 2 * kWorkClasses;
 // (the last one: the rest) instead of one long serial chain.
 constexpr int kSplitMax = 3;                // recorded boundaries per tile
 constexpr int kSplitItems = kSplitMax + 1;  // backward work items per tile
-constexpr int kSplitVals = 7;               // T, colour (3), feature (3) per pixel
+constexpr int kSplitVals = 8;               // per pixel {T, colour (3)}, {feature (3), -}
+constexpr int kSplitSlots = kSplitMax + 1;  // per tile: the boundaries' states, then the final sums
 
 constexpr int kRadixThreads = 256;
 // preprocess workgroups: the SH staging takes 4 (3M + 1) bytes of LDS per thread, so 128-thread
@@ -81,7 +82,7 @@ struct Layout {
     size_t geom_bytes;
     // image (per pixel / tile)
     size_t counters, ranges, final_T, n_contrib, tile_lists, loss_partial, loss_code;
-    size_t split_desc, split_pool;  // per tile {boundaries, -}; per tile kSplitMax x kSplitVals x 256 floats
+    size_t split_desc, split_pool;  // per tile {boundaries, -}; per tile kSplitSlots x kSplitVals x 256 floats
     size_t image_bytes;
     // binning (point_list per tile instance, the rest per super-tile entry / segment)
     size_t point_list, cover, super_keys, super_vals, alt_keys, alt_vals, bin_radix_hist, bin_radix_hist_scan;
@@ -167,7 +168,7 @@ inline Layout make_layout(int P, int W, int H, int64_t R, int64_t E)
     L.loss_partial = take(8 * T);                    // fused loss, P == 0: one double per workgroup
     L.loss_code = take(HW > 0 ? HW : 1);             // fused loss: per-pixel sign / mask code
     L.split_desc = take(16 * T);
-    L.split_pool = take(4 * (size_t)kSplitMax * kSplitVals * kTilePixels * T);
+    L.split_pool = take(4 * (size_t)kSplitSlots * kSplitVals * kTilePixels * T);
     L.image_bytes = o;
 
     o = 0;

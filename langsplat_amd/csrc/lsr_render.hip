@@ -526,29 +526,25 @@ __global__ __launch_bounds__(kTilePixels, 7) void k_render_forward(RenderParams 
             break;
         }
         if (kStats) ph.batches++;
+        const uint32_t idx = base + t;
+        float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a, c = a;
+        if (idx < end) {  // the batch's record gathers first ...
+            const uint32_t g = g_next;
+            a = p.record[3 * (size_t)g];
+            b = p.record[3 * (size_t)g + 1];
+            c = p.record[3 * (size_t)g + 2];
+        }
         if (p.split_pool && base != start && base - start <= (uint32_t)(kSplitMax * kThreads)) {
-            // split replay: every pixel's state before list entry 256 j while some pixel composites,
-            // in the tile's own slot j - 1 (no allocation: a grid-wide counter cost ~40 us of
-            // contended cross-XCD atomics)
-            // (a pixel already done is never started from here: its last contributor lies before)
-            if (q.T > 0.0f) {
-                float* st = p.split_pool + ((size_t)tile * kSplitMax + nrec) * (kSplitVals * kThreads) + t;
-                st[0] = q.T;
-                st[kThreads] = q.C01.x;
-                st[2 * kThreads] = q.C01.y;
-                st[3 * kThreads] = q.C2F0.x;
-                st[4 * kThreads] = q.C2F0.y;
-                st[5 * kThreads] = q.F12.x;
-                st[6 * kThreads] = q.F12.y;
-            }
+            // ... then (younger, so the gathers' wait does not include them) split replay: every
+            // pixel's state before list entry 256 j while some pixel composites, two float4 per pixel
+            // in the tile's own slot j - 1 (a grid-wide slot counter cost ~40 us of contended
+            // cross-XCD atomics); a pixel already done is never started from here
+            float4* st = reinterpret_cast<float4*>(p.split_pool) + ((size_t)tile * kSplitSlots + nrec) * (2 * kThreads);
+            st[2 * t] = make_float4(q.T, q.C01.x, q.C01.y, q.C2F0.x);
+            st[2 * t + 1] = make_float4(q.C2F0.y, q.F12.x, q.F12.y, 0.0f);
             nrec++;
         }
-        const uint32_t idx = base + t;
         if (idx < end) {
-            const uint32_t g = g_next;
-            const float4 a = p.record[3 * (size_t)g];
-            const float4 b = p.record[3 * (size_t)g + 1];
-            const float4 c = p.record[3 * (size_t)g + 2];
             const float cut = power_cutoff(b.y);
             sA[t] = make_float4(a.x, a.y, -0.5f * a.z, -0.5f * b.x);
             sB[t] = make_float4(a.w, b.y, cut, 0.0f);
@@ -611,37 +607,29 @@ __global__ __launch_bounds__(kTilePixels, 7) void k_render_forward(RenderParams 
     // s_last (split replay), each appended to the class of its length
     const uint32_t maxl = s_last;
     const uint32_t nsplit = p.split_pool && maxl > 0 ? min(nrec, (maxl - 1u) / (uint32_t)kThreads) : 0u;
-    if (t == 0 && p.sched_counts && maxl > 0) {
-        uint32_t* bwd_lists = p.sched_lists + (size_t)kWorkClasses * T;
-        if (p.split_pool) p.split_desc[tile] = make_uint4(nsplit, 0u, 0u, 0u);
-        for (uint32_t k = 0; k <= nsplit; k++) {
-            const uint32_t lo = k * (uint32_t)kThreads, hi = k < nsplit ? lo + (uint32_t)kThreads : maxl;
-            schedule_tile(p.sched_counts + kCntBwdClass, bwd_lists, kSplitItems * T, kSplitItems * tile + (int)k,
-                          hi - lo);
+    // the backward's items into the longest-first class lists: the tile's full 256-entry chunks with
+    // ONE returning atomic on their class (+nsplit), its last chunk with another, in parallel (thread
+    // 1): an atomic per chunk put every heavy tile's chunks on one hot counter across the XCDs
+    if (t < 2 && p.sched_counts && maxl > 0) {
+        uint32_t* counts = p.sched_counts + kCntBwdClass;
+        uint32_t* lists = p.sched_lists + (size_t)kWorkClasses * T;
+        const size_t stride = (size_t)kSplitItems * T;
+        if (t == 0 && p.split_pool) p.split_desc[tile] = make_uint4(nsplit, maxl, 0u, 0u);
+        if (t == 0 && nsplit > 0) {
+            const int c = work_class((uint32_t)kThreads);
+            const uint32_t base = atomicAdd(&counts[c], nsplit);
+            for (uint32_t k = 0; k < nsplit; k++) lists[(size_t)c * stride + base + k] = kSplitItems * tile + k;
         }
+        if (t == (nsplit > 0 ? 1 : 0))
+            schedule_tile(counts, lists, (int)stride, kSplitItems * tile + (int)nsplit, maxl - nsplit * kThreads);
     }
-    // the recorded sums become the colour / feature composited BEHIND each boundary, normalised by
-    // the transmittance there -- the backward's running `acc` at that point: (C_final - C_front) / T_b.
-    // Every slot's loads are issued before any is used: one memory round trip on the tile's
-    // critical path, not two per boundary.
-    // Only slots the backward reads: boundary 256 (j + 1) of a pixel whose last contributor lies past it
-    // (it was compositing there, so the forward stored its state).
+    // the final sums, for the backward's running `acc` at each boundary, (C_final - C_front) / T_b: a
+    // store here (the tile's extra slot), the arithmetic in the backward -- normalising the slots in
+    // place needed a load round trip at the end of every long tile, i.e. on the kernel's critical path
     if (nsplit > 0) {
-        float* st0 = p.split_pool + (size_t)tile * kSplitMax * (kSplitVals * kThreads) + t;
-        auto used = [&](int j) { return (uint32_t)j < nsplit && qlast > (uint32_t)(kThreads * (j + 1)); };
-        float v[kSplitMax][kSplitVals];
-#pragma unroll
-        for (int j = 0; j < kSplitMax; j++)
-#pragma unroll
-            for (int c = 0; c < kSplitVals; c++) v[j][c] = used(j) ? st0[(j * kSplitVals + c) * kThreads] : 1.0f;
-        const float cf[kSplitVals - 1] = {q.C01.x, q.C01.y, q.C2F0.x, q.C2F0.y, q.F12.x, q.F12.y};
-#pragma unroll
-        for (int j = 0; j < kSplitMax; j++) {
-            if (!used(j)) continue;
-            const float inv = 1.0f / v[j][0];
-#pragma unroll
-            for (int c = 1; c < kSplitVals; c++) st0[(j * kSplitVals + c) * kThreads] = (cf[c - 1] - v[j][c]) * inv;
-        }
+        float4* fin = reinterpret_cast<float4*>(p.split_pool) + ((size_t)tile * kSplitSlots + kSplitMax) * (2 * kThreads);
+        fin[2 * t] = make_float4(q.C01.x, q.C01.y, q.C2F0.x, q.C2F0.y);
+        fin[2 * t + 1] = make_float4(q.F12.x, q.F12.y, 0.0f, 0.0f);
     }
     if (kStats) {
         if (!ph.stopped && ph.batches) ph.lap(ph.walk);  // the last batch's walk
@@ -1210,17 +1198,22 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
         const uint4 desc = p.split_desc[tile];
         const uint32_t hi = lo + (uint32_t)kThreads;
         if (chunk < desc.x && q.last > hi) {
-            const float* st = p.split_pool + ((size_t)tile * kSplitMax + chunk) * (kSplitVals * kThreads) + t;
-            q.T = st[0];
+            // the boundary's {T, colour sums}, {feature sums} and the tile's final sums (extra slot)
+            const float4* st = reinterpret_cast<const float4*>(p.split_pool) + (size_t)tile * kSplitSlots * (2 * kThreads);
+            const float4 s0 = st[chunk * 2 * kThreads + 2 * t], f0 = st[kSplitMax * 2 * kThreads + 2 * t];
+            const float inv = 1.0f / s0.x;
+            q.T = s0.x;
             if (kColor) {
-                q.acc0 = st[kThreads];
-                q.acc1 = st[2 * kThreads];
-                q.acc2 = st[3 * kThreads];
+                q.acc0 = (f0.x - s0.y) * inv;
+                q.acc1 = (f0.y - s0.z) * inv;
+                q.acc2 = (f0.z - s0.w) * inv;
             }
             if (kFeat) {
-                q.accF0 = st[4 * kThreads];
-                q.accF1 = st[5 * kThreads];
-                q.accF2 = st[6 * kThreads];
+                const float4 s1 = st[chunk * 2 * kThreads + 2 * t + 1];
+                const float4 f1 = st[kSplitMax * 2 * kThreads + 2 * t + 1];
+                q.accF0 = (f0.w - s1.x) * inv;
+                q.accF1 = (f1.x - s1.y) * inv;
+                q.accF2 = (f1.y - s1.z) * inv;
             }
             q.last = hi;
         }
