@@ -10,6 +10,7 @@ cfg=${2:-C3}
 root=$(pwd)
 export TMPDIR=/tmp
 export LSR_BENCH_RGB=0  # the RGB step is reported beside the bench line, not profiled here
+export LSR_PIPELINE=0   # serial forms only: overlapped kernels would stretch the per-kernel averages
 out=$root/gpurun_out
 b="$root/bench.py --config $cfg --no-cpu-baseline"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/${tag}_${cfg}_trace" -o trace -- \
