@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define LSR_ABI_VERSION 10
+#define LSR_ABI_VERSION 11
 
 enum lsr_status {
     LSR_OK = 0,
@@ -85,7 +85,13 @@ enum lsr_raw_flags {
  * LSR_FWD_ZERO_GRAD_RECORDS, and lsr_backward_args.dL_dloss only for a forward that fused the loss
  * (out_loss set): the forward records both in its image buffer, and with settings.debug the
  * backward checks them and fails with LSR_ERR_INVALID instead of reading stale records or codes. */
-enum lsr_forward_flags { LSR_FWD_ZERO_GRAD_RECORDS = 1 };
+/* LSR_FWD_NO_COLOR_GRAD: the caller promises that the backward of this forward gets no colour
+ * gradient (lsr_backward_args.dL_dout_color == NULL), as in LangSplat's language step
+ * (train.py:96-104: the loss reads the language image only).  The compositing kernel then stores
+ * only the transmittance and feature sums of its split-replay states (half the state traffic).  A
+ * backward with dL_dout_color after such a forward would start long tiles' replay chunks from
+ * missing colour sums: it is invalid, and with settings.debug it fails with LSR_ERR_INVALID. */
+enum lsr_forward_flags { LSR_FWD_ZERO_GRAD_RECORDS = 1, LSR_FWD_NO_COLOR_GRAD = 2 };
 enum lsr_backward_flags { LSR_BWD_RECORDS_ZEROED = 1 };
 
 /* GaussianRasterizationSettings (gaussian_renderer/__init__.py:37-51), device-pointer form. */

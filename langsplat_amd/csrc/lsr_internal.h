@@ -24,6 +24,8 @@ enum Counter : int {
 constexpr uint32_t kFwdZeroedRecords = 1u;  // the language step's gradient records cleared (the render
                                             // backward clears this bit: only its first use is valid)
 constexpr uint32_t kFwdFusedLoss = 2u;      // loss codes written (dL_dloss is valid)
+constexpr uint32_t kFwdNoColorState = 4u;   // split-replay states without the colour sums (no colour
+                                            // gradient may follow: LSR_FWD_NO_COLOR_GRAD)
 // longest-first tile schedule (lsr_render.hip): tiles per work class, forward and backward,
 // right after the counters so one memset clears both
 constexpr int kWorkClasses = 64;
@@ -38,7 +40,7 @@ constexpr int kCntWords = kCntSlots + 2 * kWorkClasses;
 // (the last one: the rest) instead of one long serial chain.
 constexpr int kSplitMax = 3;                // recorded boundaries per tile
 constexpr int kSplitItems = kSplitMax + 1;  // backward work items per tile
-constexpr int kSplitVals = 8;               // per pixel {T, colour (3)}, {feature (3), -}
+constexpr int kSplitVals = 8;               // per pixel {T, feature (3)}, {colour (3), -}
 constexpr int kSplitSlots = kSplitMax + 1;  // per tile: the boundaries' states, then the final sums
 
 constexpr int kRadixThreads = 256;
@@ -250,6 +252,7 @@ struct RenderParams {
     // a descriptor {boundaries recorded below the replay length, -, -, -}
     float* split_pool;
     uint4* split_desc;
+    int split_color;  // forward: store the colour sums' half of every state (off: LSR_FWD_NO_COLOR_GRAD)
     int prio;  // wave priority by launch position (longest tiles highest), 0: off
     int geo;   // backward: the conic / opacity partials are needed (geometry gradients)
     float4* zero_records;  // forward: clear these zero_records_n4 float4s (grid-stride), or null

@@ -539,9 +539,11 @@ __global__ __launch_bounds__(kTilePixels, 7) void k_render_forward(RenderParams 
             // pixel's state before list entry 256 j while some pixel composites, two float4 per pixel
             // in the tile's own slot j - 1 (a grid-wide slot counter cost ~40 us of contended
             // cross-XCD atomics); a pixel already done is never started from here
+            // {T, feature sums}, then {colour sums} unless no colour gradient can follow (the language
+            // step: half the state traffic)
             float4* st = reinterpret_cast<float4*>(p.split_pool) + ((size_t)tile * kSplitSlots + nrec) * (2 * kThreads);
-            st[2 * t] = make_float4(q.T, q.C01.x, q.C01.y, q.C2F0.x);
-            st[2 * t + 1] = make_float4(q.C2F0.y, q.F12.x, q.F12.y, 0.0f);
+            st[2 * t] = make_float4(q.T, q.C2F0.y, q.F12.x, q.F12.y);
+            if (p.split_color) st[2 * t + 1] = make_float4(q.C01.x, q.C01.y, q.C2F0.x, 0.0f);
             nrec++;
         }
         if (idx < end) {
@@ -628,8 +630,8 @@ __global__ __launch_bounds__(kTilePixels, 7) void k_render_forward(RenderParams 
     // place needed a load round trip at the end of every long tile, i.e. on the kernel's critical path
     if (nsplit > 0) {
         float4* fin = reinterpret_cast<float4*>(p.split_pool) + ((size_t)tile * kSplitSlots + kSplitMax) * (2 * kThreads);
-        fin[2 * t] = make_float4(q.C01.x, q.C01.y, q.C2F0.x, q.C2F0.y);
-        fin[2 * t + 1] = make_float4(q.F12.x, q.F12.y, 0.0f, 0.0f);
+        fin[2 * t] = make_float4(q.C2F0.y, q.F12.x, q.F12.y, 0.0f);
+        if (p.split_color) fin[2 * t + 1] = make_float4(q.C01.x, q.C01.y, q.C2F0.x, 0.0f);
     }
     if (kStats) {
         if (!ph.stopped && ph.batches) ph.lap(ph.walk);  // the last batch's walk
@@ -773,10 +775,22 @@ static bool scheduled()
     return v;
 }
 
+// LSR_SPLIT_COLOR=1 stores the colour half of the split-replay states even under
+// LSR_FWD_NO_COLOR_GRAD (measurement aid: same-box A/B of the state traffic)
+static bool split_color_forced()
+{
+    static const bool v = [] {
+        const char* e = getenv("LSR_SPLIT_COLOR");
+        return e && e[0] == '1';
+    }();
+    return v;
+}
+
 hipError_t launch_render_forward(const RenderParams& pin, int tiles, hipStream_t s)
 {
     if (tiles == 0) return hipSuccess;
     RenderParams p = pin;
+    if (split_color_forced()) p.split_color = 1;
     if (!scheduled()) p.sched_counts = p.sched_lists = nullptr;
     if (!p.sched_counts || !split_replay()) p.split_pool = nullptr;
     p.prio = p.sched_counts ? prio_levels() : 0;
@@ -1198,22 +1212,24 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
         const uint4 desc = p.split_desc[tile];
         const uint32_t hi = lo + (uint32_t)kThreads;
         if (chunk < desc.x && q.last > hi) {
-            // the boundary's {T, colour sums}, {feature sums} and the tile's final sums (extra slot)
+            // the boundary's {T, feature sums}, {colour sums} and the tile's final sums (extra slot);
+            // the colour halves exist unless the forward was told no colour gradient follows (a
+            // colour variant is then refused by the host: include/lsr.h LSR_FWD_NO_COLOR_GRAD)
             const float4* st = reinterpret_cast<const float4*>(p.split_pool) + (size_t)tile * kSplitSlots * (2 * kThreads);
             const float4 s0 = st[chunk * 2 * kThreads + 2 * t], f0 = st[kSplitMax * 2 * kThreads + 2 * t];
             const float inv = 1.0f / s0.x;
             q.T = s0.x;
             if (kColor) {
-                q.acc0 = (f0.x - s0.y) * inv;
-                q.acc1 = (f0.y - s0.z) * inv;
-                q.acc2 = (f0.z - s0.w) * inv;
-            }
-            if (kFeat) {
                 const float4 s1 = st[chunk * 2 * kThreads + 2 * t + 1];
                 const float4 f1 = st[kSplitMax * 2 * kThreads + 2 * t + 1];
-                q.accF0 = (f0.w - s1.x) * inv;
-                q.accF1 = (f1.x - s1.y) * inv;
-                q.accF2 = (f1.y - s1.z) * inv;
+                q.acc0 = (f1.x - s1.x) * inv;
+                q.acc1 = (f1.y - s1.y) * inv;
+                q.acc2 = (f1.z - s1.z) * inv;
+            }
+            if (kFeat) {
+                q.accF0 = (f0.x - s0.y) * inv;
+                q.accF1 = (f0.y - s0.z) * inv;
+                q.accF2 = (f0.z - s0.w) * inv;
             }
             q.last = hi;
         }

@@ -193,13 +193,26 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
         # a backward will follow: let the compositing kernel clear its gradient records
         flags = _native.FWD_ZERO_GRAD_RECORDS if any(ctx.needs_input_grad) else 0
         ctx.records_zeroed = flags != 0
-        out = _guarded(raster_settings, "snapshot_fw.dump",
-                       "\nAn error occured in forward. Please forward snapshot_fw.dump for debugging.",
-                       lambda *a: _native.rasterize_gaussians(raster_settings, *a[:8], raw=raw, shs_rest=a[8],
-                                                              visible=a[9], loss_target=a[10], loss_mask=a[11],
-                                                              out_loss=a[12], flags=flags),
-                       (m3, dc, None, ln, op, sc, ro, None, rest, visible, loss_target, loss_mask,
-                        loss if fuse_loss else None))
+        # the language step (train.py:96-104): the loss is the fused language loss, so the colour
+        # image is expected off the loss path and the split-replay states skip the colour sums; a
+        # colour gradient arriving anyway is served by rasterizing again with them (backward below)
+        ctx.no_color = fuse_loss and flags != 0
+        if ctx.no_color:
+            flags |= _native.FWD_NO_COLOR_GRAD
+
+        def run(fwd_flags, vis, out_loss):
+            return _guarded(raster_settings, "snapshot_fw.dump",
+                            "\nAn error occured in forward. Please forward snapshot_fw.dump for debugging.",
+                            lambda *a: _native.rasterize_gaussians(raster_settings, *a[:8], raw=raw, shs_rest=a[8],
+                                                                   visible=a[9], loss_target=a[10], loss_mask=a[11],
+                                                                   out_loss=a[12], flags=fwd_flags),
+                            (m3, dc, None, ln, op, sc, ro, None, rest, vis, loss_target, loss_mask,
+                             out_loss if fuse_loss else None))
+        out = run(flags, visible, loss)
+        if ctx.no_color:
+            dev = m3.device  # (the closure holds inputs only: an output in ctx would form a cycle)
+            ctx.rerun = lambda: run(flags & ~_native.FWD_NO_COLOR_GRAD, torch.empty((P,), dtype=torch.bool, device=dev),
+                                    torch.empty((), dtype=torch.float32, device=dev))
         num_rendered, color, language_feature, radii, geom, binning, image = out
         ctx.raster_settings = raster_settings
         ctx.num_rendered = num_rendered
@@ -220,6 +233,16 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
     def backward(ctx, grad_out_color, grad_out_language_feature, _grad_radii, _grad_visible, grad_loss=None):
         rs = ctx.raster_settings
         m3, dc, rest, ln, op, sc, ro, radii, geom, binning, image = ctx.saved_tensors
+        num_rendered = ctx.num_rendered
+        if grad_out_color is not None and ctx.no_color:
+            # the forward kept no colour sums (include/lsr.h LSR_FWD_NO_COLOR_GRAD): the same forward
+            # again with them (bit-identical outputs), then the backward reads its buffers
+            if (torch.cuda.is_current_stream_capturing() or _native.static_buffers.active() is not None
+                    or _native.language_ready.active() is not None):
+                raise RuntimeError("a colour gradient reached a rasterizer call made with language_target "
+                                   "inside a captured or pipelined step; render with language_target=None and "
+                                   "form the language loss as a torch op when the colour image is in the loss")
+            num_rendered, _, _, _, geom, binning, image = ctx.rerun()
         rest = rest if rest.numel() > 0 else None  # grad_out_color None: zero colour gradient
         gl = grad_out_language_feature if ctx.use_lang else None
         geometry = _native.geometry_grads_needed(ctx.needs_input_grad, (0, 2, 3, 4, 5, 6))
@@ -231,7 +254,7 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
                                                                      opacities=a[15], geometry=geometry,
                                                                      grad_loss=a[16], flags=flags),
                      (m3, dc, None, ln if ctx.use_lang else None, sc, ro, None, radii, grad_out_color, gl,
-                      ctx.num_rendered, geom, binning, image, rest, op,
+                      num_rendered, geom, binning, image, rest, op,
                       grad_loss if ctx.fuse_loss and ctx.use_lang else None))
 
         def want(i, t):

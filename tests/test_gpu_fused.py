@@ -192,8 +192,9 @@ def test_language_step_skips_geometry_gradients(fused, colour, monkeypatch):
     assert out[False][0].abs().sum() > 0
 
 
-def _language_step(g, cam, gt, mask, fused_loss, monkeypatch, extra=None, geometry_frozen=True):
-    """One language-feature train step (train.py:76-104): render, Ll1, backward."""
+def _language_step(g, cam, gt, mask, fused_loss, monkeypatch, extra=None, geometry_frozen=True, colour_extra=None):
+    """One language-feature train step (train.py:76-104): render, Ll1, backward.  colour_extra: the
+    colour image also feeds a loss term (sum of image * colour_extra)."""
     monkeypatch.setenv("LANGSPLAT_AMD_FUSED", "1")
     m = _Model(g, DEV)
     if geometry_frozen:
@@ -206,6 +207,8 @@ def _language_step(g, cam, gt, mask, fused_loss, monkeypatch, extra=None, geomet
         pkg = render(cam, m, _Pipe, torch.zeros(3, device=DEV), _Opt)
         loss = torch.abs(pkg["language_feature_image"] * mask - gt * mask).mean()
     total = loss if extra is None else loss + (pkg["language_feature_image"] * extra).sum()
+    if colour_extra is not None:
+        total = total + (pkg["render"] * colour_extra).sum()
     total.backward()
     grads = {"language_feature": m._language_feature.grad.detach().cpu().numpy(),
              "viewspace": pkg["viewspace_points"].grad.detach().cpu().numpy()}
@@ -235,6 +238,30 @@ def test_fused_language_loss_matches_torch_loss(W, H, extra, frozen, monkeypatch
     for k in g0:
         assert_grad_close(k, g1[k], g0[k])
     assert np.abs(g1["language_feature"]).sum() > 0
+
+
+@pytest.mark.parametrize("colour,frozen", [(False, True), (True, True), (True, False)])
+def test_language_step_without_colour_state(colour, frozen, monkeypatch):
+    """With language_target the forward is told no colour gradient follows (include/lsr.h
+    LSR_FWD_NO_COLOR_GRAD): its split-replay states hold T and the feature sums only.  On a dense
+    scene whose tiles composite past entries 256 / 512 / 768 (split replay active) the language step
+    matches the unfused-loss step, whose forward keeps the colour sums.  colour: the colour image is
+    in the loss too, so the backward rasterizes again with the colour sums (rasterizer.py) -- still
+    the same gradients, geometry frozen or not."""
+    W, H = 96, 80
+    g = make_gaussians(40000, seed=21, scale_range=(0.02, 0.12))
+    cam = make_cameras(1, W, H, device=DEV)[0]
+    gen = torch.Generator().manual_seed(5)
+    gt = torch.nn.functional.normalize(torch.randn((3, H, W), generator=gen), dim=0).to(DEV)
+    mask = (torch.rand((1, H, W), generator=gen) < 0.8).to(DEV)
+    cex = (torch.randn((3, H, W), generator=gen) / (3 * H * W)).to(DEV) if colour else None
+    l0, img0, g0 = _language_step(g, cam, gt, mask, False, monkeypatch, None, frozen, cex)
+    l1, img1, g1 = _language_step(g, cam, gt, mask, True, monkeypatch, None, frozen, cex)
+    assert torch.equal(img0, img1)
+    torch.testing.assert_close(l1, l0, rtol=2e-6, atol=0)
+    for k in g0:
+        assert_grad_close(k, g1[k], g0[k])
+    assert np.abs(g1["viewspace"]).sum() > 0
 
 
 def test_fused_language_loss_empty_scene(monkeypatch):
