@@ -166,7 +166,16 @@ typedef struct lsr_forward_args {
      * call without it.  In capacity mode (a graph capture) the event is one recorded in the same
      * capture (a join of two branches). */
     void* language_ready;
+    /* Forward in two calls (capacity mode only; the ABI 11 pipelined graph step): LSR_PHASE_GEOMETRY
+     * enqueues the preprocess (language feature deferred), depth order and binning and returns;
+     * LSR_PHASE_COMPOSITE, with the same arguments and an allocator that returns the same buffers,
+     * enqueues the rest: the language feature into the records and the compositing (+ fused loss).
+     * Whatever the caller orders between the two calls on the stream (e.g. a wait for the feature's
+     * update) runs between them, so the two halves can be captured into two HIP graphs replayed on
+     * different streams.  LSR_PHASE_ALL (0): one call does everything. */
+    int32_t phase;
 } lsr_forward_args;
+enum lsr_forward_phase { LSR_PHASE_ALL = 0, LSR_PHASE_GEOMETRY = 1, LSR_PHASE_COMPOSITE = 2 };
 
 /* Inputs/outputs of _C.rasterize_gaussians_backward.  Every non-NULL output is fully written
  * (zeros for culled Gaussians).  dL_dsh may be NULL when shs is NULL; dL_dscales/dL_drotations

@@ -57,7 +57,7 @@ class LsrForwardArgs(ctypes.Structure):
     ] + [("raw", ctypes.c_int32), ("flags", ctypes.c_int32), ("shs_rest", _vp), ("visible", _vp),
          ("loss_target", _vp), ("loss_mask", _vp), ("out_loss", _vp), ("capacity_rendered", ctypes.c_int64),
          ("capacity_entries", ctypes.c_int64), ("overflow", _vp), ("out_num_entries", ctypes.POINTER(ctypes.c_int64)),
-         ("language_ready", _vp)]
+         ("language_ready", _vp), ("phase", ctypes.c_int32)]
 
 
 class LsrBackwardArgs(ctypes.Structure):
@@ -290,6 +290,33 @@ class language_ready:
         language_ready._tls.cur = self._prev
 
 
+class forward_phase:
+    """Within the block, the rasterizer forwards of this thread enqueue one half of the forward
+    (include/lsr.h lsr_forward_args.phase; capacity mode only): GEOMETRY = preprocess, depth order
+    and binning; COMPOSITE = the language feature into the records, the compositing and the fused
+    loss, into the buffers the geometry call of the same static_buffers set wrote."""
+
+    GEOMETRY, COMPOSITE = 1, 2
+    _tls = threading.local()
+
+    def __init__(self, phase: int):
+        if phase not in (0, 1, 2):
+            raise ValueError("forward_phase: 0 (all), 1 (geometry) or 2 (composite)")
+        self.phase = int(phase)
+
+    @staticmethod
+    def active() -> int:
+        return getattr(forward_phase._tls, "cur", 0)
+
+    def __enter__(self):
+        self._prev = forward_phase.active()
+        forward_phase._tls.cur = self.phase
+        return self
+
+    def __exit__(self, *exc):
+        forward_phase._tls.cur = self._prev
+
+
 class static_buffers:
     """Within the block, the rasterizer forwards of this thread put their scratch buffers and output
     tensors into this object's persistent tensors instead of fresh allocations: the same addresses at
@@ -459,6 +486,7 @@ def rasterize_gaussians(rs, means3D, shs, colors_precomp, language_feature, opac
     if ready is not None and language_feature is not None:
         a.language_ready = ready.cuda_event
         keep.append(ready)
+    a.phase = forward_phase.active()
     if cap is not None:
         a.capacity_rendered = cap.rendered
         a.capacity_entries = cap.entries

@@ -377,6 +377,9 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
         a->capacity_rendered > 0xFFFFFFFFll || a->capacity_entries > 0xFFFFFFFFll)
         return fail(LSR_ERR_INVALID, "lsr_forward: capacity mode needs capacity_rendered > 0 and capacity_entries > 0 "
                                      "(both < 2^32)");
+    if (a->phase < LSR_PHASE_ALL || a->phase > LSR_PHASE_COMPOSITE ||
+        (a->phase != LSR_PHASE_ALL && (a->capacity_rendered <= 0 || a->language_ready)))
+        return fail(LSR_ERR_INVALID, "lsr_forward: a forward phase needs capacity mode and no language_ready");
     if (a->out_num_entries) *a->out_num_entries = 0;
     if (a->out_loss && (!s->include_feature || (P > 0 && !a->language_feature) || !a->loss_target || !a->loss_mask))
         return fail(LSR_ERR_INVALID, "lsr_forward: the fused loss needs include_feature, language_feature, "
@@ -458,9 +461,25 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
     pp.raw = a->raw;
     pp.shs_rest = a->shs_rest;
     pp.partial = reinterpret_cast<uint4*>(geom + L.pre_partial);
-    // deferred language feature: geometry first, the feature after the caller's event
-    const bool deferred = a->language_ready && s->include_feature && a->language_feature;
+    // deferred language feature: geometry first, the feature after the caller's event (or, split in
+    // phases, in the composite call)
+    const bool deferred = (a->language_ready || a->phase != LSR_PHASE_ALL) && s->include_feature && a->language_feature;
     pp.lang_deferred = deferred ? 1 : 0;
+    if (a->phase == LSR_PHASE_COMPOSITE) {
+        // the geometry call's buffers (same allocator keys and sizes): the feature, then the compositing
+        const int64_t R_cap = a->capacity_rendered;
+        const int64_t E_cap = !depth_order_uses_pass_count(P) ? std::min<int64_t>(a->capacity_entries, L.fused_cap)
+                                                                : a->capacity_entries;
+        L = make_layout(P, W, H, R_cap, E_cap);
+        char* binning = static_cast<char*>(alloc(user, LSR_BUF_BINNING, L.binning_bytes));
+        if (!binning) return fail(LSR_ERR_ALLOC, "lsr_forward: binning buffer allocation failed");
+        *num_rendered = R_cap;
+        if (deferred)
+            LSR_TRY(launch_fill_language(P, a->language_feature, a->raw, a->radii,
+                                         reinterpret_cast<float4*>(geom + L.record), stream),
+                    "fill language");
+        return render_forward_and_finish(s, a, L, geom, image, binning, hb, stream, debug);
+    }
     LSR_TRY(launch_preprocess(pp, stream), "preprocess");
     hm.mark();
 
@@ -496,6 +515,7 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
                                DevCount{counters + kCntSuper, counters + kCntOverflow}),
                 "binning");
         *num_rendered = R_cap;
+        if (a->phase == LSR_PHASE_GEOMETRY) return LSR_OK;
         if (deferred) LSR_TRY(wait_and_fill_language(a, L, geom, stream), "fill language");
         return render_forward_and_finish(s, a, L, geom, image, binning, hb, stream, debug);
     }

@@ -91,27 +91,37 @@ class ViewPipeline:
 
 
 class PipelinedGraphStep:
-    """ViewPipeline's order captured into HIP graphs: every replay is one full language step --
-    view k's backward and Adam on one branch, view k+1's geometry stages on the other, joined before
-    view k+1's compositing -- with no host work between the kernels (langsplat_amd.graph.GraphedStep
-    is the unpipelined form).
+    """ViewPipeline's order as HIP graphs on two streams: view k+1's geometry stages run on stream B
+    while view k's compositing, loss, backward and Adam run on stream A, with no host work between
+    the kernels (langsplat_amd.graph.GraphedStep is the unpipelined form).
 
-    The HIP runtime launches a graph's kernels on one queue in capture order, so the two branches
-    overlap only where independent kernels meet (measured); the eager ViewPipeline
-    overlaps more when the host keeps ahead.  (Two graphs on two streams joined by external event
-    nodes would overlap fully, but this runtime refuses hipEventRecordExternal in a capture and
-    crashes on an external wait.)
+    The rasterizer forward is split in two calls (include/lsr.h lsr_forward_args.phase, capacity
+    mode): the geometry half (preprocess, depth order, binning; the language feature deferred) and
+    the composite half (the feature into the records, compositing, fused loss).  Per static buffer
+    set p (_native.static_buffers: the same addresses at every forward) two graphs are captured:
 
-    A replay's backward reads what the PREVIOUS replay's forward wrote, so the forwards alternate
-    between two static buffer sets (_native.static_buffers: the same addresses at every forward) and
-    two graphs, G1 (backward of set 0, forward into set 1) and G0 (the reverse), replayed in turn.
+        G_geo[p]:  the geometry half of the view, into set p                      (stream B)
+        G_step[p]: the composite half of set p + loss.backward() + optimizer.step() (stream A)
+
+    and replay k runs (p = k % 2, q = 1 - p):
+
+        stream A:  wait geo[p]  -> G_step[p] -> record step[p]
+        stream B:  wait step[q] -> G_geo[q]  -> record geo[q]      (set q is free once step q ran)
+
+    so a replay is one full language step (the loss it returns is that of the view it composited and
+    updated from) and the next view's geometry overlaps it.  Two graphs on two streams are separate
+    queues: unlike one graph with two branches (which this HIP runtime launches on one queue in
+    capture order), they run concurrently.  The geometry reads nothing the step
+    writes (the language step freezes the geometry, scene/gaussian_model.py:203-217); the step's
+    feature fill reads what the previous step's Adam wrote (stream A order).
+
     The rasterizer runs in capacity mode (capacities from eager warm-up views, with headroom; a view
-    over capacity is flagged, check() re-captures).  N = 1: the optimizer is captured (its step count
-    advances on the device); a collective is not captured.
+    over capacity is flagged per set, check() re-captures).  N = 1: the optimizer is captured (its
+    step count advances on the device); a collective is not captured.
 
         g = PipelinedGraphStep(lambda: render(...)["language_l1"], [gaussians._language_feature], optimizer)
         for it in range(iterations):
-            loss = g.replay()   # the loss of the view this replay composited (its backward: next replay)
+            loss = g.replay()   # this replay's view's loss (on the caller's stream after the replay)
         g.check(); g.sync()
 
     forward_fn() runs render() + the loss and returns the loss (no backward).  The graphs own the
@@ -125,11 +135,16 @@ class PipelinedGraphStep:
         self.warmup = int(warmup)
         dev = self.params[0].device
         self.sets = (_native.static_buffers(), _native.static_buffers())
-        self.streams = (torch.cuda.Stream(dev), torch.cuda.Stream(dev))
-        self.overflow = torch.zeros((), dtype=torch.int32, device=dev)
-        self.graphs = [None, None]
+        self.streams = (torch.cuda.Stream(dev), torch.cuda.Stream(dev))  # A: step, B: geometry
+        self.overflow = (torch.zeros((), dtype=torch.int32, device=dev),
+                         torch.zeros((), dtype=torch.int32, device=dev))
+        self.g_geo = [None, None]
+        self.g_step = [None, None]
         self.static_loss = [None, None]
-        self.next = 1
+        self.ev_geo = [None, None]
+        self.ev_step = [None, None]
+        self.next = 0
+        self.primed = False
         self.captures = 0
         self.rendered = self.entries = 0
 
@@ -144,6 +159,8 @@ class PipelinedGraphStep:
                 self.forward_fn().backward()
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
+        for p in self.params:
+            p.grad = None
         if not _native.LAST_COUNTS:
             raise RuntimeError("PipelinedGraphStep: forward_fn ran no rasterizer forward")
         r = max(v[0] for v in _native.LAST_COUNTS.values())
@@ -153,61 +170,80 @@ class PipelinedGraphStep:
 
     def capture(self, min_rendered: int = 0, min_entries: int = 0):
         self._measure(min_rendered, min_entries)
-        self.graphs = [None, None]
+        self.g_geo = [None, None]
+        self.g_step = [None, None]
         self.static_loss = [None, None]
         self.optimizer.prepare_capture()
-        cap = _native.capacity(self.rendered, self.entries, self.overflow)
         cur = torch.cuda.current_stream()
+        sa, sb = self.streams
         for s in self.streams:
             s.wait_stream(cur)
-        # eager forwards allocate both sets at their capacity sizes (no allocation may happen during a
-        # capture); set 0's is the prologue: the first replay (G1) runs its backward
-        for parity in (1, 0):
-            with torch.cuda.stream(self.streams[parity]), cap, self.sets[parity]:
-                prev = self.forward_fn()
-        pool = torch.cuda.graph_pool_handle()
-        for parity in (1, 0):
-            bwd_s, fwd_s = self.streams[1 - parity], self.streams[parity]
-            for p in self.params:
-                p.grad = None  # the captured backward assigns its own .grad (no accumulate)
+        caps = [_native.capacity(self.rendered, self.entries, self.overflow[p]) for p in (0, 1)]
+        # eager forwards allocate both sets at their capacity sizes (no allocation may happen during
+        # a capture); nothing is updated
+        for p in (0, 1):
+            with torch.cuda.stream(sa), caps[p], self.sets[p]:
+                self.forward_fn()
+        sb.wait_stream(sa)
+        for p in (0, 1):
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=pool, stream=bwd_s):
-                fork = torch.cuda.Event()
-                fork.record(bwd_s)
-                fwd_s.wait_event(fork)
-                prev.backward()       # on bwd_s: autograd runs it on its forward's stream
-                prev = None           # release the autograd graph (and its AccumulateGrad nodes)
+            with torch.cuda.graph(g, stream=sb), caps[p], self.sets[p], \
+                    _native.forward_phase(_native.forward_phase.GEOMETRY):
+                self.forward_fn()  # its outputs are written by the composite half
+            self.g_geo[p] = g
+            for q in self.params:
+                q.grad = None  # the captured backward assigns its own .grad (no accumulate)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=sa), caps[p], self.sets[p], \
+                    _native.forward_phase(_native.forward_phase.COMPOSITE):
+                loss = self.forward_fn()
+                loss.backward()
                 self.optimizer.step()
-                ready = torch.cuda.Event()
-                ready.record(bwd_s)
-                with torch.cuda.stream(fwd_s), cap, self.sets[parity], _native.language_ready(ready):
-                    loss = self.forward_fn()
-                bwd_s.wait_stream(fwd_s)
-            self.graphs[parity] = g
-            self.static_loss[parity] = loss.detach()  # the set's static loss tensor
-            prev = loss
-            loss = None
-        # G0's forward (set 0) is never backwarded by Python: the graphs hold the kernels it captured
-        # (replays change the views' data in place, e.g. a camera's matrices copied into the tensors
-        # the captured settings point at; the graphs' launches stay the same)
-        del prev
-        cur.wait_stream(self.streams[0])
-        cur.wait_stream(self.streams[1])
-        self.next = 1
+            self.g_step[p] = g
+            self.static_loss[p] = loss.detach()  # the set's static loss tensor
+            del loss
+        cur.wait_stream(sa)
+        cur.wait_stream(sb)
+        self.ev_geo = [torch.cuda.Event(), torch.cuda.Event()]
+        self.ev_step = [torch.cuda.Event(), torch.cuda.Event()]
+        self.next = 0
+        self.primed = False
         self.captures += 1
         return self
 
     def replay(self) -> torch.Tensor:
-        if self.graphs[0] is None:
+        if self.g_step[0] is None:
             self.capture()
-        k = self.next
-        self.graphs[k].replay()
-        self.next = 1 - k
-        return self.static_loss[k]
+        sa, sb = self.streams
+        cur = torch.cuda.current_stream()
+        p = self.next
+        q = 1 - p
+        if not self.primed:  # the first view's geometry (set p is free: nothing ran since the capture)
+            sb.wait_stream(cur)
+            with torch.cuda.stream(sb):
+                self.g_geo[p].replay()
+            self.ev_geo[p].record(sb)
+            self.primed = True
+        # the caller's earlier work (e.g. a learning-rate change on the device) precedes the step
+        sa.wait_stream(cur)
+        sa.wait_event(self.ev_geo[p])
+        with torch.cuda.stream(sa):
+            self.g_step[p].replay()
+        self.ev_step[p].record(sa)
+        # the next view's geometry into set q, once the step that last read set q has run
+        sb.wait_event(self.ev_step[q])  # (an event never recorded: no wait)
+        with torch.cuda.stream(sb):
+            self.g_geo[q].replay()
+        self.ev_geo[q].record(sb)
+        cur.wait_event(self.ev_step[p])
+        self.next = q
+        return self.static_loss[p]
 
     def synchronize(self):
-        """A replay runs on the caller's current stream (its branches join before it ends): nothing
-        to wait for beyond stream order."""
+        """The caller's current stream waits for every replay enqueued so far (both streams)."""
+        cur = torch.cuda.current_stream()
+        for s in self.streams:
+            cur.wait_stream(s)
 
     def sync(self):
         """The optimizer state's step counts from the device (a device-to-host copy)."""
@@ -216,9 +252,11 @@ class PipelinedGraphStep:
     def check(self) -> bool:
         """True if every replay's view fitted its capacities.  Otherwise re-capture with twice the
         capacities (the over-capacity views were not rasterized) and return False."""
-        if int(self.overflow.item()) == 0:
+        self.synchronize()
+        if int(self.overflow[0].item()) == 0 and int(self.overflow[1].item()) == 0:
             return True
         self.sync()
-        self.overflow.zero_()
+        for o in self.overflow:
+            o.zero_()
         self.capture(2 * self.rendered, 2 * self.entries)
         return False

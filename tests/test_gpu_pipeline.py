@@ -67,9 +67,10 @@ def test_view_pipeline_uses_two_streams(monkeypatch):
 
 
 def test_pipelined_graph_matches_serial_steps(monkeypatch):
-    """PipelinedGraphStep: after one eager step, the capture's prologue forward composites view 1 and
-    replay r runs view r's backward and Adam, then view r+1's forward -- so the losses it leaves in the
-    two buffer sets and the parameters after K replays are those of K more serial steps."""
+    """PipelinedGraphStep: the forward split in its geometry and composite halves
+    (lsr_forward_args.phase), the next view's geometry graph on its own stream beside this view's
+    step graph.  After one eager step, K replays are K more serial steps: the same losses (the first
+    bit for bit), parameters and Adam moments; the step count advanced on the device."""
     from langsplat_amd.pipeline import PipelinedGraphStep
     monkeypatch.setenv("LANGSPLAT_AMD_FUSED", "1")
     K = 5
@@ -86,16 +87,11 @@ def test_pipelined_graph_matches_serial_steps(monkeypatch):
                 losses.append(step().detach().clone())
                 opt.step()
                 opt.zero_grad(set_to_none=True)
-            losses.append(step().detach().clone())  # view K + 1's loss (the last replay's forward)
-            m._language_feature.grad = None
         else:
             g = PipelinedGraphStep(step.forward, [m._language_feature], opt).capture()
-            torch.cuda.synchronize()
-            losses.append(g.static_loss[0].clone())  # the prologue's view
             for _ in range(K):
-                loss = g.replay()
-                g.synchronize()  # the loss is written on the pipeline's forward stream
-                losses.append(loss.clone())
+                losses.append(g.replay().clone())  # on the caller's stream: ordered after the replay
+            g.synchronize()
             torch.cuda.synchronize()
             assert g.check() and g.captures == 1
             g.sync()
@@ -109,3 +105,37 @@ def test_pipelined_graph_matches_serial_steps(monkeypatch):
     torch.testing.assert_close(pg, ps, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(mg, ms, rtol=1e-4, atol=1e-9)
     torch.testing.assert_close(vg, vs, rtol=1e-4, atol=1e-12)
+
+
+def test_forward_phases_match_one_call(monkeypatch):
+    """lsr_forward in two calls (GEOMETRY, then COMPOSITE into the same static buffers) produces the
+    one-call capacity-mode forward's image, language image, radii and loss bit for bit, and the
+    backward over it the same gradients; a phase outside capacity mode is refused."""
+    from langsplat_amd import _native
+    monkeypatch.setenv("LANGSPLAT_AMD_FUSED", "1")
+    m, step = _language_setup(P=5000)
+    outs = []
+    for split in (False, True):
+        sb = _native.static_buffers()
+        ov = torch.zeros((), dtype=torch.int32, device="cuda")
+        m._language_feature.grad = None
+        with _native.capacity(1 << 20, 1 << 20, ov), sb:
+            if split:
+                with _native.forward_phase(_native.forward_phase.GEOMETRY):
+                    step.forward()
+                with _native.forward_phase(_native.forward_phase.COMPOSITE):
+                    loss = step.forward()
+            else:
+                loss = step.forward()
+            loss.backward()
+        torch.cuda.synchronize()
+        assert int(ov.item()) == 0
+        outs.append((loss.detach().clone(), sb.tensors[("out", "color")].clone(),
+                     sb.tensors[("out", "language")].clone(), sb.tensors[("out", "radii")].clone(),
+                     m._language_feature.grad.detach().clone()))
+    (l0, c0, f0, r0, g0), (l1, c1, f1, r1, g1) = outs
+    assert torch.equal(l0, l1) and torch.equal(c0, c1) and torch.equal(f0, f1) and torch.equal(r0, r1)
+    torch.testing.assert_close(g1, g0, rtol=1e-5, atol=1e-9)
+    with pytest.raises(RuntimeError, match="phase"):
+        with _native.forward_phase(_native.forward_phase.GEOMETRY):
+            step.forward()
