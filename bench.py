@@ -525,9 +525,9 @@ def main():
         run().item()
     torch.cuda.synchronize()
     elapsed_sync = time.perf_counter() - ts
-    # (6) N = 1: the pipelined order captured into HIP graphs (langsplat_amd.pipeline.PipelinedGraphStep):
-    # each replay is one full step -- this view's backward and Adam beside the next view's geometry
-    # stages, then the next view's compositing and loss -- with no host work inside
+    # (6) N = 1: the pipelined order as HIP graphs on two streams (langsplat_amd.pipeline.PipelinedGraphStep):
+    # each replay is one full step -- this view's compositing, loss, backward and Adam on one stream, the
+    # next view's geometry stages (the forward's first half) on the other -- with no host work inside
     elapsed_pg = float("inf")
     if world == 1 and graphed and os.environ.get("LSR_PIPELINE", "1") != "0":
         pg = PipelinedGraphStep(lambda: render(cam, model, Pipe, bg, Opt, language_target=(gt, mask))["language_l1"],
@@ -661,8 +661,9 @@ def main():
                       "pipelined": "eager launches, consecutive views on two streams (the next view's geometry "
                                    "beside this view's backward" + (", RCCL all-reduce" if world > 1 else "")
                                    + " and Adam)",
-                      "pipelined_graph": "HIP graph replays of the pipelined step (this view's backward + Adam "
-                                         "beside the next view's geometry, then its compositing + loss)"}[best],
+                      "pipelined_graph": "HIP graphs on two streams: this view's compositing + loss, backward and "
+                                         "Adam on one, the next view's geometry (forward split in two calls) on "
+                                         "the other"}[best],
         "ms_per_step_forms": {n: (round(1000.0 * v / args.steps, 4) if v < 1e29 else None) for n, v in times.items()},
         "ms_per_step_all_gradients": round(1000.0 * elapsed_all / args.steps, 4),
         "ms_per_step_rgb": None if rgb_ms is None else round(rgb_ms, 4),

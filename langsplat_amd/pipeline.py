@@ -32,6 +32,7 @@ stay bound to the previous step's stream.
 from __future__ import annotations
 
 import contextlib
+import os
 
 import torch
 
@@ -100,13 +101,18 @@ class PipelinedGraphStep:
     the composite half (the feature into the records, compositing, fused loss).  Per static buffer
     set p (_native.static_buffers: the same addresses at every forward) two graphs are captured:
 
-        G_geo[p]:  the geometry half of the view, into set p                      (stream B)
-        G_step[p]: the composite half of set p + loss.backward() + optimizer.step() (stream A)
+        G_geo[p]:  the geometry half of the view, into set p                  (stream B)
+        G_comp[p]: the composite half of set p and the loss                     (stream A)
+        G_step[p]: loss.backward() + optimizer.step()                           (stream A)
 
     and replay k runs (p = k % 2, q = 1 - p):
 
-        stream A:  wait geo[p]  -> G_step[p] -> record step[p]
-        stream B:  wait step[q] -> G_geo[q]  -> record geo[q]      (set q is free once step q ran)
+        stream A:  wait geo[p] -> G_comp[p] -> record comp[p] -> G_step[p] -> record step[p]
+        stream B:  wait step[q] -> G_geo[q] -> record geo[q]      (set q is free once step q ran)
+
+    Beside the compositing kernels, which hold every CU slot, the geometry's short launches stretch
+    (kernel trace: publish 5 -> 60 us), but starting it only after the compositing (LSR_PG_GEO=fwd)
+    measured slower: 0.54 against 0.49 ms per step at C3.
 
     so a replay is one full language step (the loss it returns is that of the view it composited and
     updated from) and the next view's geometry overlaps it.  Two graphs on two streams are separate
@@ -135,13 +141,22 @@ class PipelinedGraphStep:
         self.warmup = int(warmup)
         dev = self.params[0].device
         self.sets = (_native.static_buffers(), _native.static_buffers())
-        self.streams = (torch.cuda.Stream(dev), torch.cuda.Stream(dev))  # A: step, B: geometry
+        # A: step, B: geometry.  (Stream priorities measured worse: a high-priority geometry stream
+        # 0.82 ms per step, a high-priority step stream 0.57, none 0.48; LSR_PG_PRIO=geo / step)
+        prio = os.environ.get("LSR_PG_PRIO", "none")
+        # the next view's geometry starts with the step ("start") or after this view's compositing
+        # ("fwd": beside the backward and Adam only); measured C3: start 0.49, fwd 0.54 ms per step
+        self.geo_after_fwd = os.environ.get("LSR_PG_GEO", "start") == "fwd"
+        self.streams = (torch.cuda.Stream(dev, priority=-1 if prio == "step" else 0),
+                        torch.cuda.Stream(dev, priority=-1 if prio == "geo" else 0))
         self.overflow = (torch.zeros((), dtype=torch.int32, device=dev),
                          torch.zeros((), dtype=torch.int32, device=dev))
         self.g_geo = [None, None]
+        self.g_comp = [None, None]
         self.g_step = [None, None]
         self.static_loss = [None, None]
         self.ev_geo = [None, None]
+        self.ev_comp = [None, None]
         self.ev_step = [None, None]
         self.next = 0
         self.primed = False
@@ -171,6 +186,7 @@ class PipelinedGraphStep:
     def capture(self, min_rendered: int = 0, min_entries: int = 0):
         self._measure(min_rendered, min_entries)
         self.g_geo = [None, None]
+        self.g_comp = [None, None]
         self.g_step = [None, None]
         self.static_loss = [None, None]
         self.optimizer.prepare_capture()
@@ -197,6 +213,9 @@ class PipelinedGraphStep:
             with torch.cuda.graph(g, stream=sa), caps[p], self.sets[p], \
                     _native.forward_phase(_native.forward_phase.COMPOSITE):
                 loss = self.forward_fn()
+            self.g_comp[p] = g
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=sa):  # the backward runs on its forward's stream (sa)
                 loss.backward()
                 self.optimizer.step()
             self.g_step[p] = g
@@ -205,6 +224,7 @@ class PipelinedGraphStep:
         cur.wait_stream(sa)
         cur.wait_stream(sb)
         self.ev_geo = [torch.cuda.Event(), torch.cuda.Event()]
+        self.ev_comp = [torch.cuda.Event(), torch.cuda.Event()]
         self.ev_step = [torch.cuda.Event(), torch.cuda.Event()]
         self.next = 0
         self.primed = False
@@ -228,10 +248,14 @@ class PipelinedGraphStep:
         sa.wait_stream(cur)
         sa.wait_event(self.ev_geo[p])
         with torch.cuda.stream(sa):
+            self.g_comp[p].replay()
+            self.ev_comp[p].record(sa)
             self.g_step[p].replay()
         self.ev_step[p].record(sa)
         # the next view's geometry into set q, once the step that last read set q has run
         sb.wait_event(self.ev_step[q])  # (an event never recorded: no wait)
+        if self.geo_after_fwd:
+            sb.wait_event(self.ev_comp[p])
         with torch.cuda.stream(sb):
             self.g_geo[q].replay()
         self.ev_geo[q].record(sb)
