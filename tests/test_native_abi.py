@@ -60,6 +60,33 @@ def test_invalid_arguments_report_errors_without_gpu():
     assert lib.lsr_mark_visible(-5, None, None, None, None, None) != 0
 
 
+def test_forward_flag_and_phase_validation_without_gpu():
+    """lsr_forward refuses an unknown flag, and a forward phase (include/lsr.h lsr_forward_phase)
+    outside capacity mode, before any device work (dummy non-null pointers, never dereferenced)."""
+    import ctypes
+    lib = _native.load()
+    dummy = ctypes.c_void_p(256)
+    s = _native.LsrSettings()
+    s.image_height, s.image_width, s.tanfovx, s.tanfovy, s.sh_degree = 8, 8, 0.5, 0.5, 0
+    s.bg = s.viewmatrix = s.projmatrix = s.campos = dummy
+    nr = ctypes.c_int64(0)
+
+    def call(**kw):
+        a = _native.LsrForwardArgs()
+        a.P, a.M = 4, 1
+        a.means3D = a.shs = a.opacities = a.scales = a.rotations = dummy
+        a.out_color = a.out_language_feature = a.radii = dummy
+        for k, v in kw.items():
+            setattr(a, k, v)
+        return lib.lsr_forward(ctypes.byref(s), ctypes.byref(a), _native._ALLOC_CB, None, None, ctypes.byref(nr))
+
+    assert call(flags=4) != 0 and "unknown flag" in _native.last_error()
+    assert call(phase=_native.forward_phase.GEOMETRY) != 0 and "phase" in _native.last_error()
+    assert call(phase=3, capacity_rendered=16, capacity_entries=16) != 0 and "phase" in _native.last_error()
+    assert call(phase=_native.forward_phase.COMPOSITE, capacity_rendered=16, capacity_entries=16,
+                language_ready=dummy) != 0 and "phase" in _native.last_error()
+
+
 def test_spin_limit_knob_round_trips_without_gpu():
     lib = _native.load()
     old = lib.lsr_debug_set_spin_limit(7)
