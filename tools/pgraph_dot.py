@@ -41,7 +41,8 @@ def main():
     pg = PipelinedGraphStep(fwd, [model._language_feature], optim).capture()
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     for k in (0, 1):
-        pg.graphs[k].debug_dump(os.path.join(ROOT, "gpurun_out", f"pgraph_{k}.dot"))
+        for name, g in (("geo", pg.g_geo[k]), ("comp", pg.g_comp[k]), ("step", pg.g_step[k])):
+            g.debug_dump(os.path.join(ROOT, "gpurun_out", f"pgraph_{name}_{k}.dot"))
 
 
 if __name__ == "__main__":
