@@ -182,8 +182,12 @@ class RGBStep:
         pkg = render(self.cam, self.model, Pipe, self.bg, OptRGB)
         image = pkg["render"]
         Ll1 = torch.abs(image - self.gt).mean()
-        loss = (1.0 - OptRGB.lambda_dssim) * Ll1 + OptRGB.lambda_dssim * (1.0 - ssim(image, self.gt))
-        loss.backward()
+        # MIOpen has no tuned kernel for SSIM's fp32 depthwise 11 x 1 / 1 x 11 convolutions and falls
+        # back to its naive ones (~9 of the 9.7 ms RGB step, profiles/r04_C3_rgb_kernel_stats.csv); ATen's
+        # own depthwise kernels run them, forward and backward (LSR_SSIM_MIOPEN=1 keeps MIOpen)
+        with torch.backends.cudnn.flags(enabled=os.environ.get("LSR_SSIM_MIOPEN", "0") == "1"):
+            loss = (1.0 - OptRGB.lambda_dssim) * Ll1 + OptRGB.lambda_dssim * (1.0 - ssim(image, self.gt))
+            loss.backward()
         vgrad = pkg["viewspace_points"].grad
         if self.bucket is None:
             _native.densification_stats(pkg["radii"], vgrad, self.max_radii2D, self.xyz_gradient_accum, self.denom)
@@ -525,13 +529,14 @@ def main():
         run().item()
     torch.cuda.synchronize()
     elapsed_sync = time.perf_counter() - ts
-    # (6) N = 1: the pipelined order as HIP graphs on two streams (langsplat_amd.pipeline.PipelinedGraphStep):
+    # (6) the pipelined order as HIP graphs on two streams (langsplat_amd.pipeline.PipelinedGraphStep):
     # each replay is one full step -- this view's compositing, loss, backward and Adam on one stream, the
     # next view's geometry stages (the forward's first half) on the other -- with no host work inside
     elapsed_pg = float("inf")
-    if world == 1 and graphed and os.environ.get("LSR_PIPELINE", "1") != "0":
+    if graphed and os.environ.get("LSR_PIPELINE", "1") != "0":
+        # N > 1: the bucket's all-reduce (RCCL) is launched between each set's backward and Adam graphs
         pg = PipelinedGraphStep(lambda: render(cam, model, Pipe, bg, Opt, language_target=(gt, mask))["language_l1"],
-                                model.trainable(), optim)
+                                model.trainable(), optim, bucket=bucket)
         pg.capture()
         for _ in range(4):
             pg.replay()
@@ -540,10 +545,16 @@ def main():
             for _ in range(2):
                 pg.replay()
             torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
         tq = time.perf_counter()
         for _ in range(args.steps):
             pg.replay()
+        pg.synchronize()
         torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
         elapsed_pg = time.perf_counter() - tq
         if not pg.check():
             raise RuntimeError("a pipelined view exceeded its capacities during the timed steps")

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define LSR_ABI_VERSION 11
+#define LSR_ABI_VERSION 12
 
 enum lsr_status {
     LSR_OK = 0,
@@ -175,7 +175,11 @@ typedef struct lsr_forward_args {
      * different streams.  LSR_PHASE_ALL (0): one call does everything. */
     int32_t phase;
 } lsr_forward_args;
-enum lsr_forward_phase { LSR_PHASE_ALL = 0, LSR_PHASE_GEOMETRY = 1, LSR_PHASE_COMPOSITE = 2 };
+/* LSR_PHASE_COMPOSITE_FILLED (ABI 12): as LSR_PHASE_COMPOSITE, but the records' language slots already
+ * hold the activated feature -- written by a fused update's fill_record (lsr_backward_args), which
+ * may run before or while the geometry call runs: the geometry call of a split forward never writes
+ * those slots. */
+enum lsr_forward_phase { LSR_PHASE_ALL = 0, LSR_PHASE_GEOMETRY = 1, LSR_PHASE_COMPOSITE = 2, LSR_PHASE_COMPOSITE_FILLED = 3 };
 
 /* Inputs/outputs of _C.rasterize_gaussians_backward.  Every non-NULL output is fully written
  * (zeros for culled Gaussians).  dL_dsh may be NULL when shs is NULL; dL_dscales/dL_drotations
@@ -219,6 +223,22 @@ typedef struct lsr_backward_args {
     const float* dL_dloss;           /* NULL, or the device scalar dL/d(out_loss) of a forward that fused
                                         the loss: its gradient dL/dloss * sign(f m - gt m) * m / (3 H W)
                                         (autograd's) is added to dL_dout_language_feature (NULL = 0) */
+    /* ABI 12: LangSplat's language step with its optimiser step fused into the backward's epilogue
+     * (train.py:104 + 134-137 at N = 1, where nothing happens between the two: langsplat_amd.graph /
+     * langsplat_amd.pipeline use it in their captured steps).  update != NULL needs the language-only
+     * backward (every geometry output NULL, dL_dout_color NULL), raw & LSR_RAW_LANGUAGE and
+     * update->param == language_feature.  Then, after the render backward, ONE pass per Gaussian reads
+     * its gradient record, writes dL_dmeans2D and dL_dlanguage_feature as always, and applies the
+     * Adam step of lsr_adam_multi (device form: update_step_dev is that call's step block, tensor 0;
+     * update_skip its skip flag) to param / exp_avg / exp_avg_sq -- the same operations, so the same
+     * values as lsr_backward followed by lsr_adam_multi.  fill_record (NULL: off) is the record array
+     * (lsr_state_layout.record) of another forward's geometry buffer over the same P Gaussians: every
+     * Gaussian's language slots there receive the activated updated feature (skipped or not), so that
+     * forward's composite call (LSR_PHASE_COMPOSITE_FILLED) needs no fill of its own. */
+    const struct lsr_adam_tensor* update;  /* (defined with lsr_adam_multi below) */
+    int64_t* update_step_dev;
+    const int32_t* update_skip;
+    float* fill_record;
 } lsr_backward_args;
 
 /* Byte offsets of the internal state inside the forward buffers, for inspection by tests and
@@ -355,13 +375,25 @@ int32_t lsr_adam_step(int64_t n, float* param, const float* grad, float* exp_avg
  * scene/gaussian_model.py:219-226, each with its own lr, betas, eps and step count, i.e. torch's
  * per-parameter state).  Every gradient is multiplied by grad_scale first (e.g. the 1 / N of a
  * gradient all-reduced as a SUM over N ranks; 1 = none).
- * step_dev (device int64[LSR_ADAM_STEP_WORDS], ABI 10) replaces the tensors' step fields for a step
- * replayed from a HIP graph: step_dev[0] is the step count; a one-wave kernel first advances it by
- * one and writes that step's bias-corrected scalars of every tensor into the words after it, which
- * the update reads, so each replay advances the count on the device; at most 16 tensors then.  `ticket` (a
- * device uint32 that is 0, or NULL) serves only the measurement variant LSR_ADAM_ADVANCE=0, where
- * the launch's last workgroup stores the step instead.  step_dev NULL: the host's step counts. */
-#define LSR_ADAM_STEP_WORDS 49 /* the count + 16 tensors' scalars (24 B each) */
+ * step_dev (device int64[LSR_ADAM_STEP_WORDS], ABI 12) replaces the tensors' step fields AND learning
+ * rates for a step replayed from a HIP graph (at most 16 tensors then):
+ *   step_dev[0]                      the step count;
+ *   step_dev[1 .. 48]                scratch: a one-wave kernel first advances the count by one and
+ *                                    writes that step's bias-corrected scalars of every tensor here,
+ *                                    which the update reads;
+ *   step_dev[LSR_ADAM_WORD_SKIPPED]  the number of steps skipped through `skip` (below);
+ *   step_dev[LSR_ADAM_WORD_LR + k]   tensor k's learning rate (a double's bits), which the caller keeps
+ *                                    current (a learning-rate schedule, scene/gaussian_model.py:231-241,
+ *                                    changes it between replays without a re-capture); the table's lr
+ *                                    is not read.
+ * step_dev NULL: the host's step counts and lrs.
+ * skip (device int32, or NULL): when *skip != 0 at run time the launch changes nothing -- no
+ * parameter, moment or step count -- and, with step_dev, adds one to the skipped count.  A captured
+ * train step passes its rasterizer's capacity overflow flag (lsr_forward_args.overflow), so a view
+ * that was not rasterized is a no-op for the optimiser, exactly as if it had been left out. */
+#define LSR_ADAM_STEP_WORDS 66   /* count, 16 x 3 scalar words, skipped count, 16 lrs */
+#define LSR_ADAM_WORD_SKIPPED 49
+#define LSR_ADAM_WORD_LR 50
 typedef struct lsr_adam_tensor {
     int64_t n;
     float* param;
@@ -372,7 +404,7 @@ typedef struct lsr_adam_tensor {
     int64_t step;                /* 1-based, after this update */
 } lsr_adam_tensor;
 int32_t lsr_adam_multi(int32_t count, const lsr_adam_tensor* tensors, float grad_scale, int64_t* step_dev,
-                       uint32_t* ticket, void* stream);
+                       const int32_t* skip, void* stream);
 
 /* Densification statistics of one rendered view, one pass (train.py:125-126 with
  * GaussianModel.add_densification_stats, scene/gaussian_model.py:480-482), for Gaussians with

@@ -22,8 +22,9 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LSR_LIB") or os.path.join(_HERE, "liblsr.so")
 
 LSR_BUF_GEOM, LSR_BUF_BINNING, LSR_BUF_IMAGE, LSR_BUF_BACKWARD = 0, 1, 2, 3
-ABI_VERSION = 11
-ADAM_STEP_WORDS = 49  # include/lsr.h LSR_ADAM_STEP_WORDS
+ABI_VERSION = 12
+ADAM_STEP_WORDS = 66  # include/lsr.h LSR_ADAM_STEP_WORDS
+ADAM_WORD_SKIPPED, ADAM_WORD_LR = 49, 50  # LSR_ADAM_WORD_SKIPPED / LSR_ADAM_WORD_LR
 # lsr_raw_flags (include/lsr.h): inputs are GaussianModel's raw parameters
 RAW_OPACITY, RAW_SCALES, RAW_ROTATIONS, RAW_LANGUAGE = 1, 2, 4, 8
 FWD_ZERO_GRAD_RECORDS, FWD_NO_COLOR_GRAD = 1, 2  # lsr_forward_flags
@@ -60,6 +61,12 @@ class LsrForwardArgs(ctypes.Structure):
          ("language_ready", _vp), ("phase", ctypes.c_int32)]
 
 
+class LsrAdamTensor(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int64), ("param", _vp), ("grad", _vp), ("exp_avg", _vp), ("exp_avg_sq", _vp),
+                ("lr", ctypes.c_double), ("beta1", ctypes.c_double), ("beta2", ctypes.c_double),
+                ("eps", ctypes.c_double), ("step", ctypes.c_int64)]
+
+
 class LsrBackwardArgs(ctypes.Structure):
     _fields_ = [("P", ctypes.c_int32), ("M", ctypes.c_int32), ("num_rendered", ctypes.c_int64)] + [
         (n, _vp) for n in ("means3D", "shs", "colors_precomp", "language_feature", "opacities", "scales",
@@ -68,7 +75,8 @@ class LsrBackwardArgs(ctypes.Structure):
                            "dL_dlanguage_feature", "dL_dopacity", "dL_dmeans3D", "dL_dcov3D", "dL_dsh",
                            "dL_dscales", "dL_drotations")
     ] + [("raw", ctypes.c_int32), ("flags", ctypes.c_int32), ("shs_rest", _vp), ("dL_dsh_rest", _vp),
-         ("dL_dloss", _vp)]
+         ("dL_dloss", _vp), ("update", ctypes.POINTER(LsrAdamTensor)), ("update_step_dev", _vp),
+         ("update_skip", _vp), ("fill_record", _vp)]
 
 
 class LsrStateLayout(ctypes.Structure):
@@ -79,12 +87,6 @@ class LsrStateLayout(ctypes.Structure):
 
 class LsrKernelStat(ctypes.Structure):
     _fields_ = [("name", ctypes.c_char * 32), ("launches", ctypes.c_int64), ("total_ms", ctypes.c_double)]
-
-
-class LsrAdamTensor(ctypes.Structure):
-    _fields_ = [("n", ctypes.c_int64), ("param", _vp), ("grad", _vp), ("exp_avg", _vp), ("exp_avg_sq", _vp),
-                ("lr", ctypes.c_double), ("beta1", ctypes.c_double), ("beta2", ctypes.c_double),
-                ("eps", ctypes.c_double), ("step", ctypes.c_int64)]
 
 
 ALLOC_FN = ctypes.CFUNCTYPE(_vp, _vp, ctypes.c_int32, ctypes.c_size_t)
@@ -294,14 +296,17 @@ class forward_phase:
     """Within the block, the rasterizer forwards of this thread enqueue one half of the forward
     (include/lsr.h lsr_forward_args.phase; capacity mode only): GEOMETRY = preprocess, depth order
     and binning; COMPOSITE = the language feature into the records, the compositing and the fused
-    loss, into the buffers the geometry call of the same static_buffers set wrote."""
+    loss, into the buffers the geometry call of the same static_buffers set wrote; COMPOSITE_FILLED =
+    the same without the feature fill (a fused update wrote the records' language slots: fused_update
+    with fill)."""
 
-    GEOMETRY, COMPOSITE = 1, 2
+    GEOMETRY, COMPOSITE, COMPOSITE_FILLED = 1, 2, 3
     _tls = threading.local()
 
     def __init__(self, phase: int):
-        if phase not in (0, 1, 2):
-            raise ValueError("forward_phase: 0 (all), 1 (geometry) or 2 (composite)")
+        if phase not in (0, 1, 2, 3):
+            raise ValueError("forward_phase: 0 (all), 1 (geometry), 2 (composite) or 3 (composite, feature "
+                             "already in the records)")
         self.phase = int(phase)
 
     @staticmethod
@@ -353,6 +358,47 @@ class static_buffers:
 
     def __exit__(self, *exc):
         static_buffers._tls.cur = self._prev
+
+
+class fused_update:
+    """Within the block, a language-only rasterizer backward of `param` (the raw _language_feature,
+    the fused-activation path) also applies `optimizer`'s Adam step to it in the same pass
+    (include/lsr.h lsr_backward_args.update; train.py:104 + 134-137 at N = 1), and optimizer.step()
+    then leaves it alone.  The optimizer must be a langsplat_amd.optim.Adam prepared for a capture
+    (its device step block; only inside a graph capture) with `param` its one parameter.  skip: its
+    skip flag (the overflow flag); fill: a device pointer to another forward's record array whose
+    language slots receive the updated activated feature (langsplat_amd.pipeline), or None."""
+
+    # process-wide, not thread-local: autograd runs a CUDA node's backward on its device thread, not
+    # on the thread that called loss.backward()
+    _cur = None
+
+    def __init__(self, optimizer, param: torch.Tensor, skip: Optional[torch.Tensor] = None, fill: Optional[int] = None):
+        self.optimizer, self.param, self.skip, self.fill = optimizer, param, skip, fill
+        self.used = False
+
+    @staticmethod
+    def active():
+        return fused_update._cur
+
+    def __enter__(self):
+        self._prev = fused_update._cur
+        fused_update._cur = self
+        return self
+
+    def __exit__(self, *exc):
+        fused_update._cur = self._prev
+
+    def table(self):
+        """The lsr_adam_tensor of the update (the optimizer's state and group hyper-parameters)."""
+        opt, p = self.optimizer, self.param
+        gi = next(i for i, g in enumerate(opt.param_groups) if any(q is p for q in g["params"]))
+        g = opt.param_groups[gi]
+        st = opt.state[p]
+        beta1, beta2 = g["betas"]
+        opt._register_fused(gi)
+        return LsrAdamTensor(p.numel(), p.data_ptr(), None, st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(),
+                             float(g["lr"]), float(beta1), float(beta2), float(g["eps"]), 0)
 
 
 def output_tensor(key, shape, dtype, device) -> torch.Tensor:
@@ -518,12 +564,14 @@ def geometry_grads_needed(needs_input_grad, geometry_inputs):
 def rasterize_gaussians_backward(rs, means3D, shs, colors_precomp, language_feature, scales, rotations,
                                  cov3D_precomp, radii, grad_color, grad_language, num_rendered, geom, binning,
                                  image, raw=0, shs_rest=None, opacities=None, geometry=True, grad_loss=None,
-                                 flags=0):
+                                 flags=0, update=None):
     """Native backward: returns the gradient tensors keyed like the reference's inputs (with raw
     flags: w.r.t. the raw parameters; "shs" is then dL/dfeatures_dc and "shs_rest"
     dL/dfeatures_rest).  geometry=False (no geometry input needs a gradient): only "means2D" and
     "language_feature_precomp" are computed, the other entries are None (include/lsr.h).
-    grad_loss: dL/d(the fused loss of the forward), a () device tensor, or None."""
+    grad_loss: dL/d(the fused loss of the forward), a () device tensor, or None.  update: a
+    fused_update whose Adam step the backward applies to language_feature (include/lsr.h
+    lsr_backward_args.update)."""
     lib = load()
     device = means3D.device
     P = int(means3D.shape[0])
@@ -598,6 +646,14 @@ def rasterize_gaussians_backward(rs, means3D, shs, colors_precomp, language_feat
     a.dL_dsh = _ptr(g["shs"])
     a.dL_dscales = _ptr(g["scales"])
     a.dL_drotations = _ptr(g["rotations"])
+    if update is not None:
+        tab = update.table()
+        keep.append(tab)
+        a.update = ctypes.pointer(tab)
+        a.update_step_dev = ctypes.c_void_p(update.optimizer._step_dev.data_ptr())
+        a.update_skip = _ptr(update.skip)
+        a.fill_record = None if update.fill is None else ctypes.c_void_p(int(update.fill))
+        update.used = True
     alloc = _Allocator(device)
     with _on_device(device), alloc:
         _check(lib.lsr_backward(ctypes.byref(s), ctypes.byref(a), _ALLOC_CB, None, _stream(device)), "lsr_backward")

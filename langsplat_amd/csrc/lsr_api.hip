@@ -377,7 +377,7 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
         a->capacity_rendered > 0xFFFFFFFFll || a->capacity_entries > 0xFFFFFFFFll)
         return fail(LSR_ERR_INVALID, "lsr_forward: capacity mode needs capacity_rendered > 0 and capacity_entries > 0 "
                                      "(both < 2^32)");
-    if (a->phase < LSR_PHASE_ALL || a->phase > LSR_PHASE_COMPOSITE ||
+    if (a->phase < LSR_PHASE_ALL || a->phase > LSR_PHASE_COMPOSITE_FILLED ||
         (a->phase != LSR_PHASE_ALL && (a->capacity_rendered <= 0 || a->language_ready)))
         return fail(LSR_ERR_INVALID, "lsr_forward: a forward phase needs capacity mode and no language_ready");
     if (a->out_num_entries) *a->out_num_entries = 0;
@@ -465,8 +465,9 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
     // phases, in the composite call)
     const bool deferred = (a->language_ready || a->phase != LSR_PHASE_ALL) && s->include_feature && a->language_feature;
     pp.lang_deferred = deferred ? 1 : 0;
-    if (a->phase == LSR_PHASE_COMPOSITE) {
-        // the geometry call's buffers (same allocator keys and sizes): the feature, then the compositing
+    if (a->phase == LSR_PHASE_COMPOSITE || a->phase == LSR_PHASE_COMPOSITE_FILLED) {
+        // the geometry call's buffers (same allocator keys and sizes): the feature (unless a fused
+        // update already wrote it, LSR_PHASE_COMPOSITE_FILLED), then the compositing
         const int64_t R_cap = a->capacity_rendered;
         const int64_t E_cap = !depth_order_uses_pass_count(P) ? std::min<int64_t>(a->capacity_entries, L.fused_cap)
                                                                 : a->capacity_entries;
@@ -474,7 +475,7 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
         char* binning = static_cast<char*>(alloc(user, LSR_BUF_BINNING, L.binning_bytes));
         if (!binning) return fail(LSR_ERR_ALLOC, "lsr_forward: binning buffer allocation failed");
         *num_rendered = R_cap;
-        if (deferred)
+        if (deferred && a->phase == LSR_PHASE_COMPOSITE)
             LSR_TRY(launch_fill_language(P, a->language_feature, a->raw, a->radii,
                                          reinterpret_cast<float4*>(geom + L.record), stream),
                     "fill language");
@@ -605,6 +606,17 @@ int32_t lsr_backward(const lsr_settings* s, const lsr_backward_args* a, lsr_allo
         return fail(LSR_ERR_INVALID, "lsr_backward: shs_rest needs shs, M >= 2 and dL_dsh_rest");
     if ((a->raw & LSR_RAW_OPACITY) && P > 0 && !a->opacities)
         return fail(LSR_ERR_INVALID, "lsr_backward: raw opacities missing");
+    if (a->update) {
+        const lsr_adam_tensor& u = *a->update;
+        if (geometry || a->dL_dout_color || !(a->raw & LSR_RAW_LANGUAGE) || !s->include_feature || !a->language_feature ||
+            u.param != a->language_feature || u.n != 3 * (int64_t)P || !u.exp_avg || !u.exp_avg_sq ||
+            !a->update_step_dev || !a->dL_dlanguage_feature)
+            return fail(LSR_ERR_INVALID, "lsr_backward: a fused update needs the language-only backward of the raw "
+                                         "language feature (update->param), its moments, a step block and "
+                                         "dL_dlanguage_feature");
+    } else if (a->fill_record || a->update_step_dev || a->update_skip) {
+        return fail(LSR_ERR_INVALID, "lsr_backward: fill_record / update_step_dev / update_skip need update");
+    }
     hipStream_t stream = reinterpret_cast<hipStream_t>(stream_ptr);
     const bool debug = s->debug != 0;
     if (P == 0) return LSR_OK;
@@ -668,6 +680,16 @@ int32_t lsr_backward(const lsr_settings* s, const lsr_backward_args* a, lsr_allo
     rp.fwd_flags = reinterpret_cast<uint32_t*>(image + L.counters) + kCntFwdFlags;
     rp.geo = geometry ? 1 : 0;
     if (a->num_rendered > 0) LSR_TRY(launch_render_backward(rp, L.tiles, stream), "render backward");
+    if (a->update) {
+        // the language step's tail in one pass: epilogue + Adam (+ the next forward's feature slots)
+        const lsr_adam_tensor& u = *a->update;
+        AdamHyper h{u.lr, u.beta1, u.beta2, u.eps};
+        LSR_TRY(launch_language_tail(P, a->radii, grad, const_cast<float*>(a->language_feature), u.exp_avg, u.exp_avg_sq,
+                                     a->dL_dmeans2D, a->dL_dlanguage_feature, h, a->update_step_dev, a->update_skip,
+                                     reinterpret_cast<float4*>(a->fill_record), stream),
+                "language tail");
+        return LSR_OK;
+    }
     if (!geometry) {
         LSR_TRY(launch_grad_epilogue(P, a->radii, grad, stride, a->language_feature,
                                      (a->raw & LSR_RAW_LANGUAGE) ? 1 : 0, a->dL_dmeans2D,
@@ -890,11 +912,11 @@ int32_t lsr_adam_step(int64_t n, float* param, const float* grad, float* exp_avg
 }
 
 int32_t lsr_adam_multi(int32_t count, const lsr_adam_tensor* tensors, float grad_scale, int64_t* step_dev,
-                       uint32_t* ticket, void* stream_ptr)
+                       const int32_t* skip, void* stream_ptr)
 {
     if (count < 0 || (count > 0 && !tensors)) return fail(LSR_ERR_INVALID, "lsr_adam_multi: invalid argument");
-    if ((step_dev != nullptr) != (ticket != nullptr) || (step_dev && count > kAdamMaxTensors))
-        return fail(LSR_ERR_INVALID, "lsr_adam_multi: step_dev needs a ticket and at most 16 tensors");
+    if (step_dev && count > kAdamMaxTensors)
+        return fail(LSR_ERR_INVALID, "lsr_adam_multi: step_dev allows at most 16 tensors");
     hipStream_t stream = reinterpret_cast<hipStream_t>(stream_ptr);
     const bool debug = false;
     for (int32_t k0 = 0; k0 < count; k0 += kAdamMaxTensors) {
@@ -915,7 +937,7 @@ int32_t lsr_adam_multi(int32_t count, const lsr_adam_tensor* tensors, float grad
             g.a = adam_scalars(t.lr, t.beta1, t.beta2, t.eps, t.step < 1 ? 1 : t.step);
         }
         tab.step_dev = step_dev;
-        tab.ticket = ticket;
+        tab.skip = skip;
         LSR_TRY(launch_adam_multi(tab, grad_scale, stream), "adam");
     }
     return LSR_OK;

@@ -363,11 +363,19 @@ struct AdamHyper {
 struct AdamTable {
     int count;
     AdamSegment seg[kAdamMaxTensors];
-    AdamHyper hyper[kAdamMaxTensors];  // used with step_dev: the scalars are formed on the device
+    AdamHyper hyper[kAdamMaxTensors];  // used with step_dev: the scalars are formed on the device (lr
+                                       // from step_dev[LSR_ADAM_WORD_LR + k])
     int64_t* step_dev;                 // null: the host's step counts (seg[].a)
-    uint32_t* ticket;                  // zero at launch (the last workgroup resets it)
+    const int32_t* skip;               // *skip != 0: the launch is a no-op (null: never)
 };
 hipError_t launch_adam_multi(AdamTable& tab, float grad_scale, hipStream_t s);
+// lsr_backward_args.update: k_adam_advance (one tensor, the skip flag), then one pass per Gaussian: the
+// gradient epilogue (dmeans2D, dlang from the 20-B records and the raw feature), the Adam step of the
+// raw feature (its device scalars; nothing on *skip) and, with fill, the activated updated feature
+// into fill's language slots of every Gaussian
+hipError_t launch_language_tail(int P, const int32_t* radii, const float* grad, float* lang, float* exp_avg,
+                                float* exp_avg_sq, float* dmeans2D, float* dlang, const AdamHyper& h, int64_t* step_dev,
+                                const int32_t* skip, float4* fill, hipStream_t s);
 hipError_t launch_densification_stats(int P, const int* radii, const float* dmeans2D, float* max_radii, float* accum,
                                       float* denom, hipStream_t s);
 

@@ -18,8 +18,6 @@
 
 namespace lsr {
 
-constexpr int64_t kAdamDevBlocks = 512;  // device-step launches: 2 per CU
-
 __device__ __forceinline__ void adam_one(float& p, float g, float& m, float& v, const AdamScalars& a)
 {
     // torch lerp: weight < 0.5 ? self + weight * (end - self) : end - (end - self) * (1 - weight),
@@ -70,11 +68,9 @@ __device__ __forceinline__ void adam_segment(const AdamSegment& g, int64_t chunk
 // Device step count (tab.step_dev, for a step replayed from a HIP graph): a one-wave kernel
 // advances *step_dev first and forms every tensor's bias-corrected scalars of that step once (torch's
 // formulas, in double); the update's workgroups read them.  (Round 3's first form had every
-// workgroup evaluate the double pow()s itself: 18.5 us against 15.4 us eager in the graph's trace.)  Measured on the graph-replayed C3 step (tools/ab_env.sh): 5 us
-// faster than the alternative kept behind LSR_ADAM_ADVANCE=0, where the workgroup that finishes
-// last (the last ticket) stores step + 1 and resets the ticket (same-address atomics from a small
-// grid, and a long tail).
-__device__ __forceinline__ AdamScalars adam_scalars_dev(const AdamHyper& h, int64_t step)
+// workgroup evaluate the double pow()s itself: 18.5 us against 15.4 us eager in the graph's trace;
+// a form where the last workgroup stored the advanced count measured 5 us slower still.)
+__device__ __forceinline__ AdamScalars adam_scalars_dev(const AdamHyper& h, double lr, int64_t step)
 {
     const double bc1 = 1.0 - pow(h.beta1, (double)step);
     const double bc2 = 1.0 - pow(h.beta2, (double)step);
@@ -84,47 +80,42 @@ __device__ __forceinline__ AdamScalars adam_scalars_dev(const AdamHyper& h, int6
     a.w2 = (float)(1.0 - h.beta2);
     a.inv_bc2_sqrt = 1.0f / (float)sqrt(bc2);
     a.eps = (float)h.eps;
-    a.neg_step_size = (float)(-(h.lr / bc1));
+    a.neg_step_size = (float)(-(lr / bc1));
     return a;
 }
 
 // One wave: every lane reads the step count before lane 0 stores it advanced, and lane k < count
-// forms tensor k's scalars of the new step (torch's formulas, in double) into the words after the
-// count -- once per step instead of once per workgroup of the update.
+// forms tensor k's scalars of the new step (torch's formulas, in double; the lr the caller keeps in
+// step_dev) into the words after the count -- once per step instead of once per workgroup of the
+// update.  A skipped step (*skip != 0: the view was not rasterized) advances nothing but the skipped
+// count.
 __global__ void k_adam_advance(int64_t* step_dev, AdamTable tab)
 {
-    const int64_t step = *step_dev + 1;
     const int k = (int)threadIdx.x;
-    if (k < tab.count) reinterpret_cast<AdamScalars*>(step_dev + 1)[k] = adam_scalars_dev(tab.hyper[k], step);
+    if (tab.skip && *tab.skip) {
+        if (k == 0) step_dev[LSR_ADAM_WORD_SKIPPED] = step_dev[LSR_ADAM_WORD_SKIPPED] + 1;
+        return;
+    }
+    const int64_t step = *step_dev + 1;
+    if (k < tab.count) {
+        const double lr = __longlong_as_double((long long)step_dev[LSR_ADAM_WORD_LR + k]);
+        reinterpret_cast<AdamScalars*>(step_dev + 1)[k] = adam_scalars_dev(tab.hyper[k], lr, step);
+    }
     if (k == 0) *step_dev = step;
 }
 
-// Workgroups take 256-thread chunks grid-stride (chunk -> tensor through block0); with the ticket
-// the grid is small (kAdamDevBlocks), so few tickets meet on the one counter.
+// Workgroups take 256-thread chunks grid-stride (chunk -> tensor through block0).
 __global__ __launch_bounds__(256) void k_adam_multi(AdamTable tab, int64_t chunks, float grad_scale)
 {
-    // device step: k_adam_advance formed the scalars (ticket null), or every workgroup forms them
-    // from the count (the ticket form)
-    const int64_t dstep = tab.step_dev && tab.ticket ? *tab.step_dev + 1 : 0;
-    const AdamScalars* dev_scalars = tab.step_dev && !tab.ticket
-        ? reinterpret_cast<const AdamScalars*>(tab.step_dev + 1) : nullptr;
+    if (tab.skip && *tab.skip) return;  // uniform: the whole launch is a no-op
+    // device step: k_adam_advance formed the scalars
+    const AdamScalars* dev_scalars = tab.step_dev ? reinterpret_cast<const AdamScalars*>(tab.step_dev + 1) : nullptr;
     for (int64_t c = blockIdx.x; c < chunks; c += gridDim.x) {
         int s = 0;
         while (s + 1 < tab.count && c >= tab.seg[s + 1].block0) s++;
         AdamSegment g = tab.seg[s];
         if (dev_scalars) g.a = dev_scalars[s];
-        else if (tab.step_dev) g.a = adam_scalars_dev(tab.hyper[s], dstep);
         adam_segment(g, c, grad_scale);
-    }
-    if (!tab.step_dev || !tab.ticket) return;
-    __syncthreads();  // every wave of the workgroup has consumed its read of *step_dev
-    if (threadIdx.x == 0) {
-        // no fence: the reads were consumed (they formed the scalars above) before the ticket; the
-        // stores reach the next launch at the kernel boundary
-        if (__hip_atomic_fetch_add(tab.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
-            *tab.step_dev = dstep;
-            *tab.ticket = 0u;
-        }
     }
 }
 
@@ -139,24 +130,87 @@ hipError_t launch_adam_multi(AdamTable& tab, float grad_scale, hipStream_t s)
         const int64_t work = g.vec ? (g.n + 3) / 4 : g.n;
         blocks += (work + 255) / 256;
     }
-    if (blocks == 0) return hipSuccess;
-    static const int64_t dev_blocks = [] {  // LSR_ADAM_DEV_BLOCKS: measurement knob
-        const char* e = getenv("LSR_ADAM_DEV_BLOCKS");
-        return e ? (int64_t)atoll(e) : kAdamDevBlocks;
-    }();
-    static const bool advance = [] {  // LSR_ADAM_ADVANCE=0: the ticket form (measurement knob)
-        const char* e = getenv("LSR_ADAM_ADVANCE");
-        return !(e && e[0] == '0');
-    }();
-    if (tab.step_dev && advance) {
-        tab.ticket = nullptr;
+    if (tab.step_dev) {  // even with no work: the count advances (or the skip is counted)
         hipLaunchKernelGGL(k_adam_advance, dim3(1), dim3(64), 0, s, tab.step_dev, tab);
-        const int64_t grid = std::min<int64_t>(blocks, 1 << 20);
-        hipLaunchKernelGGL(k_adam_multi, dim3((unsigned)grid), dim3(256), 0, s, tab, blocks, grad_scale);
-        return hipGetLastError();
+        if (blocks == 0) return hipGetLastError();
     }
-    const int64_t grid = tab.step_dev ? std::min<int64_t>(blocks, dev_blocks) : std::min<int64_t>(blocks, 1 << 20);
+    if (blocks == 0) return hipSuccess;
+    const int64_t grid = std::min<int64_t>(blocks, 1 << 20);
     hipLaunchKernelGGL(k_adam_multi, dim3((unsigned)grid), dim3(256), 0, s, tab, blocks, grad_scale);
+    return hipGetLastError();
+}
+
+// The language step's tail in one pass (lsr_backward_args.update, N = 1): what k_grad_epilogue writes
+// (dmeans2D, dlang from the packed 20-B record {dx, dy, l0, l1, l2} and the raw feature), then the Adam
+// step of the raw feature from dlang (adam_one, the scalars k_adam_advance formed: the same operations
+// as lsr_adam_multi after the epilogue), then -- fill set -- the activated updated feature into the
+// language slots of another forward's records.  Per Gaussian every load is issued before any use
+// (record, radius, feature, moments: one memory round trip).  The records' 20-B stride keeps their
+// loads dword-sized; the 12-B feature / moment rows are read as three dwords by consecutive lanes.
+__global__ __launch_bounds__(256) void k_language_tail(int P, const int32_t* __restrict__ radii,
+                                                       const float* __restrict__ grad, float* __restrict__ lang,
+                                                       float* __restrict__ m, float* __restrict__ v,
+                                                       float* __restrict__ dmeans2D, float* __restrict__ dlang,
+                                                       const int64_t* __restrict__ step_dev,
+                                                       const int32_t* __restrict__ skip, float4* __restrict__ fill)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    const size_t i3 = 3 * (size_t)i;
+    const float* r = grad + (size_t)i * kGradStrideLang;
+    const float r0 = r[0], r1 = r[1], r2 = r[2], r3 = r[3], r4 = r[4];
+    const int rad = radii[i];
+    float l[3] = {lang[i3], lang[i3 + 1], lang[i3 + 2]};
+    float mm[3] = {m[i3], m[i3 + 1], m[i3 + 2]};
+    float vv[3] = {v[i3], v[i3 + 1], v[i3 + 2]};
+    const bool skipped = skip && *skip;
+    const bool live = rad > 0;
+    if (dmeans2D) {
+        dmeans2D[i3] = live ? r0 : 0.f;
+        dmeans2D[i3 + 1] = live ? r1 : 0.f;
+        dmeans2D[i3 + 2] = 0.f;
+    }
+    float3 d = make_float3(0.f, 0.f, 0.f);
+    if (live) d = act_lang_backward(l[0], l[1], l[2], r2, r3, r4);
+    dlang[i3] = d.x;
+    dlang[i3 + 1] = d.y;
+    dlang[i3 + 2] = d.z;
+    if (!skipped) {
+        const AdamScalars a = *reinterpret_cast<const AdamScalars*>(step_dev + 1);  // tensor 0
+        adam_one(l[0], d.x, mm[0], vv[0], a);
+        adam_one(l[1], d.y, mm[1], vv[1], a);
+        adam_one(l[2], d.z, mm[2], vv[2], a);
+        lang[i3] = l[0];
+        lang[i3 + 1] = l[1];
+        lang[i3 + 2] = l[2];
+        m[i3] = mm[0];
+        m[i3 + 1] = mm[1];
+        m[i3 + 2] = mm[2];
+        v[i3] = vv[0];
+        v[i3 + 1] = vv[1];
+        v[i3 + 2] = vv[2];
+    }
+    if (fill) {  // record[3 i + 2] = {b, f0, f1, f2}: the three language slots, b untouched
+        const float3 f = act_lang(l[0], l[1], l[2]);
+        float* slot = reinterpret_cast<float*>(fill + 3 * (size_t)i + 2);
+        slot[1] = f.x;
+        *reinterpret_cast<float2*>(slot + 2) = make_float2(f.y, f.z);
+    }
+}
+
+hipError_t launch_language_tail(int P, const int32_t* radii, const float* grad, float* lang, float* exp_avg,
+                                float* exp_avg_sq, float* dmeans2D, float* dlang, const AdamHyper& h, int64_t* step_dev,
+                                const int32_t* skip, float4* fill, hipStream_t s)
+{
+    AdamTable tab{};
+    tab.count = 1;
+    tab.hyper[0] = h;
+    tab.step_dev = step_dev;
+    tab.skip = skip;
+    hipLaunchKernelGGL(k_adam_advance, dim3(1), dim3(64), 0, s, step_dev, tab);
+    if (P == 0) return hipGetLastError();
+    hipLaunchKernelGGL(k_language_tail, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, P, radii, grad, lang,
+                       exp_avg, exp_avg_sq, dmeans2D, dlang, (const int64_t*)step_dev, skip, fill);
     return hipGetLastError();
 }
 

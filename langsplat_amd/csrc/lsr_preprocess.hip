@@ -363,7 +363,10 @@ __global__ __launch_bounds__(kPreThreads) __attribute__((amdgpu_waves_per_eu(
     float4* rec = p.record + 3 * (size_t)i;
     rec[0] = make_float4(ix, iy, cx, cy);
     rec[1] = make_float4(cz, opacity, rgb[0], rgb[1]);
-    rec[2] = make_float4(rgb[2], f0, f1, f2);
+    if (p.lang_deferred)  // the language slots belong to the fill (which may already have run:
+        reinterpret_cast<float*>(rec + 2)[0] = rgb[2];  // LSR_PHASE_COMPOSITE_FILLED); b only
+    else
+        rec[2] = make_float4(rgb[2], f0, f1, f2);
     my_tiles = area;
     my_supers = (uint32_t)(((r4[2] + kSuper - 1) / kSuper - r4[0] / kSuper) *
                            ((r4[3] + kSuper - 1) / kSuper - r4[1] / kSuper));

@@ -37,6 +37,7 @@ import os
 import torch
 
 from . import _native
+from .graph import _as_view, _fused_tail_enabled, _nullctx
 
 
 class ViewPipeline:
@@ -92,38 +93,45 @@ class ViewPipeline:
 
 
 class PipelinedGraphStep:
-    """ViewPipeline's order as HIP graphs on two streams: view k+1's geometry stages run on stream B
-    while view k's compositing, loss, backward and Adam run on stream A, with no host work between
-    the kernels (langsplat_amd.graph.GraphedStep is the unpipelined form).
+    """ViewPipeline's order as HIP graphs on two streams: the geometry stages of a later view run on
+    stream B while view k's compositing, loss, backward and Adam run on stream A, with no host work
+    between the kernels (langsplat_amd.graph.GraphedStep is the unpipelined form).
 
     The rasterizer forward is split in two calls (include/lsr.h lsr_forward_args.phase, capacity
     mode): the geometry half (preprocess, depth order, binning; the language feature deferred) and
     the composite half (the feature into the records, compositing, fused loss).  Per static buffer
-    set p (_native.static_buffers: the same addresses at every forward) two graphs are captured:
+    set p (_native.static_buffers: the same addresses at every forward; S sets, default 2) the graphs
 
         G_geo[p]:  the geometry half of the view, into set p                  (stream B)
         G_comp[p]: the composite half of set p and the loss                     (stream A)
-        G_step[p]: loss.backward() + optimizer.step()                           (stream A)
+        G_step[p]: loss.backward() + optimizer.step(skip=overflow[p])           (stream A)
+                   (N > 1: G_bwd[p], the bucket's all-reduce launched between, G_adam[p])
 
-    and replay k runs (p = k % 2, q = 1 - p):
+    are captured, and replay k runs (p = k % S; set r = (k + S - 1) % S receives view k + S - 1,
+    S - 1 views ahead; its last reader was step k - 1):
 
         stream A:  wait geo[p] -> G_comp[p] -> record comp[p] -> G_step[p] -> record step[p]
-        stream B:  wait step[q] -> G_geo[q] -> record geo[q]      (set q is free once step q ran)
-
-    Beside the compositing kernels, which hold every CU slot, the geometry's short launches stretch
-    (kernel trace: publish 5 -> 60 us), but starting it only after the compositing (LSR_PG_GEO=fwd)
-    measured slower: 0.54 against 0.49 ms per step at C3.
+        stream B:  [wait comp[p]] -> G_geo[r] -> record geo[r]
 
     so a replay is one full language step (the loss it returns is that of the view it composited and
-    updated from) and the next view's geometry overlaps it.  Two graphs on two streams are separate
+    updated from) and later views' geometry overlaps it.  Two graphs on two streams are separate
     queues: unlike one graph with two branches (which this HIP runtime launches on one queue in
     capture order), they run concurrently.  The geometry reads nothing the step
     writes (the language step freezes the geometry, scene/gaussian_model.py:203-217); the step's
     feature fill reads what the previous step's Adam wrote (stream A order).
 
-    The rasterizer runs in capacity mode (capacities from eager warm-up views, with headroom; a view
-    over capacity is flagged per set, check() re-captures).  N = 1: the optimizer is captured (its
-    step count advances on the device); a collective is not captured.
+    A sequence of views (train.py:85-87): pass slots=[ViewSlot(...) for each set] and a
+    forward_fn(slot) that renders from the slot; capture(views=[v0, ..., v_{S-2}]) takes the first
+    S - 1 views and replay(next_view=v) the view S - 1 replays ahead (it is copied into that view's
+    set on the caller's stream, after that set's last reader finished; each set keeps its own camera
+    and target, so a replay never pairs one view's geometry with another's target).  Without slots
+    forward_fn() renders one fixed view.
+
+    The rasterizer runs in capacity mode (capacities from eager warm-up views, with headroom).  A
+    view over capacity is flagged per set; N = 1: the captured Adam skips on that flag (no parameter,
+    moment or step count changes: the view is left out, include/lsr.h lsr_adam_multi), check()
+    counts the skipped steps and re-captures.  N > 1: an over-capacity view contributes a zero
+    gradient to the all-reduce and every rank steps (the ranks stay identical).
 
         g = PipelinedGraphStep(lambda: render(...)["language_l1"], [gaussians._language_feature], optimizer)
         for it in range(iterations):
@@ -131,47 +139,66 @@ class PipelinedGraphStep:
         g.check(); g.sync()
 
     forward_fn() runs render() + the loss and returns the loss (no backward).  The graphs own the
-    parameters' .grad tensors."""
+    parameters' .grad tensors.
 
-    def __init__(self, forward_fn, params, optimizer, headroom: float = 1.125, warmup: int = 2):
+    Knobs (measured at C3): LSR_PG_SETS (2 or 3), LSR_PG_GEO=fwd (the geometry starts
+    only after this view's compositing), LSR_PG_PRIO=geo|step (stream priorities)."""
+
+    def __init__(self, forward_fn, params, optimizer, headroom: float = 1.125, warmup: int = 2, bucket=None,
+                 slots=None, sets: int = None):
         self.forward_fn = forward_fn
         self.params = [p for p in params]
         self.optimizer = optimizer
+        self.bucket = bucket
         self.headroom = float(headroom)
         self.warmup = int(warmup)
         dev = self.params[0].device
-        self.sets = (_native.static_buffers(), _native.static_buffers())
+        S = int(sets if sets is not None else (len(slots) if slots else os.environ.get("LSR_PG_SETS", "2")))
+        if S < 2:
+            raise ValueError("PipelinedGraphStep: at least two buffer sets")
+        if slots is not None and len(slots) != S:
+            raise ValueError("PipelinedGraphStep: one ViewSlot per buffer set")
+        self.S = S
+        self.slots = list(slots) if slots is not None else None
+        self.sets = tuple(_native.static_buffers() for _ in range(S))
         # A: step, B: geometry.  (Stream priorities measured worse: a high-priority geometry stream
         # 0.82 ms per step, a high-priority step stream 0.57, none 0.48; LSR_PG_PRIO=geo / step)
         prio = os.environ.get("LSR_PG_PRIO", "none")
-        # the next view's geometry starts with the step ("start") or after this view's compositing
-        # ("fwd": beside the backward and Adam only); measured C3: start 0.49, fwd 0.54 ms per step
+        # the later view's geometry starts with the step ("start") or after this view's compositing
+        # ("fwd": beside the backward and Adam only); measured C3 with 2 sets: start 0.49, fwd 0.54 ms
         self.geo_after_fwd = os.environ.get("LSR_PG_GEO", "start") == "fwd"
         self.streams = (torch.cuda.Stream(dev, priority=-1 if prio == "step" else 0),
                         torch.cuda.Stream(dev, priority=-1 if prio == "geo" else 0))
-        self.overflow = (torch.zeros((), dtype=torch.int32, device=dev),
-                         torch.zeros((), dtype=torch.int32, device=dev))
-        self.g_geo = [None, None]
-        self.g_comp = [None, None]
-        self.g_step = [None, None]
-        self.static_loss = [None, None]
-        self.ev_geo = [None, None]
-        self.ev_comp = [None, None]
-        self.ev_step = [None, None]
-        self.next = 0
-        self.primed = False
+        self.overflow = tuple(torch.zeros((), dtype=torch.int32, device=dev) for _ in range(S))
+        self._one = torch.ones((), device=dev)
+        self._reset_graphs()
         self.captures = 0
         self.rendered = self.entries = 0
+        self._skipped_base = 0
+        self._loaded = [None] * S  # the view each set's slot holds (slots only)
+
+    def _reset_graphs(self):
+        S = self.S
+        self.g_geo, self.g_comp, self.g_step, self.g_adam = [None] * S, [None] * S, [None] * S, [None] * S
+        self.grads = [None] * S
+        self.static_loss = [None] * S
+        self.ev_geo = self.ev_comp = self.ev_step = [None] * S
+        self.k = 0
+        self.primed = False
+
+    def _fwd(self, p):
+        return self.forward_fn(self.slots[p]) if self.slots is not None else self.forward_fn()
 
     def _measure(self, min_rendered, min_entries):
         _native.LAST_COUNTS.clear()
         side = torch.cuda.Stream(device=self.params[0].device)
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
-            for _ in range(self.warmup):
+            for i in range(self.warmup):
                 for p in self.params:
                     p.grad = None
-                self.forward_fn().backward()
+                # every set's view when they differ: the capacities cover the views loaded so far
+                self._fwd(i % (self.S - 1)).backward()
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
         for p in self.params:
@@ -183,84 +210,141 @@ class PipelinedGraphStep:
         self.rendered = max(int(r * self.headroom) + 1024, int(min_rendered))
         self.entries = max(int(e * self.headroom) + 1024, int(min_entries))
 
-    def capture(self, min_rendered: int = 0, min_entries: int = 0):
+    def capture(self, min_rendered: int = 0, min_entries: int = 0, views=None):
+        """views: the first S - 1 views (camera, gt, mask) when the step renders from ViewSlots (a
+        shorter list repeats its last view); the capacities are measured on them."""
+        S = self.S
+        if self.slots is not None:
+            if not views:
+                raise ValueError("PipelinedGraphStep.capture: the first views are needed with slots")
+            views = list(views)[:S - 1]
+            views += [views[-1]] * (S - 1 - len(views))
+            for j in range(S - 1):
+                self.slots[j].load(*_as_view(views[j]))
+                self._loaded[j] = views[j]
         self._measure(min_rendered, min_entries)
-        self.g_geo = [None, None]
-        self.g_comp = [None, None]
-        self.g_step = [None, None]
-        self.static_loss = [None, None]
+        self._reset_graphs()
         self.optimizer.prepare_capture()
+        self._skipped_base = self.optimizer.skipped_steps()
         cur = torch.cuda.current_stream()
         sa, sb = self.streams
         for s in self.streams:
             s.wait_stream(cur)
-        caps = [_native.capacity(self.rendered, self.entries, self.overflow[p]) for p in (0, 1)]
-        # eager forwards allocate both sets at their capacity sizes (no allocation may happen during
-        # a capture); nothing is updated
-        for p in (0, 1):
+        caps = [_native.capacity(self.rendered, self.entries, self.overflow[p]) for p in range(S)]
+        # eager forwards allocate every set at its capacity sizes (no allocation may happen during a
+        # capture); nothing is updated
+        for p in range(S):
             with torch.cuda.stream(sa), caps[p], self.sets[p]:
-                self.forward_fn()
+                self._fwd(p)
         sb.wait_stream(sa)
-        for p in (0, 1):
+        skip = None if self.bucket is not None else self.overflow  # N > 1: every rank steps
+        # N = 1 language step: Adam inside the backward's epilogue pass, which also writes the updated
+        # feature into the NEXT set's records (the next composite needs no fill; the geometry call never
+        # writes those slots, so it may run before, during or after)
+        fused = skip is not None and len(self.params) == 1 and _fused_tail_enabled()
+        self.fused = fused
+        comp_phase = _native.forward_phase.COMPOSITE_FILLED if fused else _native.forward_phase.COMPOSITE
+        self.g_comp0 = None
+        for p in range(S):
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, stream=sb), caps[p], self.sets[p], \
                     _native.forward_phase(_native.forward_phase.GEOMETRY):
-                self.forward_fn()  # its outputs are written by the composite half
+                self._fwd(p)  # its outputs are written by the composite half
             self.g_geo[p] = g
             for q in self.params:
                 q.grad = None  # the captured backward assigns its own .grad (no accumulate)
+            if fused and p == 0:  # the first composite after a capture fills its own records
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=sa), caps[p], self.sets[p], \
+                        _native.forward_phase(_native.forward_phase.COMPOSITE):
+                    self._fwd(p)
+                self.g_comp0 = g
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, stream=sa), caps[p], self.sets[p], \
-                    _native.forward_phase(_native.forward_phase.COMPOSITE):
-                loss = self.forward_fn()
+            with torch.cuda.graph(g, stream=sa), caps[p], self.sets[p], _native.forward_phase(comp_phase):
+                loss = self._fwd(p)
             self.g_comp[p] = g
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, stream=sa):  # the backward runs on its forward's stream (sa)
-                loss.backward()
-                self.optimizer.step()
+            fu = _native.fused_update(self.optimizer, self.params[0], skip=self.overflow[p],
+                                      fill=self._record_ptr((p + 1) % S)) if fused else _nullctx()
+            with torch.cuda.graph(g, stream=sa), fu:  # the backward runs on its forward's stream (sa)
+                loss.backward(self._one)  # dL/dloss = 1 from a static tensor: no seed-fill kernel
+                if skip is not None:
+                    self.optimizer.step(skip=skip[p])
             self.g_step[p] = g
+            self.grads[p] = [q.grad for q in self.params]  # this set's graph-owned gradients
+            if skip is None:  # the all-reduce sits between the backward and Adam graphs
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=sa):
+                    self.optimizer.step()
+                self.g_adam[p] = g
             self.static_loss[p] = loss.detach()  # the set's static loss tensor
             del loss
         cur.wait_stream(sa)
         cur.wait_stream(sb)
-        self.ev_geo = [torch.cuda.Event(), torch.cuda.Event()]
-        self.ev_comp = [torch.cuda.Event(), torch.cuda.Event()]
-        self.ev_step = [torch.cuda.Event(), torch.cuda.Event()]
-        self.next = 0
-        self.primed = False
+        self.ev_geo = [torch.cuda.Event() for _ in range(S)]
+        self.ev_comp = [torch.cuda.Event() for _ in range(S)]
+        self.ev_step = [torch.cuda.Event() for _ in range(S)]
         self.captures += 1
         return self
 
-    def replay(self) -> torch.Tensor:
+    def _record_ptr(self, p):
+        """Device address of set p's per-Gaussian render records (include/lsr.h lsr_state_layout.record)."""
+        geom = self.sets[p].tensors[("scratch", _native.LSR_BUF_GEOM)]
+        _, H, W = self.sets[p].tensors[("out", "color")].shape
+        P = int(self.params[0].shape[0])
+        return geom.data_ptr() + _native.state_layout(P, int(W), int(H), 0)["record"]
+
+    def _geometry(self, r, after=None):
+        """Set r's geometry graph on stream B, after everything the caller's stream holds (the set's
+        view loaded, its last reader finished) [and after `after`]."""
+        sb = self.streams[1]
+        sb.wait_stream(torch.cuda.current_stream())
+        if after is not None:
+            sb.wait_event(after)
+        with torch.cuda.stream(sb):
+            self.g_geo[r].replay()
+        self.ev_geo[r].record(sb)
+
+    def replay(self, next_view=None) -> torch.Tensor:
+        """One language step of the view loaded S - 1 replays ago (or at capture); next_view
+        (camera, gt, mask) is the view of the replay S - 1 ahead (ViewSlots only; None: the view of
+        its set stays)."""
         if self.g_step[0] is None:
             self.capture()
+        S = self.S
         sa, sb = self.streams
         cur = torch.cuda.current_stream()
-        p = self.next
-        q = 1 - p
-        if not self.primed:  # the first view's geometry (set p is free: nothing ran since the capture)
-            sb.wait_stream(cur)
-            with torch.cuda.stream(sb):
-                self.g_geo[p].replay()
-            self.ev_geo[p].record(sb)
+        p = self.k % S
+        r = (self.k + S - 1) % S
+        if not self.primed:  # the first S - 1 views' geometry (nothing ran since the capture)
+            for j in range(S - 1):
+                self._geometry((self.k + j) % S)
             self.primed = True
-        # the caller's earlier work (e.g. a learning-rate change on the device) precedes the step
+        if next_view is not None:
+            if self.slots is None:
+                raise RuntimeError("PipelinedGraphStep.replay(next_view=...) needs ViewSlots")
+            # set r's last reader was step k - 1, which the caller's stream waited for (below)
+            self.slots[r].load(*_as_view(next_view))
+            self._loaded[r] = next_view
+        self.optimizer.sync_lr()
+        # the caller's earlier work (e.g. a learning-rate change) precedes the step
         sa.wait_stream(cur)
         sa.wait_event(self.ev_geo[p])
         with torch.cuda.stream(sa):
-            self.g_comp[p].replay()
+            first = self.k == 0 and self.g_comp0 is not None
+            (self.g_comp0 if first else self.g_comp[p]).replay()
             self.ev_comp[p].record(sa)
             self.g_step[p].replay()
+            if self.g_adam[p] is not None:
+                for q, g in zip(self.params, self.grads[p]):
+                    q.grad = g
+                self.bucket.all_reduce(average=True)
+                self.g_adam[p].replay()
         self.ev_step[p].record(sa)
-        # the next view's geometry into set q, once the step that last read set q has run
-        sb.wait_event(self.ev_step[q])  # (an event never recorded: no wait)
-        if self.geo_after_fwd:
-            sb.wait_event(self.ev_comp[p])
-        with torch.cuda.stream(sb):
-            self.g_geo[q].replay()
-        self.ev_geo[q].record(sb)
+        # view k + S - 1's geometry into set r
+        self._geometry(r, after=self.ev_comp[p] if self.geo_after_fwd else None)
         cur.wait_event(self.ev_step[p])
-        self.next = q
+        self.k += 1
         return self.static_loss[p]
 
     def synchronize(self):
@@ -275,12 +359,16 @@ class PipelinedGraphStep:
 
     def check(self) -> bool:
         """True if every replay's view fitted its capacities.  Otherwise re-capture with twice the
-        capacities (the over-capacity views were not rasterized) and return False."""
+        capacities and return False: the over-capacity views were not rasterized, and at N = 1 their
+        steps changed nothing (optimizer.skipped_steps() counts them; train those views again)."""
         self.synchronize()
-        if int(self.overflow[0].item()) == 0 and int(self.overflow[1].item()) == 0:
+        skipped = self.optimizer.skipped_steps() - self._skipped_base
+        if skipped == 0 and all(int(o.item()) == 0 for o in self.overflow):
             return True
         self.sync()
         for o in self.overflow:
             o.zero_()
-        self.capture(2 * self.rendered, 2 * self.entries)
+        # the replays continue with the views already loaded for the next S - 1 steps
+        views = [self._loaded[(self.k + j) % self.S] for j in range(self.S - 1)] if self.slots else None
+        self.capture(2 * self.rendered, 2 * self.entries, views=views)
         return False

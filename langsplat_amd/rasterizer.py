@@ -248,11 +248,16 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
         geometry = _native.geometry_grads_needed(ctx.needs_input_grad, (0, 2, 3, 4, 5, 6))
         flags = _native.BWD_RECORDS_ZEROED if ctx.records_zeroed else 0
         ctx.records_zeroed = False  # a second backward (retain_graph) clears its own records
+        # a captured N = 1 language step may fuse its Adam step into this backward's epilogue
+        fu = _native.fused_update.active()
+        if not (fu is not None and ctx.use_lang and not geometry and grad_out_color is None
+                and ctx.needs_input_grad[7] and ln.numel() > 0 and ln.data_ptr() == fu.param.data_ptr()):
+            fu = None
         g = _guarded(rs, "snapshot_bw.dump",
                      "\nAn error occured in backward. Writing snapshot_bw.dump for debugging.\n",
                      lambda *a: _native.rasterize_gaussians_backward(rs, *a[:14], raw=ctx.raw, shs_rest=a[14],
                                                                      opacities=a[15], geometry=geometry,
-                                                                     grad_loss=a[16], flags=flags),
+                                                                     grad_loss=a[16], flags=flags, update=fu),
                      (m3, dc, None, ln if ctx.use_lang else None, sc, ro, None, radii, grad_out_color, gl,
                       num_rendered, geom, binning, image, rest, op,
                       grad_loss if ctx.fuse_loss and ctx.use_lang else None))

@@ -12,6 +12,7 @@ import os
 
 import torch
 
+from . import _native
 from .rasterizer import GaussianRasterizationSettings, GaussianRasterizer, rasterize_gaussians_fused
 
 
@@ -142,6 +143,12 @@ def render(viewpoint_camera, pc, pipe, bg_color: torch.Tensor, opt, scaling_modi
     else:
         colors_precomp = override_color
     if opt.include_feature:
+        ready = _native.language_ready.active()
+        if ready is not None:
+            # a pipelined / overlapped step (language_ready): the feature's update runs on another
+            # stream; the fused path defers the feature inside the rasterizer, this path reads it
+            # here, so the stream waits for the update first
+            torch.cuda.current_stream().wait_event(ready)
         language_feature_precomp = pc.get_language_feature
         language_feature_precomp = language_feature_precomp / (
             language_feature_precomp.norm(dim=-1, keepdim=True) + 1e-9)

@@ -1,0 +1,543 @@
+"""The captured step forms at the size they are benched at, over view sequences, and on overflow
+(VERDICT r03 "next round" item 1).
+
+bench.py's `value` comes from langsplat_amd.pipeline.PipelinedGraphStep (capacity mode, the forward
+split in its geometry and composite halves, graphs on two streams).  Here, at full C3 (BASELINE.json
+configs[2]) and C5 (configs[4], the LSD depth order):
+  - the capacity-mode forward is bit-identical to the eager one and its backward matches it;
+  - the benched pipelined form's first replay matches the oracle's language step (images bit for
+    bit, loss, d(loss)/d(_language_feature)), and its later replays equal eager serial steps.
+Over a rotating C4 view sequence (train.py:85-87 picks a random view every iteration), GraphedStep
+and PipelinedGraphStep (2 and 3 buffer sets) load each view -- camera and language target -- into
+their ViewSlots and reproduce the eager loop.  A view forced over capacity mid-sequence is a no-op
+for the optimiser (parameters, moments and step count bit-unchanged across that replay: the view is
+left out), check() reports it and the replays continue after a re-capture.
+
+Tolerances: images and losses of the first step bit-exact / 2e-6 (the oracle); later steps carry
+the backward's float-atomic rounding (its order varies between any two runs), so losses agree to
+1e-5 relative and parameters / moments as in tests/test_gpu_pipeline.py, on all but 1e-5 of the
+entries (an entry whose gradient cancels to ~0 can flip the sign of Adam's first update).
+"""
+import numpy as np
+import pytest
+import torch
+
+from langsplat_amd import _native
+from langsplat_amd.graph import GraphedStep, ViewSlot
+from langsplat_amd.optim import Adam
+from langsplat_amd.pipeline import PipelinedGraphStep
+from langsplat_amd.render import render
+from langsplat_amd.synthetic import CONFIGS, activated_inputs, make_cameras, make_gaussians
+from tests.scenes import settings_for
+from tests.test_gpu_fused import _Model, _Opt, _Pipe
+from tests.test_gpu_parity import assert_grad_close, state
+from tests.test_gpu_timed_step import bench_target, oracle_language_step
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+LR = 0.0025  # bench.py's language-feature lr (scene/gaussian_model.py:203-217 with the default args)
+
+
+def _frozen_model(g):
+    m = _Model(g, DEV)
+    for n in ("xyz", "features_dc", "features_rest", "scaling", "rotation", "opacity"):
+        getattr(m, "_" + n).requires_grad_(False)
+    return m
+
+
+def _adam(m, lr=LR):
+    """The language step's Adam (scene/gaussian_model.py:217-229) with eps 1e-8 instead of 1e-15: with
+    1e-15 a Gaussian whose gradient is float-atomic noise (~1e-12, an occluded one) moves by a full
+    +-lr whose sign is that noise, so two runs of ANY form drift apart by ~1e-4 of the loss within a
+    few steps (measured at C3).  1e-8 keeps such updates ~1e-4 lr while every gradient of a visible
+    Gaussian (~1e-6) still takes a ~full-size step: the comparisons below then test the forms, not
+    the noise.  (bench.py and the single-step oracle checks keep 1e-15.)"""
+    return Adam([{"params": [m._language_feature], "lr": lr, "name": "language_feature"}], lr=0.0, eps=1e-8)
+
+
+def _state(m, opt):
+    st = opt.state[m._language_feature]
+    return (m._language_feature.detach().clone(), st["exp_avg"].clone(), st["exp_avg_sq"].clone())
+
+
+def assert_close_mostly(name, got, want, rtol, atol, outliers=1e-5):
+    """|got - want| <= atol + rtol |want| on all but `outliers` of the entries."""
+    got, want = got.double(), want.double()
+    bad = (got - want).abs() > atol + rtol * want.abs()
+    n = int(bad.sum().item())
+    assert n <= outliers * bad.numel(), f"{name}: {n} / {bad.numel()} entries off " \
+                                        f"(max |diff| {float((got - want).abs().max().item()):.3e})"
+
+
+def assert_states_close(a, b, tag):
+    for name, x, y, rtol, atol in (("param", a[0], b[0], 1e-5, 1e-6), ("exp_avg", a[1], b[1], 1e-4, 1e-9),
+                                   ("exp_avg_sq", a[2], b[2], 1e-4, 1e-12)):
+        assert_close_mostly(f"{tag} {name}", x, y, rtol, atol)
+
+
+def _eager_step(m, opt, cam, gt, mask):
+    loss = render(cam, m, _Pipe, torch.zeros(3, device=DEV), _Opt, language_target=(gt, mask))["language_l1"]
+    loss.backward()
+    opt.step()
+    opt.zero_grad(set_to_none=True)
+    return loss.detach().clone()
+
+
+# ---- capacity mode at full size --------------------------------------------------------------------
+
+@pytest.mark.parametrize("cfg", ["C3", "C5"])
+def test_capacity_mode_matches_eager_full_size(cfg, monkeypatch):
+    """The benched language step's forward (fused activations + fused loss, raw parameters) in
+    capacity mode against the eager forward at full size: images, radii, loss, per-tile ranges and
+    order, final T and contributor counts bit-identical; the language-step backward's gradients
+    within the parity tolerance.  C5 (3M Gaussians) takes the LSD depth order."""
+    monkeypatch.setenv("LANGSPLAT_AMD_FUSED", "1")
+    c = CONFIGS[cfg]
+    P, W, H = c["P"], c["width"], c["height"]
+    g = make_gaussians(P, seed=0)
+    cam = make_cameras(c["views"], W, H, device=DEV)[0]
+    gt, mask = (t.to(DEV) for t in bench_target(H, W, 0))
+    outs = []
+    for mode in ("eager", "capacity"):
+        m = _frozen_model(g)
+        sb = _native.static_buffers()
+        ov = torch.full((), 7, dtype=torch.int32, device=DEV)
+        if mode == "eager":
+            with sb:
+                pkg = render(cam, m, _Pipe, torch.zeros(3, device=DEV), _Opt, language_target=(gt, mask))
+            R, E = _native.LAST_COUNTS[(P, W, H)]
+        else:
+            with sb, _native.capacity(int(R * 1.125) + 1024, int(E * 1.125) + 1024, ov):
+                pkg = render(cam, m, _Pipe, torch.zeros(3, device=DEV), _Opt, language_target=(gt, mask))
+        pkg["language_l1"].backward()
+        torch.cuda.synchronize()
+        if mode == "capacity":
+            assert int(ov.item()) == 0
+        geom, binning, image = (sb.tensors[("scratch", k)] for k in (0, 1, 2))
+        outs.append(dict(color=pkg["render"].detach().clone(), lang=pkg["language_feature_image"].detach().clone(),
+                         radii=pkg["radii"].clone(), loss=pkg["language_l1"].detach().clone(),
+                         grad=m._language_feature.grad.detach().cpu().numpy(),
+                         vgrad=pkg["viewspace_points"].grad.detach().cpu().numpy(),
+                         st=state((R, None, None, None, geom, binning, image), P, W, H)))
+    e, cp = outs
+    for k in ("color", "lang", "radii", "loss"):
+        assert torch.equal(e[k], cp[k]), k
+    for k in ("ranges", "final_T", "n_contrib"):
+        np.testing.assert_array_equal(e["st"][k], cp["st"][k])
+    np.testing.assert_array_equal(e["st"]["point_list"][:R], cp["st"]["point_list"][:R])
+    assert_grad_close("language_feature (raw)", cp["grad"], e["grad"])
+    assert_grad_close("viewspace_points", cp["vgrad"], e["vgrad"])
+
+
+# ---- the benched form at the benched size ------------------------------------------------------------
+
+def test_pipelined_graph_full_c3_matches_oracle_and_eager(monkeypatch):
+    """bench.py's PipelinedGraphStep at C3: the first replay against oracle_language_step (images bit
+    for bit, loss, the raw language-feature gradient), then K replays against K eager serial steps of
+    the same view (losses, parameters, Adam moments, device step count)."""
+    monkeypatch.setenv("LANGSPLAT_AMD_FUSED", "1")
+    c = CONFIGS["C3"]
+    P, W, H = c["P"], c["width"], c["height"]
+    g = make_gaussians(P, seed=0)
+    cam_cpu = make_cameras(1, W, H)[0]
+    gt_cpu, mask_cpu = bench_target(H, W, 0)
+    run, loss_ref, d_lang_ref, _ = oracle_language_step(g, cam_cpu, gt_cpu, mask_cpu)
+    cam, gt, mask = cam_cpu.to(DEV), gt_cpu.to(DEV), mask_cpu.to(DEV)
+    K = 4
+    # eager serial steps
+    me = _frozen_model(g)
+    oe = _adam(me)
+    eager_losses = [_eager_step(me, oe, cam, gt, mask) for _ in range(1 + K)]
+    se = _state(me, oe)
+    # the benched form
+    mg = _frozen_model(g)
+    og = _adam(mg)
+    bg = torch.zeros(3, device=DEV)
+    pg = PipelinedGraphStep(lambda: render(cam, mg, _Pipe, bg, _Opt, language_target=(gt, mask))["language_l1"],
+                            [mg._language_feature], og, sets=2).capture()
+    first = pg.replay().clone()
+    pg.synchronize()
+    torch.cuda.synchronize()
+    out = pg.sets[0].tensors
+    np.testing.assert_array_equal(out[("out", "color")].detach().cpu().numpy(), run.color)
+    np.testing.assert_array_equal(out[("out", "language")].detach().cpu().numpy(), run.language)
+    np.testing.assert_array_equal(out[("out", "radii")].detach().cpu().numpy(), run.radii)
+    assert abs(float(first.item()) - loss_ref) <= 2e-6 * loss_ref
+    assert_grad_close("language_feature (raw), first replay", pg.grads[0][0].detach().cpu().numpy(), d_lang_ref)
+    losses = [first] + [pg.replay().clone() for _ in range(K)]
+    pg.synchronize()
+    torch.cuda.synchronize()
+    assert pg.check() and pg.captures == 1
+    pg.sync()
+    assert int(og.state[mg._language_feature]["step"].item()) == 1 + K
+    assert torch.equal(losses[0], eager_losses[0])
+    torch.testing.assert_close(torch.stack(losses), torch.stack(eager_losses), rtol=1e-5, atol=0)
+    assert_states_close(_state(mg, og), se, "C3 pipelined graph")
+
+
+def test_graphed_step_full_c5_matches_eager(monkeypatch):
+    """GraphedStep (one graph: render + loss + backward + Adam) at C5, where the depth order is the
+    LSD passes with the pass count of the last eager forward: 3 replays equal 3 eager steps."""
+    monkeypatch.setenv("LANGSPLAT_AMD_FUSED", "1")
+    c = CONFIGS["C5"]
+    P, W, H = c["P"], c["width"], c["height"]
+    g = make_gaussians(P, seed=0)
+    cam = make_cameras(c["views"], W, H, device=DEV)[0]
+    gt, mask = (t.to(DEV) for t in bench_target(H, W, 0))
+    K = 3
+    me = _frozen_model(g)
+    oe = _adam(me)
+    eager_losses = [_eager_step(me, oe, cam, gt, mask) for _ in range(K)]
+    se = _state(me, oe)
+    del me, oe
+    mg = _frozen_model(g)
+    og = _adam(mg)
+    bg = torch.zeros(3, device=DEV)
+
+    def step():
+        loss = render(cam, mg, _Pipe, bg, _Opt, language_target=(gt, mask))["language_l1"]
+        loss.backward()
+        return loss
+    gs = GraphedStep(step, [mg._language_feature], optimizer=og).capture()
+    losses = [gs.replay().clone() for _ in range(K)]
+    torch.cuda.synchronize()
+    assert gs.check() and gs.captures == 1
+    gs.sync()
+    assert int(og.state[mg._language_feature]["step"].item()) == K
+    assert torch.equal(losses[0], eager_losses[0])
+    torch.testing.assert_close(torch.stack(losses), torch.stack(eager_losses), rtol=1e-5, atol=0)
+    assert_states_close(_state(mg, og), se, "C5 graph")
+
+
+# ---- a rotating view sequence ------------------------------------------------------------------------
+
+SEQ = [0, 3, 5, 1, 7, 2, 6, 4]
+
+
+def _c4_views(seq=SEQ, radius=4.0, cfg="C4", P=None):
+    c = CONFIGS[cfg]
+    W, H = c["width"], c["height"]
+    cams = make_cameras(8, W, H, radius=radius, device=DEV)
+    views = []
+    for v in seq:
+        gt, mask = bench_target(H, W, v)
+        views.append((cams[v], gt.to(DEV), mask.to(DEV)))
+    return views
+
+
+def _eager_sequence(g, views):
+    m = _frozen_model(g)
+    opt = _adam(m)
+    R = E = 0
+    losses = []
+    for cam, gt, mask in views:
+        losses.append(_eager_step(m, opt, cam, gt, mask))
+        r, e = next(iter(_native.LAST_COUNTS.values()))
+        R, E = max(R, r), max(E, e)
+    torch.cuda.synchronize()
+    return losses, _state(m, opt), (int(R * 1.05) + 1024, int(E * 1.05) + 1024)
+
+
+def _slot_forward(m):
+    bg = torch.zeros(3, device=DEV)
+    return lambda slot: render(slot, m, _Pipe, bg, _Opt, language_target=slot.language_target)["language_l1"]
+
+
+def test_graphed_step_over_a_view_sequence(monkeypatch):
+    """GraphedStep with a ViewSlot: replay(view=...) loads each view's camera and target; the replays
+    reproduce the eager loop over the same rotating C4 sequence."""
+    monkeypatch.setenv("LANGSPLAT_AMD_FUSED", "1")
+    g = make_gaussians(CONFIGS["C4"]["P"], seed=0)
+    views = _c4_views()
+    losses_e, se, (Rc, Ec) = _eager_sequence(g, views)
+    m = _frozen_model(g)
+    opt = _adam(m)
+    slot = ViewSlot(*views[0])
+    fwd = _slot_forward(m)
+
+    def step():
+        loss = fwd(slot)
+        loss.backward()
+        return loss
+    gs = GraphedStep(step, [m._language_feature], optimizer=opt, view=slot).capture(Rc, Ec)
+    losses = [gs.replay(view=v).clone() for v in views]
+    torch.cuda.synchronize()
+    assert gs.check() and gs.captures == 1
+    gs.sync()
+    assert int(opt.state[m._language_feature]["step"].item()) == len(views)
+    assert torch.equal(losses[0], losses_e[0])
+    torch.testing.assert_close(torch.stack(losses), torch.stack(losses_e), rtol=1e-5, atol=0)
+    assert_states_close(_state(m, opt), se, "graph sequence")
+
+
+@pytest.mark.parametrize("sets", [2, 3])
+def test_pipelined_graph_over_a_view_sequence(sets, monkeypatch):
+    """PipelinedGraphStep with one ViewSlot per buffer set: capture(views=the first S - 1 views),
+    replay(next_view=the view S - 1 ahead); every replay composites its own view's geometry with its
+    own target, and the sequence reproduces the eager loop."""
+    monkeypatch.setenv("LANGSPLAT_AMD_FUSED", "1")
+    g = make_gaussians(CONFIGS["C4"]["P"], seed=0)
+    views = _c4_views()
+    losses_e, se, (Rc, Ec) = _eager_sequence(g, views)
+    m = _frozen_model(g)
+    opt = _adam(m)
+    slots = [ViewSlot(*views[0]) for _ in range(sets)]
+    pg = PipelinedGraphStep(_slot_forward(m), [m._language_feature], opt, slots=slots)
+    pg.capture(Rc, Ec, views=views[:sets - 1])
+    L = sets - 1
+    losses = []
+    for k in range(len(views)):
+        nxt = views[k + L] if k + L < len(views) else None
+        losses.append(pg.replay(next_view=nxt).clone())
+    pg.synchronize()
+    torch.cuda.synchronize()
+    assert pg.check() and pg.captures == 1
+    pg.sync()
+    assert int(opt.state[m._language_feature]["step"].item()) == len(views)
+    assert torch.equal(losses[0], losses_e[0])
+    torch.testing.assert_close(torch.stack(losses), torch.stack(losses_e), rtol=1e-5, atol=0)
+    assert_states_close(_state(m, opt), se, f"pipelined graph sequence, {sets} sets")
+
+
+# ---- a view over capacity mid-sequence ---------------------------------------------------------------
+
+def _overflow_views(W=320, H=240):
+    """Five views of a small scene; the third is a camera pulled in close (same field of view), with
+    several times the tile instances of the others."""
+    far = make_cameras(8, W, H, radius=4.0, device=DEV)
+    near = make_cameras(8, W, H, radius=1.6, device=DEV)
+    cams = [far[0], far[2], near[1], far[5], far[3]]
+    out = []
+    for i, cam in enumerate(cams):
+        gt, mask = bench_target(H, W, i)
+        out.append((cam, gt.to(DEV), mask.to(DEV)))
+    return out
+
+
+def _snap(m, opt):
+    st = opt.state[m._language_feature]
+    return (m._language_feature.detach().clone(), st["exp_avg"].clone(), st["exp_avg_sq"].clone(),
+            int(opt._step_dev[0].item()))
+
+
+def _assert_bit_equal(a, b):
+    for x, y in zip(a[:3], b[:3]):
+        assert torch.equal(x, y)
+    assert a[3] == b[3]
+
+
+@pytest.mark.parametrize("form", ["graph", "pipelined2", "pipelined3"])
+def test_overflowed_view_is_a_noop_for_the_optimizer(form, monkeypatch):
+    """Capacities from the far views (headroom 1.0); the near view overflows: its replay leaves the
+    language feature, both Adam moments and the device step count bit-unchanged, its gradient is zero
+    (nothing was rasterized), the optimizer counts one skipped step, check() re-captures -- and the
+    parameters then match the eager loop over the sequence WITHOUT that view."""
+    monkeypatch.setenv("LANGSPLAT_AMD_FUSED", "1")
+    P = 20000
+    g = make_gaussians(P, seed=5, scale_range=(0.005, 0.04))
+    views = _overflow_views()
+    bad = 2
+    kept = [v for i, v in enumerate(views) if i != bad]
+    losses_e, se, _ = _eager_sequence(g, kept)
+    m = _frozen_model(g)
+    opt = _adam(m)
+    fwd = _slot_forward(m)
+    far_views = [v for i, v in enumerate(views) if i != bad]
+    # capacities: the largest far view, no headroom
+    R = E = 0
+    for cam, gt, mask in far_views:
+        mm = _frozen_model(g)
+        with torch.no_grad():
+            render(cam, mm, _Pipe, torch.zeros(3, device=DEV), _Opt, language_target=(gt, mask))
+        r, e = _native.LAST_COUNTS[(P, 320, 240)]
+        R, E = max(R, r), max(E, e)
+    with torch.no_grad():
+        render(views[bad][0], _frozen_model(g), _Pipe, torch.zeros(3, device=DEV), _Opt,
+               language_target=views[bad][1:])
+    assert _native.LAST_COUNTS[(P, 320, 240)][0] > 1.2 * R + 1024  # the near view needs more than the capacity
+    snaps, losses = [], []
+    if form == "graph":
+        slot = ViewSlot(*views[0])
+
+        def step():
+            loss = fwd(slot)
+            loss.backward()
+            return loss
+        gs = GraphedStep(step, [m._language_feature], optimizer=opt, view=slot, headroom=1.0)
+        gs.capture(R, E)
+        gs.headroom = 1.0
+        for i, v in enumerate(views):
+            snaps.append(_snap(m, opt))
+            losses.append(gs.replay(view=v).clone())
+            torch.cuda.synchronize()
+            if i == bad:
+                assert int(gs.overflow.item()) == 1
+                assert not m._language_feature.grad.any()  # nothing rasterized: a zero gradient
+        snaps.append(_snap(m, opt))
+        assert opt.skipped_steps() == 1
+        assert not gs.check() and gs.captures == 2
+    else:
+        S = 2 if form == "pipelined2" else 3
+        slots = [ViewSlot(*views[0]) for _ in range(S)]
+        pg = PipelinedGraphStep(fwd, [m._language_feature], opt, slots=slots, headroom=1.0)
+        pg.capture(R, E, views=views[:S - 1])
+        L = S - 1
+        for k in range(len(views)):
+            snaps.append(_snap(m, opt))
+            nxt = views[k + L] if k + L < len(views) else None
+            losses.append(pg.replay(next_view=nxt).clone())
+            pg.synchronize()
+            torch.cuda.synchronize()
+            if k == bad:
+                assert int(pg.overflow[k % S].item()) == 1
+                assert not pg.grads[k % S][0].any()
+        snaps.append(_snap(m, opt))
+        assert opt.skipped_steps() == 1
+        assert not pg.check() and pg.captures == 2
+    # the overflowed replay changed nothing; every other replay stepped
+    _assert_bit_equal(snaps[bad], snaps[bad + 1])
+    for i in range(len(views)):
+        if i != bad:
+            assert not torch.equal(snaps[i][0], snaps[i + 1][0]) and snaps[i + 1][3] == snaps[i][3] + 1
+    opt.sync_steps()
+    assert int(opt.state[m._language_feature]["step"].item()) == len(kept)
+    got = [l for i, l in enumerate(losses) if i != bad]
+    assert torch.equal(got[0], losses_e[0])
+    torch.testing.assert_close(torch.stack(got), torch.stack(losses_e), rtol=1e-5, atol=0)
+    assert_states_close(_state(m, opt), se, f"{form}, overflowed view left out")
+
+
+# ---- Adam on the device: skip flag, learning-rate schedule, recapture --------------------------------
+
+def test_captured_adam_skip_lr_schedule_and_recapture():
+    """lsr_adam_multi with a device step block, captured: replays match torch.optim.Adam under a
+    changing learning rate (sync_lr before each replay), a replay with the skip flag set changes
+    nothing, eager steps interleave with replays, and a second prepare_capture (another capture of
+    the same optimizer) leaves the first graph valid."""
+    torch.manual_seed(0)
+    n = 100003
+    p0 = torch.randn(n, device=DEV)
+    mine = torch.nn.Parameter(p0.clone())
+    ref = torch.nn.Parameter(p0.clone())
+    opt = Adam([{"params": [mine], "lr": 0.01, "name": "x"}], lr=0.0, eps=1e-15)
+    topt = torch.optim.Adam([{"params": [ref], "lr": 0.01, "name": "x"}], lr=0.0, eps=1e-15, foreach=False)
+    grads = [torch.randn(n, device=DEV) for _ in range(8)]
+    gbuf = torch.zeros(n, device=DEV)
+    skip = torch.zeros((), dtype=torch.int32, device=DEV)
+    mine.grad = gbuf
+    opt.prepare_capture()
+    graph = torch.cuda.CUDAGraph()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side), torch.cuda.graph(graph):
+        opt.step(skip=skip)
+    torch.cuda.current_stream().wait_stream(side)
+    lrs = [0.01, 0.005, 0.002, 0.002, 0.001, 0.0005, 0.0005, 0.0001]
+
+    def ref_step(k):
+        for gr in topt.param_groups:
+            gr["lr"] = lrs[k]
+        ref.grad = grads[k].clone()
+        topt.step()
+
+    for k in range(3):
+        opt.param_groups[0]["lr"] = lrs[k]
+        gbuf.copy_(grads[k])
+        opt.sync_lr()
+        graph.replay()
+        ref_step(k)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(mine.detach(), ref.detach(), rtol=1e-6, atol=1e-7)
+    # a skipped replay: bit-unchanged parameters, moments and count
+    before = (mine.detach().clone(), opt.state[mine]["exp_avg"].clone(), opt.state[mine]["exp_avg_sq"].clone())
+    skip.fill_(1)
+    gbuf.copy_(grads[3])
+    opt.sync_lr()
+    graph.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(before[0], mine.detach()) and torch.equal(before[1], opt.state[mine]["exp_avg"])
+    assert torch.equal(before[2], opt.state[mine]["exp_avg_sq"])
+    assert opt.skipped_steps() == 1 and int(opt._step_dev[0].item()) == 3
+    skip.fill_(0)
+    # an eager step between replays continues the count (host and device)
+    opt.param_groups[0]["lr"] = lrs[3]
+    mine.grad = grads[3].clone()
+    opt.step()
+    ref_step(3)
+    mine.grad = gbuf
+    assert int(opt.state[mine]["step"].item()) == 4 and int(opt._step_dev[0].item()) == 4
+    # another capture of the same optimizer: the device block is re-seeded in place
+    opt.prepare_capture()
+    for k in range(4, 8):
+        opt.param_groups[0]["lr"] = lrs[k]
+        gbuf.copy_(grads[k])
+        opt.sync_lr()
+        graph.replay()
+        ref_step(k)
+    torch.cuda.synchronize()
+    opt.sync_steps()
+    assert int(opt.state[mine]["step"].item()) == 8
+    torch.testing.assert_close(mine.detach(), ref.detach(), rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(opt.state[mine]["exp_avg"], topt.state[ref]["exp_avg"], rtol=1e-5, atol=1e-8)
+    torch.testing.assert_close(opt.state[mine]["exp_avg_sq"], topt.state[ref]["exp_avg_sq"], rtol=1e-5, atol=1e-10)
+
+
+# ---- the fused language-step tail -----------------------------------------------------------------------
+
+@pytest.mark.parametrize("form", ["graph", "pipelined2", "pipelined3"])
+def test_fused_tail_matches_separate_launches(form, monkeypatch):
+    """N = 1 captured steps apply Adam inside the backward's epilogue pass (include/lsr.h
+    lsr_backward_args.update; the pipelined form also writes the updated feature into the next set's
+    records, whose composite then skips its fill).  Against the same form with the separate epilogue,
+    Adam and fill launches (LSR_FUSED_TAIL=0): the same losses, gradients, parameters and moments over
+    five replays of a two-view sequence."""
+    monkeypatch.setenv("LANGSPLAT_AMD_FUSED", "1")
+    P, W, H = 60000, 640, 360
+    g = make_gaussians(P, seed=9, scale_range=(0.004, 0.03))
+    cams = make_cameras(8, W, H, device=DEV)
+    views = []
+    for v in (0, 3, 6, 1, 5):
+        gt, mask = bench_target(H, W, v)
+        views.append((cams[v], gt.to(DEV), mask.to(DEV)))
+    runs = {}
+    for fused in ("1", "0"):
+        monkeypatch.setenv("LSR_FUSED_TAIL", fused)
+        m = _frozen_model(g)
+        opt = _adam(m, lr=0.01)
+        fwd = _slot_forward(m)
+        losses, grads = [], []
+        if form == "graph":
+            slot = ViewSlot(*views[0])
+
+            def step():
+                loss = fwd(slot)
+                loss.backward()
+                return loss
+            gs = GraphedStep(step, [m._language_feature], optimizer=opt, view=slot).capture(1 << 22, 1 << 20)
+            for v in views:
+                losses.append(gs.replay(view=v).clone())
+                grads.append(m._language_feature.grad.detach().clone())
+            assert gs.check()
+            gs.sync()
+        else:
+            S = int(form[-1])
+            slots = [ViewSlot(*views[0]) for _ in range(S)]
+            pg = PipelinedGraphStep(fwd, [m._language_feature], opt, slots=slots)
+            pg.capture(1 << 22, 1 << 20, views=views[:S - 1])
+            assert pg.fused == (fused == "1")
+            for k in range(len(views)):
+                nxt = views[k + S - 1] if k + S - 1 < len(views) else None
+                losses.append(pg.replay(next_view=nxt).clone())
+                grads.append(pg.grads[k % S][0].detach().clone())  # read before set k % S is reused
+            pg.synchronize()
+            assert pg.check()
+            pg.sync()
+        torch.cuda.synchronize()
+        assert int(opt.state[m._language_feature]["step"].item()) == len(views)
+        runs[fused] = (torch.stack(losses), grads, _state(m, opt))
+    (lf, gf, sf), (ls, gs_, ss) = runs["1"], runs["0"]
+    assert torch.equal(lf[0], ls[0])  # the first step's loss: same bits (its gradient: float atomics)
+    torch.testing.assert_close(lf, ls, rtol=1e-5, atol=0)
+    for k, (a, b) in enumerate(zip(gf, gs_)):
+        assert_grad_close(f"{form} step {k} language gradient", a.cpu().numpy(), b.cpu().numpy())
+    assert_states_close(sf, ss, f"{form} fused vs separate tail")

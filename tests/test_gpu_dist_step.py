@@ -1,0 +1,65 @@
+"""bench.py's N = 2 language step as two gloo ranks sharing cuda:0.
+
+tests/dist_worker.py runs, on each rank, camera `rank` of C4 (BASELINE.json configs[3]) through the
+eager step (render + fused loss, backward, GradBucket all-reduce, Adam) and through the pipelined
+graph form with the all-reduce launched between its backward and Adam graphs.  The averaged
+language gradient must equal the mean of the two views' oracle gradients (the per-view oracle step of
+tests/test_gpu_timed_step.py), be identical on both ranks, and leave both ranks with identical
+parameters.  gloo reduces on the host: this checks the N > 1 data flow, not RCCL's speed (the RCCL
+path itself runs in tests/test_gpu_rccl.py)."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from langsplat_amd.synthetic import CONFIGS, make_cameras, make_gaussians
+from tests.test_gpu_parity import assert_grad_close
+from tests.test_gpu_timed_step import bench_target, oracle_language_step
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_two_rank_language_step_averages_the_views_gradients(tmp_path):
+    env = dict(os.environ, LSR_DIST_BACKEND="gloo", LANGSPLAT_AMD_FUSED="1", OMP_NUM_THREADS="4")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "tests", "dist_worker.py"), str(tmp_path)]
+    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    outs = [torch.load(tmp_path / f"rank{k}.pt", weights_only=True) for k in (0, 1)]
+    c = CONFIGS["C4"]
+    P, W, H = c["P"], c["width"], c["height"]
+    g = make_gaussians(P, seed=0)
+    cams = make_cameras(c["views"], W, H)
+    refs = []
+    for v in (0, 1):
+        gt, mask = bench_target(H, W, v)
+        run, loss_ref, d_lang, _ = oracle_language_step(g, cams[v], gt, mask)
+        refs.append((loss_ref, d_lang))
+        del run
+    mean = 0.5 * (refs[0][1].astype(np.float64) + refs[1][1].astype(np.float64))
+    for form in ("eager", "pipelined_graph"):
+        for k in (0, 1):
+            o = outs[k][form]
+            # each rank's own loss is its view's
+            assert abs(float(o["loss"]) - refs[k][0]) <= 2e-6 * refs[k][0], (form, k)
+            assert_grad_close(f"{form} rank {k} averaged language gradient", o["grad"].numpy(), mean)
+        assert torch.equal(outs[0][form]["grad"], outs[1][form]["grad"]), form
+        assert torch.equal(outs[0][form]["param"], outs[1][form]["param"]), form
+    assert outs[0]["pipelined_graph"]["step"] == 1
+    # the two forms take the same Adam step from the same averaged gradient (to its rounding: Adam's
+    # first step is lr * g / |g|, so an entry whose gradient cancels to ~0 may differ in sign)
+    a, b = outs[0]["pipelined_graph"]["param"].double(), outs[0]["eager"]["param"].double()
+    off = int(((a - b).abs() > 1e-6 + 1e-5 * b.abs()).sum())
+    assert off <= 1e-5 * a.numel(), off

@@ -31,13 +31,17 @@ def test_library_loads_and_exports_every_declared_symbol():
     for name in _declared_functions():
         assert hasattr(lib, name), name
         assert name in _native.SIGNATURES, f"ctypes binding misses {name}"
-    assert lib.lsr_abi_version() == _native.ABI_VERSION == 11
+    assert lib.lsr_abi_version() == _native.ABI_VERSION == 12
 
 
 def test_header_constants_match_the_python_side():
     hdr = open(os.path.join(ROOT, "include", "lsr.h")).read()
     assert int(re.search(r"#define LSR_ABI_VERSION (\d+)", hdr).group(1)) == _native.ABI_VERSION
     assert int(re.search(r"#define LSR_ADAM_STEP_WORDS (\d+)", hdr).group(1)) == _native.ADAM_STEP_WORDS
+    assert int(re.search(r"#define LSR_ADAM_WORD_SKIPPED (\d+)", hdr).group(1)) == _native.ADAM_WORD_SKIPPED
+    assert int(re.search(r"#define LSR_ADAM_WORD_LR (\d+)", hdr).group(1)) == _native.ADAM_WORD_LR
+    # 16 lr words after the skipped count fit the block
+    assert _native.ADAM_WORD_LR + 16 <= _native.ADAM_STEP_WORDS
 
 
 def test_sizes_and_layout_are_consistent():
@@ -82,9 +86,48 @@ def test_forward_flag_and_phase_validation_without_gpu():
 
     assert call(flags=4) != 0 and "unknown flag" in _native.last_error()
     assert call(phase=_native.forward_phase.GEOMETRY) != 0 and "phase" in _native.last_error()
-    assert call(phase=3, capacity_rendered=16, capacity_entries=16) != 0 and "phase" in _native.last_error()
+    assert call(phase=4, capacity_rendered=16, capacity_entries=16) != 0 and "phase" in _native.last_error()
+    assert call(phase=_native.forward_phase.COMPOSITE_FILLED) != 0 and "phase" in _native.last_error()
     assert call(phase=_native.forward_phase.COMPOSITE, capacity_rendered=16, capacity_entries=16,
                 language_ready=dummy) != 0 and "phase" in _native.last_error()
+
+
+def test_backward_fused_update_validation_without_gpu():
+    """lsr_backward_args.update (ABI 12, the language step's Adam fused into the epilogue) is refused
+    before any device work unless it is the language-only backward of the raw feature it updates; the
+    update's companions without an update are refused too (dummy pointers, never dereferenced)."""
+    import ctypes
+    lib = _native.load()
+    dummy = ctypes.c_void_p(256)
+    s = _native.LsrSettings()
+    s.image_height, s.image_width, s.tanfovx, s.tanfovy, s.sh_degree, s.include_feature = 8, 8, 0.5, 0.5, 0, 1
+    s.bg = s.viewmatrix = s.projmatrix = s.campos = dummy
+    P = 4
+
+    def call(update_param=256, geometry=False, raw=_native.RAW_LANGUAGE, with_update=True, **kw):
+        a = _native.LsrBackwardArgs()
+        a.P, a.M, a.num_rendered = P, 1, 16
+        a.means3D = a.shs = a.opacities = a.scales = a.rotations = a.radii = dummy
+        a.language_feature = ctypes.c_void_p(256)
+        a.geom_buffer = a.binning_buffer = a.image_buffer = dummy
+        a.dL_dmeans2D = a.dL_dlanguage_feature = dummy
+        a.raw = raw
+        if geometry:
+            a.dL_dcolors = a.dL_dopacity = a.dL_dmeans3D = a.dL_dsh = a.dL_dscales = a.dL_drotations = dummy
+        t = _native.LsrAdamTensor(3 * P, update_param, None, 512, 768, 0.01, 0.9, 0.999, 1e-15, 0)
+        if with_update:
+            a.update = ctypes.pointer(t)
+            a.update_step_dev = dummy
+        for k, v in kw.items():
+            setattr(a, k, v)
+        return lib.lsr_backward(ctypes.byref(s), ctypes.byref(a), _native._ALLOC_CB, None, None)
+
+    assert call(geometry=True) != 0 and "fused update" in _native.last_error()
+    assert call(raw=0) != 0 and "fused update" in _native.last_error()
+    assert call(update_param=1024) != 0 and "fused update" in _native.last_error()
+    assert call(dL_dout_color=dummy) != 0 and "fused update" in _native.last_error()
+    assert call(update_step_dev=None) != 0 and "fused update" in _native.last_error()
+    assert call(with_update=False, fill_record=dummy) != 0 and "need update" in _native.last_error()
 
 
 def test_spin_limit_knob_round_trips_without_gpu():
