@@ -1,0 +1,145 @@
+"""Densification at C5 scale (BASELINE.json configs[4]: "HBM-bound stress + densification-scale";
+VERDICT r03 item 8): the RGB stage's adaptive density control (train.py:120-131,
+scene/gaussian_model.py:359-478; langsplat_amd.densify) on the 3M-Gaussian scene, with the HIP Adam
+and the densification-statistics kernel, then training continues at the new P:
+  - the first step after the surgery matches the oracle at the new P (forward bit-exact, every
+    raw-parameter gradient within the full-size parity tolerance);
+  - a captured step (langsplat_amd.graph.GraphedStep, re-captured because every parameter was
+    re-allocated) replays the eager step at the new P.
+"""
+import numpy as np
+import pytest
+import torch
+
+from langsplat_amd.densify import Densifier
+from langsplat_amd.graph import GraphedStep
+from langsplat_amd.optim import Adam
+from langsplat_amd.render import render
+from langsplat_amd.synthetic import CONFIGS, GaussianParams, make_cameras, make_gaussians
+from oracle import oracle
+from tests.scenes import grad_seed, settings_for
+from tests.test_gpu_fused import _Model, _Pipe
+from tests.test_gpu_parity import assert_grad_close
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+class _OptRGB:
+    include_feature = False
+
+
+def _rgb_model(g):
+    m = _Model(g, DEV)
+    m._language_feature.requires_grad_(False)  # RGB stage: the language feature is not trained
+    lr = {"xyz": 1.6e-4, "f_dc": 2.5e-3, "f_rest": 2.5e-3 / 20, "opacity": 0.05, "scaling": 5e-3, "rotation": 1e-3}
+    attrs = {"xyz": "_xyz", "f_dc": "_features_dc", "f_rest": "_features_rest", "opacity": "_opacity",
+             "scaling": "_scaling", "rotation": "_rotation"}
+    opt = Adam([{"params": [getattr(m, a)], "lr": lr[n], "name": n} for n, a in attrs.items()], lr=0.0, eps=1e-15)
+    return m, opt
+
+
+def _l1_step(m, opt, cam, gt, dens=None):
+    pkg = render(cam, m, _Pipe, torch.zeros(3, device=DEV), _OptRGB)
+    loss = torch.abs(pkg["render"] - gt).mean()
+    loss.backward()
+    if dens is not None:
+        dens.add_stats(pkg["radii"], pkg["viewspace_points"].grad)
+    opt.step()
+    opt.zero_grad(set_to_none=True)
+    return loss.detach()
+
+
+def test_densify_at_c5_then_train_at_the_new_size(monkeypatch):
+    monkeypatch.setenv("LANGSPLAT_AMD_FUSED", "1")
+    c = CONFIGS["C5"]
+    P, W, H = c["P"], c["width"], c["height"]
+    g = make_gaussians(P, seed=0)
+    cams = make_cameras(c["views"], W, H, device=DEV)
+    gen = torch.Generator().manual_seed(7)
+    gts = [torch.rand((3, H, W), generator=gen).to(DEV) for _ in range(4)]
+    m, opt = _rgb_model(g)
+    dens = Densifier(m, opt, percent_dense=0.01)
+    for v in range(3):
+        _l1_step(m, opt, cams[v], gts[v], dens)
+    # thresholds that select ~10 % of the seen Gaussians (the reference's 2e-4 is tuned to real scenes)
+    grads = (dens.xyz_gradient_accum / dens.denom).nan_to_num(0.0).squeeze()
+    thr = float(torch.quantile(grads[grads > 0][:1_000_000].float(), 0.9))
+    scale_max = torch.exp(m._scaling).max(dim=1).values
+    sel = grads >= thr
+    n_clone = int((sel & (scale_max <= 0.01)).sum())
+    n_split = int((sel & (scale_max > 0.01)).sum())
+    assert n_clone > 1000 and n_split > 1000
+    torch.manual_seed(11)
+    P1 = dens.densify_and_prune(thr, 0.005, 1.0, None)
+    # clone adds n_clone, split replaces n_split by 2 n_split, then the transparent ones go
+    assert P < P1 <= P + n_clone + n_split
+    assert bool((torch.sigmoid(m._opacity) >= 0.005).all())
+    for grp in opt.param_groups:
+        p = grp["params"][0]
+        assert p.shape[0] == P1 and opt.state[p]["exp_avg"].shape == p.shape
+        assert int(opt.state[p]["step"].item()) == 3
+    assert dens.xyz_gradient_accum.shape == (P1, 1) and not dens.denom.any()
+    # the new scene against the oracle (RGB mode: no language feature), view 3
+    g1 = GaussianParams(*(getattr(m, "_" + n).detach().cpu() for n in
+                          ("xyz", "features_dc", "features_rest", "scaling", "rotation", "opacity")),
+                        torch.zeros((P1, 3)), max_sh_degree=3)
+    cam_cpu = make_cameras(c["views"], W, H)[3]
+    st = settings_for(cam_cpu, sh_degree=3, include_feature=False)
+    a_op, a_sc, a_rot, _ = oracle.activate(oracle.RAW_ALL & ~oracle.RAW_LANGUAGE, g1.opacity, g1.scaling,
+                                          g1.rotation, g1.language_feature)
+    inp = dict(means3D=g1.xyz.clone(), opacities=torch.from_numpy(a_op), scales=torch.from_numpy(a_sc),
+               rotations=torch.from_numpy(a_rot),
+               shs=torch.cat((g1.features_dc, g1.features_rest), dim=1).contiguous())
+    run = oracle.forward(st, **inp)
+    gc, _ = grad_seed(H, W, seed=12)
+    ref = run.backward(gc, None)
+    pkg = render(cams[3], m, _Pipe, torch.zeros(3, device=DEV), _OptRGB)
+    (pkg["render"] * gc.to(DEV)).sum().backward()
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(pkg["render"].detach().cpu().numpy(), run.color)
+    np.testing.assert_array_equal(pkg["radii"].cpu().numpy(), run.radii)
+    d_op, d_sc, d_rot, _ = oracle.activate_backward(
+        oracle.RAW_ALL & ~oracle.RAW_LANGUAGE, (g1.opacity, g1.scaling, g1.rotation, g1.language_feature),
+        (ref["opacities"], ref["scales"], ref["rotations"], np.zeros((P1, 3), np.float32)))
+    out = 1e-5  # the full-size allowance of tests/test_gpu_parity.py (cancelling per-pixel terms)
+    assert_grad_close("xyz", m._xyz.grad.cpu().numpy(), ref["means3D"], outliers=out)
+    assert_grad_close("features_dc", m._features_dc.grad.cpu().numpy(), ref["shs"][:, :1], outliers=out)
+    assert_grad_close("features_rest", m._features_rest.grad.cpu().numpy(), ref["shs"][:, 1:], outliers=out)
+    assert_grad_close("opacity", m._opacity.grad.cpu().numpy(), d_op, outliers=out)
+    assert_grad_close("scaling", m._scaling.grad.cpu().numpy(), d_sc, outliers=out)
+    assert_grad_close("rotation", m._rotation.grad.cpu().numpy(), d_rot, outliers=out)
+    assert_grad_close("viewspace", pkg["viewspace_points"].grad.cpu().numpy(), ref["means2D"], outliers=out)
+    opt.zero_grad(set_to_none=True)
+    # training continues at P1: eager steps, and a captured step re-captured over the new tensors
+    state0 = {g_["name"]: (g_["params"][0].detach().clone(), opt.state[g_["params"][0]]["exp_avg"].clone(),
+                           opt.state[g_["params"][0]]["exp_avg_sq"].clone()) for g_ in opt.param_groups}
+    eager = [_l1_step(m, opt, cams[4], gts[3]) for _ in range(2)]
+    after_eager = {g_["name"]: g_["params"][0].detach().clone() for g_ in opt.param_groups}
+    for g_ in opt.param_groups:  # back to the state before the two eager steps
+        p = g_["params"][0]
+        p.data.copy_(state0[g_["name"]][0])
+        opt.state[p]["exp_avg"].copy_(state0[g_["name"]][1])
+        opt.state[p]["exp_avg_sq"].copy_(state0[g_["name"]][2])
+        opt.state[p]["step"] = torch.tensor(3.0)
+    m2, opt2 = m, opt
+    bg = torch.zeros(3, device=DEV)
+    params = [g_["params"][0] for g_ in opt2.param_groups]
+
+    def step():
+        pkg = render(cams[4], m2, _Pipe, bg, _OptRGB)
+        loss = torch.abs(pkg["render"] - gts[3]).mean()
+        loss.backward()
+        return loss
+    gs = GraphedStep(step, params, optimizer=opt2).capture()
+    losses = [gs.replay().detach().clone() for _ in range(2)]
+    torch.cuda.synchronize()
+    assert gs.check()
+    gs.sync()
+    assert int(opt2.state[params[0]]["step"].item()) == 5
+    assert torch.equal(losses[0], eager[0])
+    torch.testing.assert_close(losses[1], eager[1], rtol=1e-5, atol=0)
+    for g_ in opt2.param_groups:
+        a, b = g_["params"][0].detach(), after_eager[g_["name"]]
+        bad = ((a - b).abs() > 1e-6 + 1e-5 * b.abs()).sum()
+        assert int(bad) <= 1e-4 * a.numel(), (g_["name"], int(bad))
