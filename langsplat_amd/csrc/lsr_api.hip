@@ -390,8 +390,8 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
     const size_t HW = (size_t)W * H;
     if (P == 0) {
         // upstream leaves the images at their zero initialisation when there is nothing to draw
-        LSR_TRY(hipMemsetAsync(a->out_color, 0, 3 * HW * 4, stream), "memset color");
-        LSR_TRY(hipMemsetAsync(a->out_language_feature, 0, 3 * HW * 4, stream), "memset language");
+        LSR_TRY(zero_fill(a->out_color, 3 * HW * 4, stream), "memset color");
+        LSR_TRY(zero_fill(a->out_language_feature, 3 * HW * 4, stream), "memset language");
         if (a->out_loss) {
             const Layout L0 = make_layout(0, W, H, 0, 0);
             char* image = static_cast<char*>(alloc(user, LSR_BUF_IMAGE, L0.image_bytes));
@@ -556,7 +556,7 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
         const int passes = bits <= 8 ? 1 : (bits + 7) / 8;
         if (depth_order_uses_pass_count(P)) hb->depth_passes = passes;
         if (depth_order_uses_pass_count(P) && passes > guess) {  // short guess: clear the scan status, sort again
-            LSR_TRY(hipMemsetAsync(geom + L.scan_regions, 0, 4 * kDepthScans * L.scan_region_geom, stream),
+            LSR_TRY(zero_fill(geom + L.scan_regions, 4 * kDepthScans * L.scan_region_geom, stream),
                     "clear scan status");
             LSR_TRY(launch_depth_order(P, passes, L, geom, counters, &hb->stall, stream, debug), "depth order");
         }
@@ -564,7 +564,7 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
 
     const bool emitted = fused_emit && (int64_t)host_cnt[kCntSuper] <= L.fused_cap;
     if (fused_emit && !emitted) {  // entries beyond the fused capacity: the depth order again, unfused
-        LSR_TRY(hipMemsetAsync(geom + L.scan_regions, 0, 4 * L.zero_words, stream), "clear scan status");
+        LSR_TRY(zero_fill(geom + L.scan_regions, 4 * L.zero_words, stream), "clear scan status");
         LSR_TRY(launch_depth_order(P, guess, L, geom, counters, &hb->stall, stream, debug, false), "depth order");
     }
     L = make_layout(P, W, H, R, (int64_t)host_cnt[kCntSuper]);
@@ -652,7 +652,7 @@ int32_t lsr_backward(const lsr_settings* s, const lsr_backward_args* a, lsr_allo
     } else {
         grad = static_cast<float*>(alloc(user, LSR_BUF_BACKWARD, lsr_backward_bytes(P)));
         if (!grad) return fail(LSR_ERR_ALLOC, "lsr_backward: gradient scratch allocation failed");
-        LSR_TRY(hipMemsetAsync(grad, 0, 4 * (size_t)stride * (size_t)P, stream), "memset grad");
+        LSR_TRY(zero_fill(grad, 4 * (size_t)stride * (size_t)P, stream), "memset grad");
     }
 
     RenderParams rp{};
@@ -696,7 +696,7 @@ int32_t lsr_backward(const lsr_settings* s, const lsr_backward_args* a, lsr_allo
                                      rp.include_feature ? a->dL_dlanguage_feature : nullptr, stream),
                 "gradient epilogue");
         if (!rp.include_feature && a->dL_dlanguage_feature)
-            LSR_TRY(hipMemsetAsync(a->dL_dlanguage_feature, 0, (size_t)P * 3 * 4, stream), "memset dlang");
+            LSR_TRY(zero_fill(a->dL_dlanguage_feature, (size_t)P * 3 * 4, stream), "memset dlang");
         return LSR_OK;
     }
 
@@ -737,7 +737,7 @@ int32_t lsr_backward(const lsr_settings* s, const lsr_backward_args* a, lsr_allo
     bp.shs_rest = a->shs_rest;
     bp.dsh_rest = a->dL_dsh_rest;
     if (!a->shs && a->dL_dsh && a->M > 0)
-        LSR_TRY(hipMemsetAsync(a->dL_dsh, 0, (size_t)P * a->M * 3 * 4, stream), "memset dsh");
+        LSR_TRY(zero_fill(a->dL_dsh, (size_t)P * a->M * 3 * 4, stream), "memset dsh");
     LSR_TRY(launch_preprocess_backward(bp, stream), "preprocess backward");
     return LSR_OK;
 }

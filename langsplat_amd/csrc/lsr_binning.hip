@@ -1927,7 +1927,7 @@ hipError_t launch_binning(int P, int64_t R, const Layout& L, char* geom, char* i
                           hipStream_t s, bool debug, bool emitted, DevCount dc)
 {
     uint2* ranges = reinterpret_cast<uint2*>(image + L.ranges);
-    if (R == 0) return hipMemsetAsync(ranges, 0, 8 * (size_t)L.tiles, s);
+    if (R == 0) return zero_fill(ranges, 8 * (size_t)L.tiles, s);
     const int64_t E = L.super_entries;
     uint32_t* regions = reinterpret_cast<uint32_t*>(binning + L.bin_scan_regions);
     uint32_t* kA = reinterpret_cast<uint32_t*>(binning + L.super_keys);

@@ -214,6 +214,40 @@ hipError_t launch_language_tail(int P, const int32_t* radii, const float* grad, 
     return hipGetLastError();
 }
 
+// Zero fill by a kernel instead of hipMemsetAsync: inside a stream capture the runtime turns a
+// memset into a graph memset node, and instantiating a graph that held a ~220 MB one (the full
+// backward's gradient records at 3.4M Gaussians) crashed the host runtime (tests/test_gpu_densify.py,
+// round 4); a kernel node is what every other launch of a step is.
+__global__ __launch_bounds__(256) void k_zero(uint4* __restrict__ p16, int64_t n16, uint8_t* __restrict__ tail,
+                                              int ntail)
+{
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += stride) p16[i] = z;
+    if (blockIdx.x == 0 && (int)threadIdx.x < ntail) tail[threadIdx.x] = 0;
+}
+
+hipError_t zero_fill(void* p, size_t bytes, hipStream_t s)
+{
+    if (bytes == 0) return hipSuccess;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    const size_t head = (16 - (a & 15)) & 15;  // bytes before the first 16-B boundary
+    if (head != 0) {                           // unaligned start: a byte kernel over the first head bytes
+        const size_t h = head < bytes ? head : bytes;
+        hipLaunchKernelGGL(k_zero, dim3(1), dim3(256), 0, s, (uint4*)nullptr, (int64_t)0, static_cast<uint8_t*>(p),
+                           (int)h);
+        if (h == bytes) return hipGetLastError();
+    }
+    uint8_t* body = static_cast<uint8_t*>(p) + head;
+    const size_t rest = bytes - head;
+    const int64_t n16 = (int64_t)(rest / 16);
+    const int ntail = (int)(rest % 16);
+    const int64_t blocks = std::min<int64_t>(std::max<int64_t>((n16 + 255) / 256, 1), 4096);
+    hipLaunchKernelGGL(k_zero, dim3((unsigned)blocks), dim3(256), 0, s, reinterpret_cast<uint4*>(body), n16,
+                       body + 16 * n16, ntail);
+    return hipGetLastError();
+}
+
 // Densification statistics of one view (train.py:125-126: max_radii2D[vis] = max(max_radii2D[vis],
 // radii[vis]) and add_densification_stats, scene/gaussian_model.py:480-482: xyz_gradient_accum[vis]
 // += ||viewspace.grad[vis, :2]||, denom[vis] += 1), vis = radii > 0, in one pass.

@@ -229,20 +229,21 @@ struct FwdPixel {
 // One front-to-back blend of the entry at LDS byte offset o (slot o / 16) with alpha al (upstream
 // FORWARD::renderCUDA; the operation order of oracle render_pixel): stop before the entry once T
 // would fall below 1e-4 (then T -> -T: done).  lb16 = 16 (list index of slot 0 + 1).
+// Cc / Ff: the entry's colour record {r, g, b, f0} and {f1, f2}, read by the caller (both entries of a
+// pair at once, so their LDS latency is paid once per pair)
 template <bool kFeat>
-__device__ __forceinline__ void fwd_pixel_blend(FwdPixel& q, float al, uint32_t o, uint32_t lb16, const char* sC,
-                                                const char* sF)
+__device__ __forceinline__ void fwd_pixel_blend(FwdPixel& q, float al, uint32_t o, uint32_t lb16, const float4& Cc,
+                                                const lsr_f2& Ff)
 {
     const float test_T = q.T * (1.0f - al);
     const bool go = !(test_T < 0.0001f);
     if (go) {
-        const float4 Cc = *reinterpret_cast<const float4*>(sC + o);
         const float w = al * q.T;
         const lsr_f2 w2 = make_f2(w, w);
         q.C01 = __builtin_elementwise_fma(make_f2(Cc.x, Cc.y), w2, q.C01);
         if (kFeat) {
             q.C2F0 = __builtin_elementwise_fma(make_f2(Cc.z, Cc.w), w2, q.C2F0);
-            q.F12 = __builtin_elementwise_fma(*reinterpret_cast<const lsr_f2*>(sF + o), w2, q.F12);
+            q.F12 = __builtin_elementwise_fma(Ff, w2, q.F12);
         } else {
             q.C2F0.x = fma_(Cc.z, w, q.C2F0.x);
         }
@@ -476,8 +477,10 @@ __global__ __launch_bounds__(kTilePixels, 7) void k_render_forward(RenderParams 
     __shared__ float4 sF[kThreads];  // f1, f2, -, -  (16-B slots: every record of slot s at byte 16 s)
     __shared__ uint8_t sM[kThreads];  // entry_cover mask
     // per-wave culled slot lists, as byte offsets 16 s; slot n holds offset 0, so the walk reads the
-    // second entry of a pair without testing i + 1 < n (its result is discarded then)
-    __shared__ uint16_t sL[kThreads / 64][kThreads + 1];
+    // second entry of a pair without testing i + 1 < n (its result is discarded then).  Rows of
+    // kThreads + 2 (4-B aligned): a pair's two offsets are one 32-bit read, and the walk reads the
+    // next pair's (up to slot n + 1) one pair ahead
+    __shared__ uint16_t sL[kThreads / 64][kThreads + 2];
     __shared__ uint32_t s_last;
 
     const int T = p.gx * p.gy;
@@ -574,11 +577,16 @@ __global__ __launch_bounds__(kTilePixels, 7) void k_render_forward(RenderParams 
         // so the two chains interleave; only the transmittance test and the blend are sequential.
         // Same operations per entry as one at a time (bit-identical results).  The list holds byte
         // offsets, so every record read addresses LDS with the list value itself.
+        // the pair's two offsets come from one 32-bit read issued during the previous pair, so a
+        // pair's record reads do not wait behind a dependent read of their offsets
+        const uint32_t* const sL2 = reinterpret_cast<const uint32_t*>(sL[wave]);
+        uint32_t oo = sL2[0];
         for (int i = 0; i < n; i += 2) {
             if (__ballot(q.T > 0.0f) == 0ull) break;
-            const uint32_t o0 = sL[wave][i];
+            const uint32_t o0 = oo & 0xFFFFu;
             const bool has1 = i + 1 < n;
-            const uint32_t o1 = sL[wave][i + 1];
+            const uint32_t o1 = oo >> 16;
+            oo = sL2[(i >> 1) + 1];  // slots i + 2, i + 3 (<= n + 1)
             const float4 A0 = *reinterpret_cast<const float4*>(cA + o0), B0 = *reinterpret_cast<const float4*>(cB + o0);
             const float4 A1 = *reinterpret_cast<const float4*>(cA + o1), B1 = *reinterpret_cast<const float4*>(cB + o1);
             // per entry {dx, dy} and {A.z dx, A.w dy} as packed ops on the record's own register pairs
@@ -593,8 +601,13 @@ __global__ __launch_bounds__(kTilePixels, 7) void k_render_forward(RenderParams 
             const float al1 = fminf(0.99f, B1.y * G2.y);
             const bool ok0 = !(pw0 > 0.0f || pw0 < B0.z) && !(al0 < 1.0f / 255.0f);
             const bool ok1 = has1 && !(pw1 > 0.0f || pw1 < B1.z) && !(al1 < 1.0f / 255.0f);
-            if (ok0 && q.T > 0.0f) fwd_pixel_blend<kFeat>(q, al0, o0, lb16, cC, cF);
-            if (ok1 && q.T > 0.0f) fwd_pixel_blend<kFeat>(q, al1, o1, lb16, cC, cF);
+            // both entries' colour records in one LDS round trip (the records' arrays are padded:
+            // every slot, and slot n's offset 0, is readable)
+            const float4 Cc0 = *reinterpret_cast<const float4*>(cC + o0), Cc1 = *reinterpret_cast<const float4*>(cC + o1);
+            const lsr_f2 Ff0 = kFeat ? *reinterpret_cast<const lsr_f2*>(cF + o0) : make_f2(0.f, 0.f);
+            const lsr_f2 Ff1 = kFeat ? *reinterpret_cast<const lsr_f2*>(cF + o1) : make_f2(0.f, 0.f);
+            if (ok0 && q.T > 0.0f) fwd_pixel_blend<kFeat>(q, al0, o0, lb16, Cc0, Ff0);
+            if (ok1 && q.T > 0.0f) fwd_pixel_blend<kFeat>(q, al1, o1, lb16, Cc1, Ff1);
         }
     }
     const uint32_t qlast = q.last16 >> 4;

@@ -100,7 +100,7 @@ class PipelinedGraphStep:
     The rasterizer forward is split in two calls (include/lsr.h lsr_forward_args.phase, capacity
     mode): the geometry half (preprocess, depth order, binning; the language feature deferred) and
     the composite half (the feature into the records, compositing, fused loss).  Per static buffer
-    set p (_native.static_buffers: the same addresses at every forward; S sets, default 2) the graphs
+    set p (_native.static_buffers: the same addresses at every forward; S sets, default 3) the graphs
 
         G_geo[p]:  the geometry half of the view, into set p                  (stream B)
         G_comp[p]: the composite half of set p and the loss                     (stream A)
@@ -153,7 +153,10 @@ class PipelinedGraphStep:
         self.headroom = float(headroom)
         self.warmup = int(warmup)
         dev = self.params[0].device
-        S = int(sets if sets is not None else (len(slots) if slots else os.environ.get("LSR_PG_SETS", "2")))
+        # three sets by default: measured at C3 (tools/pg_sweep.py, one box) 0.435 ms per step against
+        # 0.482 with two; a view's geometry then runs two steps ahead, beside the backward and the
+        # next compositing, and no compositing waits on a cross-stream event that is not yet signalled
+        S = int(sets if sets is not None else (len(slots) if slots else os.environ.get("LSR_PG_SETS", "3")))
         if S < 2:
             raise ValueError("PipelinedGraphStep: at least two buffer sets")
         if slots is not None and len(slots) != S:

@@ -154,7 +154,8 @@ def test_pipelined_graph_full_c3_matches_oracle_and_eager(monkeypatch):
     og = _adam(mg)
     bg = torch.zeros(3, device=DEV)
     pg = PipelinedGraphStep(lambda: render(cam, mg, _Pipe, bg, _Opt, language_target=(gt, mask))["language_l1"],
-                            [mg._language_feature], og, sets=2).capture()
+                            [mg._language_feature], og).capture()
+    assert pg.S == 3 and pg.fused  # bench.py's form: three buffer sets, the fused language-step tail
     first = pg.replay().clone()
     pg.synchronize()
     torch.cuda.synchronize()
