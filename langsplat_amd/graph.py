@@ -21,6 +21,11 @@ that view had been left out of the sequence.  Without an optimizer
 after each replay on the gradients the graph wrote into the parameters' .grad tensors.  Either way
 the graph owns those .grad tensors: do not set them to None.
 
+Before capture(), drop the outputs of any eager step (loss, render package): an autograd graph still
+alive binds the parameters' AccumulateGrad nodes to the stream it ran on, the captured backward then
+waits on that non-capturing stream, and this HIP runtime crashes at the end of the capture
+(DESIGN.md §5a).
+
 A sequence of views (train.py:85-87 picks a random camera every iteration): pass view=ViewSlot(...)
 and have step_fn render from the slot (it is Camera-like, and carries the language target), then
 replay(view=(camera, gt, mask)) copies that view into the slot on the current stream before the

@@ -111,6 +111,10 @@ def test_densify_at_c5_then_train_at_the_new_size(monkeypatch):
     assert_grad_close("rotation", m._rotation.grad.cpu().numpy(), d_rot, outliers=out)
     assert_grad_close("viewspace", pkg["viewspace_points"].grad.cpu().numpy(), ref["means2D"], outliers=out)
     opt.zero_grad(set_to_none=True)
+    # no autograd graph of an eager step may stay alive into a capture: its AccumulateGrad nodes are
+    # bound to the stream they were created on, and the capture would then wait on that (default,
+    # non-capturing) stream -- which this HIP runtime does not report but crashes on at capture end
+    del pkg
     # training continues at P1: eager steps, and a captured step re-captured over the new tensors
     state0 = {g_["name"]: (g_["params"][0].detach().clone(), opt.state[g_["params"][0]]["exp_avg"].clone(),
                            opt.state[g_["params"][0]]["exp_avg_sq"].clone()) for g_ in opt.param_groups}

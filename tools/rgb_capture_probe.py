@@ -1,7 +1,9 @@
 """Captures the RGB-stage step (render + L1 + backward through every gradient + 6-group Adam) into a
 langsplat_amd.graph.GraphedStep at a given size and replays it once (diagnostic aid):
 
-    python3 tools/rgb_capture_probe.py P W H [adam|noadam]
+    python3 tools/rgb_capture_probe.py P W H [adam|noadam] [keepgraph]
+
+keepgraph: an eager step's autograd graph stays alive (its output held) across the capture.
 """
 import faulthandler
 import os
@@ -28,6 +30,11 @@ def main():
     gt = torch.rand((3, H, W), generator=torch.Generator().manual_seed(1)).to(dev)
     m, opt = _rgb_model(g)
     _l1_step(m, opt, cam, gt)
+    keep = None
+    if "keepgraph" in sys.argv:
+        keep = render(cam, m, _Pipe, torch.zeros(3, device=dev), _OptRGB)
+        (keep["render"] * 1.0).sum().backward(retain_graph=True)
+        opt.zero_grad(set_to_none=True)
     bg = torch.zeros(3, device=dev)
     params = [g_["params"][0] for g_ in opt.param_groups]
 
