@@ -643,6 +643,11 @@ def main():
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(cfg)
+        # the like-for-like GPU figure: the oracle times a forward + FULL backward (every gradient),
+        # which is the step of ms_per_step_all_gradients, not the language step of `value`
+        cpu["pairs_with"] = {"gpu_form": "ms_per_step_all_gradients",
+                             "gpu_value": round(blends_all * args.steps / elapsed_all, 1),
+                             "gpu_over_cpu": round(blends_all * args.steps / elapsed_all / cpu["value"], 1)}
     out = {
         "metric": METRIC,
         "value": round(value, 1),
