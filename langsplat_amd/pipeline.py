@@ -85,6 +85,11 @@ class ViewPipeline:
         ev.record()
         self.ready = ev
 
+    def follow_caller(self):
+        """The next replays wait for everything the caller's stream holds now (e.g. parameters the
+        caller changed between replays)."""
+        self._since_capture = 0
+
     def synchronize(self):
         """The caller's current stream waits for every step enqueued so far."""
         cur = torch.cuda.current_stream()
@@ -139,7 +144,9 @@ class PipelinedGraphStep:
         g.check(); g.sync()
 
     forward_fn() runs render() + the loss and returns the loss (no backward).  The graphs own the
-    parameters' .grad tensors.
+    parameters' .grad tensors.  Work the caller enqueues on its stream between replays (a .clone()
+    of the returned loss) precedes the device work of the replay S - 1 later, not of the next one;
+    after changing the parameters or the optimizer state between replays, call follow_caller().
 
     Knobs (measured at C3): LSR_PG_SETS (2 or 3), LSR_PG_GEO=fwd (the geometry starts
     only after this view's compositing), LSR_PG_PRIO=geo|step (stream priorities)."""
@@ -287,6 +294,8 @@ class PipelinedGraphStep:
         self.ev_geo = [torch.cuda.Event() for _ in range(S)]
         self.ev_comp = [torch.cuda.Event() for _ in range(S)]
         self.ev_step = [torch.cuda.Event() for _ in range(S)]
+        self.ev_cur = [torch.cuda.Event() for _ in range(S)]
+        self._since_capture = 0
         self.captures += 1
         return self
 
@@ -329,11 +338,21 @@ class PipelinedGraphStep:
             # set r's last reader was step k - 1, which the caller's stream waited for (below)
             self.slots[r].load(*_as_view(next_view))
             self._loaded[r] = next_view
-        self.optimizer.sync_lr()
-        # the caller's earlier work (e.g. a learning-rate change) precedes the step
-        sa.wait_stream(cur)
+        # Stream A does not wait for the caller's stream as it is now: that stream waits for the
+        # previous step (below), so the wait would be a round trip between two queues (measured ~35 us
+        # of idle stream A per step at C3).  It waits instead for the caller's work up
+        # to the start of replay k - S + 1, long done: the caller's uses of the loss of replay k - S
+        # (whose tensor composite k rewrites) precede that.  The first S - 1 replays after a capture
+        # wait for the caller's stream itself.
+        self.ev_cur[self.k % S].record(cur)
+        if self._since_capture < S - 1:
+            sa.wait_stream(cur)
+        else:
+            sa.wait_event(self.ev_cur[(self.k + 1) % S])  # recorded at replay k - S + 1
+        self._since_capture += 1
         sa.wait_event(self.ev_geo[p])
         with torch.cuda.stream(sa):
+            self.optimizer.sync_lr()  # a changed learning rate: a host-to-device copy on stream A
             first = self.k == 0 and self.g_comp0 is not None
             (self.g_comp0 if first else self.g_comp[p]).replay()
             self.ev_comp[p].record(sa)
@@ -349,6 +368,11 @@ class PipelinedGraphStep:
         cur.wait_event(self.ev_step[p])
         self.k += 1
         return self.static_loss[p]
+
+    def follow_caller(self):
+        """The next replays wait for everything the caller's stream holds now (e.g. parameters the
+        caller changed between replays)."""
+        self._since_capture = 0
 
     def synchronize(self):
         """The caller's current stream waits for every replay enqueued so far (both streams)."""
