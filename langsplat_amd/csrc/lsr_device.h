@@ -115,6 +115,44 @@ __device__ __forceinline__ lsr_f2 expf_exact_render2(lsr_f2 x)
     return p * sc;
 }
 
+// expf_exact_render2's constants held in scalar registers across a loop: defined by asm, so the
+// compiler cannot re-materialise them (it re-created each one with an s_mov, or a v_mov for the two it
+// put in vector registers, at every use: 8 issue slots per pair of entries in the forward walk)
+struct ExpK {
+    float log2e, shift, nln2, c6, c5, c4, c3, c2;
+};
+__device__ __forceinline__ ExpK exp_consts()
+{
+    ExpK k;
+    asm("s_mov_b32 %0, 0x3fb8aa3b" : "=s"(k.log2e));  // 1.44269504088896341f
+    asm("s_mov_b32 %0, 0x4b400000" : "=s"(k.shift));  // kExpShift
+    asm("s_mov_b32 %0, 0xbf317218" : "=s"(k.nln2));   // -0.693147182464599609375f
+    asm("s_mov_b32 %0, 0x3ab511e6" : "=s"(k.c6));     // 1.38145383e-3f
+    asm("s_mov_b32 %0, 0x3c091d10" : "=s"(k.c5));     // 8.36874545e-3f
+    asm("s_mov_b32 %0, 0x3d2aac79" : "=s"(k.c4));     // 4.16683890e-2f
+    asm("s_mov_b32 %0, 0x3e2aaa49" : "=s"(k.c3));     // 1.66665211e-1f
+    asm("s_mov_b32 %0, 0x3efffffe" : "=s"(k.c2));     // 4.99999940e-1f
+    return k;
+}
+// expf_exact_render2 with the constants of exp_consts() (the same operations)
+__device__ __forceinline__ lsr_f2 expf_exact_render2(lsr_f2 x, const ExpK& k)
+{
+    const lsr_f2 t = __builtin_elementwise_fma(x, (lsr_f2)(k.log2e), (lsr_f2)(k.shift));
+    const lsr_f2 n = t - k.shift;
+    const lsr_f2 r = __builtin_elementwise_fma(n, (lsr_f2)(k.nln2), x);
+    lsr_f2 p = (lsr_f2)(k.c6);
+    p = __builtin_elementwise_fma(p, r, (lsr_f2)(k.c5));
+    p = __builtin_elementwise_fma(p, r, (lsr_f2)(k.c4));
+    p = __builtin_elementwise_fma(p, r, (lsr_f2)(k.c3));
+    p = __builtin_elementwise_fma(p, r, (lsr_f2)(k.c2));
+    p = __builtin_elementwise_fma(p, r, (lsr_f2)(1.0f));
+    p = __builtin_elementwise_fma(p, r, (lsr_f2)(1.0f));
+    lsr_f2 sc;
+    sc.x = exp_scale(t.x);
+    sc.y = exp_scale(t.y);
+    return p * sc;
+}
+
 __device__ __forceinline__ float fma_(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
 
 // ---- parameter activations of the fused path (lsr_raw_flags; oracle lso_act_* restate them) ----

@@ -227,29 +227,33 @@ struct FwdPixel {
 };
 
 // One front-to-back blend of the entry at LDS byte offset o (slot o / 16) with alpha al (upstream
-// FORWARD::renderCUDA; the operation order of oracle render_pixel): stop before the entry once T
-// would fall below 1e-4 (then T -> -T: done).  lb16 = 16 (list index of slot 0 + 1).
-// Cc / Ff: the entry's colour record {r, g, b, f0} and {f1, f2}, read by the caller (both entries of a
-// pair at once, so their LDS latency is paid once per pair)
+// FORWARD::renderCUDA; the operation order of oracle render_pixel): ok = the entry passes the
+// pixel's alpha tests; stop before the entry once T would fall below 1e-4 (then T -> -T: done).
+// lo = the offset of the batch's last blended entry (the walk adds the batch's base once).  Cc / Ff: the entry's colour record {r, g, b, f0} and
+// {f1, f2}, read by the caller (both entries of a pair at once, so their LDS latency is paid once
+// per pair).
+// Without branches: an entry that fails its tests blends with alpha 0 (T * (1 - 0) = T and the sums
+// gain +-0 exactly: the records are finite), a lane that is done keeps T (< 0, so the stop test
+// holds and -|T| = T), so every lane runs the same instructions: the same values as the branchy form,
+// without its exec-mask branches (~24 scalar instructions per pair of the walk's ~110 issue slots).
 template <bool kFeat>
-__device__ __forceinline__ void fwd_pixel_blend(FwdPixel& q, float al, uint32_t o, uint32_t lb16, const float4& Cc,
-                                                const lsr_f2& Ff)
+__device__ __forceinline__ void fwd_pixel_blend(FwdPixel& q, float al, bool ok, uint32_t o, uint32_t& lo,
+                                                const float4& Cc, const lsr_f2& Ff)
 {
-    const float test_T = q.T * (1.0f - al);
+    const float a = ok ? al : 0.0f;
+    const float test_T = q.T * (1.0f - a);
     const bool go = !(test_T < 0.0001f);
-    if (go) {
-        const float w = al * q.T;
-        const lsr_f2 w2 = make_f2(w, w);
-        q.C01 = __builtin_elementwise_fma(make_f2(Cc.x, Cc.y), w2, q.C01);
-        if (kFeat) {
-            q.C2F0 = __builtin_elementwise_fma(make_f2(Cc.z, Cc.w), w2, q.C2F0);
-            q.F12 = __builtin_elementwise_fma(Ff, w2, q.F12);
-        } else {
-            q.C2F0.x = fma_(Cc.z, w, q.C2F0.x);
-        }
-        q.last16 = lb16 + o;
+    const float w = go ? a * q.T : 0.0f;
+    const lsr_f2 w2 = make_f2(w, w);
+    q.C01 = __builtin_elementwise_fma(make_f2(Cc.x, Cc.y), w2, q.C01);
+    if (kFeat) {
+        q.C2F0 = __builtin_elementwise_fma(make_f2(Cc.z, Cc.w), w2, q.C2F0);
+        q.F12 = __builtin_elementwise_fma(Ff, w2, q.F12);
+    } else {
+        q.C2F0.x = fma_(Cc.z, w, q.C2F0.x);
     }
-    q.T = go ? test_T : -q.T;
+    lo = go && ok ? o : lo;
+    q.T = go ? test_T : -fabsf(q.T);
 }
 
 // ---- fused language-feature loss (train.py:96-99: Ll1 = l1_loss(lang * mask, gt * mask)) ----
@@ -466,8 +470,17 @@ __device__ float render_empty_tiles(const RenderParams& p, int j, int M)
 // 7 waves per SIMD (<= 72 VGPRs): the fused-loss variant's rare bounded-wait fallback
 // (loss_block_publish) would otherwise raise its register count to 83 (6 waves); with the bound the
 // compiler spills three values, stored once per workgroup and reloaded on that path only.
+#ifndef LSR_FWD_WAVES  // waves per SIMD the forward is compiled for (measurement knob)
+#define LSR_FWD_WAVES 7
+#endif
+#ifndef LSR_FWD_QUAD  // 1: four list entries per walk step (two packed exp chains), 0: two
+#define LSR_FWD_QUAD 0
+#endif
+#ifndef LSR_FWD_PREFETCH  // 1: the next batch's records are gathered during the walk
+#define LSR_FWD_PREFETCH 0
+#endif
 template <bool kStats, bool kFeat, bool kLoss>
-__global__ __launch_bounds__(kTilePixels, 7) void k_render_forward(RenderParams p)
+__global__ __launch_bounds__(kTilePixels, LSR_FWD_WAVES) void k_render_forward(RenderParams p)
 {
     const uint64_t t_start = kStats ? wall_clock64() : 0;
     constexpr int kThreads = kTilePixels;
@@ -476,11 +489,11 @@ __global__ __launch_bounds__(kTilePixels, 7) void k_render_forward(RenderParams 
     __shared__ float4 sC[kThreads];  // r, g, b, f0
     __shared__ float4 sF[kThreads];  // f1, f2, -, -  (16-B slots: every record of slot s at byte 16 s)
     __shared__ uint8_t sM[kThreads];  // entry_cover mask
-    // per-wave culled slot lists, as byte offsets 16 s; slot n holds offset 0, so the walk reads the
-    // second entry of a pair without testing i + 1 < n (its result is discarded then).  Rows of
-    // kThreads + 2 (4-B aligned): a pair's two offsets are one 32-bit read, and the walk reads the
-    // next pair's (up to slot n + 1) one pair ahead
-    __shared__ uint16_t sL[kThreads / 64][kThreads + 2];
+    // per-wave culled slot lists, as byte offsets 16 s; slots n .. n + 3 hold offset 0, so the walk
+    // reads the entries of a step past the list's end without testing (their results are discarded).
+    // Rows of kThreads + 8 (8-B aligned): a step's offsets are one 32- or 64-bit read, and the walk
+    // reads the next step's one step ahead (up to slot n + 7)
+    __shared__ __attribute__((aligned(8))) uint16_t sL[kThreads / 64][kThreads + 8];
     __shared__ uint32_t s_last;
 
     const int T = p.gx * p.gy;
@@ -518,9 +531,22 @@ __global__ __launch_bounds__(kTilePixels, 7) void k_render_forward(RenderParams 
     FwdPixel q{inside ? 1.0f : -1.0f, make_f2(0.f, 0.f), make_f2(0.f, 0.f), make_f2(0.f, 0.f), 0u, 0u};
     PhaseTicks ph;
     if (kStats) ph.begin();
-    // the point_list id of this thread's entry in the next batch is loaded before the current batch's
-    // walk, so a batch's load phase waits for one memory round trip (the record gather), not two
+    // Software pipeline over the batches: a batch's records are gathered during the previous batch's
+    // walk (into registers the walk leaves free), and the point_list ids one batch earlier still, so
+    // a batch's load phase waits for no memory round trip (the timeline showed ~9 us of load phase per
+    // batch on the heaviest tiles, a quarter of their time, mostly the gather's latency)
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a, c = a;
+#if LSR_FWD_PREFETCH
+    if (start + t < end) {
+        const uint32_t g = p.point_list[start + t];
+        a = p.record[3 * (size_t)g];
+        b = p.record[3 * (size_t)g + 1];
+        c = p.record[3 * (size_t)g + 2];
+    }
+    uint32_t g_next = start + kThreads + t < end ? p.point_list[start + kThreads + t] : 0u;
+#else
     uint32_t g_next = start + t < end ? p.point_list[start + t] : 0u;
+#endif
     for (uint32_t base = start; base < end; base += kThreads) {
         const bool all_done = __syncthreads_count(q.T < 0.0f) == kThreads;
         if (kStats && base != start) ph.lap(ph.walk);
@@ -530,18 +556,19 @@ __global__ __launch_bounds__(kTilePixels, 7) void k_render_forward(RenderParams 
         }
         if (kStats) ph.batches++;
         const uint32_t idx = base + t;
-        float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a, c = a;
-        if (idx < end) {  // the batch's record gathers first ...
+#if !LSR_FWD_PREFETCH
+        a = b = c = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (idx < end) {
             const uint32_t g = g_next;
             a = p.record[3 * (size_t)g];
             b = p.record[3 * (size_t)g + 1];
             c = p.record[3 * (size_t)g + 2];
         }
+#endif
         if (p.split_pool && base != start && base - start <= (uint32_t)(kSplitMax * kThreads)) {
-            // ... then (younger, so the gathers' wait does not include them) split replay: every
-            // pixel's state before list entry 256 j while some pixel composites, two float4 per pixel
-            // in the tile's own slot j - 1 (a grid-wide slot counter cost ~40 us of contended
-            // cross-XCD atomics); a pixel already done is never started from here
+            // split replay: every pixel's state before list entry 256 j while some pixel composites,
+            // two float4 per pixel in the tile's own slot j - 1 (a grid-wide slot counter cost ~40 us
+            // of contended cross-XCD atomics); a pixel already done is never started from here
             // {T, feature sums}, then {colour sums} unless no colour gradient can follow (the language
             // step: half the state traffic)
             float4* st = reinterpret_cast<float4*>(p.split_pool) + ((size_t)tile * kSplitSlots + nrec) * (2 * kThreads);
@@ -564,51 +591,94 @@ __global__ __launch_bounds__(kTilePixels, 7) void k_render_forward(RenderParams 
         const int cnt = (int)min((uint32_t)kThreads, end - base);
         const int n = __builtin_amdgcn_readfirstlane(
             wave_compact(sM, cnt, 1u << wave, lane, sL[wave]));
-        if (lane == 0) sL[wave][n] = 0;
+        if (lane < 4) sL[wave][n + lane] = 0;
         __syncthreads();  // list visible to the wave's other lanes
         if (kStats) ph.lap(ph.compact);
+#if LSR_FWD_PREFETCH
+        if (idx + kThreads < end) {  // the next batch's records, and the ids of the one after
+            const uint32_t g = g_next;
+            a = p.record[3 * (size_t)g];
+            b = p.record[3 * (size_t)g + 1];
+            c = p.record[3 * (size_t)g + 2];
+        }
+        if (idx + 2 * kThreads < end) g_next = p.point_list[idx + 2 * kThreads];
+#else
         if (idx + kThreads < end) g_next = p.point_list[idx + kThreads];
+#endif
         const uint32_t lb16 = 16u * (base - start + 1u);  // 16 x (list index of slot 0 + 1)
         const char* const cA = reinterpret_cast<const char*>(sA);
         const char* const cB = reinterpret_cast<const char*>(sB);
         const char* const cC = reinterpret_cast<const char*>(sC);
         const char* const cF = reinterpret_cast<const char*>(sF);
-        // two list entries per iteration: their power / exp / alpha do not depend on the pixel state,
-        // so the two chains interleave; only the transmittance test and the blend are sequential.
-        // Same operations per entry as one at a time (bit-identical results).  The list holds byte
-        // offsets, so every record read addresses LDS with the list value itself.
-        // the pair's two offsets come from one 32-bit read issued during the previous pair, so a
-        // pair's record reads do not wait behind a dependent read of their offsets
-        const uint32_t* const sL2 = reinterpret_cast<const uint32_t*>(sL[wave]);
-        uint32_t oo = sL2[0];
-        for (int i = 0; i < n; i += 2) {
-            if (__ballot(q.T > 0.0f) == 0ull) break;
-            const uint32_t o0 = oo & 0xFFFFu;
-            const bool has1 = i + 1 < n;
-            const uint32_t o1 = oo >> 16;
-            oo = sL2[(i >> 1) + 1];  // slots i + 2, i + 3 (<= n + 1)
-            const float4 A0 = *reinterpret_cast<const float4*>(cA + o0), B0 = *reinterpret_cast<const float4*>(cB + o0);
-            const float4 A1 = *reinterpret_cast<const float4*>(cA + o1), B1 = *reinterpret_cast<const float4*>(cB + o1);
+        // Per list entry: power, exp and alpha do not depend on the pixel state, only the transmittance
+        // test and the blend are sequential.  Two entries' exps run as one packed chain
+        // (expf_exact_render2: the same IEEE operations per element).  The list holds byte offsets,
+        // so every record read addresses LDS with the list value itself.  A step's offsets come from
+        // one read issued during the previous step, so its record reads do not wait behind them.
+        uint32_t lo = 0xFFFFFFFFu;  // offset of the batch's last blended entry, per lane
+        // the alpha of the entries at offsets oa, ob (ob: only if hb) and their alpha tests
+        auto pair_alpha = [&](uint32_t oa, uint32_t ob, bool hb, float& ala, float& alb, bool& oka, bool& okb) {
+            const float4 Aa = *reinterpret_cast<const float4*>(cA + oa), Ba = *reinterpret_cast<const float4*>(cB + oa);
+            const float4 Ab = *reinterpret_cast<const float4*>(cA + ob), Bb = *reinterpret_cast<const float4*>(cB + ob);
             // per entry {dx, dy} and {A.z dx, A.w dy} as packed ops on the record's own register pairs
-            const lsr_f2 d0 = make_f2(A0.x, A0.y) - pxy, d1 = make_f2(A1.x, A1.y) - pxy;
-            const lsr_f2 m0 = make_f2(A0.z, A0.w) * d0, m1 = make_f2(A1.z, A1.w) * d1;
+            const lsr_f2 da = make_f2(Aa.x, Aa.y) - pxy, db = make_f2(Ab.x, Ab.y) - pxy;
+            const lsr_f2 ma = make_f2(Aa.z, Aa.w) * da, mb = make_f2(Ab.z, Ab.w) * db;
             // power = dx (A.z dx - conic.y dy) + (A.w dy) dy: 4 operations after {A.z dx, A.w dy}
             // (the oracle's render_pixel / backward_pixel and the backward walk use the same order)
-            const float pw0 = fma_(d0.x, fma_(-B0.x, d0.y, m0.x), m0.y * d0.y);
-            const float pw1 = fma_(d1.x, fma_(-B1.x, d1.y, m1.x), m1.y * d1.y);
-            const lsr_f2 G2 = expf_exact_render2(make_f2(pw0, pw1));
-            const float al0 = fminf(0.99f, B0.y * G2.x);
-            const float al1 = fminf(0.99f, B1.y * G2.y);
-            const bool ok0 = !(pw0 > 0.0f || pw0 < B0.z) && !(al0 < 1.0f / 255.0f);
-            const bool ok1 = has1 && !(pw1 > 0.0f || pw1 < B1.z) && !(al1 < 1.0f / 255.0f);
-            // both entries' colour records in one LDS round trip (the records' arrays are padded:
-            // every slot, and slot n's offset 0, is readable)
-            const float4 Cc0 = *reinterpret_cast<const float4*>(cC + o0), Cc1 = *reinterpret_cast<const float4*>(cC + o1);
-            const lsr_f2 Ff0 = kFeat ? *reinterpret_cast<const lsr_f2*>(cF + o0) : make_f2(0.f, 0.f);
-            const lsr_f2 Ff1 = kFeat ? *reinterpret_cast<const lsr_f2*>(cF + o1) : make_f2(0.f, 0.f);
-            if (ok0 && q.T > 0.0f) fwd_pixel_blend<kFeat>(q, al0, o0, lb16, Cc0, Ff0);
-            if (ok1 && q.T > 0.0f) fwd_pixel_blend<kFeat>(q, al1, o1, lb16, Cc1, Ff1);
-        }
+            const float pwa = fma_(da.x, fma_(-Ba.x, da.y, ma.x), ma.y * da.y);
+            const float pwb = fma_(db.x, fma_(-Bb.x, db.y, mb.x), mb.y * db.y);
+            const lsr_f2 G2 = expf_exact_render2(make_f2(pwa, pwb));
+            ala = fminf(0.99f, Ba.y * G2.x);
+            alb = fminf(0.99f, Bb.y * G2.y);
+            oka = !(pwa > 0.0f || pwa < Ba.z) && !(ala < 1.0f / 255.0f);
+            okb = hb && !(pwb > 0.0f || pwb < Bb.z) && !(alb < 1.0f / 255.0f);
+        };
+        auto blend_at = [&](float al, bool ok, uint32_t o) {
+            const float4 Cc = *reinterpret_cast<const float4*>(cC + o);
+            const lsr_f2 Ff = kFeat ? *reinterpret_cast<const lsr_f2*>(cF + o) : make_f2(0.f, 0.f);
+            fwd_pixel_blend<kFeat>(q, al, ok, o, lo, Cc, Ff);
+        };
+        // one basic block per step (the blends have no branches, the wave's "all done" test closes the
+        // iteration), so the next step's offset read stays beside this step's record reads
+        int i = 0;
+#if LSR_FWD_QUAD
+        // four entries per step: two independent packed exp chains, so a wave has twice the
+        // instruction-level parallelism between its dependent operations
+        const uint2* const sL4 = reinterpret_cast<const uint2*>(sL[wave]);
+        uint2 oo = sL4[0];
+        if (n > 0 && __ballot(q.T > 0.0f) != 0ull) do {
+            const uint32_t o0 = oo.x & 0xFFFFu, o1 = oo.x >> 16, o2 = oo.y & 0xFFFFu, o3 = oo.y >> 16;
+            oo = sL4[(i >> 2) + 1];  // slots i + 4 .. i + 7 (<= n + 7)
+            float al0, al1, al2, al3;
+            bool ok0, ok1, ok2, ok3;
+            pair_alpha(o0, o1, i + 1 < n, al0, al1, ok0, ok1);
+            pair_alpha(o2, o3, i + 3 < n, al2, al3, ok2, ok3);
+            ok2 = ok2 && i + 2 < n;
+            blend_at(al0, ok0, o0);
+            blend_at(al1, ok1, o1);
+            blend_at(al2, ok2, o2);
+            blend_at(al3, ok3, o3);
+            // the next offsets are this iteration's value: the compiler may not defer their read to
+            // the next iteration's start (where the record reads would wait behind it)
+            asm volatile("" : "+v"(oo.x), "+v"(oo.y));
+            i += 4;
+        } while (i < n && __ballot(q.T > 0.0f) != 0ull);
+#else
+        const uint32_t* const sL2 = reinterpret_cast<const uint32_t*>(sL[wave]);
+        uint32_t oo = sL2[0];
+        if (n > 0 && __ballot(q.T > 0.0f) != 0ull) do {
+            const uint32_t o0 = oo & 0xFFFFu, o1 = oo >> 16;
+            oo = sL2[(i >> 1) + 1];  // slots i + 2, i + 3 (<= n + 1)
+            float al0, al1;
+            bool ok0, ok1;
+            pair_alpha(o0, o1, i + 1 < n, al0, al1, ok0, ok1);
+            blend_at(al0, ok0, o0);
+            blend_at(al1, ok1, o1);
+            asm volatile("" : "+v"(oo));
+            i += 2;
+        } while (i < n && __ballot(q.T > 0.0f) != 0ull);
+#endif
+        if (lo != 0xFFFFFFFFu) q.last16 = lb16 + lo;
     }
     const uint32_t qlast = q.last16 >> 4;
     // the tile's replay length, for the backward's launch order
@@ -652,17 +722,21 @@ __global__ __launch_bounds__(kTilePixels, 7) void k_render_forward(RenderParams 
     }
     const size_t HW = (size_t)p.W * p.H;
     const size_t pix = (size_t)py * p.W + px;
-    if (kLoss) loss_block_publish(p, inside ? loss_pixel(p, pix, HW, q.C2F0.y, q.F12.x, q.F12.y) : 0.0f);
-    if (!inside) return;
-    const float Tf = fabsf(q.T);
-    p.final_T[pix] = Tf;
-    p.n_contrib[pix] = qlast;
-    p.out_color[pix] = fma_(Tf, p.bg[0], q.C01.x);
-    p.out_color[HW + pix] = fma_(Tf, p.bg[1], q.C01.y);
-    p.out_color[2 * HW + pix] = fma_(Tf, p.bg[2], q.C2F0.x);
-    p.out_lang[pix] = q.C2F0.y;
-    p.out_lang[HW + pix] = q.F12.x;
-    p.out_lang[2 * HW + pix] = q.F12.y;
+    const float part = kLoss && inside ? loss_pixel(p, pix, HW, q.C2F0.y, q.F12.x, q.F12.y) : 0.0f;
+    // the outputs before the loss share's publication: the pixel state is dead during it (the last
+    // workgroup's word gather holds 32 registers)
+    if (inside) {
+        const float Tf = fabsf(q.T);
+        p.final_T[pix] = Tf;
+        p.n_contrib[pix] = qlast;
+        p.out_color[pix] = fma_(Tf, p.bg[0], q.C01.x);
+        p.out_color[HW + pix] = fma_(Tf, p.bg[1], q.C01.y);
+        p.out_color[2 * HW + pix] = fma_(Tf, p.bg[2], q.C2F0.x);
+        p.out_lang[pix] = q.C2F0.y;
+        p.out_lang[HW + pix] = q.F12.x;
+        p.out_lang[2 * HW + pix] = q.F12.y;
+    }
+    if (kLoss) loss_block_publish(p, part);
 }
 
 // P == 0: the language image is 0 everywhere; its loss terms, one workgroup per 256 pixels.
