@@ -85,6 +85,15 @@ class ViewPipeline:
         ev.record()
         self.ready = ev
 
+    def last_grads(self):
+        """The gradient tensors the last replay wrote (graph-owned; the first replay after a fused
+        capture has its own)."""
+        if self.k == 0:
+            raise RuntimeError("PipelinedGraphStep.last_grads: no replay yet")
+        if self.k == 1 and self.merged and self.g_comp0 is not None:
+            return self.grads0
+        return self.grads[(self.k - 1) % self.S]
+
     def follow_caller(self):
         """The next replays wait for everything the caller's stream holds now (e.g. parameters the
         caller changed between replays)."""
@@ -108,15 +117,18 @@ class PipelinedGraphStep:
     set p (_native.static_buffers: the same addresses at every forward; S sets, default 3) the graphs
 
         G_geo[p]:  the geometry half of the view, into set p                  (stream B)
-        G_comp[p]: the composite half of set p and the loss                     (stream A)
-        G_step[p]: loss.backward() + optimizer.step(skip=overflow[p])           (stream A)
-                   (N > 1: G_bwd[p], the bucket's all-reduce launched between, G_adam[p])
+        G_comp[p]: the composite half of set p and the loss, then loss.backward() and
+                   optimizer.step(skip=overflow[p])                             (stream A)
+                   (N > 1: the backward only; the bucket's all-reduce launched after it, G_adam[p])
 
     are captured, and replay k runs (p = k % S; set r = (k + S - 1) % S receives view k + S - 1,
     S - 1 views ahead; its last reader was step k - 1):
 
-        stream A:  wait geo[p] -> G_comp[p] -> record comp[p] -> G_step[p] -> record step[p]
-        stream B:  [wait comp[p]] -> G_geo[r] -> record geo[r]
+        stream A:  wait geo[p] -> G_comp[p] -> record step[p]
+        stream B:  G_geo[r] -> record geo[r]
+
+    (LSR_PG_MERGE=0 or LSR_PG_GEO=fwd: the composite and the step as two graphs, with the event
+    comp[p] between them; the geometry then may wait for it.)
 
     so a replay is one full language step (the loss it returns is that of the view it composited and
     updated from) and later views' geometry overlaps it.  Two graphs on two streams are separate
@@ -254,7 +266,27 @@ class PipelinedGraphStep:
         fused = skip is not None and len(self.params) == 1 and _fused_tail_enabled()
         self.fused = fused
         comp_phase = _native.forward_phase.COMPOSITE_FILLED if fused else _native.forward_phase.COMPOSITE
+        # fused: the first composite after a capture fills set 0's feature records itself (G_comp0, run
+        # by replay k = 0 instead of G_comp[0]; it owns its own gradients, grads0); later sets are
+        # filled by the step before
         self.g_comp0 = None
+        self.grads0 = None
+        # the composite and the step in ONE graph per set (default): a graph boundary on stream A
+        # costs ~16-24 us of idle queue at C3 (rocprofv3 trace, round 4), and nothing needs the point
+        # between them unless the geometry waits for the compositing (LSR_PG_GEO=fwd)
+        merged = not self.geo_after_fwd and os.environ.get("LSR_PG_MERGE", "1") != "0"
+        self.merged = merged
+
+        def update_ctx(p):
+            return _native.fused_update(self.optimizer, self.params[0], skip=self.overflow[p],
+                                        fill=self._record_ptr((p + 1) % S)) if fused else _nullctx()
+
+        def step_body(p, loss):
+            with update_ctx(p):  # the backward runs on its forward's stream (sa)
+                loss.backward(self._one)  # dL/dloss = 1 from a static tensor: no seed-fill kernel
+                if skip is not None:
+                    self.optimizer.step(skip=skip[p])
+
         for p in range(S):
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, stream=sb), caps[p], self.sets[p], \
@@ -263,24 +295,33 @@ class PipelinedGraphStep:
             self.g_geo[p] = g
             for q in self.params:
                 q.grad = None  # the captured backward assigns its own .grad (no accumulate)
-            if fused and p == 0:  # the first composite after a capture fills its own records
+            if fused and p == 0:
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, stream=sa), caps[p], self.sets[p], \
-                        _native.forward_phase(_native.forward_phase.COMPOSITE):
-                    self._fwd(p)
+                with torch.cuda.graph(g, stream=sa):
+                    with caps[p], self.sets[p], _native.forward_phase(_native.forward_phase.COMPOSITE):
+                        loss = self._fwd(p)
+                    if merged:
+                        step_body(p, loss)
+                if merged:
+                    self.grads0 = [q.grad for q in self.params]
+                    del loss
+                    for q in self.params:
+                        q.grad = None
+                else:
+                    del loss
                 self.g_comp0 = g
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, stream=sa), caps[p], self.sets[p], _native.forward_phase(comp_phase):
-                loss = self._fwd(p)
+            with torch.cuda.graph(g, stream=sa):
+                with caps[p], self.sets[p], _native.forward_phase(comp_phase):
+                    loss = self._fwd(p)
+                if merged:
+                    step_body(p, loss)
             self.g_comp[p] = g
-            g = torch.cuda.CUDAGraph()
-            fu = _native.fused_update(self.optimizer, self.params[0], skip=self.overflow[p],
-                                      fill=self._record_ptr((p + 1) % S)) if fused else _nullctx()
-            with torch.cuda.graph(g, stream=sa), fu:  # the backward runs on its forward's stream (sa)
-                loss.backward(self._one)  # dL/dloss = 1 from a static tensor: no seed-fill kernel
-                if skip is not None:
-                    self.optimizer.step(skip=skip[p])
-            self.g_step[p] = g
+            if not merged:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=sa):
+                    step_body(p, loss)
+                self.g_step[p] = g
             self.grads[p] = [q.grad for q in self.params]  # this set's graph-owned gradients
             if skip is None:  # the all-reduce sits between the backward and Adam graphs
                 g = torch.cuda.CUDAGraph()
@@ -321,7 +362,7 @@ class PipelinedGraphStep:
         """One language step of the view loaded S - 1 replays ago (or at capture); next_view
         (camera, gt, mask) is the view of the replay S - 1 ahead (ViewSlots only; None: the view of
         its set stays)."""
-        if self.g_step[0] is None:
+        if self.g_comp[0] is None:
             self.capture()
         S = self.S
         sa, sb = self.streams
@@ -355,8 +396,9 @@ class PipelinedGraphStep:
             self.optimizer.sync_lr()  # a changed learning rate: a host-to-device copy on stream A
             first = self.k == 0 and self.g_comp0 is not None
             (self.g_comp0 if first else self.g_comp[p]).replay()
-            self.ev_comp[p].record(sa)
-            self.g_step[p].replay()
+            if not self.merged:
+                self.ev_comp[p].record(sa)
+                self.g_step[p].replay()
             if self.g_adam[p] is not None:
                 for q, g in zip(self.params, self.grads[p]):
                     q.grad = g
@@ -364,10 +406,19 @@ class PipelinedGraphStep:
                 self.g_adam[p].replay()
         self.ev_step[p].record(sa)
         # view k + S - 1's geometry into set r
-        self._geometry(r, after=self.ev_comp[p] if self.geo_after_fwd else None)
+        self._geometry(r, after=self.ev_comp[p] if self.geo_after_fwd and not self.merged else None)
         cur.wait_event(self.ev_step[p])
         self.k += 1
         return self.static_loss[p]
+
+    def last_grads(self):
+        """The gradient tensors the last replay wrote (graph-owned; the first replay after a fused
+        capture has its own)."""
+        if self.k == 0:
+            raise RuntimeError("PipelinedGraphStep.last_grads: no replay yet")
+        if self.k == 1 and self.merged and self.g_comp0 is not None:
+            return self.grads0
+        return self.grads[(self.k - 1) % self.S]
 
     def follow_caller(self):
         """The next replays wait for everything the caller's stream holds now (e.g. parameters the

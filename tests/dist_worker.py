@@ -71,7 +71,7 @@ def main():
     torch.cuda.synchronize()
     assert pg.check()
     pg.sync()
-    out["pipelined_graph"] = dict(grad=pg.grads[0][0].detach().cpu(), loss=loss.cpu(),
+    out["pipelined_graph"] = dict(grad=pg.last_grads()[0].detach().cpu(), loss=loss.cpu(),
                                   param=m._language_feature.detach().cpu(),
                                   step=int(opt.state[m._language_feature]["step"].item()))
     torch.save(out, os.path.join(out_dir, f"rank{rank}.pt"))

@@ -164,7 +164,7 @@ def test_pipelined_graph_full_c3_matches_oracle_and_eager(monkeypatch):
     np.testing.assert_array_equal(out[("out", "language")].detach().cpu().numpy(), run.language)
     np.testing.assert_array_equal(out[("out", "radii")].detach().cpu().numpy(), run.radii)
     assert abs(float(first.item()) - loss_ref) <= 2e-6 * loss_ref
-    assert_grad_close("language_feature (raw), first replay", pg.grads[0][0].detach().cpu().numpy(), d_lang_ref)
+    assert_grad_close("language_feature (raw), first replay", pg.last_grads()[0].detach().cpu().numpy(), d_lang_ref)
     losses = [first] + [pg.replay().clone() for _ in range(K)]
     pg.synchronize()
     torch.cuda.synchronize()
@@ -391,7 +391,7 @@ def test_overflowed_view_is_a_noop_for_the_optimizer(form, monkeypatch):
             torch.cuda.synchronize()
             if k == bad:
                 assert int(pg.overflow[k % S].item()) == 1
-                assert not pg.grads[k % S][0].any()
+                assert not pg.last_grads()[0].any()
         snaps.append(_snap(m, opt))
         assert opt.skipped_steps() == 1
         assert not pg.check() and pg.captures == 2
@@ -529,7 +529,7 @@ def test_fused_tail_matches_separate_launches(form, monkeypatch):
             for k in range(len(views)):
                 nxt = views[k + S - 1] if k + S - 1 < len(views) else None
                 losses.append(pg.replay(next_view=nxt).clone())
-                grads.append(pg.grads[k % S][0].detach().clone())  # read before set k % S is reused
+                grads.append(pg.last_grads()[0].detach().clone())  # read before set k % S is reused
             pg.synchronize()
             assert pg.check()
             pg.sync()

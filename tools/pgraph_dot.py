@@ -42,7 +42,8 @@ def main():
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     for k in (0, 1):
         for name, g in (("geo", pg.g_geo[k]), ("comp", pg.g_comp[k]), ("step", pg.g_step[k])):
-            g.debug_dump(os.path.join(ROOT, "gpurun_out", f"pgraph_{name}_{k}.dot"))
+            if g is not None:  # no separate step graph when the composite and step are merged
+                g.debug_dump(os.path.join(ROOT, "gpurun_out", f"pgraph_{name}_{k}.dot"))
 
 
 if __name__ == "__main__":
