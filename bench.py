@@ -11,7 +11,8 @@ Adam step, zero_grad.  The timed backward computes the gradients autograd asks f
 language step every geometry parameter is frozen (scene/gaussian_model.py:203-217), so the
 rasterizer backward replays every blend but produces only dL/dmeans2D and dL/dlanguage_feature.
 The same step with every geometry gradient computed as well (what the reference extension does)
-is timed separately and reported beside it as `ms_per_step_all_gradients`, never as `value`.
+is timed separately and reported beside it as `ms_per_step_all_gradients`, never as `value`; so is
+the inference forward (render.py's render() under torch.no_grad(), `ms_forward_only`).
 
 N = 1 runs BASELINE configs[2] (C3: 1M Gaussians, one 1920x1080 camera); N > 1 runs configs[3]
 (C4: the same scene, camera `rank % 8` of 8 on a circle, one per GPU: weak scaling).  Data is
@@ -426,6 +427,19 @@ def main():
     torch.cuda.synchronize()
     elapsed_all = time.perf_counter() - t1
     _native.FORCE_GEOMETRY_GRADS = os.environ.get("LSR_ALL_GRADS", "0") == "1"
+    # (2b) the inference form (render.py:24-55: render() under torch.no_grad(), LSR_FWD_NO_BACKWARD):
+    # the forward alone, reported beside, never as `value`
+    with torch.no_grad():
+        for _ in range(2):
+            render(cam, model, Pipe, bg, Opt)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            render(cam, model, Pipe, bg, Opt)
+        torch.cuda.synchronize()
+        elapsed_fwd = time.perf_counter() - t1
     # (3) the eager step itself (the host enqueues every launch, one wait per forward)
     if world > 1:
         dist.barrier()
@@ -549,8 +563,9 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
         tq = time.perf_counter()
+        # wait=False: the caller's stream is joined once, by synchronize(), inside the timed region
         for _ in range(args.steps):
-            pg.replay()
+            pg.replay(wait=False)
         pg.synchronize()
         torch.cuda.synchronize()
         if world > 1:
@@ -682,6 +697,7 @@ def main():
                                          "the other"}[best],
         "ms_per_step_forms": {n: (round(1000.0 * v / args.steps, 4) if v < 1e29 else None) for n, v in times.items()},
         "ms_per_step_all_gradients": round(1000.0 * elapsed_all / args.steps, 4),
+        "ms_forward_only": round(1000.0 * elapsed_fwd / args.steps, 4),
         "ms_per_step_rgb": None if rgb_ms is None else round(rgb_ms, 4),
         "raster_ms_per_step": round(raster_ms, 4),
         "stages_ms_per_step": {k: round(v["total_ms"] / prof_steps, 4) for k, v in sorted(prof.items())},

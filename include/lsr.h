@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define LSR_ABI_VERSION 12
+#define LSR_ABI_VERSION 13
 
 enum lsr_status {
     LSR_OK = 0,
@@ -91,7 +91,13 @@ enum lsr_raw_flags {
  * only the transmittance and feature sums of its split-replay states (half the state traffic).  A
  * backward with dL_dout_color after such a forward would start long tiles' replay chunks from
  * missing colour sums: it is invalid, and with settings.debug it fails with LSR_ERR_INVALID. */
-enum lsr_forward_flags { LSR_FWD_ZERO_GRAD_RECORDS = 1, LSR_FWD_NO_COLOR_GRAD = 2 };
+/* LSR_FWD_NO_BACKWARD (ABI 13): the caller promises that no lsr_backward follows this forward
+ * (inference: render.py:24-55 renders under torch.no_grad()).  The compositing kernel then writes
+ * only the images (and the fused loss, if asked): not the state only the backward reads -- the
+ * per-instance cover masks, the split-replay states, the backward's work lists, and the image
+ * buffer's final transmittance and contributor counts.  With settings.debug a backward of such a
+ * forward fails with LSR_ERR_INVALID. */
+enum lsr_forward_flags { LSR_FWD_ZERO_GRAD_RECORDS = 1, LSR_FWD_NO_COLOR_GRAD = 2, LSR_FWD_NO_BACKWARD = 4 };
 enum lsr_backward_flags { LSR_BWD_RECORDS_ZEROED = 1 };
 
 /* GaussianRasterizationSettings (gaussian_renderer/__init__.py:37-51), device-pointer form. */

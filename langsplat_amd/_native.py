@@ -22,12 +22,12 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LSR_LIB") or os.path.join(_HERE, "liblsr.so")
 
 LSR_BUF_GEOM, LSR_BUF_BINNING, LSR_BUF_IMAGE, LSR_BUF_BACKWARD = 0, 1, 2, 3
-ABI_VERSION = 12
+ABI_VERSION = 13
 ADAM_STEP_WORDS = 66  # include/lsr.h LSR_ADAM_STEP_WORDS
 ADAM_WORD_SKIPPED, ADAM_WORD_LR = 49, 50  # LSR_ADAM_WORD_SKIPPED / LSR_ADAM_WORD_LR
 # lsr_raw_flags (include/lsr.h): inputs are GaussianModel's raw parameters
 RAW_OPACITY, RAW_SCALES, RAW_ROTATIONS, RAW_LANGUAGE = 1, 2, 4, 8
-FWD_ZERO_GRAD_RECORDS, FWD_NO_COLOR_GRAD = 1, 2  # lsr_forward_flags
+FWD_ZERO_GRAD_RECORDS, FWD_NO_COLOR_GRAD, FWD_NO_BACKWARD = 1, 2, 4  # lsr_forward_flags
 BWD_RECORDS_ZEROED = 1     # lsr_backward_flags
 _vp = ctypes.c_void_p
 

@@ -282,6 +282,10 @@ static int32_t render_forward_and_finish(const lsr_settings* s, const lsr_forwar
     rp.out_color = a->out_color;
     rp.out_lang = a->out_language_feature;
     rp.split_color = (a->flags & LSR_FWD_NO_COLOR_GRAD) ? 0 : 1;
+    if (a->flags & LSR_FWD_NO_BACKWARD) {  // inference: no split states, no backward work lists
+        rp.no_bwd = 1;
+        rp.split_pool = nullptr;
+    }
     if (a->flags & LSR_FWD_ZERO_GRAD_RECORDS) {
         rp.zero_records = reinterpret_cast<float4*>(geom + L.grad_records);
         rp.zero_records_n4 = ((int64_t)P * kGradStrideLang + 3) / 4;
@@ -369,7 +373,7 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
         return fail(LSR_ERR_INVALID, "lsr_forward: settings tensors missing");
     if (a->raw & ~(LSR_RAW_OPACITY | LSR_RAW_SCALES | LSR_RAW_ROTATIONS | LSR_RAW_LANGUAGE))
         return fail(LSR_ERR_INVALID, "lsr_forward: unknown raw flag");
-    if (a->flags & ~(LSR_FWD_ZERO_GRAD_RECORDS | LSR_FWD_NO_COLOR_GRAD))
+    if (a->flags & ~(LSR_FWD_ZERO_GRAD_RECORDS | LSR_FWD_NO_COLOR_GRAD | LSR_FWD_NO_BACKWARD))
         return fail(LSR_ERR_INVALID, "lsr_forward: unknown flag");
     if (a->shs_rest && (!a->shs || a->M < 2))
         return fail(LSR_ERR_INVALID, "lsr_forward: shs_rest needs shs (features_dc) and M >= 2");
@@ -492,7 +496,8 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
     // Should the range need more passes than guessed, the sort is run again below.
     const uint32_t fwd_flags = ((a->flags & LSR_FWD_ZERO_GRAD_RECORDS) ? kFwdZeroedRecords : 0u) |
                                ((a->out_loss && s->include_feature && a->language_feature) ? kFwdFusedLoss : 0u) |
-                               ((a->flags & LSR_FWD_NO_COLOR_GRAD) ? kFwdNoColorState : 0u);
+                               ((a->flags & LSR_FWD_NO_COLOR_GRAD) ? kFwdNoColorState : 0u) |
+                               ((a->flags & LSR_FWD_NO_BACKWARD) ? kFwdNoBackward : 0u);
     if (a->capacity_rendered > 0) {
         // Capacity mode: nothing waits for the device.  The counters stay on the device, the binning's
         // grids and buffers come from the capacities and its kernels read the true counts; a view over
@@ -626,7 +631,7 @@ int32_t lsr_backward(const lsr_settings* s, const lsr_backward_args* a, lsr_allo
     char* geom = static_cast<char*>(a->geom_buffer);
     char* image = static_cast<char*>(a->image_buffer);
     char* binning = static_cast<char*>(a->binning_buffer);
-    if (debug && (a->flags & LSR_BWD_RECORDS_ZEROED || a->dL_dloss || a->dL_dout_color)) {
+    if (debug) {
         // what the forward prepared (counters[kCntFwdFlags]; the render backward clears the records
         // bit, so a second backward cannot reuse accumulated records)
         uint32_t ff = 0;
@@ -641,6 +646,8 @@ int32_t lsr_backward(const lsr_settings* s, const lsr_backward_args* a, lsr_allo
         if (a->dL_dout_color && (ff & kFwdNoColorState))
             return fail(LSR_ERR_INVALID, "lsr_backward: dL_dout_color, but the forward was told no colour gradient "
                                          "follows (LSR_FWD_NO_COLOR_GRAD)");
+        if (ff & kFwdNoBackward)
+            return fail(LSR_ERR_INVALID, "lsr_backward: the forward was told no backward follows (LSR_FWD_NO_BACKWARD)");
     }
     // the render backward's 5-value form (no geometry, no colour gradient) keeps 20-B records; the
     // first backward of a forward that cleared them (LSR_FWD_ZERO_GRAD_RECORDS) uses them directly

@@ -24,6 +24,12 @@ __device__ __forceinline__ float4 load_f4u(const void* ptr)
     const lsr_f4u v = *reinterpret_cast<const lsr_f4u*>(ptr);
     return make_float4(v.x, v.y, v.z, v.w);
 }
+// load_f4u with the non-temporal hint (streamed-once data: the cache keeps what other kernels reuse)
+__device__ __forceinline__ float4 load_f4u_nt(const void* ptr)
+{
+    const lsr_f4u v = __builtin_nontemporal_load(reinterpret_cast<const lsr_f4u*>(ptr));
+    return make_float4(v.x, v.y, v.z, v.w);
+}
 
 // SH constants, utils/sh_utils.py:26-45
 constexpr float SH_C0 = 0.28209479177387814f;

@@ -26,6 +26,7 @@ constexpr uint32_t kFwdZeroedRecords = 1u;  // the language step's gradient reco
 constexpr uint32_t kFwdFusedLoss = 2u;      // loss codes written (dL_dloss is valid)
 constexpr uint32_t kFwdNoColorState = 4u;   // split-replay states without the colour sums (no colour
                                             // gradient may follow: LSR_FWD_NO_COLOR_GRAD)
+constexpr uint32_t kFwdNoBackward = 8u;     // no backward state written (LSR_FWD_NO_BACKWARD)
 // longest-first tile schedule (lsr_render.hip): tiles per work class, forward and backward,
 // right after the counters so one memset clears both
 constexpr int kWorkClasses = 64;
@@ -253,6 +254,7 @@ struct RenderParams {
     float* split_pool;
     uint4* split_desc;
     int split_color;  // forward: store the colour sums' half of every state (off: LSR_FWD_NO_COLOR_GRAD)
+    int no_bwd;       // forward: write no state for a backward (LSR_FWD_NO_BACKWARD)
     int prio;  // wave priority by launch position (longest tiles highest), 0: off
     int geo;   // backward: the conic / opacity partials are needed (geometry gradients)
     float4* zero_records;  // forward: clear these zero_records_n4 float4s (grid-stride), or null

@@ -161,6 +161,9 @@ static size_t sh_lds_bytes(const float* shs, const float* shs_rest, int M)
 // count against another
 enum ShMode { kShLds = 0, kShDma = 1, kShDirect = 2 };
 
+#ifndef LSR_PRE_NT  // 1: the SH rows (192 of the ~250 B read per Gaussian) loaded non-temporally
+#define LSR_PRE_NT 0
+#endif
 #ifndef LSR_PRE_DIRECT_WAVES  // measurement knob: occupancy target of the kShDirect instance (0: none)
 #define LSR_PRE_DIRECT_WAVES 0
 #endif
@@ -225,7 +228,7 @@ __global__ __launch_bounds__(kPreThreads) __attribute__((amdgpu_waves_per_eu(
         const char* row = reinterpret_cast<const char*>(p.shs_rest) + ic * 180u;
 #pragma unroll
         for (int k = 0; k < 11; k++) {
-            const float4 v = load_f4u(row + 16 * k);
+            const float4 v = LSR_PRE_NT ? load_f4u_nt(row + 16 * k) : load_f4u(row + 16 * k);
             rr[4 * k] = v.x;
             rr[4 * k + 1] = v.y;
             rr[4 * k + 2] = v.z;

@@ -454,8 +454,10 @@ __device__ float render_empty_tiles(const RenderParams& p, int j, int M)
         pixel_map(u % p.gx, u / p.gx, (int)threadIdx.x, px, py);
         if (!(px < p.W && py < p.H)) continue;
         const size_t pix = (size_t)py * p.W + px;
-        p.final_T[pix] = 1.0f;
-        p.n_contrib[pix] = 0u;
+        if (!p.no_bwd) {
+            p.final_T[pix] = 1.0f;
+            p.n_contrib[pix] = 0u;
+        }
         p.out_color[pix] = fma_(1.0f, p.bg[0], 0.0f);
         p.out_color[HW + pix] = fma_(1.0f, p.bg[1], 0.0f);
         p.out_color[2 * HW + pix] = fma_(1.0f, p.bg[2], 0.0f);
@@ -584,7 +586,7 @@ __global__ __launch_bounds__(kTilePixels, LSR_FWD_WAVES) void k_render_forward(R
             sF[t] = make_float4(c.z, c.w, 0.0f, 0.0f);
             const uint8_t m = (uint8_t)entry_cover(a.x, a.y, a.z, a.w, b.x, cut, tx0, ty0);
             sM[t] = m;
-            p.cover[idx] = m;  // for the backward (coalesced: one byte per thread)
+            if (!p.no_bwd) p.cover[idx] = m;  // for the backward (coalesced: one byte per thread)
         }
         __syncthreads();
         if (kStats) ph.lap(ph.load);
@@ -695,7 +697,7 @@ __global__ __launch_bounds__(kTilePixels, LSR_FWD_WAVES) void k_render_forward(R
     // the backward's items into the longest-first class lists: the tile's full 256-entry chunks with
     // ONE returning atomic on their class (+nsplit), its last chunk with another, in parallel (thread
     // 1): an atomic per chunk put every heavy tile's chunks on one hot counter across the XCDs
-    if (t < 2 && p.sched_counts && maxl > 0) {
+    if (t < 2 && p.sched_counts && maxl > 0 && !p.no_bwd) {
         uint32_t* counts = p.sched_counts + kCntBwdClass;
         uint32_t* lists = p.sched_lists + (size_t)kWorkClasses * T;
         const size_t stride = (size_t)kSplitItems * T;
@@ -727,8 +729,10 @@ __global__ __launch_bounds__(kTilePixels, LSR_FWD_WAVES) void k_render_forward(R
     // workgroup's word gather holds 32 registers)
     if (inside) {
         const float Tf = fabsf(q.T);
-        p.final_T[pix] = Tf;
-        p.n_contrib[pix] = qlast;
+        if (!p.no_bwd) {  // the backward's state
+            p.final_T[pix] = Tf;
+            p.n_contrib[pix] = qlast;
+        }
         p.out_color[pix] = fma_(Tf, p.bg[0], q.C01.x);
         p.out_color[HW + pix] = fma_(Tf, p.bg[1], q.C01.y);
         p.out_color[2 * HW + pix] = fma_(Tf, p.bg[2], q.C2F0.x);
@@ -1174,6 +1178,9 @@ __device__ __forceinline__ BwdEntry load_entry(const float4* sA, const float4* s
     return e;
 }
 
+#ifndef LSR_BWD_F_EARLY  // 1: the language step's feature record read beside A and B (measurement knob)
+#define LSR_BWD_F_EARLY 1
+#endif
 // One entry of a wave's back-to-front walk: the exact skip tests of the forward, the blend and the
 // wave reduce-scatter of its partials into the tile sums (sG = this lane's value slot of entry 0,
 // entry j at + j kGS).  kk = the entry's list index.
@@ -1186,6 +1193,11 @@ __device__ __forceinline__ void bwd_walk_entry(BwdPixel& q, const BwdEntry& E, i
     const float4& B = E.B;
     const float dx = A.x - pfx, dy = A.y - pfy;
     const float pw = fma_(dx, fma_(-B.x, dy, A.z * dx), (A.w * dy) * dy);  // the forward's order
+    // the language step's feature record is read with A and B, not after the skip test below (the
+    // compiler sinks it into the blend's block, a second LDS round trip on the visit's chain): the
+    // empty asm takes it as an operand here, after the power, by when it has landed with A and B
+    float4 Fv = E.F;
+    if (k5 && LSR_BWD_F_EARLY) asm volatile("" : "+v"(Fv.x), "+v"(Fv.y), "+v"(Fv.z), "+v"(Fv.w));
     bool h = kk < (int)q.last && pw <= 0.0f && pw >= B.z;
     if (__ballot(h) == 0ull) return;  // wave-uniform skip
     // hardware exp (a few ulp): gradients need 1e-4.  Only the 1/255 skip decision must equal the
@@ -1224,10 +1236,10 @@ __device__ __forceinline__ void bwd_walk_entry(BwdPixel& q, const BwdEntry& E, i
         C = make_float3(E.C.x, E.C.y, E.C.z);
         if (kFeat) F = make_float3(E.C.w, B.w, E.F.x);
     } else if (kFeat) {
-        F = kGeo ? make_float3(E.F.x, B.w, E.F.y) : make_float3(E.F.x, E.F.y, E.F.z);
+        F = kGeo ? make_float3(Fv.x, B.w, Fv.y) : make_float3(Fv.x, Fv.y, Fv.z);
     }
     float v[12];
-    bwd_pixel_blend<kFeat, kColor, kGeo>(q, G, og, al, dx, dy, A, B, C, F, (kColor || kGeo) ? -0.5f * B.x : E.F.w,
+    bwd_pixel_blend<kFeat, kColor, kGeo>(q, G, og, al, dx, dy, A, B, C, F, (kColor || kGeo) ? -0.5f * B.x : Fv.w,
                                          v);
     if (k5) {
         const float tot = wave_reduce_scatter5(v, lane);

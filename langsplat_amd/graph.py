@@ -70,6 +70,12 @@ class ViewSlot:
     def language_target(self):
         return (self.gt, self.mask) if self.gt is not None else None
 
+    @staticmethod
+    def sources(camera, gt: Optional[torch.Tensor] = None, mask: Optional[torch.Tensor] = None):
+        """The device tensors load() reads (for record_stream when it runs on another stream)."""
+        ts = [camera.world_view_transform, camera.full_proj_transform, camera.camera_center, gt, mask]
+        return [t for t in ts if torch.is_tensor(t) and t.is_cuda]
+
     def load(self, camera, gt: Optional[torch.Tensor] = None, mask: Optional[torch.Tensor] = None):
         """Copy a view into the slot (on the current stream)."""
         if (float(camera.FoVx), float(camera.FoVy)) != (self.FoVx, self.FoVy) or \

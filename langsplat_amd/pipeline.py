@@ -337,6 +337,7 @@ class PipelinedGraphStep:
         self.ev_step = [torch.cuda.Event() for _ in range(S)]
         self.ev_cur = [torch.cuda.Event() for _ in range(S)]
         self._since_capture = 0
+        self._fast = False
         self.captures += 1
         return self
 
@@ -347,21 +348,34 @@ class PipelinedGraphStep:
         P = int(self.params[0].shape[0])
         return geom.data_ptr() + _native.state_layout(P, int(W), int(H), 0)["record"]
 
-    def _geometry(self, r, after=None):
+    def _geometry(self, r, after=None, released=None):
         """Set r's geometry graph on stream B, after everything the caller's stream holds (the set's
-        view loaded, its last reader finished) [and after `after`]."""
+        view loaded, its last reader finished) or, with `released` (an event: the set's last reader
+        done), after that alone [and after `after`]."""
         sb = self.streams[1]
-        sb.wait_stream(torch.cuda.current_stream())
+        if released is not None:
+            sb.wait_event(released)
+        else:
+            sb.wait_stream(torch.cuda.current_stream())
         if after is not None:
             sb.wait_event(after)
         with torch.cuda.stream(sb):
             self.g_geo[r].replay()
         self.ev_geo[r].record(sb)
 
-    def replay(self, next_view=None) -> torch.Tensor:
+    def replay(self, next_view=None, wait: bool = True) -> torch.Tensor:
         """One language step of the view loaded S - 1 replays ago (or at capture); next_view
         (camera, gt, mask) is the view of the replay S - 1 ahead (ViewSlots only; None: the view of
-        its set stays)."""
+        its set stays).
+
+        wait=False: the caller's stream is not chained to the replay -- the returned loss (and the
+        graph-owned gradients) are valid on it only after synchronize() (and only those of the
+        last S replays: a set's next composite rewrites them), and nothing of the replay
+        goes through the caller's stream (its queue carries no event or wait per step: on this
+        runtime the two streams' packets can share a hardware queue with it, and a wait there held
+        stream A ~20-28 us per step).  The caller must not change the parameters
+        between such replays without follow_caller().  bench.py times this form, with the
+        synchronize() inside the timed region."""
         if self.g_comp[0] is None:
             self.capture()
         S = self.S
@@ -373,23 +387,41 @@ class PipelinedGraphStep:
             for j in range(S - 1):
                 self._geometry((self.k + j) % S)
             self.primed = True
+        fast = not wait and self._since_capture >= S - 1
+        if wait and self._fast:  # back from fast replays: the lagged events were not recorded
+            self._since_capture = 0
+        self._fast = fast
+        # set r's last reader was step k - 1 (the view S - 1 ahead goes there)
+        released = self.ev_step[(self.k - 1) % S] if self.k > 0 else None
         if next_view is not None:
             if self.slots is None:
                 raise RuntimeError("PipelinedGraphStep.replay(next_view=...) needs ViewSlots")
-            # set r's last reader was step k - 1, which the caller's stream waited for (below)
-            self.slots[r].load(*_as_view(next_view))
+            if fast:
+                # on stream B, after step k - 1 and after the caller's stream (the view's tensors)
+                sb.wait_stream(cur)
+                if released is not None:
+                    sb.wait_event(released)
+                view = _as_view(next_view)
+                with torch.cuda.stream(sb):
+                    self.slots[r].load(*view)
+                for t in self.slots[r].sources(*view):
+                    t.record_stream(sb)
+            else:
+                # the caller's stream waited for step k - 1 at the end of the previous replay
+                self.slots[r].load(*_as_view(next_view))
             self._loaded[r] = next_view
-        # Stream A does not wait for the caller's stream as it is now: that stream waits for the
-        # previous step (below), so the wait would be a round trip between two queues (measured ~35 us
-        # of idle stream A per step at C3).  It waits instead for the caller's work up
-        # to the start of replay k - S + 1, long done: the caller's uses of the loss of replay k - S
-        # (whose tensor composite k rewrites) precede that.  The first S - 1 replays after a capture
-        # wait for the caller's stream itself.
-        self.ev_cur[self.k % S].record(cur)
-        if self._since_capture < S - 1:
-            sa.wait_stream(cur)
-        else:
-            sa.wait_event(self.ev_cur[(self.k + 1) % S])  # recorded at replay k - S + 1
+        if not fast:
+            # Stream A does not wait for the caller's stream as it is now: that stream waits for the
+            # previous step (below), so the wait would be a round trip between two queues (measured
+            # ~35 us of idle stream A per step at C3).  It waits instead for the
+            # caller's work up to the start of replay k - S + 1, long done: the caller's uses of the
+            # loss of replay k - S (whose tensor composite k rewrites) precede that.  The first
+            # S - 1 replays after a capture wait for the caller's stream itself.
+            self.ev_cur[self.k % S].record(cur)
+            if self._since_capture < S - 1:
+                sa.wait_stream(cur)
+            else:
+                sa.wait_event(self.ev_cur[(self.k + 1) % S])  # recorded at replay k - S + 1
         self._since_capture += 1
         sa.wait_event(self.ev_geo[p])
         with torch.cuda.stream(sa):
@@ -406,8 +438,13 @@ class PipelinedGraphStep:
                 self.g_adam[p].replay()
         self.ev_step[p].record(sa)
         # view k + S - 1's geometry into set r
-        self._geometry(r, after=self.ev_comp[p] if self.geo_after_fwd and not self.merged else None)
-        cur.wait_event(self.ev_step[p])
+        after = self.ev_comp[p] if self.geo_after_fwd and not self.merged else None
+        if fast:
+            # the set's view (if any) was loaded on stream B itself
+            self._geometry(r, after=after, released=self.ev_step[(self.k - 1) % S])
+        else:
+            self._geometry(r, after=after)
+            cur.wait_event(self.ev_step[p])
         self.k += 1
         return self.static_loss[p]
 

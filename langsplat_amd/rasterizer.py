@@ -69,9 +69,10 @@ class _RasterizeGaussians(torch.autograd.Function):
         lang_in = _f32(lang) if use_lang else None
         args = (_f32(means3D), _f32(sh), _f32(colors_precomp), lang_in, _f32(opacities), _f32(scales),
                 _f32(rotations), _f32(cov3Ds_precomp))
-        # a backward will follow: let the compositing kernel clear its gradient records
-        flags = _native.FWD_ZERO_GRAD_RECORDS if any(ctx.needs_input_grad) else 0
-        ctx.records_zeroed = flags != 0
+        # a backward will follow: let the compositing kernel clear its gradient records; none will
+        # (inference, render.py:24-55 under torch.no_grad()): it writes no state for one
+        flags = _native.FWD_ZERO_GRAD_RECORDS if any(ctx.needs_input_grad) else _native.FWD_NO_BACKWARD
+        ctx.records_zeroed = flags == _native.FWD_ZERO_GRAD_RECORDS
         if raster_settings.debug:
             cpu_args = _cpu_deep_copy(args)
             try:
@@ -190,13 +191,14 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
             raise ValueError("the fused language loss needs include_feature=True")
         # without the fused loss this output is never handed to the caller (no fill kernel)
         loss = _native.output_tensor("loss", (), torch.float32, m3.device)
-        # a backward will follow: let the compositing kernel clear its gradient records
-        flags = _native.FWD_ZERO_GRAD_RECORDS if any(ctx.needs_input_grad) else 0
-        ctx.records_zeroed = flags != 0
+        # a backward will follow: let the compositing kernel clear its gradient records; none will
+        # (inference, render.py:24-55 under torch.no_grad()): it writes no state for one
+        flags = _native.FWD_ZERO_GRAD_RECORDS if any(ctx.needs_input_grad) else _native.FWD_NO_BACKWARD
+        ctx.records_zeroed = flags == _native.FWD_ZERO_GRAD_RECORDS
         # the language step (train.py:96-104): the loss is the fused language loss, so the colour
         # image is expected off the loss path and the split-replay states skip the colour sums; a
         # colour gradient arriving anyway is served by rasterizing again with them (backward below)
-        ctx.no_color = fuse_loss and flags != 0
+        ctx.no_color = fuse_loss and ctx.records_zeroed
         if ctx.no_color:
             flags |= _native.FWD_NO_COLOR_GRAD
 

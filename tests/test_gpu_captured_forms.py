@@ -271,11 +271,13 @@ def test_graphed_step_over_a_view_sequence(monkeypatch):
     assert_states_close(_state(m, opt), se, "graph sequence")
 
 
-@pytest.mark.parametrize("sets", [2, 3])
-def test_pipelined_graph_over_a_view_sequence(sets, monkeypatch):
+@pytest.mark.parametrize("sets,wait", [(2, True), (3, True), (3, False)])
+def test_pipelined_graph_over_a_view_sequence(sets, wait, monkeypatch):
     """PipelinedGraphStep with one ViewSlot per buffer set: capture(views=the first S - 1 views),
     replay(next_view=the view S - 1 ahead); every replay composites its own view's geometry with its
-    own target, and the sequence reproduces the eager loop."""
+    own target, and the sequence reproduces the eager loop.  wait=False (bench.py's form): no
+    per-replay join with the caller's stream, the views loaded on the geometry stream; the last S
+    losses (valid after synchronize()) and the final state reproduce the eager loop."""
     monkeypatch.setenv("LANGSPLAT_AMD_FUSED", "1")
     g = make_gaussians(CONFIGS["C4"]["P"], seed=0)
     views = _c4_views()
@@ -289,15 +291,22 @@ def test_pipelined_graph_over_a_view_sequence(sets, monkeypatch):
     losses = []
     for k in range(len(views)):
         nxt = views[k + L] if k + L < len(views) else None
-        losses.append(pg.replay(next_view=nxt).clone())
+        if wait:
+            losses.append(pg.replay(next_view=nxt).clone())
+        else:
+            losses.append(pg.replay(next_view=nxt, wait=False))
     pg.synchronize()
     torch.cuda.synchronize()
+    if not wait:  # only the last S replays' static losses are still theirs
+        losses = [t.clone() for t in losses[-sets:]]
+        losses_e = losses_e[-sets:]
     assert pg.check() and pg.captures == 1
     pg.sync()
     assert int(opt.state[m._language_feature]["step"].item()) == len(views)
-    assert torch.equal(losses[0], losses_e[0])
+    if wait:
+        assert torch.equal(losses[0], losses_e[0])
     torch.testing.assert_close(torch.stack(losses), torch.stack(losses_e), rtol=1e-5, atol=0)
-    assert_states_close(_state(m, opt), se, f"pipelined graph sequence, {sets} sets")
+    assert_states_close(_state(m, opt), se, f"pipelined graph sequence, {sets} sets, wait={wait}")
 
 
 # ---- a view over capacity mid-sequence ---------------------------------------------------------------

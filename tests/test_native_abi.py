@@ -31,7 +31,7 @@ def test_library_loads_and_exports_every_declared_symbol():
     for name in _declared_functions():
         assert hasattr(lib, name), name
         assert name in _native.SIGNATURES, f"ctypes binding misses {name}"
-    assert lib.lsr_abi_version() == _native.ABI_VERSION == 12
+    assert lib.lsr_abi_version() == _native.ABI_VERSION == 13
 
 
 def test_header_constants_match_the_python_side():
@@ -42,6 +42,11 @@ def test_header_constants_match_the_python_side():
     assert int(re.search(r"#define LSR_ADAM_WORD_LR (\d+)", hdr).group(1)) == _native.ADAM_WORD_LR
     # 16 lr words after the skipped count fit the block
     assert _native.ADAM_WORD_LR + 16 <= _native.ADAM_STEP_WORDS
+    fwd = re.search(r"enum lsr_forward_flags \{([^}]*)\}", hdr).group(1)
+    vals = dict((k.strip(), int(v)) for k, v in (e.split("=") for e in fwd.split(",")))
+    assert vals == {"LSR_FWD_ZERO_GRAD_RECORDS": _native.FWD_ZERO_GRAD_RECORDS,
+                    "LSR_FWD_NO_COLOR_GRAD": _native.FWD_NO_COLOR_GRAD,
+                    "LSR_FWD_NO_BACKWARD": _native.FWD_NO_BACKWARD}
 
 
 def test_sizes_and_layout_are_consistent():
@@ -84,7 +89,7 @@ def test_forward_flag_and_phase_validation_without_gpu():
             setattr(a, k, v)
         return lib.lsr_forward(ctypes.byref(s), ctypes.byref(a), _native._ALLOC_CB, None, None, ctypes.byref(nr))
 
-    assert call(flags=4) != 0 and "unknown flag" in _native.last_error()
+    assert call(flags=8) != 0 and "unknown flag" in _native.last_error()
     assert call(phase=_native.forward_phase.GEOMETRY) != 0 and "phase" in _native.last_error()
     assert call(phase=4, capacity_rendered=16, capacity_entries=16) != 0 and "phase" in _native.last_error()
     assert call(phase=_native.forward_phase.COMPOSITE_FILLED) != 0 and "phase" in _native.last_error()

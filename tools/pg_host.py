@@ -1,6 +1,6 @@
 """Host enqueue time vs device time of the pipelined graph step at C3 (measurement aid):
 
-    python3 tools/pg_host.py [--steps 300]
+    python3 tools/pg_host.py [--steps 300] [--nowait]
 
 Prints the host time per replay() call (enqueue only) and the wall time per step to the final
 synchronize: when they are close the host, not the GPU, sets the step rate.
@@ -33,14 +33,15 @@ def main():
     pg = PipelinedGraphStep(lambda: bench.render(cam, model, bench.Pipe, bg, bench.Opt,
                                                  language_target=(gt, mask))["language_l1"],
                             [model._language_feature], optim).capture()
+    wait = "--nowait" not in sys.argv
     for _ in range(20):
-        pg.replay()
+        pg.replay(wait=wait)
     pg.synchronize()
     torch.cuda.synchronize()
     for rep in range(3):
         t0 = time.perf_counter()
         for _ in range(steps):
-            pg.replay()
+            pg.replay(wait=wait)
         t1 = time.perf_counter()
         pg.synchronize()
         torch.cuda.synchronize()
