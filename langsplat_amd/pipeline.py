@@ -90,6 +90,8 @@ class ViewPipeline:
         capture has its own)."""
         if self.k == 0:
             raise RuntimeError("PipelinedGraphStep.last_grads: no replay yet")
+        if self.R > 1 and self.k <= self.R and self.g_rot0 is not None:
+            return self.g_rot0[1][self.k - 1]
         if self.k == 1 and self.merged and self.g_comp0 is not None:
             return self.grads0
         return self.grads[(self.k - 1) % self.S]
@@ -160,11 +162,16 @@ class PipelinedGraphStep:
     of the returned loss) precedes the device work of the replay S - 1 later, not of the next one;
     after changing the parameters or the optimizer state between replays, call follow_caller().
 
+    Rotation mode (rotation=R > 1, N = 1; LSR_PG_ROT): 2 R buffer sets in two groups; every R-th
+    replay launches the next R steps as ONE stream-A graph (fewer graph boundaries: ~20-28 us of idle
+    queue each at C3) and the following R views' geometry on stream B; the replays in between launch
+    nothing.  Parameters, learning rates and check() apply at rotation boundaries (k % R == 0).
+
     Knobs (measured at C3): LSR_PG_SETS (2 or 3), LSR_PG_GEO=fwd (the geometry starts
-    only after this view's compositing), LSR_PG_PRIO=geo|step (stream priorities)."""
+    only after this view's compositing), LSR_PG_PRIO=geo|step (stream priorities), LSR_PG_ROT."""
 
     def __init__(self, forward_fn, params, optimizer, headroom: float = 1.125, warmup: int = 2, bucket=None,
-                 slots=None, sets: int = None):
+                 slots=None, sets: int = None, rotation: int = None):
         self.forward_fn = forward_fn
         self.params = [p for p in params]
         self.optimizer = optimizer
@@ -175,9 +182,17 @@ class PipelinedGraphStep:
         # three sets by default: measured at C3 (tools/pg_sweep.py, one box) 0.435 ms per step against
         # 0.482 with two; a view's geometry then runs two steps ahead, beside the backward and the
         # next compositing, and no compositing waits on a cross-stream event that is not yet signalled
-        S = int(sets if sets is not None else (len(slots) if slots else os.environ.get("LSR_PG_SETS", "3")))
+        # rotation R > 1: R consecutive steps per stream-A graph over 2 R buffer sets (N = 1 only)
+        R = int(rotation if rotation is not None else os.environ.get("LSR_PG_ROT", "1"))
+        if R < 1 or (R > 1 and bucket is not None):
+            raise ValueError("PipelinedGraphStep: rotation >= 1, and > 1 only without a bucket (N = 1)")
+        self.R = R
+        S = int(sets if sets is not None else (len(slots) if slots else
+                                               (2 * R if R > 1 else os.environ.get("LSR_PG_SETS", "3"))))
         if S < 2:
             raise ValueError("PipelinedGraphStep: at least two buffer sets")
+        if R > 1 and S != 2 * R:
+            raise ValueError("PipelinedGraphStep: a rotation of R steps takes 2 R buffer sets")
         if slots is not None and len(slots) != S:
             raise ValueError("PipelinedGraphStep: one ViewSlot per buffer set")
         self.S = S
@@ -198,6 +213,7 @@ class PipelinedGraphStep:
         self.rendered = self.entries = 0
         self._skipped_base = 0
         self._loaded = [None] * S  # the view each set's slot holds (slots only)
+        self._assigned = [None] * S  # rotation mode: the view each set's next geometry renders
 
     def _reset_graphs(self):
         S = self.S
@@ -205,6 +221,7 @@ class PipelinedGraphStep:
         self.grads = [None] * S
         self.static_loss = [None] * S
         self.ev_geo = self.ev_comp = self.ev_step = [None] * S
+        self.g_rot = self.g_rot0 = None
         self.k = 0
         self.primed = False
 
@@ -243,7 +260,7 @@ class PipelinedGraphStep:
             views += [views[-1]] * (S - 1 - len(views))
             for j in range(S - 1):
                 self.slots[j].load(*_as_view(views[j]))
-                self._loaded[j] = views[j]
+                self._loaded[j] = self._assigned[j] = views[j]
         self._measure(min_rendered, min_entries)
         self._reset_graphs()
         self.optimizer.prepare_capture()
@@ -295,6 +312,8 @@ class PipelinedGraphStep:
             self.g_geo[p] = g
             for q in self.params:
                 q.grad = None  # the captured backward assigns its own .grad (no accumulate)
+            if self.R > 1:
+                continue  # the steps are captured per rotation below
             if fused and p == 0:
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, stream=sa):
@@ -330,8 +349,11 @@ class PipelinedGraphStep:
                 self.g_adam[p] = g
             self.static_loss[p] = loss.detach()  # the set's static loss tensor
             del loss
+        if self.R > 1:
+            self._capture_rotations(caps, comp_phase, fused, step_body)
         cur.wait_stream(sa)
         cur.wait_stream(sb)
+        self.ev_rot = [torch.cuda.Event() for _ in range(2)]
         self.ev_geo = [torch.cuda.Event() for _ in range(S)]
         self.ev_comp = [torch.cuda.Event() for _ in range(S)]
         self.ev_step = [torch.cuda.Event() for _ in range(S)]
@@ -340,6 +362,86 @@ class PipelinedGraphStep:
         self._fast = False
         self.captures += 1
         return self
+
+    def _capture_rotations(self, caps, comp_phase, fused, step_body):
+        """Rotation mode: per group j of R sets (j = 0: sets 0..R-1, j = 1: sets R..2R-1) one graph
+        of R full steps, composite + loss + backward + Adam each (and, fused, a variant of group 0
+        whose first composite fills its own records, for the first replay after a capture)."""
+        R, sa = self.R, self.streams[0]
+
+        def rot(j, first):
+            g = torch.cuda.CUDAGraph()
+            grads = []
+            with torch.cuda.graph(g, stream=sa):
+                for p in range(j * R, (j + 1) * R):
+                    for q in self.params:
+                        q.grad = None  # each step's backward assigns its own .grad
+                    phase = _native.forward_phase.COMPOSITE if (first and p == 0) else comp_phase
+                    with caps[p], self.sets[p], _native.forward_phase(phase):
+                        loss = self._fwd(p)
+                    step_body(p, loss)
+                    grads.append([q.grad for q in self.params])
+                    self.static_loss[p] = loss.detach()  # the set's static loss (same tensor in every graph)
+                    del loss
+            return g, grads
+
+        self.g_rot = [rot(0, False), rot(1, False)]
+        self.g_rot0 = rot(0, True) if fused else None
+        for j in range(2):
+            for i, gr in enumerate(self.g_rot[j][1]):
+                self.grads[j * R + i] = gr
+
+    def _replay_rotation(self, next_view, wait):
+        """replay() in rotation mode: at a rotation start (k % R == 0) the group's R steps are launched
+        as one graph on stream A, and the next rotation's geometry (the other group, whose sets the
+        previous rotation released) on stream B; the other replays launch nothing."""
+        S, R = self.S, self.R
+        sa, sb = self.streams
+        cur = torch.cuda.current_stream()
+        k = self.k
+        if next_view is not None:
+            if self.slots is None:
+                raise RuntimeError("PipelinedGraphStep.replay(next_view=...) needs ViewSlots")
+            self._assigned[(k + S - 1) % S] = next_view
+        if k % R == 0:
+            j = (k // R) % 2
+            if not self.primed:  # group 0's geometry (its views were loaded at capture)
+                for p in range(R):
+                    self._geometry(p)
+                self.primed = True
+            if wait or self._since_capture == 0:
+                sa.wait_stream(cur)  # the caller's earlier work (parameters, learning rates) first
+            for p in range(j * R, (j + 1) * R):
+                sa.wait_event(self.ev_geo[p])
+            with torch.cuda.stream(sa):
+                self.optimizer.sync_lr()
+                g, _ = self.g_rot0 if (k == 0 and self.g_rot0 is not None) else self.g_rot[j]
+                g.replay()
+            self.ev_rot[j].record(sa)
+            # the other group's sets were last read by the previous rotation (none before the first)
+            o = 1 - j
+            if k >= R:
+                sb.wait_event(self.ev_rot[o])
+            if self.slots is not None:
+                sb.wait_stream(cur)  # the views' tensors
+            for p in range(o * R, (o + 1) * R):
+                if self.slots is not None and self._assigned[p] is not None:
+                    view = _as_view(self._assigned[p])
+                    with torch.cuda.stream(sb):
+                        self.slots[p].load(*view)
+                    for t in self.slots[p].sources(*view):
+                        t.record_stream(sb)
+                    self._loaded[p] = self._assigned[p]
+                with torch.cuda.stream(sb):
+                    self.g_geo[p].replay()
+                self.ev_geo[p].record(sb)
+            if wait:
+                cur.wait_event(self.ev_rot[j])
+        elif wait:
+            cur.wait_event(self.ev_rot[(k // R) % 2])
+        self._since_capture += 1
+        self.k += 1
+        return self.static_loss[k % S]
 
     def _record_ptr(self, p):
         """Device address of set p's per-Gaussian render records (include/lsr.h lsr_state_layout.record)."""
@@ -376,8 +478,10 @@ class PipelinedGraphStep:
         stream A ~20-28 us per step).  The caller must not change the parameters
         between such replays without follow_caller().  bench.py times this form, with the
         synchronize() inside the timed region."""
-        if self.g_comp[0] is None:
+        if self.g_comp[0] is None and getattr(self, "g_rot", None) is None:
             self.capture()
+        if self.R > 1:
+            return self._replay_rotation(next_view, wait)
         S = self.S
         sa, sb = self.streams
         cur = torch.cuda.current_stream()
@@ -453,6 +557,8 @@ class PipelinedGraphStep:
         capture has its own)."""
         if self.k == 0:
             raise RuntimeError("PipelinedGraphStep.last_grads: no replay yet")
+        if self.R > 1 and self.k <= self.R and self.g_rot0 is not None:
+            return self.g_rot0[1][self.k - 1]
         if self.k == 1 and self.merged and self.g_comp0 is not None:
             return self.grads0
         return self.grads[(self.k - 1) % self.S]
@@ -475,7 +581,10 @@ class PipelinedGraphStep:
     def check(self) -> bool:
         """True if every replay's view fitted its capacities.  Otherwise re-capture with twice the
         capacities and return False: the over-capacity views were not rasterized, and at N = 1 their
-        steps changed nothing (optimizer.skipped_steps() counts them; train those views again)."""
+        steps changed nothing (optimizer.skipped_steps() counts them; train those views again).
+        Rotation mode: only between rotations (k % R == 0), where no launched step is pending."""
+        if self.R > 1 and self.k % self.R != 0:
+            raise RuntimeError("PipelinedGraphStep.check: in rotation mode only at a rotation boundary")
         self.synchronize()
         skipped = self.optimizer.skipped_steps() - self._skipped_base
         if skipped == 0 and all(int(o.item()) == 0 for o in self.overflow):
@@ -484,6 +593,7 @@ class PipelinedGraphStep:
         for o in self.overflow:
             o.zero_()
         # the replays continue with the views already loaded for the next S - 1 steps
-        views = [self._loaded[(self.k + j) % self.S] for j in range(self.S - 1)] if self.slots else None
+        src = self._assigned if self.R > 1 else self._loaded
+        views = [src[(self.k + j) % self.S] for j in range(self.S - 1)] if self.slots else None
         self.capture(2 * self.rendered, 2 * self.entries, views=views)
         return False

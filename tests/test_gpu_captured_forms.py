@@ -309,6 +309,37 @@ def test_pipelined_graph_over_a_view_sequence(sets, wait, monkeypatch):
     assert_states_close(_state(m, opt), se, f"pipelined graph sequence, {sets} sets, wait={wait}")
 
 
+@pytest.mark.parametrize("rot,wait", [(2, True), (2, False), (4, False)])
+def test_pipelined_graph_rotation_over_a_view_sequence(rot, wait, monkeypatch):
+    """Rotation mode (R steps per stream-A graph over 2 R buffer sets): the 8-view C4 sequence
+    (a multiple of R replays) reproduces the eager loop -- the last R losses after synchronize()
+    and the final parameters, moments and step count."""
+    monkeypatch.setenv("LANGSPLAT_AMD_FUSED", "1")
+    g = make_gaussians(CONFIGS["C4"]["P"], seed=0)
+    views = _c4_views()
+    assert len(views) % rot == 0
+    losses_e, se, (Rc, Ec) = _eager_sequence(g, views)
+    m = _frozen_model(g)
+    opt = _adam(m)
+    S = 2 * rot
+    slots = [ViewSlot(*views[0]) for _ in range(S)]
+    pg = PipelinedGraphStep(_slot_forward(m), [m._language_feature], opt, slots=slots, rotation=rot)
+    assert pg.S == S and pg.R == rot
+    pg.capture(Rc, Ec, views=views[:S - 1])
+    losses = []
+    for k in range(len(views)):
+        nxt = views[k + S - 1] if k + S - 1 < len(views) else None
+        losses.append(pg.replay(next_view=nxt, wait=wait))
+    pg.synchronize()
+    torch.cuda.synchronize()
+    losses = [t.clone() for t in losses[-rot:]]
+    assert pg.check() and pg.captures == 1
+    pg.sync()
+    assert int(opt.state[m._language_feature]["step"].item()) == len(views)
+    torch.testing.assert_close(torch.stack(losses), torch.stack(losses_e[-rot:]), rtol=1e-5, atol=0)
+    assert_states_close(_state(m, opt), se, f"pipelined graph rotation {rot}, wait={wait}")
+
+
 # ---- a view over capacity mid-sequence ---------------------------------------------------------------
 
 def _overflow_views(W=320, H=240):

@@ -9,6 +9,7 @@ Four forms, 50 repetitions each, every graph one ~40 us elementwise kernel on a 
   graph_ev  graph replay, an event recorded after each
   graph_w   graph replay, an event recorded after each and the stream waiting on another stream's
             (long completed) event before each
+  graph3    one graph holding three of the kernels (the gaps inside a graph, and between graphs)
 The report prints the median gap between one kernel's end and the next one's start per form.
 """
 import os
@@ -17,7 +18,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-FORMS = ("eager", "graph", "graph_ev", "graph_w")
+FORMS = ("eager", "graph", "graph_ev", "graph_w", "graph3")
 SCALES = {f: 1.0 + 0.001 * (i + 1) for i, f in enumerate(FORMS)}  # tells the forms apart in the trace
 
 
@@ -39,13 +40,14 @@ def run():
         with torch.cuda.stream(s):
             x.mul_(SCALES[f])  # warm-up outside the capture
         with torch.cuda.graph(g, stream=s):
-            x.mul_(SCALES[f])
+            for _ in range(3 if f == "graph3" else 1):
+                x.mul_(SCALES[f])
         graphs[f] = g
     torch.cuda.synchronize()
     ev = torch.cuda.Event()
     for f in FORMS:
         with torch.cuda.stream(s):
-            for _ in range(50):
+            for _ in range(17 if f == "graph3" else 50):
                 if f == "eager":
                     x.mul_(SCALES[f])
                     continue
@@ -63,9 +65,9 @@ def report(path):
     rows = [r for r in rows if "elementwise" in r["Kernel_Name"] or "mul" in r["Kernel_Name"].lower()]
     # the forms ran in order, 50 kernels each (plus the warm-ups): split by position
     n = len(rows)
-    tail = rows[n - 4 * 50:]
+    tail = rows[n - 4 * 50 - 51:]
     for i, f in enumerate(FORMS):
-        seg = tail[50 * i:50 * (i + 1)]
+        seg = tail[50 * i:50 * (i + 1)] if f != "graph3" else tail[200:251]
         gaps = sorted((int(b["Start_Timestamp"]) - int(a["End_Timestamp"])) / 1e3 for a, b in zip(seg, seg[1:]))
         durs = sorted((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in seg)
         print(f"graph_gap {f:9s} median gap {gaps[len(gaps) // 2]:6.2f} us  (p90 {gaps[int(0.9 * len(gaps))]:6.2f})"
