@@ -305,6 +305,8 @@ class PipelinedGraphStep:
                     self.optimizer.step(skip=skip[p])
 
         for p in range(S):
+            if self.R > 1:
+                continue  # geometry and steps are captured per rotation group below
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, stream=sb), caps[p], self.sets[p], \
                     _native.forward_phase(_native.forward_phase.GEOMETRY):
@@ -312,8 +314,6 @@ class PipelinedGraphStep:
             self.g_geo[p] = g
             for q in self.params:
                 q.grad = None  # the captured backward assigns its own .grad (no accumulate)
-            if self.R > 1:
-                continue  # the steps are captured per rotation below
             if fused and p == 0:
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, stream=sa):
@@ -387,6 +387,16 @@ class PipelinedGraphStep:
 
         self.g_rot = [rot(0, False), rot(1, False)]
         self.g_rot0 = rot(0, True) if fused else None
+        # each group's R geometries as one stream-B graph as well
+        sb = self.streams[1]
+        self.g_geo_rot = []
+        for j in range(2):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=sb):
+                for p in range(j * R, (j + 1) * R):
+                    with caps[p], self.sets[p], _native.forward_phase(_native.forward_phase.GEOMETRY):
+                        self._fwd(p)
+            self.g_geo_rot.append(g)
         for j in range(2):
             for i, gr in enumerate(self.g_rot[j][1]):
                 self.grads[j * R + i] = gr
@@ -406,13 +416,14 @@ class PipelinedGraphStep:
         if k % R == 0:
             j = (k // R) % 2
             if not self.primed:  # group 0's geometry (its views were loaded at capture)
-                for p in range(R):
-                    self._geometry(p)
+                sb.wait_stream(cur)
+                with torch.cuda.stream(sb):
+                    self.g_geo_rot[0].replay()
+                self.ev_geo[0].record(sb)
                 self.primed = True
             if wait or self._since_capture == 0:
                 sa.wait_stream(cur)  # the caller's earlier work (parameters, learning rates) first
-            for p in range(j * R, (j + 1) * R):
-                sa.wait_event(self.ev_geo[p])
+            sa.wait_event(self.ev_geo[j * R])  # the group's geometry graph
             with torch.cuda.stream(sa):
                 self.optimizer.sync_lr()
                 g, _ = self.g_rot0 if (k == 0 and self.g_rot0 is not None) else self.g_rot[j]
@@ -432,9 +443,9 @@ class PipelinedGraphStep:
                     for t in self.slots[p].sources(*view):
                         t.record_stream(sb)
                     self._loaded[p] = self._assigned[p]
-                with torch.cuda.stream(sb):
-                    self.g_geo[p].replay()
-                self.ev_geo[p].record(sb)
+            with torch.cuda.stream(sb):
+                self.g_geo_rot[o].replay()
+            self.ev_geo[o * R].record(sb)
             if wait:
                 cur.wait_event(self.ev_rot[j])
         elif wait:
