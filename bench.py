@@ -547,16 +547,24 @@ def main():
     # each replay is one full step -- this view's compositing, loss, backward and Adam on one stream, the
     # next view's geometry stages (the forward's first half) on the other -- with no host work inside
     elapsed_pg = float("inf")
+    pg_rot = None
     if graphed and os.environ.get("LSR_PIPELINE", "1") != "0":
         # N > 1: the bucket's all-reduce (RCCL) is launched between each set's backward and Adam graphs
+        # rotation (N = 1): R steps per stream-A graph (pipeline.py), R dividing the timed steps
+        rot = 1
+        if bucket is None:
+            want = int(os.environ.get("LSR_PG_ROT", "1"))
+            rot = max(r for r in range(1, want + 1) if args.steps % r == 0)
         pg = PipelinedGraphStep(lambda: render(cam, model, Pipe, bg, Opt, language_target=(gt, mask))["language_l1"],
-                                model.trainable(), optim, bucket=bucket)
+                                model.trainable(), optim, bucket=bucket, rotation=rot)
         pg.capture()
-        for _ in range(4):
+        pg_rot = rot
+        warm = rot * max(1, 4 // rot)
+        for _ in range(warm):
             pg.replay()
         torch.cuda.synchronize()
         if not pg.check():
-            for _ in range(2):
+            for _ in range(warm):
                 pg.replay()
             torch.cuda.synchronize()
         if world > 1:
@@ -695,6 +703,7 @@ def main():
                       "pipelined_graph": "HIP graphs on two streams: this view's compositing + loss, backward and "
                                          "Adam on one, the next view's geometry (forward split in two calls) on "
                                          "the other"}[best],
+        "pipelined_graph_rotation": pg_rot,
         "ms_per_step_forms": {n: (round(1000.0 * v / args.steps, 4) if v < 1e29 else None) for n, v in times.items()},
         "ms_per_step_all_gradients": round(1000.0 * elapsed_all / args.steps, 4),
         "ms_forward_only": round(1000.0 * elapsed_fwd / args.steps, 4),
