@@ -50,8 +50,10 @@ def run(mode, steps=30):
                                                      language_target=(gt, mask))["language_l1"],
                                 [model._language_feature], optim).capture()
 
+        wait = os.environ.get("LSR_TRACE_NOWAIT", "0") != "1"
+
         def step():
-            pg.replay()
+            pg.replay(wait=wait)
     else:
         def step():
             fwd_bwd()
