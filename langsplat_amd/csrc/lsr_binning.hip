@@ -777,12 +777,13 @@ __device__ __forceinline__ uint32_t scan256(uint32_t v, uint32_t* wsum)
     return before + x - v;
 }
 
-// One stable pass of the LDS sort: the values val[] (kBucketRounds per thread, wave w holding
-// positions [w R 64, (w + 1) R 64) round by round) are placed by digit dig[] into out.  Ranks: per
+// One stable pass of the LDS sort: the values val[] (R <= kBucketRounds per thread, wave w holding
+// positions [w R 64, (w + 1) R 64) round by round; R = the rounds a bucket of nb keys needs, so a
+// bucket half the capacity spreads over every wave in half the rounds) are placed by digit dig[] into out.  Ranks: per
 // wave, round by round (ballot match + the wave's running digit counts); then per digit the wave
 // offsets and the digit starts.
 __device__ void bucket_rank_scatter(BucketLds& L, const uint32_t (&dig)[kBucketRounds],
-                                    const uint32_t (&val)[kBucketRounds], int nb, int nbits, uint32_t* out)
+                                    const uint32_t (&val)[kBucketRounds], int nb, int nbits, uint32_t* out, int R)
 {
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
     for (int i = t; i < kBucketWaves * 256; i += kBucketThreads) (&L.wcnt[0][0])[i] = 0;
@@ -790,7 +791,8 @@ __device__ void bucket_rank_scatter(BucketLds& L, const uint32_t (&dig)[kBucketR
     uint32_t rank[kBucketRounds];
 #pragma unroll
     for (int r = 0; r < kBucketRounds; r++) {
-        const bool valid = (w * kBucketRounds + r) * 64 + lane < nb;
+        if (r >= R) break;  // workgroup-uniform: the rounds in use
+        const bool valid = (w * R + r) * 64 + lane < nb;
         const uint64_t peers = match_digit(dig[r], valid, nbits);
         const uint32_t rr = (uint32_t)__popcll(peers & lanemask_lt());
         const uint32_t c = L.wcnt[w][dig[r]];
@@ -810,8 +812,10 @@ __device__ void bucket_rank_scatter(BucketLds& L, const uint32_t (&dig)[kBucketR
     if (t < 256) L.dstart[t] = ex;
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < kBucketRounds; r++)
-        if ((w * kBucketRounds + r) * 64 + lane < nb) out[L.dstart[dig[r]] + L.wcnt[w][dig[r]] + rank[r]] = val[r];
+    for (int r = 0; r < kBucketRounds; r++) {
+        if (r >= R) break;
+        if ((w * R + r) * 64 + lane < nb) out[L.dstart[dig[r]] + L.wcnt[w][dig[r]] + rank[r]] = val[r];
+    }
     __syncthreads();
 }
 
@@ -965,18 +969,29 @@ __device__ uint32_t bucket_entry_base(const BucketEmit& em, int d, const uint32_
     if (t < 64) {
         uint32_t part = 0, spins = 0;
         bool ok = true;
-        for (int b0 = 0; b0 < d && ok; b0 += 64) {
-            const int b = b0 + t;
-            uint64_t w = b < d ? __hip_atomic_load(&em.status[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kFlagAgg;
-            while (em.spin_limit == 0u || __ballot((w >> 62) == 0ull) != 0ull) {
+        // every predecessor's word requested at once (up to 4 per lane: one memory round trip when
+        // they are all published, instead of one per 64 predecessors), then the missing ones polled
+        constexpr int kPer = 256 / 64;
+        uint64_t w[kPer];
+#pragma unroll
+        for (int k = 0; k < kPer; k++) {
+            const int b = k * 64 + t;
+            w[k] = b < d ? __hip_atomic_load(&em.status[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kFlagAgg;
+        }
+#pragma unroll
+        for (int k = 0; k < kPer; k++) {
+            if (k * 64 >= d || !ok) break;  // wave-uniform
+            const int b = k * 64 + t;
+            while (em.spin_limit == 0u || __ballot((w[k] >> 62) == 0ull) != 0ull) {
                 if (em.spin_limit == 0u || ++spins > em.spin_limit) {
                     ok = false;
                     break;
                 }
                 __builtin_amdgcn_s_sleep(1);
-                if ((w >> 62) == 0ull) w = __hip_atomic_load(&em.status[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if ((w[k] >> 62) == 0ull)
+                    w[k] = __hip_atomic_load(&em.status[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
-            part += (uint32_t)w;
+            part += (uint32_t)w[k];
         }
         part = wave_sum(part);
         if (t == 0) {
@@ -1050,15 +1065,21 @@ void k_depth_bucket_sort(
     BucketLds& L = *reinterpret_cast<BucketLds*>(s_bucket_raw);
     const int t = threadIdx.x;
     int d = (int)blockIdx.x;
+    // every bucket's start from the scanned [bucket][block] histogram, loaded while the ticket is
+    // taken (the range no longer waits behind the ticket's round trip)
+    __shared__ uint32_t s_start[257];
+    if (t < 256) s_start[t] = hist_scan[(size_t)t * nblk];
+    if (t == 256) s_start[256] = (uint32_t)n;
     if (em.keys) {  // fused emission: buckets by ticket (a waiting workgroup's predecessors run)
         __shared__ int s_d;
         if (t == 0) s_d = (int)atomicAdd(reinterpret_cast<uint32_t*>(em.status + 256), 1u);
         __syncthreads();
         d = s_d;
+    } else {
+        __syncthreads();
     }
-    // bucket range from the scanned [bucket][block] histogram
-    const uint32_t start = hist_scan[(size_t)d * nblk];
-    const uint32_t end = d < 255 ? hist_scan[(size_t)(d + 1) * nblk] : (uint32_t)n;
+    const uint32_t start = s_start[d];
+    const uint32_t end = s_start[d + 1];
     const int nb = (int)(end - start);
     guard.nb = nb;
     if (nb <= 0) {  // no key in this depth interval
@@ -1070,12 +1091,14 @@ void k_depth_bucket_sort(
     const int w = t >> 6, lane = t & 63;
     uint32_t kr[kBucketRounds];
     uint32_t klo = 0xFFFFFFFFu, khi = 0u;
+    // rounds of 64 keys per wave in use: every wave holds a share of the bucket
+    const int R = (nb + kBucketThreads - 1) / kBucketThreads;
     if (nb <= kBucketCap) {
 #pragma unroll
         for (int r = 0; r < kBucketRounds; r++) {
-            const int idx = (w * kBucketRounds + r) * 64 + lane;
-            kr[r] = idx < nb ? keys[start + idx] : 0u;
-            if (idx < nb) {
+            const int idx = (w * R + r) * 64 + lane;
+            kr[r] = r < R && idx < nb ? keys[start + idx] : 0u;
+            if (r < R && idx < nb) {
                 klo = min(klo, kr[r]);
                 khi = max(khi, kr[r]);
             }
@@ -1114,10 +1137,10 @@ void k_depth_bucket_sort(
         // the packed word {bits 8.., local index} as the value
 #pragma unroll
         for (int r = 0; r < kBucketRounds; r++) {
-            const int idx = (w * kBucketRounds + r) * 64 + lane;
-            const uint32_t k = idx < nb ? kr[r] - klo : 0u;
+            const int idx = (w * R + r) * 64 + lane;
+            const uint32_t k = r < R && idx < nb ? kr[r] - klo : 0u;
             dig[r] = k & 0xFFu;
-            val[r] = ((k >> 8) << kIdxBits) | (uint32_t)idx;
+            val[r] = ((k >> 8) << kIdxBits) | (uint32_t)(idx & (kBucketCap - 1));
         }
         if (timeline) {  // measurement only: the keys' arrival
             __builtin_amdgcn_s_waitcnt(0);
@@ -1125,24 +1148,24 @@ void k_depth_bucket_sort(
         }
         int src = 0;
         if (lowbits > 0) {
-            bucket_rank_scatter(L, dig, val, nb, min(8, lowbits), L.w[0]);
+            bucket_rank_scatter(L, dig, val, nb, min(8, lowbits), L.w[0], R);
             guard.mark(0);
         } else {
 #pragma unroll
             for (int r = 0; r < kBucketRounds; r++) {
-                const int idx = (w * kBucketRounds + r) * 64 + lane;
-                if (idx < nb) L.w[0][idx] = val[r];
+                const int idx = (w * R + r) * 64 + lane;
+                if (r < R && idx < nb) L.w[0][idx] = val[r];
             }
             __syncthreads();
         }
         for (int sh = 8; sh < lowbits; sh += 8) {  // later passes: the digit from the packed word
 #pragma unroll
             for (int r = 0; r < kBucketRounds; r++) {
-                const int idx = (w * kBucketRounds + r) * 64 + lane;
-                val[r] = idx < nb ? L.w[src][idx] : 0u;
+                const int idx = (w * R + r) * 64 + lane;
+                val[r] = r < R && idx < nb ? L.w[src][idx] : 0u;
                 dig[r] = (val[r] >> (kIdxBits + sh - 8)) & 0xFFu;
             }
-            bucket_rank_scatter(L, dig, val, nb, min(8, lowbits - sh), L.w[src ^ 1]);
+            bucket_rank_scatter(L, dig, val, nb, min(8, lowbits - sh), L.w[src ^ 1], R);
             src ^= 1;
         }
         guard.mark(1);
@@ -1151,13 +1174,14 @@ void k_depth_bucket_sort(
         // staged in the two free 32 KB LDS buffers and gathered there through the local indices
         // (lidx).  rect_ranked is permuted in place: all of its loads have landed in LDS before the
         // barriers that precede the stores.  The entry counts then go through LDS so that each thread
-        // scans a contiguous run of kBucketRounds of them.
+        // scans a contiguous run of R of them.
         uint32_t* S = L.w[src];
         uint32_t* X = L.w[src ^ 1];
         uint32_t lidx[kBucketRounds], id[kBucketRounds], ry[kBucketRounds];
         uint2 rc[kBucketRounds];
 #pragma unroll
         for (int r = 0; r < kBucketRounds; r++) {
+            if (r >= R) break;  // workgroup-uniform
             const int i = t + r * kBucketThreads;
             lidx[r] = i < nb ? S[i] & (kBucketCap - 1u) : 0u;
             id[r] = i < nb ? ids[start + i] : 0u;
@@ -1166,6 +1190,7 @@ void k_depth_bucket_sort(
         __syncthreads();  // S read by everyone
 #pragma unroll
         for (int r = 0; r < kBucketRounds; r++) {
+            if (r >= R) break;  // workgroup-uniform
             const int i = t + r * kBucketThreads;
             if (i < nb) {
                 X[i] = id[r];
@@ -1176,21 +1201,27 @@ void k_depth_bucket_sort(
         __syncthreads();
 #pragma unroll
         for (int r = 0; r < kBucketRounds; r++) {
+            if (r >= R) break;
             id[r] = X[lidx[r]];
             rc[r].x = S[lidx[r]];
         }
         __syncthreads();
 #pragma unroll
         for (int r = 0; r < kBucketRounds; r++) {
+            if (r >= R) break;  // workgroup-uniform
             const int i = t + r * kBucketThreads;
             if (i < nb) X[i] = ry[r];
         }
         __syncthreads();
 #pragma unroll
-        for (int r = 0; r < kBucketRounds; r++) rc[r].y = X[lidx[r]];
+        for (int r = 0; r < kBucketRounds; r++) {
+            if (r >= R) break;
+            rc[r].y = X[lidx[r]];
+        }
         __syncthreads();
 #pragma unroll
         for (int r = 0; r < kBucketRounds; r++) {
+            if (r >= R) break;  // workgroup-uniform
             const int i = t + r * kBucketThreads;
             if (i < nb) {
                 if (!em.keys) {  // fused emission: no later kernel reads the depth-order arrays
@@ -1206,7 +1237,8 @@ void k_depth_bucket_sort(
         uint32_t c[kBucketRounds], run = 0;
 #pragma unroll
         for (int k = 0; k < kBucketRounds; k++) {
-            const int j = kBucketRounds * t + k;
+            if (k >= R) break;
+            const int j = R * t + k;
             c[k] = j < nb ? X[j] : 0u;
             run += c[k];
         }
@@ -1214,7 +1246,8 @@ void k_depth_bucket_sort(
         uint32_t acc = scan1024(run, L.wsum, &tot);
 #pragma unroll
         for (int k = 0; k < kBucketRounds; k++) {
-            const int j = kBucketRounds * t + k;
+            if (k >= R) break;
+            const int j = R * t + k;
             if (j < nb) X[j] = acc;
             acc += c[k];
         }
@@ -1223,6 +1256,7 @@ void k_depth_bucket_sort(
         if (!em.keys) {
 #pragma unroll
             for (int r = 0; r < kBucketRounds; r++) {
+                if (r >= R) break;
                 const int i = t + r * kBucketThreads;
                 if (i < nb) local_off[start + i] = X[i];
             }
@@ -1247,6 +1281,7 @@ void k_depth_bucket_sort(
         }
 #pragma unroll
         for (int r = 0; r < kBucketRounds; r++) {
+            if (r >= R) break;  // workgroup-uniform
             const int i = t + r * kBucketThreads;
             if (i < nb) emit_entries(em, ebase + X[i], id[r], rc[r], hl, b0, nbl);
         }
