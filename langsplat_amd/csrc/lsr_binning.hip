@@ -1025,6 +1025,9 @@ __device__ uint32_t bucket_entry_base(const BucketEmit& em, int d, const uint32_
 // which the first pass, all passes and the output gathers ended.
 __device__ uint32_t g_bucket_timeline[256 * 8];
 
+#ifndef LSR_BUCKET_MARK_BASE  // measurement knob: the timeline's 4th mark when the entry base is known
+#define LSR_BUCKET_MARK_BASE 0
+#endif
 #ifndef LSR_BUCKET_WAVES  // one bucket workgroup per CU: no need to squeeze registers for two
 #define LSR_BUCKET_WAVES 4
 #endif
@@ -1142,7 +1145,7 @@ void k_depth_bucket_sort(
             dig[r] = k & 0xFFu;
             val[r] = ((k >> 8) << kIdxBits) | (uint32_t)(idx & (kBucketCap - 1));
         }
-        if (timeline) {  // measurement only: the keys' arrival
+        if (timeline && !LSR_BUCKET_MARK_BASE) {  // measurement only: the keys' arrival
             __builtin_amdgcn_s_waitcnt(0);
             guard.mark(3);
         }
@@ -1268,6 +1271,7 @@ void k_depth_bucket_sort(
         // workgroup's critical path instead)
         publish_bucket_total(em, d, tot);
         const uint32_t ebase = bucket_entry_base(em, d, kxf, L.wsum);
+        if (LSR_BUCKET_MARK_BASE) guard.mark(3);  // measurement only: the entry base known
         if ((uint64_t)ebase + tot > (uint64_t)em.cap) return;  // over capacity: the host re-runs unfused
         // the bucket's entries [ebase, ebase + tot) meet nbl blocks of the super-tile pass: their
         // [super-tile][block] counts in LDS (the free buffer S), then one atomic per non-zero count
