@@ -741,15 +741,20 @@ __device__ __forceinline__ uint64_t transpose64(uint64_t x)
 // dense far beyond the average) is sorted by its workgroup in global memory, 1024 keys at a time.
 constexpr int kBucketThreads = 1024;
 constexpr int kBucketWaves = kBucketThreads / 64;
-constexpr int kBucketCap = 8192;
+#ifndef LSR_BUCKET_CAP  // keys a bucket sorts in LDS (a multiple of 1024 up to 8192; measurement knob):
+#define LSR_BUCKET_CAP 8192  // the LDS a bucket workgroup takes, 8 B per key + 8 KB, sets how many
+#endif                       // render workgroups can share its CU while it runs
+constexpr int kBucketCap = LSR_BUCKET_CAP;
+static_assert(kBucketCap % 1024 == 0 && kBucketCap <= 8192, "bucket capacity");
 constexpr int kBucketRounds = kBucketCap / kBucketThreads;  // rounds of 64 keys per wave
 constexpr int64_t kMsdMaxKeys = 2000000;                    // above: expected buckets exceed LDS
 
 // A bucket in LDS is kBucketCap packed words {key bits not yet ranked, local index (13 bits)}:
 // pass 0 ranks on the low 8 key bits held in registers and packs the rest (<= 16 bits) above the
 // index, so the two ping-pong buffers take 64 KB and two workgroups share a CU.
-constexpr int kIdxBits = 13;  // local index within a bucket (kBucketCap = 1 << kIdxBits)
-static_assert((1 << kIdxBits) == kBucketCap, "local index width");
+constexpr int kIdxBits = 13;  // local index within a bucket (kBucketCap <= 1 << kIdxBits)
+constexpr uint32_t kIdxMask = (1u << kIdxBits) - 1u;
+static_assert((1 << kIdxBits) >= kBucketCap, "local index width");
 struct BucketLds {
     uint32_t w[2][kBucketCap];
     uint16_t wcnt[kBucketWaves][256];  // per wave: running digit counts, then the wave's offset in the digit
@@ -1143,7 +1148,7 @@ void k_depth_bucket_sort(
             const int idx = (w * R + r) * 64 + lane;
             const uint32_t k = r < R && idx < nb ? kr[r] - klo : 0u;
             dig[r] = k & 0xFFu;
-            val[r] = ((k >> 8) << kIdxBits) | (uint32_t)(idx & (kBucketCap - 1));
+            val[r] = ((k >> 8) << kIdxBits) | ((uint32_t)idx & kIdxMask);
         }
         if (timeline && !LSR_BUCKET_MARK_BASE) {  // measurement only: the keys' arrival
             __builtin_amdgcn_s_waitcnt(0);
@@ -1186,7 +1191,7 @@ void k_depth_bucket_sort(
         for (int r = 0; r < kBucketRounds; r++) {
             if (r >= R) break;  // workgroup-uniform
             const int i = t + r * kBucketThreads;
-            lidx[r] = i < nb ? S[i] & (kBucketCap - 1u) : 0u;
+            lidx[r] = i < nb ? S[i] & kIdxMask : 0u;
             id[r] = i < nb ? ids[start + i] : 0u;
             rc[r] = i < nb ? rect_ranked[start + i] : make_uint2(0u, 0u);
         }

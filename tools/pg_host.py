@@ -38,7 +38,8 @@ def main():
         pg.replay(wait=wait)
     pg.synchronize()
     torch.cuda.synchronize()
-    for rep in range(3):
+    walls = []
+    for rep in range(int(os.environ.get("PG_HOST_REPS", "3"))):
         t0 = time.perf_counter()
         for _ in range(steps):
             pg.replay(wait=wait)
@@ -48,6 +49,9 @@ def main():
         t2 = time.perf_counter()
         print(f"pg_host rep {rep}: host enqueue {1e3 * (t1 - t0) / steps:.4f} ms/replay, "
               f"wall {1e3 * (t2 - t0) / steps:.4f} ms/step", flush=True)
+        walls.append(1e3 * (t2 - t0) / steps)
+    walls.sort()
+    print(f"pg_host summary: min {walls[0]:.4f} median {walls[len(walls) // 2]:.4f} ms/step", flush=True)
 
 
 if __name__ == "__main__":
