@@ -462,6 +462,12 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
     pp.counters = counters;
     pp.zero = reinterpret_cast<uint32_t*>(geom + L.scan_regions);
     pp.zero_words = (int)L.zero_words;  // depth-sort scan status and the fused loss's words
+    // placed emission (the MSD depth order's fused emission at super-tile-major positions)
+    const bool placed = !depth_order_uses_pass_count(P) && placed_emit(L, a->phase == LSR_PHASE_GEOMETRY);
+    if (placed) {  // the bucket sort's count table
+        pp.zero2 = reinterpret_cast<uint32_t*>(geom + L.sup_status);
+        pp.zero2_words = (int)kSupWords;
+    }
     pp.raw = a->raw;
     pp.shs_rest = a->shs_rest;
     pp.partial = reinterpret_cast<uint4*>(geom + L.pre_partial);
@@ -512,13 +518,13 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
                                         fwd_flags, (uint32_t)R_cap, (uint32_t)E_cap, a->overflow, passes, stream),
                 "publish counters");
         LSR_TRY(launch_depth_order(P, fused ? 4 : passes, L, geom, counters, &hb->stall, stream, debug, fused,
-                                   (uint32_t)E_cap),
+                                   (uint32_t)E_cap, placed),
                 "depth order");
         L = make_layout(P, W, H, R_cap, E_cap);
         char* binning = static_cast<char*>(alloc(user, LSR_BUF_BINNING, L.binning_bytes));
         if (!binning) return fail(LSR_ERR_ALLOC, "lsr_forward: binning buffer allocation failed");
         LSR_TRY(launch_binning(P, R_cap, L, geom, image, binning, &hb->stall, stream, debug, fused,
-                               DevCount{counters + kCntSuper, counters + kCntOverflow}),
+                               DevCount{counters + kCntSuper, counters + kCntOverflow}, placed),
                 "binning");
         *num_rendered = R_cap;
         if (a->phase == LSR_PHASE_GEOMETRY) return LSR_OK;
@@ -533,7 +539,8 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
     // MSD path: the bucket sort also emits the super-tile entries (into geometry arrays of fixed
     // capacity, so no host value is needed); used below when they fitted
     const bool fused_emit = !depth_order_uses_pass_count(P) && fused_emit_enabled();
-    LSR_TRY(launch_depth_order(P, guess, L, geom, counters, &hb->stall, stream, debug, fused_emit), "depth order");
+    LSR_TRY(launch_depth_order(P, guess, L, geom, counters, &hb->stall, stream, debug, fused_emit, 0, placed),
+            "depth order");
     hm.mark();
     // the binning buffer from the last forward's size while the GPU works (the allocator callback
     // is host work that would otherwise sit between the wait and the binning launches)
@@ -581,7 +588,9 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
     hb->hint_W = W;
     hb->hint_H = H;
     hb->binning_hint = L.binning_bytes + L.binning_bytes / 8;  // 12.5 % headroom for the next view
-    LSR_TRY(launch_binning(P, R, L, geom, image, binning, &hb->stall, stream, debug, emitted), "binning");
+    LSR_TRY(launch_binning(P, R, L, geom, image, binning, &hb->stall, stream, debug, emitted, DevCount{nullptr, nullptr},
+                           placed),
+            "binning");
     if (deferred) LSR_TRY(wait_and_fill_language(a, L, geom, stream), "fill language");
     hm.mark();
     const int32_t rc = render_forward_and_finish(s, a, L, geom, image, binning, hb, stream, debug);

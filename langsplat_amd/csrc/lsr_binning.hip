@@ -438,14 +438,20 @@ __device__ __forceinline__ void zero_words_strided(const ZeroList& z)
         for (int w = r; w < z.n[k]; w += stride) z.p[k][w] = 0u;
 }
 
+// srect (MSD pass with placed emission): the keys' tile rectangles by index; the block's super-tile
+// entry counts then also go to rows 256 + s (s < supers) of hist, so the scan that yields the
+// bucket starts also yields every super-tile's base in the super-tile-major entry list (+ n).
 template <int kItems>
 __global__ __launch_bounds__(kRadixThreads) void k_radix_hist(const uint32_t* __restrict__ keys, int n, int shift,
                                                               int nbits, uint32_t* __restrict__ hist, int nblk,
                                                               const uint32_t* __restrict__ kxf, int remap, int msd,
-                                                              ZeroList zero, DevCount dc)
+                                                              ZeroList zero, DevCount dc,
+                                                              const uint2* __restrict__ srect = nullptr,
+                                                              int supers = 0, int sgx = 0)
 {
     constexpr int kWaves = kRadixThreads / 64;
     __shared__ uint32_t wcnt[kWaves][256];
+    __shared__ uint32_t scnt[256];
     zero_words_strided(zero);
     if (dc.abort && *dc.abort) return;
     if (dc.n) n = min(n, (int)*dc.n);
@@ -460,15 +466,18 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_hist(const uint32_t* __
     const uint32_t mask = (1u << nbits) - 1u;
 #pragma unroll
     for (int w = 0; w < kWaves; w++) wcnt[w][t] = 0;
+    scnt[t] = 0;
     __syncthreads();
     const int base = blk * kRadixThreads * kItems + wave * 64 * kItems;
     uint32_t d[kItems];
     bool valid[kItems];
+    uint2 rc[kItems];
 #pragma unroll
     for (int it = 0; it < kItems; it++) {
         const int idx = base + it * 64 + lane;
         valid[it] = idx < n;
         uint32_t k = valid[it] ? keys[idx] : 0u;
+        rc[it] = srect && valid[it] ? srect[idx] : make_uint2(0u, 0u);
         if (kxf) k = key_xf(k, kxf);
         d[it] = valid[it] ? (msd ? msd_bucket(k, mm) : (k >> shift) & mask) : 0u;
     }
@@ -477,6 +486,16 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_hist(const uint32_t* __
         const uint64_t peers = match_digit(d[it], valid[it], nbits);
         if (valid[it] && (peers & lanemask_lt()) == 0) wcnt[wave][d[it]] += (uint32_t)__popcll(peers);
     }
+    if (srect) {
+#pragma unroll
+        for (int it = 0; it < kItems; it++) {
+            if (rc[it].x == rc[it].y) continue;  // culled or past n: no entries
+            int sx0, sy0, sx1, sy1;
+            super_rect(rc[it], sx0, sy0, sx1, sy1);
+            for (int y = sy0; y < sy1; y++)
+                for (int x = sx0; x < sx1; x++) atomicAdd(&scnt[y * sgx + x], 1u);
+        }
+    }
     __syncthreads();
     if (t <= (int)mask) {
         uint32_t c = 0;
@@ -484,6 +503,7 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_hist(const uint32_t* __
         for (int w = 0; w < kWaves; w++) c += wcnt[w][t];
         hist[t * nblk + blk] = c;
     }
+    if (srect && t < supers) hist[(size_t)(256 + t) * nblk + blk] = scnt[t];
 }
 
 // Stable scatter of one block's tile.  Ranks: per wave, round by round (ballot match + the wave's
@@ -761,6 +781,8 @@ struct BucketLds {
     uint32_t dstart[256];              // digit starts (LDS passes) / running digit bases (global passes)
     uint32_t ctot[256];                // global passes: the chunk's digit totals
     uint32_t wsum[kBucketWaves];
+    uint32_t scnt[256];                // placed emission: the bucket's entries per super-tile
+    uint32_t run[256];                 // placed emission: per super-tile, the next entry's position
 };
 constexpr size_t kBucketLdsBytes = sizeof(BucketLds);
 
@@ -782,20 +804,18 @@ __device__ __forceinline__ uint32_t scan256(uint32_t v, uint32_t* wsum)
     return before + x - v;
 }
 
-// One stable pass of the LDS sort: the values val[] (R <= kBucketRounds per thread, wave w holding
-// positions [w R 64, (w + 1) R 64) round by round; R = the rounds a bucket of nb keys needs, so a
-// bucket half the capacity spreads over every wave in half the rounds) are placed by digit dig[] into out.  Ranks: per
-// wave, round by round (ballot match + the wave's running digit counts); then per digit the wave
-// offsets and the digit starts.
-__device__ void bucket_rank_scatter(BucketLds& L, const uint32_t (&dig)[kBucketRounds],
-                                    const uint32_t (&val)[kBucketRounds], int nb, int nbits, uint32_t* out, int R)
+// Ranks of the digits dig[] (R <= kRounds per thread, wave w holding positions [w R 64,
+// (w + 1) R 64) round by round): rank[r] within the wave's digit, and in LDS the digit starts
+// (L.dstart) and each wave's offset in its digit (L.wcnt); position = dstart + wcnt + rank.
+template <int kRounds>
+__device__ __forceinline__ void rank_digits(BucketLds& L, const uint32_t (&dig)[kRounds], int nb, int nbits, int R,
+                            uint32_t (&rank)[kRounds])
 {
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
     for (int i = t; i < kBucketWaves * 256; i += kBucketThreads) (&L.wcnt[0][0])[i] = 0;
     __syncthreads();
-    uint32_t rank[kBucketRounds];
 #pragma unroll
-    for (int r = 0; r < kBucketRounds; r++) {
+    for (int r = 0; r < kRounds; r++) {
         if (r >= R) break;  // workgroup-uniform: the rounds in use
         const bool valid = (w * R + r) * 64 + lane < nb;
         const uint64_t peers = match_digit(dig[r], valid, nbits);
@@ -816,8 +836,22 @@ __device__ void bucket_rank_scatter(BucketLds& L, const uint32_t (&dig)[kBucketR
     const uint32_t ex = scan256(tot, L.wsum);
     if (t < 256) L.dstart[t] = ex;
     __syncthreads();
+}
+
+// One stable pass of the LDS sort: the values val[] (R <= kBucketRounds per thread, wave w holding
+// positions [w R 64, (w + 1) R 64) round by round; R = the rounds a bucket of nb keys needs, so a
+// bucket half the capacity spreads over every wave in half the rounds) are placed by digit dig[] into out.  Ranks: per
+// wave, round by round (ballot match + the wave's running digit counts); then per digit the wave
+// offsets and the digit starts.
+template <int kRounds = kBucketRounds>
+__device__ __forceinline__ void bucket_rank_scatter(BucketLds& L, const uint32_t (&dig)[kRounds], const uint32_t (&val)[kRounds],
+                                    int nb, int nbits, uint32_t* out, int R)
+{
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    uint32_t rank[kRounds];
+    rank_digits(L, dig, nb, nbits, R, rank);
 #pragma unroll
-    for (int r = 0; r < kBucketRounds; r++) {
+    for (int r = 0; r < kRounds; r++) {
         if (r >= R) break;
         if ((w * R + r) * 64 + lane < nb) out[L.dstart[dig[r]] + L.wcnt[w][dig[r]] + rank[r]] = val[r];
     }
@@ -827,7 +861,7 @@ __device__ void bucket_rank_scatter(BucketLds& L, const uint32_t (&dig)[kBucketR
 // Bucket too large for LDS: the same stable passes through global memory, 1024 keys at a time
 // (digit bases from a histogram of the whole bucket, advanced chunk by chunk).  (k0, v0) holds the
 // bucket; (k1, v1) is scratch of the same size.  Returns the buffer index holding the result.
-__device__ int bucket_global_sort(BucketLds& L, uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, int nb,
+__device__ __forceinline__ int bucket_global_sort(BucketLds& L, uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, int nb,
                                   int lowbits)
 {
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
@@ -934,7 +968,20 @@ struct BucketEmit {
     uint32_t* shist;
     int hstride;
     int supers;
+    // placed emission (sup_status != null, supers <= 256): every entry is written at its position
+    // in the super-tile-major list the binning reads (super-tile, then depth order), so no
+    // super-tile radix pass follows.  The k-th entry of super-tile s in bucket d goes to base(s)
+    // (the MSD histogram's super-tile rows, scanned with its digit rows) + the entries of s in
+    // buckets 0..d-1 (the sum of their published counts) + k.
+    uint32_t* sup_status;       // [super-tile][bucket] {kSupAgg | count}, cleared by preprocess
+    const uint32_t* sup_base;   // sup_base[s * sup_stride] = P + base(s)
+    int sup_stride;
+    const uint32_t* etotal;     // counters[kCntSuper]: all entries of the view (no emission above cap)
+    int sbits;                  // super-tile id bits
+    const uint32_t* kxf;        // stall fallback: the bucket map
 };
+constexpr uint32_t kSupAgg = 1u << 30;  // sup_status: the flag of a published count
+constexpr uint32_t kSupVal = kSupAgg - 1u;
 static_assert(kSuperHistBlock == 4 * kRadixThreads, "super-tile pass blocks: k_radix_scatter<4> tiles");
 
 // Writes Gaussian g's entries from position o and counts them into the super-tile histogram:
@@ -966,7 +1013,7 @@ __device__ __forceinline__ void publish_bucket_total(const BucketEmit& em, int d
 }
 
 // The entry base of bucket d: the sum of the totals of buckets 0..d-1 (every thread calls it).
-__device__ uint32_t bucket_entry_base(const BucketEmit& em, int d, const uint32_t* kxf, uint32_t* wsum)
+__device__ __forceinline__ uint32_t bucket_entry_base(const BucketEmit& em, int d, const uint32_t* kxf, uint32_t* wsum)
 {
     __shared__ uint32_t s_base;
     __shared__ int s_ok;
@@ -1017,6 +1064,229 @@ __device__ uint32_t bucket_entry_base(const BucketEmit& em, int d, const uint32_
     return tot;
 }
 
+// Placed emission's counts, in em.sup_status (cleared by preprocess): [super-tile][bucket] words
+// {kSupAgg | count} (row stride 256), then per group of 16 buckets [group][super-tile] words
+// {kSupAgg | the group's count}, then 16 group arrival counters.  Every bucket publishes its
+// counts as soon as its rectangles are loaded; the last of a group to arrive also publishes the
+// group's sums.  A bucket's prefix for super-tile s is then <= 15 group sums + <= 15 counts of
+// its own group (30 words, not d), read once the bucket is sorted, when they are long published.
+constexpr size_t kSupGroupOff = 256 * 256;                       // words: the group sums
+constexpr size_t kSupArriveOff = kSupGroupOff + 256 * (256 / kSupGroup);  // words: the counters
+static_assert(kSupArriveOff + 256 / kSupGroup == kSupWords, "placed emission's count words");
+
+__device__ __forceinline__ void publish_super_counts(const BucketLds& L, const BucketEmit& em, int d)
+{
+    const int t = threadIdx.x, g = d / kSupGroup;
+    __shared__ int s_last;
+    // relaxed atomics throughout (release / acquire at agent scope would write back / invalidate the
+    // L2 per operation): every word carries its own flag, and readers poll for it
+    if (t < em.supers)
+        __hip_atomic_store(&em.sup_status[(size_t)t * 256 + d], kSupAgg | L.scnt[t], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (t == 0)
+        s_last = __hip_atomic_fetch_add(&em.sup_status[kSupArriveOff + g], 1u, __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT) == kSupGroup - 1;
+    __syncthreads();
+    if (!s_last || t >= em.supers) return;
+    // the group's last arrival: every member has published (its flags are polled all the same)
+    uint32_t v[kSupGroup];
+#pragma unroll
+    for (int j = 0; j < kSupGroup; j++)
+        v[j] = __hip_atomic_load(&em.sup_status[(size_t)t * 256 + g * kSupGroup + j], __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t sum = 0;
+#pragma unroll
+    for (int j = 0; j < kSupGroup; j++) {
+        while (!(v[j] & kSupAgg))
+            v[j] = __hip_atomic_load(&em.sup_status[(size_t)t * 256 + g * kSupGroup + j], __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+        sum += v[j] & kSupVal;
+    }
+    __hip_atomic_store(&em.sup_status[kSupGroupOff + (size_t)g * 256 + t], kSupAgg | sum, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Adds to L.run[s] the entries of super-tile s in buckets 0..d-1 (s < S; every thread calls it):
+// the group sums below d's group and the counts of d's group members below d, one word per
+// thread and pair (s, j < 30) in flight at once; false when a wait passed the spin bound.
+__device__ __forceinline__ bool super_sum(BucketLds& L, const BucketEmit& em, int d)
+{
+    const int t = threadIdx.x;
+    const int g = d / kSupGroup, r = d - g * kSupGroup;
+    constexpr int kPer = 256 * 32 / kBucketThreads;  // (s, j) pairs per thread, j < 32
+    const int total = em.supers * 32;
+    uint32_t v[kPer];
+    int at[kPer];  // word index, -1: none
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+        const int f = k * kBucketThreads + t, sj = f >> 5, j = f & 31;
+        at[k] = -1;
+        v[k] = kSupAgg;
+        if (f < total) {
+            if (j < g)
+                at[k] = (int)(kSupGroupOff + (size_t)j * 256 + sj);
+            else if (j >= 16 && j - 16 < r)
+                at[k] = sj * 256 + g * kSupGroup + (j - 16);
+            if (at[k] >= 0)
+                v[k] = __hip_atomic_load(&em.sup_status[at[k]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    uint32_t spins = 0;
+    for (;;) {
+        bool wait = false;
+#pragma unroll
+        for (int k = 0; k < kPer; k++)
+            if (at[k] >= 0 && !(v[k] & kSupAgg)) {
+                wait = true;
+                v[k] = __hip_atomic_load(&em.sup_status[at[k]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        if (!__syncthreads_or(wait)) break;
+        if (em.spin_limit == 0u || ++spins > em.spin_limit) return false;  // workgroup-uniform
+        __builtin_amdgcn_s_sleep(1);
+    }
+#pragma unroll
+    for (int k = 0; k < kPer; k++)
+        if (at[k] >= 0 && (v[k] & kSupVal)) atomicAdd(&L.run[(k * kBucketThreads + t) >> 5], v[k] & kSupVal);
+    return true;
+}
+
+// Placed emission: the write cursors L.run[s] = base(s) (thread s holds it) + the entries of
+// super-tile s in buckets 0..d-1 (every thread calls it).  A sum that waited past the spin bound
+// is computed from the inputs instead (same values).
+__device__ __forceinline__ void super_cursors(BucketLds& L, const BucketEmit& em, int d, uint32_t base_s)
+{
+    const int t = threadIdx.x;
+    __shared__ int s_ok;
+    if (t < 256) L.run[t] = 0u;
+    __syncthreads();
+    const bool ok = super_sum(L, em, d);
+    if (t == 0) s_ok = ok ? 1 : 0;
+    __syncthreads();
+    if (!s_ok) {  // stalled: per super-tile, the entries of every Gaussian whose bucket is below d
+        if (t < 256) L.run[t] = 0u;
+        __syncthreads();
+        const MsdMap mm = msd_map(em.kxf);
+        for (int gg = t; gg < em.P; gg += kBucketThreads) {
+            const uint2 rc = em.rect[gg];
+            if (rc.x == rc.y || msd_bucket(key_xf(em.depth_key[gg], em.kxf), mm) >= (uint32_t)d) continue;
+            int sx0, sy0, sx1, sy1;
+            super_rect(rc, sx0, sy0, sx1, sy1);
+            for (int y = sy0; y < sy1; y++)
+                for (int x = sx0; x < sx1; x++) atomicAdd(&L.run[y * em.sgx + x], 1u);
+        }
+        __syncthreads();
+        if (t == 0) note_stall(em.stall);
+    }
+    if (t < em.supers) L.run[t] += base_s;
+    __syncthreads();
+}
+
+// the bucket's entries per super-tile, into L.scnt
+__device__ __forceinline__ void count_supers(BucketLds& L, const BucketEmit& em, uint2 rc)
+{
+    if (rc.x == rc.y) return;
+    int sx0, sy0, sx1, sy1;
+    super_rect(rc, sx0, sy0, sx1, sy1);
+    for (int y = sy0; y < sy1; y++)
+        for (int x = sx0; x < sx1; x++) atomicAdd(&L.scnt[y * em.sgx + x], 1u);
+}
+
+// Placed emission: a list of up to kBucketCap entries {key (L.w[0]), Gaussian id (L.w[1])} in
+// LDS, in the bucket's entry order (depth order; a Gaussian's super-tiles row by row).
+// list_entries writes the entries [e0, e0 + n) of this thread's Gaussians r (id gid[r],
+// rectangle rc[r], first entry off[r] in the bucket's order; ~0u: none) at position - e0.
+template <int kG>
+__device__ __forceinline__ void list_entries(BucketLds& L, const BucketEmit& em, const uint32_t (&gid)[kG], const uint2 (&rc)[kG],
+                             const uint32_t (&off)[kG], uint32_t e0, uint32_t n)
+{
+#pragma unroll
+    for (int r = 0; r < kG; r++) {
+        if (off[r] >= e0 + n || rc[r].x == rc[r].y) continue;  // none here / culled
+        int sx0, sy0, sx1, sy1;
+        super_rect(rc[r], sx0, sy0, sx1, sy1);
+        uint32_t e = off[r];
+        for (int y = sy0; y < sy1; y++)
+            for (int x = sx0; x < sx1; x++, e++)
+                if (e >= e0 && e < e0 + n) {
+                    L.w[0][e - e0] = entry_key(rc[r], x, y, em.sgx);
+                    L.w[1][e - e0] = gid[r];
+                }
+    }
+}
+
+// Reorders the n listed entries stably by super-tile id (the key's low 8 bits), in place, with the
+// sort's ballot ranking; leaves the chunk-local super-tile starts in L.dstart.
+__device__ __forceinline__ void rank_entries(BucketLds& L, const BucketEmit& em, int n)
+{
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+    const int R = (n + kBucketThreads - 1) / kBucketThreads;
+    uint32_t a[kBucketRounds], b[kBucketRounds], dig[kBucketRounds], rank[kBucketRounds];
+#pragma unroll
+    for (int r = 0; r < kBucketRounds; r++) {
+        if (r >= R) break;  // workgroup-uniform
+        const int p = (w * R + r) * 64 + lane;
+        a[r] = p < n ? L.w[0][p] : 0u;
+        b[r] = p < n ? L.w[1][p] : 0u;
+        dig[r] = a[r] & 0xFFu;
+    }
+    rank_digits(L, dig, n, em.sbits, R, rank);  // its barriers: every load above has landed
+#pragma unroll
+    for (int r = 0; r < kBucketRounds; r++) {
+        if (r >= R) break;
+        if ((w * R + r) * 64 + lane < n) {
+            const uint32_t pos = L.dstart[dig[r]] + L.wcnt[w][dig[r]] + rank[r];
+            L.w[0][pos] = a[r];
+            L.w[1][pos] = b[r];
+        }
+    }
+    __syncthreads();
+}
+
+// Writes the n ranked entries super-tile by super-tile from the cursors L.run[s] (consecutive
+// threads on consecutive positions) and advances each cursor by its super-tile's count.
+__device__ __forceinline__ void write_entries(BucketLds& L, const BucketEmit& em, uint32_t n)
+{
+    const int t = threadIdx.x;
+    for (uint32_t j = t; j < n; j += kBucketThreads) {
+        const uint32_t k = L.w[0][j];
+        const uint32_t s = k & 0xFFu;
+        const uint32_t o = L.run[s] + j - L.dstart[s];
+        em.keys[o] = k;
+        em.vals[o] = L.w[1][j];
+    }
+    __syncthreads();
+    if (t < 256) L.run[t] += (t < 255 ? L.dstart[t + 1] : n) - L.dstart[t];
+    __syncthreads();
+}
+
+// Placed emission from global memory (a bucket beyond LDS, or one with more entries than
+// kBucketCap): 1024 Gaussians at a time in depth order (ids rid[0, nb),
+// rectangles by id), their entries listed, ranked and written kBucketCap at a time.
+__device__ __forceinline__ void place_runs(BucketLds& L, const BucketEmit& em, const uint32_t* rid, int nb)
+{
+    const int t = threadIdx.x;
+    for (int c0 = 0; c0 < nb; c0 += kBucketThreads) {
+        const int i = c0 + t;
+        uint32_t gid[1] = {0u}, off[1] = {~0u};
+        uint2 rc[1] = {make_uint2(0u, 0u)};
+        if (i < nb) {
+            gid[0] = rid[i];
+            rc[0] = em.rect[gid[0]];
+        }
+        uint32_t m;
+        const uint32_t ex = scan1024(i < nb ? super_count(rc[0]) : 0u, L.wsum, &m);
+        if (i < nb) off[0] = ex;
+        for (uint32_t e0 = 0; e0 < m; e0 += kBucketCap) {
+            const uint32_t n = min((uint32_t)kBucketCap, m - e0);
+            list_entries(L, em, gid, rc, off, e0, n);
+            __syncthreads();
+            rank_entries(L, em, (int)n);
+            write_entries(L, em, n);
+        }
+    }
+}
+
 // One workgroup per bucket (top-digit value).  keys / ids: the MSD pass's output (transformed keys,
 // bucket-contiguous, id order inside a bucket; rect_ranked holds the rectangles in the same
 // layout); hist_scan: its scanned [digit][block] histogram, whose digit starts are the bucket
@@ -1031,6 +1301,7 @@ __device__ uint32_t bucket_entry_base(const BucketEmit& em, int d, const uint32_
 __device__ uint32_t g_bucket_timeline[256 * 8];
 
 #ifndef LSR_BUCKET_MARK_BASE  // measurement knob: the timeline's 4th mark when the entry base is known
+                              // (placed emission: when the entries are listed and ranked)
 #define LSR_BUCKET_MARK_BASE 0
 #endif
 #ifndef LSR_BUCKET_WAVES  // one bucket workgroup per CU: no need to squeeze registers for two
@@ -1049,11 +1320,11 @@ void k_depth_bucket_sort(
         uint64_t t0;
         int nb;
         uint32_t ph[4];
-        __device__ void mark(int i)
+        __device__ __forceinline__ void mark(int i)
         {
             if (on) ph[i] = (uint32_t)wall_clock64();
         }
-        __device__ ~TimelineGuard()
+        __device__ __forceinline__ ~TimelineGuard()
         {
             if (!on || threadIdx.x != 0) return;
             const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
@@ -1078,6 +1349,10 @@ void k_depth_bucket_sort(
     __shared__ uint32_t s_start[257];
     if (t < 256) s_start[t] = hist_scan[(size_t)t * nblk];
     if (t == 256) s_start[256] = (uint32_t)n;
+    // placed emission: on when the view's entries fit (block-uniform); base(s) loaded early
+    const bool placed = em.sup_status && *em.etotal <= em.cap;
+    const uint32_t base_s = placed && t < em.supers ? em.sup_base[(size_t)t * em.sup_stride] - (uint32_t)em.P : 0u;
+    if (t < 256) L.scnt[t] = 0u;
     if (em.keys) {  // fused emission: buckets by ticket (a waiting workgroup's predecessors run)
         __shared__ int s_d;
         if (t == 0) s_d = (int)atomicAdd(reinterpret_cast<uint32_t*>(em.status + 256), 1u);
@@ -1092,7 +1367,8 @@ void k_depth_bucket_sort(
     guard.nb = nb;
     if (nb <= 0) {  // no key in this depth interval
         if (t == 0) totals[d] = 0u;
-        publish_bucket_total(em, d, 0u);
+        if (placed) publish_super_counts(L, em, d);  // zeros (L.scnt cleared before the ticket's barrier)
+        if (!placed) publish_bucket_total(em, d, 0u);
         return;
     }
     // the bucket's own key range [lo, hi]: it sorts key - lo on the bits that span
@@ -1111,11 +1387,22 @@ void k_depth_bucket_sort(
                 khi = max(khi, kr[r]);
             }
         }
+        if (placed) {  // the bucket's entries per super-tile (rectangles in the keys' layout)
+            uint2 q[kBucketRounds];
+#pragma unroll
+            for (int r = 0; r < kBucketRounds; r++) {
+                const int idx = (w * R + r) * 64 + lane;
+                q[r] = r < R && idx < nb ? rect_ranked[start + idx] : make_uint2(0u, 0u);
+            }
+#pragma unroll
+            for (int r = 0; r < kBucketRounds; r++) count_supers(L, em, q[r]);
+        }
     } else {
         for (int i = t; i < nb; i += kBucketThreads) {
             const uint32_t k = keys[start + i];
             klo = min(klo, k);
             khi = max(khi, k);
+            if (placed) count_supers(L, em, rect_ranked[start + i]);
         }
     }
     {
@@ -1138,6 +1425,9 @@ void k_depth_bucket_sort(
     }
     const uint32_t span = khi - klo;
     const int lowbits = span ? 32 - __clz(span) : 0;
+    if (placed) publish_super_counts(L, em, d);  // counts completed by the barrier above
+    const uint32_t* place_rid = nullptr;  // placed tail: ids in depth order, and the entry total
+    uint32_t place_etot = 0;
     // the LDS sort packs {key bits 8.., local index} in one word: at most 27 key bits
     if (nb <= kBucketCap && lowbits <= 32 - kIdxBits + 8) {
         uint32_t dig[kBucketRounds], val[kBucketRounds];
@@ -1261,6 +1551,35 @@ void k_depth_bucket_sort(
         }
         if (t == 0) totals[d] = tot;
         __syncthreads();
+        if (placed) {
+            uint32_t off[kBucketRounds];
+#pragma unroll
+            for (int r = 0; r < kBucketRounds; r++) {
+                const int i = t + r * kBucketThreads;
+                off[r] = r < R && i < nb ? X[i] : ~0u;
+            }
+            __syncthreads();  // X read: both buffers now hold the entry list
+            if (tot <= (uint32_t)kBucketCap) {
+                list_entries(L, em, id, rc, off, 0u, tot);
+                __syncthreads();
+                rank_entries(L, em, (int)tot);
+                if (LSR_BUCKET_MARK_BASE) guard.mark(3);  // measurement only: listed and ranked
+                super_cursors(L, em, d, base_s);
+                write_entries(L, em, tot);
+                return;
+            }
+            // more entries than one list: the Gaussians' ids in depth order through global memory
+            // (the placed tail below, shared with the global path)
+#pragma unroll
+            for (int r = 0; r < kBucketRounds; r++) {
+                if (r >= R) break;
+                const int i = t + r * kBucketThreads;
+                if (i < nb) sorted_ids[start + i] = id[r];
+            }
+            place_rid = sorted_ids + start;
+            place_etot = tot;
+            goto placed_tail;
+        }
         if (!em.keys) {
 #pragma unroll
             for (int r = 0; r < kBucketRounds; r++) {
@@ -1303,19 +1622,24 @@ void k_depth_bucket_sort(
         }
         return;
     }
-    // beyond LDS: global passes between (keys, ids) and (scratch_k, sorted_ids) over the bucket
+    {  // beyond LDS: global passes between (keys, ids) and (scratch_k, sorted_ids) over the bucket
     uint32_t etot = 0;
     if (em.keys) {  // the bucket's entry total first (bucket layout: any order gives the same sum)
         uint32_t part = 0;
         for (int i = t; i < nb; i += kBucketThreads) part += super_count(rect_ranked[start + i]);
         scan1024(part, L.wsum, &etot);
-        publish_bucket_total(em, d, etot);
+        if (!placed) publish_bucket_total(em, d, etot);
     }
     for (int i = t; i < nb; i += kBucketThreads) keys[start + i] -= klo;  // sort key - lo
     __syncthreads();
     const int res = bucket_global_sort(L, keys + start, ids + start, scratch_k + start, sorted_ids + start, nb,
                                        lowbits);
     const uint32_t* rid = res ? sorted_ids + start : ids + start;
+    if (placed) {
+        place_rid = rid;
+        place_etot = etot;
+        goto placed_tail;
+    }
     const uint32_t ebase = em.keys ? bucket_entry_base(em, d, kxf, L.wsum) : 0u;
     const bool emit = em.keys && (uint64_t)ebase + etot <= (uint64_t)em.cap;
     uint32_t carry = 0;
@@ -1341,6 +1665,12 @@ void k_depth_bucket_sort(
         carry += tot;
     }
     if (t == 0) totals[d] = carry;
+    return;
+    }
+placed_tail:  // placed emission from global memory: the Gaussians' ids in depth order at place_rid
+    super_cursors(L, em, d, base_s);  // its barriers also order the id stores before the reads
+    place_runs(L, em, place_rid, nb);
+    if (t == 0) totals[d] = place_etot;
 }
 
 static int bucket_timeline_on()
@@ -1384,8 +1714,22 @@ bool fused_emit_enabled()
     return v;
 }
 
+int msd_blocks(int P)
+{
+    const int tile = kRadixThreads * (radix_small(P) ? 4 : 16);
+    return (P + tile - 1) / tile;
+}
+
+bool placed_emit(const Layout& L, bool geometry_phase)
+{
+    if (L.supers > 256) return false;
+    const char* e = getenv("LSR_PLACED");
+    if (e && (e[0] == '0' || e[0] == '1')) return e[0] == '1';
+    return !geometry_phase;
+}
+
 hipError_t launch_depth_order(int P, int passes, const Layout& L, char* geom, uint32_t* counters, uint32_t* stall,
-                              hipStream_t s, bool debug, bool fused_emit, uint32_t emit_cap)
+                              hipStream_t s, bool debug, bool fused_emit, uint32_t emit_cap, bool placed_req)
 {
     if (P == 0) return hipSuccess;
     uint32_t* hist = reinterpret_cast<uint32_t*>(geom + L.radix_hist);
@@ -1414,21 +1758,25 @@ hipError_t launch_depth_order(int P, int passes, const Layout& L, char* geom, ui
         }();
         const bool small = radix_small(P);
         const int nblk = (P + kRadixThreads * (small ? 4 : 16) - 1) / (kRadixThreads * (small ? 4 : 16));
-        // the super-tile histogram the bucket sort counts into, and its scan's status words
-        const bool shist_on = fused_emit && L.super_hist_words > 0;
+        // placed emission: the MSD histogram also counts each block's super-tile entries (rows 256 +
+        // s); else the super-tile histogram the bucket sort counts into, and its scan's status words
+        const bool placed = fused_emit && placed_req && L.supers <= 256;
+        const bool shist_on = fused_emit && !placed && L.super_hist_words > 0;
         const ZeroList zmsd = shist_on
             ? ZeroList{{reinterpret_cast<uint32_t*>(geom + L.super_hist), reinterpret_cast<uint32_t*>(geom + L.super_hist_status),
                         nullptr, nullptr},
                        {(int)L.super_hist_words, (int)L.super_hist_status_words, 0, 0}}
             : ZeroList{};
+        const uint2* srect = placed ? tail.rect : nullptr;
         if (small)
             hipLaunchKernelGGL(k_radix_hist<4>, dim3(nblk), dim3(kRadixThreads), 0, s, keys, P, 0, 8, hist, nblk, kxf,
-                               remap, 1, zmsd, DevCount{nullptr, nullptr});
+                               remap, 1, zmsd, DevCount{nullptr, nullptr}, srect, L.supers, L.sgx);
         else
             hipLaunchKernelGGL(k_radix_hist<16>, dim3(nblk), dim3(kRadixThreads), 0, s, keys, P, 0, 8, hist, nblk, kxf,
-                               remap, 1, zmsd, DevCount{nullptr, nullptr});
+                               remap, 1, zmsd, DevCount{nullptr, nullptr}, srect, L.supers, L.sgx);
         if ((e = post(debug, s)) != hipSuccess) return e;
-        if ((e = scan_exclusive(hist, hist_scan, 256 * nblk, regions, nullptr, stall, s, debug)) != hipSuccess)
+        if ((e = scan_exclusive(hist, hist_scan, (256 + (placed ? L.supers : 0)) * nblk, regions, nullptr, stall, s,
+                                debug)) != hipSuccess)
             return e;
         // the rectangles ride along into rect_ranked (bucket layout); the bucket sort permutes them
         const ScatterTail carry{tail.rect, tail.rect_ranked, nullptr};
@@ -1458,6 +1806,14 @@ hipError_t launch_depth_order(int P, int passes, const Layout& L, char* geom, ui
             em.shist = shist_on ? reinterpret_cast<uint32_t*>(geom + L.super_hist) : nullptr;
             em.hstride = L.super_hist_stride;
             em.supers = L.supers;
+            if (placed) {
+                em.sup_status = reinterpret_cast<uint32_t*>(geom + L.sup_status);
+                em.sup_base = hist_scan + 256 * (size_t)nblk;
+                em.sup_stride = nblk;
+                em.etotal = counters + kCntSuper;
+                em.sbits = L.super_bits;
+                em.kxf = kxf;
+            }
         }
         hipLaunchKernelGGL(k_depth_bucket_sort, dim3(256), dim3(kBucketThreads), kBucketLdsBytes, s, P, kb, vb,
                            (const uint32_t*)hist_scan, nblk, kxf, tail.rect, va, tail.rect_ranked, off,
@@ -1747,8 +2103,14 @@ __global__ __launch_bounds__(256) void k_bin_count_fused(int S, int sgx, int sgy
                                                          uint2* __restrict__ g_sranges, uint32_t* __restrict__ g_seg_base,
                                                          uint32_t* __restrict__ g_colpre, uint32_t* __restrict__ g_rowpre,
                                                          const uint32_t* __restrict__ keys, uint32_t* __restrict__ table,
-                                                         DevCount dc)
+                                                         DevCount dc, uint32_t bias = 0, ZeroList zero = ZeroList{},
+                                                         int64_t table_words = 0)
 {
+    // placed emission (no super-tile pass before this launch): hist = the MSD histogram's scanned
+    // super-tile rows (bias = its key count), and this launch clears what the later kernels need
+    // cleared (zero: tile ranges, the table scan's status words; table_words: the count table past
+    // the slots written below)
+    zero_words_strided(zero);
     if (dc.abort && *dc.abort) return;
     if (dc.n) E = min(E, (int64_t)*dc.n);
     __shared__ uint2 sr[kFusedSupers];
@@ -1762,8 +2124,8 @@ __global__ __launch_bounds__(256) void k_bin_count_fused(int S, int sgx, int sgy
     const int t = threadIdx.x;
     uint32_t nseg = 0;
     if (t < S) {
-        const uint32_t a = hist[(size_t)t * nblk];
-        const uint32_t b = t + 1 < ndig ? hist[(size_t)(t + 1) * nblk] : (uint32_t)E;
+        const uint32_t a = hist[(size_t)t * nblk] - bias;
+        const uint32_t b = t + 1 < ndig ? hist[(size_t)(t + 1) * nblk] - bias : (uint32_t)E;
         sr[t] = make_uint2(a, b);
         nseg = super_segments(make_uint2(a, b));
     }
@@ -1793,6 +2155,9 @@ __global__ __launch_bounds__(256) void k_bin_count_fused(int S, int sgx, int sgy
         sh[0] = -1;
         sh[1] = 0;
     }
+    for (int64_t w = (int64_t)rtot + (int64_t)blockIdx.x * blockDim.x + t; w < table_words;
+         w += (int64_t)gridDim.x * blockDim.x)
+        table[w] = 0u;
     __syncthreads();
     // this workgroup's (super-tile, segment): the s with sbase[s] <= b < sbase[s + 1]
     {
@@ -1968,7 +2333,7 @@ static MsdOffsets msd_offsets(int P, const Layout& L, char* geom, char* image)
 }
 
 hipError_t launch_binning(int P, int64_t R, const Layout& L, char* geom, char* image, char* binning, uint32_t* stall,
-                          hipStream_t s, bool debug, bool emitted, DevCount dc)
+                          hipStream_t s, bool debug, bool emitted, DevCount dc, bool placed)
 {
     uint2* ranges = reinterpret_cast<uint2*>(image + L.ranges);
     if (R == 0) return zero_fill(ranges, 8 * (size_t)L.tiles, s);
@@ -2007,6 +2372,31 @@ hipError_t launch_binning(int P, int64_t R, const Layout& L, char* geom, char* i
     int passes = 0;
     uint32_t* bin_hist_scan = reinterpret_cast<uint32_t*>(binning + L.bin_radix_hist_scan);
     int hist_stride = 0, hist_rows = 1 << L.super_bits;  // of the scanned histogram count_fused reads
+    if (emitted && placed && L.supers <= 256) {
+        // the bucket sort wrote the entries super-tile-major; the super-tile starts are the MSD
+        // histogram's scanned super-tile rows (minus its P keys)
+        const bool small = radix_small(P);
+        const int nblk = (P + kRadixThreads * (small ? 4 : 16) - 1) / (kRadixThreads * (small ? 4 : 16));
+        const ZeroList zplaced{{reinterpret_cast<uint32_t*>(ranges), regions + L.super_passes * L.scan_region_bin,
+                                nullptr, nullptr},
+                               {2 * L.tiles, (int)L.scan_region_bin, 0, 0}};
+        hipLaunchKernelGGL(k_bin_count_fused, dim3((unsigned)L.seg_blocks), dim3(256), 0, s, L.supers, L.sgx, L.sgy,
+                           L.gx, L.gy, nblk, L.supers, E,
+                           (const uint32_t*)(reinterpret_cast<uint32_t*>(geom + L.radix_hist_scan) + 256 * (size_t)nblk),
+                           sranges, seg_base, colpre, rowpre, k0, table, dc, (uint32_t)P, zplaced,
+                           (int64_t)L.seg_table_words);
+        if ((e = post(debug, s)) != hipSuccess) return e;
+        uint32_t* table_scan = reinterpret_cast<uint32_t*>(binning + L.seg_table_scan);
+        if ((e = scan_exclusive(table, table_scan, (int)L.seg_table_words, regions + L.super_passes * L.scan_region_bin,
+                                nullptr, stall, s, debug)) != hipSuccess)
+            return e;
+        hipLaunchKernelGGL(k_bin_emit, dim3((unsigned)L.seg_blocks), dim3(256), 0, s, L.supers, L.sgx, L.gx, L.gy,
+                           (const uint32_t*)seg_base, (const uint2*)sranges, (const uint32_t*)colpre,
+                           (const uint32_t*)rowpre, k0, v0, (const uint32_t*)table_scan, pl, ranges,
+                           reinterpret_cast<uint32_t*>(image + L.counters) + kCntFwdClass,
+                           reinterpret_cast<uint32_t*>(image + L.tile_lists), dc);
+        return post(debug, s);
+    }
     if (emitted && L.super_hist_words > 0) {
         // the bucket sort counted the super-tile pass's [super-tile][block] histogram as it emitted
         // (blocks of kSuperHistBlock entries): no histogram launch; the scatter clears the tables

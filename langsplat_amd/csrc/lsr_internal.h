@@ -59,6 +59,11 @@ constexpr int kFusedEntries = 3;    // capacity of the fused super-tile emission
 constexpr int kSuperHistBlock = 1024;  // entries per block of the super-tile pass (k_radix_scatter<4>)
 
 size_t radix_hist_words(int64_t n);   // per-block digit histograms for n keys
+int msd_blocks(int P);                 // blocks of the MSD depth pass's histogram
+// placed emission's count words (lsr_binning.hip): [super-tile][bucket] counts, per group of
+// kSupGroup buckets the group sums, the group arrival counters
+constexpr int kSupGroup = 16;
+constexpr size_t kSupWords = 256 * 256 + 256 * (256 / kSupGroup) + 256 / kSupGroup;
 size_t scan_region_words(int64_t n);  // look-back status + ticket of one scan of n words
 constexpr int kDepthScans = 5;         // 4 depth-sort passes + the instance-offset scan
 
@@ -80,6 +85,9 @@ struct Layout {
     size_t super_hist, super_hist_scan, super_hist_status;
     size_t super_hist_words, super_hist_status_words;
     int super_hist_stride;
+    // placed emission (<= 256 super-tiles): the bucket sort's entry counts (kSupWords, cleared by
+    // preprocess); the MSD histogram then also holds one row per super-tile after its 256 digit rows
+    size_t sup_status;
     size_t grad_records;      // P x kGradStrideLang floats: the language step's gradient records (cleared
                               // by the render forward under LSR_FWD_ZERO_GRAD_RECORDS)
     size_t geom_bytes;
@@ -116,7 +124,8 @@ inline Layout make_layout(int P, int W, int H, int64_t R, int64_t E)
     L.keys_a = take(4 * p);
     L.keys_b = take(4 * p);
     L.vals_b = take(4 * p);
-    const size_t hw_p = radix_hist_words((int64_t)p);
+    // 256 digit rows, then (placed emission) <= 256 super-tile rows
+    const size_t hw_p = 2 * radix_hist_words((int64_t)p);
     L.radix_hist = take(4 * hw_p);
     L.radix_hist_scan = take(4 * hw_p);  // scans are out-of-place (k_scan's stall fallback)
     L.scan_region_geom = scan_region_words((int64_t)(hw_p > p ? hw_p : p));
@@ -141,6 +150,7 @@ inline Layout make_layout(int P, int W, int H, int64_t R, int64_t E)
         L.super_hist = take(4 * L.super_hist_words);
         L.super_hist_scan = take(4 * L.super_hist_words);
         L.super_hist_status = take(4 * L.super_hist_status_words);
+        L.sup_status = take(4 * kSupWords);
     }
     // E is ~1.5 per visible Gaussian at 1080p; a view with more than kFusedEntries per Gaussian
     // falls back to k_emit_super after the host wait
@@ -212,6 +222,8 @@ struct PreprocessParams {
     float4* record;
     uint32_t* zero;   // depth-order scan status, cleared here
     int zero_words;
+    uint32_t* zero2;  // placed emission: the bucket sort's [super-tile][bucket] counts, cleared here
+    int zero2_words;
     uint4* partial;   // per block {tile instances, super-tile entries, min / max visible depth key}
     int raw;                  // lsr_raw_flags
     const float* shs_rest;    // split SH rows (shs = dc only) or null
@@ -293,14 +305,22 @@ hipError_t launch_mark_visible(int P, const float* means, const float* view, con
 // fused_vals when they fit (E <= L.fused_cap), so k_emit_super is not launched
 // emit_cap > 0: the fused emission writes at most that many entries (capacity mode), else L.fused_cap
 hipError_t launch_depth_order(int P, int passes, const Layout& L, char* geom, uint32_t* counters, uint32_t* stall,
-                              hipStream_t s, bool debug, bool fused_emit = false, uint32_t emit_cap = 0);
+                              hipStream_t s, bool debug, bool fused_emit = false, uint32_t emit_cap = 0,
+                              bool placed = false);
 // false: the depth order reads its pass count on the device (MSD pass + per-bucket LDS sort) and
 // ignores `passes`; true (large P): LSD passes, `passes` must cover the visible key range
 bool depth_order_uses_pass_count(int P);
 // LSR_FUSED_EMIT=0 turns the fused super-tile emission off (measurement knob, read once)
 bool fused_emit_enabled();
+// placed emission: the fused emission writes every entry at its super-tile-major position, so the
+// binning's super-tile pass (scan + scatter) is not launched.  Needs <= 256 super-tiles.  Default:
+// on for a whole forward, off for the split geometry phase (whose kernels run beside the previous
+// view's render kernels, where the narrow scan + scatter launches fill gaps better than the longer
+// bucket kernel: measured); LSR_PLACED=1 / 0 forces it (read per call)
+bool placed_emit(const Layout& L, bool geometry_phase);
 // super-tile lists, per-(tile, segment) counts, scanned bases -> point_list and tile ranges.
-// emitted: the depth order's bucket sort already wrote the E entries into L.fused_keys / fused_vals.
+// emitted: the depth order's bucket sort already wrote the E entries into L.fused_keys / fused_vals
+// (super-tile-major when `placed`, the depth order's choice, else in depth order).
 // Device-read counts for launches sized from capacities: n = min(n, *n) when n is set; a set *abort
 // (counters[kCntOverflow]) makes the kernel skip its work (after the clearing the binning's first
 // launch does).  Both null: the host's counts.
@@ -310,7 +330,8 @@ struct DevCount {
 };
 // capacity mode: dc = {counters + kCntSuper, counters + kCntOverflow}, R / L from the capacities
 hipError_t launch_binning(int P, int64_t R, const Layout& L, char* geom, char* image, char* binning, uint32_t* stall,
-                          hipStream_t s, bool debug, bool emitted = false, DevCount dc = DevCount{nullptr, nullptr});
+                          hipStream_t s, bool debug, bool emitted = false, DevCount dc = DevCount{nullptr, nullptr},
+                          bool placed = false);
 
 // Look-back stall handling (k_scan, k_masked_l1_forward).  A single-pass look-back polls at most
 // stall_spin_limit() times for a predecessor's value; past that it computes the value itself from

@@ -174,6 +174,7 @@ __global__ __launch_bounds__(kPreThreads) __attribute__((amdgpu_waves_per_eu(
     extern __shared__ float s_sh[];
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     for (int w = i; w < p.zero_words; w += gridDim.x * blockDim.x) p.zero[w] = 0u;
+    for (int w = i; w < p.zero2_words; w += gridDim.x * blockDim.x) p.zero2[w] = 0u;
     // Per-Gaussian inputs are loaded first, so their latency overlaps the SH staging below
     // (issued after the barrier they would add a second memory round trip to every block).
     const bool live = i < p.P;

@@ -9,6 +9,7 @@ image).
 """
 import math
 
+import numpy as np
 import pytest
 import torch
 
@@ -67,4 +68,73 @@ def test_fused_emission_over_capacity():
     st = settings_for(cam, sh_degree=0)
     run, std, ind, out = check_forward_exact(st, inp)
     assert state(out, P, W, H)["counters"][4] > 3 * P  # E: beyond the fused capacity
+    check_backward(st, inp, run, out)
+
+
+def dense_bucket_scene(seed=51):
+    """1024 large Gaussians at one depth (one MSD bucket of the depth sort) over a 1280x720 view (60
+    super-tiles), each meeting ~9-16 super-tiles: that bucket has more entries than one LDS list
+    (kBucketCap = 8192), and more than 8192 within its one run of 1024 Gaussians; plus 7000 small
+    Gaussians over depths 0.5..50, so E stays within the fused capacity (3 P)."""
+    P1, P2, W, H = 1024, 7000, 1280, 720
+    g = torch.Generator().manual_seed(seed)
+    cam = make_cameras(1, W, H)[0]
+    tx, ty = math.tan(cam.FoVx * 0.5), math.tan(cam.FoVy * 0.5)
+    d = torch.cat([4.0 + torch.rand(P1, generator=g) * 1e-3,
+                   torch.exp(torch.rand(P2, generator=g) * (math.log(50.0) - math.log(0.5)) + math.log(0.5))])
+    P = P1 + P2
+    u, v = torch.rand(P, generator=g) * 2 - 1, torch.rand(P, generator=g) * 2 - 1
+    means = torch.stack([u * d * tx * 0.9, v * d * ty * 0.9, d - 4.0], 1)
+    s = torch.cat([torch.full((P1,), 0.28), 0.01 * d[P1:] / 4.0])
+    inp = dict(means3D=means, opacities=torch.rand((P, 1), generator=g) * 0.3 + 0.05,
+               colors_precomp=torch.rand((P, 3), generator=g),
+               language_feature_precomp=torch.nn.functional.normalize(torch.randn((P, 3), generator=g)),
+               scales=s[:, None] * (0.8 + 0.4 * torch.rand((P, 3), generator=g)),
+               rotations=torch.nn.functional.normalize(torch.randn((P, 4), generator=g)))
+    return settings_for(cam, sh_degree=0), inp
+
+
+def c3_scene():
+    from langsplat_amd.synthetic import CONFIGS, activated_inputs, make_gaussians
+    c = CONFIGS["C3"]
+    g = make_gaussians(c["P"], seed=0)
+    with torch.no_grad():
+        inp = {k: v.contiguous() for k, v in activated_inputs(g).items()}
+    cam = make_cameras(1, c["width"], c["height"])[0]
+    return settings_for(cam, sh_degree=g.max_sh_degree), inp
+
+
+@pytest.mark.parametrize("kind", ["dense_bucket", "c3"])
+def test_placed_emission_equals_depth_order_emission(kind, monkeypatch):
+    """Placed emission (the bucket sort writes every super-tile entry at its super-tile-major
+    position, from the MSD histogram's scanned [super-tile][bucket] count table) against the
+    depth-order emission it replaces (entries in depth order, then the binning's super-tile radix
+    pass; LSR_PLACED=0): the same per-tile lists, ranges and images, bit for bit.  dense_bucket also
+    takes the LDS sort's multi-list tail and place_runs' sub-lists."""
+    from tests.test_gpu_parity import native_forward, state
+    st, inp = dense_bucket_scene() if kind == "dense_bucket" else c3_scene()
+    P = inp["means3D"].shape[0]
+    W, H = st.image_width, st.image_height
+    res = {}
+    for placed in ("1", "0"):
+        monkeypatch.setenv("LSR_PLACED", placed)
+        _, _, out = native_forward(st, inp)
+        s = state(out, P, W, H)
+        s.update(nr=out[0], color=out[1].cpu().numpy(), lang=out[2].cpu().numpy(), radii=out[3].cpu().numpy())
+        res[placed] = s
+    a, b = res["1"], res["0"]
+    E = int(a["counters"][4])
+    assert E <= 3 * P  # within the fused capacity: the placed path ran
+    if kind == "dense_bucket":
+        assert E > 7000 + 8192
+    assert a["nr"] == b["nr"] > 0
+    for k in ("ranges", "point_list", "final_T", "n_contrib", "color", "lang", "radii", "counters"):
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+
+
+def test_placed_emission_dense_bucket_oracle():
+    """The dense-bucket scene (placed emission's multi-list and sub-list paths) against the oracle:
+    forward bit-exact, backward within the parity tolerance."""
+    st, inp = dense_bucket_scene()
+    run, std, ind, out = check_forward_exact(st, inp)
     check_backward(st, inp, run, out)

@@ -56,13 +56,17 @@ def main():
         d = [((t[i + 1] - t[i]) & 0xFFFFFFFF) * TICK_US for i in range(5)]
         return (f"keys {keys[b]}: load {d[0]:.1f}, pass0 {d[1]:.1f}, later passes {d[2]:.1f}, gathers {d[3]:.1f}, "
                 f"offsets {d[4]:.1f} us")
-    if os.environ.get("LSR_BUCKET_MARK_BASE") == "1":  # a library built with -DLSR_BUCKET_MARK_BASE=1
+    mb = os.environ.get("LSR_BUCKET_MARK_BASE")
+    if mb in ("1", "2"):  # a library built with -DLSR_BUCKET_MARK_BASE=1 / 2
         def phases(b):  # noqa: F811
             r = recs[b]
             if not r["ph"][2]:
                 return f"keys {keys[b]}"
             t = [r["start"], r["ph"][0], r["ph"][1], r["ph"][2], r["ph"][3], r["end"]]
             d = [((t[i + 1] - t[i]) & 0xFFFFFFFF) * TICK_US for i in range(5)]
+            if mb == "2":  # placed emission (the look-back before the sort): entries listed and ranked
+                return (f"keys {keys[b]}: to pass0 {d[0]:.1f}, later passes {d[1]:.1f}, gathers {d[2]:.1f}, "
+                        f"scan + list + rank {d[3]:.1f}, write {d[4]:.1f} us")
             return (f"keys {keys[b]}: to pass0 {d[0]:.1f}, later passes {d[1]:.1f}, gathers {d[2]:.1f}, "
                     f"scan + look-back {d[3]:.1f}, emission {d[4]:.1f} us")
     analyse(f"{cfg} depth bucket sort", recs, phases)
