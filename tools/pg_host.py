@@ -48,7 +48,7 @@ def main():
         torch.cuda.synchronize()
         t2 = time.perf_counter()
         print(f"pg_host rep {rep}: host enqueue {1e3 * (t1 - t0) / steps:.4f} ms/replay, "
-              f"wall {1e3 * (t2 - t0) / steps:.4f} ms/step", flush=True)
+              f"wall {1e3 * (t2 - t0) / steps:.4f} ms/step (ended at {time.time():.3f})", flush=True)
         walls.append(1e3 * (t2 - t0) / steps)
     walls.sort()
     print(f"pg_host summary: min {walls[0]:.4f} median {walls[len(walls) // 2]:.4f} ms/step", flush=True)
