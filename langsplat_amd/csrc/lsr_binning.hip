@@ -1088,19 +1088,24 @@ __device__ __forceinline__ void publish_super_counts(const BucketLds& L, const B
         s_last = __hip_atomic_fetch_add(&em.sup_status[kSupArriveOff + g], 1u, __ATOMIC_RELAXED,
                                         __HIP_MEMORY_SCOPE_AGENT) == kSupGroup - 1;
     __syncthreads();
-    if (!s_last || t >= em.supers) return;
+    if (!s_last || t >= em.supers || em.spin_limit == 0u) return;
     // the group's last arrival: every member has published (its flags are polled all the same)
     uint32_t v[kSupGroup];
 #pragma unroll
     for (int j = 0; j < kSupGroup; j++)
         v[j] = __hip_atomic_load(&em.sup_status[(size_t)t * 256 + g * kSupGroup + j], __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_AGENT);
-    uint32_t sum = 0;
+    uint32_t sum = 0, spins = 0;
 #pragma unroll
     for (int j = 0; j < kSupGroup; j++) {
-        while (!(v[j] & kSupAgg))
+        while (!(v[j] & kSupAgg)) {
+            // bounded: past it the group's sums are not published, and every later bucket's sum
+            // takes its own bounded wait and then its fallback (the prefixes from the inputs)
+            if (++spins > em.spin_limit) return;
+            __builtin_amdgcn_s_sleep(1);
             v[j] = __hip_atomic_load(&em.sup_status[(size_t)t * 256 + g * kSupGroup + j], __ATOMIC_RELAXED,
                                      __HIP_MEMORY_SCOPE_AGENT);
+        }
         sum += v[j] & kSupVal;
     }
     __hip_atomic_store(&em.sup_status[kSupGroupOff + (size_t)g * 256 + t], kSupAgg | sum, __ATOMIC_RELAXED,
@@ -1112,6 +1117,7 @@ __device__ __forceinline__ void publish_super_counts(const BucketLds& L, const B
 // thread and pair (s, j < 30) in flight at once; false when a wait passed the spin bound.
 __device__ __forceinline__ bool super_sum(BucketLds& L, const BucketEmit& em, int d)
 {
+    if (em.spin_limit == 0u) return false;  // never wait: the fallback (tests)
     const int t = threadIdx.x;
     const int g = d / kSupGroup, r = d - g * kSupGroup;
     constexpr int kPer = 256 * 32 / kBucketThreads;  // (s, j) pairs per thread, j < 32

@@ -388,7 +388,7 @@ def test_depth_sort_pass_counts(kind, lsd, monkeypatch):
 
 def test_lookback_stall_fallback_is_exact():
     """Every single-pass look-back (depth-sort histogram scans, super-tile offset scan, binning
-    table scan) forced onto its stall path (spin limit 0: no chunk waits for its predecessors; each
+    table scan, the placed emission's per-super-tile prefix sums) forced onto its stall path (spin limit 0: no chunk waits for its predecessors; each
     computes its prefix from the input instead) gives the same bit-exact forward, and the event is
     reported by lsr_debug_scan_stalls."""
     lib = _native.load()
