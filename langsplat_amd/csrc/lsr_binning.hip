@@ -223,7 +223,10 @@ static hipError_t scan_exclusive(const uint32_t* in, uint32_t* out, int n, uint3
 // (scan fault, the tile schedule's class counts) -- so the counters need no memset before the
 // forward -- then publishes counters[0..7] to pinned host memory (system scope) followed by the
 // sequence number the host spins on (one {value, seq} 64-bit slot per counter).
-constexpr int kPublishThreads = 1024;
+#ifndef LSR_PUBLISH_THREADS  // measurement knob: the counter reduction's workgroup size
+#define LSR_PUBLISH_THREADS 1024
+#endif
+constexpr int kPublishThreads = LSR_PUBLISH_THREADS;
 
 __global__ __launch_bounds__(kPublishThreads) void k_publish_counters(int nb, const uint4* __restrict__ partial,
                                                                       uint32_t* __restrict__ counters,
@@ -235,7 +238,7 @@ __global__ __launch_bounds__(kPublishThreads) void k_publish_counters(int nb, co
     __shared__ uint32_t red[4][kWaves];
     uint32_t t = 0, e = 0, kmin = 0xFFFFFFFFu, kmax = 0;
     // kPer loads in flight per thread before any is consumed (8k partials at 1M Gaussians: one round)
-    constexpr int kPer = 8;
+    constexpr int kPer = 8 * 1024 / kPublishThreads;
     for (int b0 = threadIdx.x; b0 < nb; b0 += kPublishThreads * kPer) {
         uint4 v[kPer];
 #pragma unroll
