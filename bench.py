@@ -504,17 +504,13 @@ def main():
             loss = render(cam, model, Pipe, bg, Opt, language_target=(gt, mask))["language_l1"]
             loss.backward()
             return loss
-        # N = 1: Adam inside the graph too (its step count advanced on the device); N > 1: the
-        # all-reduce and Adam after each replay
-        gstep = GraphedStep(fwd_bwd, model.trainable(), optimizer=optim if bucket is None else None)
+        # Adam inside the graph too (its step count advanced on the device); N > 1: the all-reduce
+        # (with the overflow flag) before it, inside the graph with RCCL
+        gstep = GraphedStep(fwd_bwd, model.trainable(), optimizer=optim, bucket=bucket, model=model)
         gstep.capture()
 
         def run():
-            loss = gstep.replay()
-            if bucket is not None:
-                bucket.all_reduce(average=True)
-                optim.step()
-            return loss
+            return gstep.replay()
         for _ in range(3):
             run()
         torch.cuda.synchronize()
@@ -556,7 +552,7 @@ def main():
             want = int(os.environ.get("LSR_PG_ROT", "1"))
             rot = max(r for r in range(1, want + 1) if args.steps % r == 0)
         pg = PipelinedGraphStep(lambda: render(cam, model, Pipe, bg, Opt, language_target=(gt, mask))["language_l1"],
-                                model.trainable(), optim, bucket=bucket, rotation=rot)
+                                model.trainable(), optim, bucket=bucket, rotation=rot, model=model)
         pg.capture()
         pg_rot = rot
         warm = rot * max(1, 4 // rot)
@@ -696,12 +692,13 @@ def main():
         "ms_per_step_with_sync": round(1000.0 * elapsed_sync / args.steps, 4),
         "ms_per_step_eager": round(1000.0 * elapsed_eager / args.steps, 4),
         "step_form": {"graph": ("HIP graph replay (render + loss + backward + Adam)" if world == 1 else
-                                "HIP graph replay (render + loss + backward), RCCL all-reduce, Adam"),
+                                "HIP graph replay (render + loss + backward + RCCL all-reduce + Adam)"),
                       "eager": "eager launches, one stream",
                       "pipelined": "eager launches, consecutive views on two streams (the next view's geometry "
                                    "beside this view's backward" + (", RCCL all-reduce" if world > 1 else "")
                                    + " and Adam)",
-                      "pipelined_graph": "HIP graphs on two streams: this view's compositing + loss, backward and "
+                      "pipelined_graph": "HIP graphs on two streams: this view's compositing + loss, backward, "
+                                         + ("RCCL all-reduce (in the graph), " if world > 1 else "") +
                                          "Adam on one, the next view's geometry (forward split in two calls) on "
                                          "the other"}[best],
         "pipelined_graph_rotation": pg_rot,

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define LSR_ABI_VERSION 13
+#define LSR_ABI_VERSION 14
 
 enum lsr_status {
     LSR_OK = 0,
@@ -154,8 +154,11 @@ typedef struct lsr_forward_args {
      * sized from them, the device reads the true counts, and the call enqueues its work without
      * waiting for the device.  *num_rendered then returns capacity_rendered (the value lsr_backward
      * needs).  A view that exceeds either capacity is not rasterized (background image, zero
-     * gradients) and sets *overflow (device int32, written by every capacity-mode forward: 1 or 0);
-     * the caller re-runs it with larger capacities.  capacity_rendered == 0: the host reads the
+     * gradients) and sets *overflow (device int32, written by every capacity-mode forward: 0, or
+     * when set 0x3F800000 -- the bits of 1.0f, ABI 14 -- so the flag tests non-zero as an int and
+     * can be all-reduced as a float beside the gradients: with a SUM or an average over ranks it is
+     * non-zero on every rank as soon as one rank's view overflowed); the caller re-runs it with
+     * larger capacities.  capacity_rendered == 0: the host reads the
      * counts after the preprocess (one wait) and sizes exactly. */
     int64_t capacity_rendered;
     int64_t capacity_entries;
@@ -314,6 +317,17 @@ int32_t lsr_profile_sample(int32_t every);
 int32_t lsr_mark_visible(int32_t P, const float* means3D, const float* viewmatrix,
                          const float* projmatrix, uint8_t* visible, void* stream);
 
+/* The language slots of a forward's render records, from the parameter (ABI 14): for every Gaussian
+ * with radii[i] > 0, record[i]'s three feature words receive language_feature[i] (activated as
+ * the forward activates it when raw has LSR_RAW_LANGUAGE: normalised).  `record` is
+ * lsr_state_layout.record of the geometry buffer of a forward made with phase LSR_PHASE_GEOMETRY
+ * over the same P Gaussians, and radii that forward's radii.  What LSR_PHASE_COMPOSITE does before
+ * compositing; a caller that changed the parameter after a fused update already filled the records
+ * (lsr_backward_args.fill_record) refills them with this before a LSR_PHASE_COMPOSITE_FILLED call
+ * (langsplat_amd/pipeline.py follow_caller). */
+int32_t lsr_fill_language(int32_t P, const float* language_feature, int32_t raw, const int32_t* radii, float* record,
+                          void* stream);
+
 /* Measurement hook, not part of the reference interface: with LSR_RENDER_STATS=1 in the
  * environment the render backward counts, per wave-iteration over a culled list entry, [0]
  * entries, [1] entries passing the power test in some lane, [2] entries some lane blends, [3]
@@ -391,7 +405,11 @@ int32_t lsr_adam_step(int64_t n, float* param, const float* grad, float* exp_avg
  *   step_dev[LSR_ADAM_WORD_LR + k]   tensor k's learning rate (a double's bits), which the caller keeps
  *                                    current (a learning-rate schedule, scene/gaussian_model.py:231-241,
  *                                    changes it between replays without a re-capture); the table's lr
- *                                    is not read.
+ *                                    is not read;
+ *   a tensor's `step` field is then its OFFSET from the count (ABI 14): tensor k's step of a replay
+ *   is step_dev[0] + 1 + tensors[k].step (0 when all counts are equal; torch's per-parameter counts
+ *   differ after replace_tensor_to_optimizer, scene/gaussian_model.py:326-339, since the replaced
+ *   group skips that iteration's step).  The offset must be > -2^40 and < 2^40.
  * step_dev NULL: the host's step counts and lrs.
  * skip (device int32, or NULL): when *skip != 0 at run time the launch changes nothing -- no
  * parameter, moment or step count -- and, with step_dev, adds one to the skipped count.  A captured

@@ -22,7 +22,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LSR_LIB") or os.path.join(_HERE, "liblsr.so")
 
 LSR_BUF_GEOM, LSR_BUF_BINNING, LSR_BUF_IMAGE, LSR_BUF_BACKWARD = 0, 1, 2, 3
-ABI_VERSION = 13
+ABI_VERSION = 14
 ADAM_STEP_WORDS = 66  # include/lsr.h LSR_ADAM_STEP_WORDS
 ADAM_WORD_SKIPPED, ADAM_WORD_LR = 49, 50  # LSR_ADAM_WORD_SKIPPED / LSR_ADAM_WORD_LR
 # lsr_raw_flags (include/lsr.h): inputs are GaussianModel's raw parameters
@@ -106,6 +106,7 @@ SIGNATURES = {
     "lsr_backward": (ctypes.c_int32, [ctypes.POINTER(LsrSettings), ctypes.POINTER(LsrBackwardArgs), ALLOC_FN, _vp,
                                       _vp]),
     "lsr_mark_visible": (ctypes.c_int32, [ctypes.c_int32, _vp, _vp, _vp, _vp, _vp]),
+    "lsr_fill_language": (ctypes.c_int32, [ctypes.c_int32, _vp, ctypes.c_int32, _vp, _vp, _vp]),
     "lsr_adam_step": (ctypes.c_int32, [ctypes.c_int64, _vp, _vp, _vp, _vp, ctypes.c_double, ctypes.c_double,
                                        ctypes.c_double, ctypes.c_double, ctypes.c_int64, _vp]),
     "lsr_adam_multi": (ctypes.c_int32, [ctypes.c_int32, ctypes.POINTER(LsrAdamTensor), ctypes.c_float, _vp, _vp,
@@ -151,6 +152,22 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         raise RuntimeError("liblsr.so ABI version mismatch")
     _lib = lib
     return lib
+
+
+_autograd = None
+
+
+def autograd_helper():
+    """The _lsr_autograd extension (csrc/lsr_autograd.cpp: a leaf tensor's cached AccumulateGrad node,
+    read and released; host code), built in-tree first if it is absent."""
+    global _autograd
+    if _autograd is None:
+        if not os.path.exists(os.path.join(_HERE, "_lsr_autograd.so")):
+            from . import build as _build
+            _build.build_autograd_helper()
+        from . import _lsr_autograd
+        _autograd = _lsr_autograd
+    return _autograd
 
 
 def last_error() -> str:
@@ -242,8 +259,9 @@ class capacity:
     """Within the block, the rasterizer forwards of this thread run in capacity mode (include/lsr.h
     lsr_forward_args.capacity_*): buffers and launch grids sized from `rendered` tile instances and
     `entries` super-tile entries, no wait for the device -- what a HIP graph capture of the step needs
-    (langsplat_amd.graph).  `overflow`: a () int32 device tensor each forward sets to 1 when its view
-    exceeds a capacity (it is then not rasterized) or 0."""
+    (langsplat_amd.graph).  `overflow`: a () int32 device tensor each forward sets to 0, or when its
+    view exceeds a capacity (it is then not rasterized) to the bits of 1.0f (non-zero as an int; 1.0
+    through overflow.view(torch.float32), which GradBucket.all_reduce(flag=) reduces over ranks)."""
 
     _tls = threading.local()
 
@@ -398,7 +416,7 @@ class fused_update:
         beta1, beta2 = g["betas"]
         opt._register_fused(gi)
         return LsrAdamTensor(p.numel(), p.data_ptr(), None, st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(),
-                             float(g["lr"]), float(beta1), float(beta2), float(g["eps"]), 0)
+                             float(g["lr"]), float(beta1), float(beta2), float(g["eps"]), opt.step_offset(p))
 
 
 def output_tensor(key, shape, dtype, device) -> torch.Tensor:
@@ -406,7 +424,10 @@ def output_tensor(key, shape, dtype, device) -> torch.Tensor:
     st = static_buffers.active()
     if st is None:
         return torch.empty(shape, dtype=dtype, device=device)
-    return st.tensor(("out", key), shape, dtype, device)
+    # a fresh alias of the persistent tensor: the autograd Function that returns it sets ITS grad_fn,
+    # so the persistent tensor never keeps an autograd graph (and the parameters' AccumulateGrad
+    # nodes, bound to the capture stream) alive past the step that produced it
+    return st.tensor(("out", key), shape, dtype, device).detach()
 
 
 # (P, W, H) -> (tile instances, super-tile entries) of this thread's last forward outside capacity mode
@@ -678,6 +699,18 @@ def densification_stats(radii, dmeans2D, max_radii2D=None, xyz_gradient_accum=No
     with _on_device(radii.device):
         _check(lib.lsr_densification_stats(P, _ptr(radii), _ptr(g), *outs, _stream(radii.device)),
                "lsr_densification_stats")
+
+
+def fill_language(language_feature: torch.Tensor, raw: int, radii: torch.Tensor, record_ptr: int):
+    """The language slots of a geometry-phase forward's render records from the parameter, on the
+    current stream (include/lsr.h lsr_fill_language)."""
+    P = int(radii.shape[0])
+    lf = _f32c(language_feature.detach())
+    if tuple(lf.shape) != (P, 3) or radii.dtype != torch.int32 or not radii.is_contiguous():
+        raise ValueError("fill_language: a (P, 3) feature and the (P,) int32 radii of the same forward")
+    with _on_device(lf.device):
+        _check(load().lsr_fill_language(P, _ptr(lf), int(raw), _ptr(radii), ctypes.c_void_p(int(record_ptr)),
+                                        _stream(lf.device)), "lsr_fill_language")
 
 
 def mark_visible(means3D, viewmatrix, projmatrix):

@@ -74,12 +74,39 @@ def build(force: bool = False, debug: bool = False, verbose: bool = False) -> st
     return LIB_PATH
 
 
+AUTOGRAD_SRC = os.path.join(CSRC, "lsr_autograd.cpp")
+AUTOGRAD_LIB = os.path.join(HERE, "_lsr_autograd.so")
+
+
+def build_autograd_helper(force: bool = False, verbose: bool = False) -> str:
+    """_lsr_autograd.so: a CPython extension over torch's autograd C++ API (host code, g++; no HIP),
+    used by the captured steps to release stale AccumulateGrad nodes (csrc/lsr_autograd.cpp)."""
+    if not force and not _stale(AUTOGRAD_LIB, [AUTOGRAD_SRC, __file__]):
+        return AUTOGRAD_LIB
+    import sysconfig
+
+    import torch
+    from torch.utils import cpp_extension
+    incs = cpp_extension.include_paths() + [sysconfig.get_paths()["include"]]
+    libdir = os.path.join(os.path.dirname(torch.__file__), "lib")
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    cmd = [os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-shared", "-fPIC", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
+           "-w"] + [f"-I{d}" for d in incs] + [AUTOGRAD_SRC, f"-L{libdir}", "-lc10", "-ltorch", "-ltorch_cpu",
+                                               "-ltorch_python", f"-Wl,-rpath,{libdir}", "-o", AUTOGRAD_LIB + ".tmp"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(AUTOGRAD_LIB + ".tmp", AUTOGRAD_LIB)
+    return AUTOGRAD_LIB
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--debug", action="store_true")
     args = ap.parse_args(argv)
     print(build(force=args.force, debug=args.debug, verbose=True))
+    print(build_autograd_helper(force=args.force, verbose=True))
 
 
 if __name__ == "__main__":

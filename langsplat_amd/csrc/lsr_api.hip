@@ -699,7 +699,7 @@ int32_t lsr_backward(const lsr_settings* s, const lsr_backward_args* a, lsr_allo
     if (a->update) {
         // the language step's tail in one pass: epilogue + Adam (+ the next forward's feature slots)
         const lsr_adam_tensor& u = *a->update;
-        AdamHyper h{u.lr, u.beta1, u.beta2, u.eps};
+        AdamHyper h{u.lr, u.beta1, u.beta2, u.eps, u.step};
         LSR_TRY(launch_language_tail(P, a->radii, grad, const_cast<float*>(a->language_feature), u.exp_avg, u.exp_avg_sq,
                                      a->dL_dmeans2D, a->dL_dlanguage_feature, h, a->update_step_dev, a->update_skip,
                                      reinterpret_cast<float4*>(a->fill_record), stream),
@@ -871,6 +871,19 @@ int32_t lsr_mark_visible(int32_t P, const float* means3D, const float* viewmatri
     return LSR_OK;
 }
 
+int32_t lsr_fill_language(int32_t P, const float* language_feature, int32_t raw, const int32_t* radii, float* record,
+                          void* stream_ptr)
+{
+    if (P < 0 || (P > 0 && (!language_feature || !radii || !record)) ||
+        (reinterpret_cast<uintptr_t>(record) & 15) != 0)
+        return fail(LSR_ERR_INVALID, "lsr_fill_language: invalid argument");
+    hipStream_t stream = reinterpret_cast<hipStream_t>(stream_ptr);
+    const bool debug = false;
+    LSR_TRY(launch_fill_language(P, language_feature, raw, radii, reinterpret_cast<float4*>(record), stream),
+            "fill language");
+    return LSR_OK;
+}
+
 size_t lsr_masked_l1_scratch_bytes(int32_t C, int64_t HW)
 {
     (void)C;
@@ -940,10 +953,10 @@ int32_t lsr_adam_multi(int32_t count, const lsr_adam_tensor* tensors, float grad
         for (int32_t k = k0; k < count && k < k0 + kAdamMaxTensors; k++) {
             const lsr_adam_tensor& t = tensors[k];
             if (t.n < 0 || (t.n > 0 && (!t.param || !t.grad || !t.exp_avg || !t.exp_avg_sq)) ||
-                (t.step < 1 && !step_dev))
+                (t.step < 1 && !step_dev) || (step_dev && (t.step < -(int64_t)1 << 40 || t.step > (int64_t)1 << 40)))
                 return fail(LSR_ERR_INVALID, "lsr_adam_multi: invalid tensor entry");
             if (t.n == 0) continue;
-            tab.hyper[tab.count] = AdamHyper{t.lr, t.beta1, t.beta2, t.eps};
+            tab.hyper[tab.count] = AdamHyper{t.lr, t.beta1, t.beta2, t.eps, step_dev ? t.step : 0};
             AdamSegment& g = tab.seg[tab.count++];
             g.param = t.param;
             g.grad = t.grad;

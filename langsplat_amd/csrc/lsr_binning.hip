@@ -293,7 +293,9 @@ __global__ __launch_bounds__(kPublishThreads) void k_publish_counters(int nb, co
         const uint32_t ovf = (red[0][0] > r_cap || red[1][0] > e_cap || (depth_passes > 0 && need > depth_passes))
             ? 1u : 0u;
         counters[kCntOverflow] = ovf;
-        if (overflow) *overflow = (int32_t)ovf;
+        // the caller's flag holds the bits of 1.0f when set: non-zero as an int (the Adam skip test)
+        // and 1.0 as a float, so ranks can all-reduce it with their gradients (include/lsr.h)
+        if (overflow) *overflow = ovf ? (int32_t)0x3F800000 : 0;
         return;
     }
     // each value travels with the sequence number in one 64-bit store (single-copy atomic): the

@@ -382,6 +382,7 @@ struct AdamSegment {
 };
 struct AdamHyper {
     double lr, beta1, beta2, eps;
+    int64_t step_offset;  // with step_dev: this tensor's count minus the device count
 };
 struct AdamTable {
     int count;

@@ -99,7 +99,9 @@ __global__ void k_adam_advance(int64_t* step_dev, AdamTable tab)
     const int64_t step = *step_dev + 1;
     if (k < tab.count) {
         const double lr = __longlong_as_double((long long)step_dev[LSR_ADAM_WORD_LR + k]);
-        reinterpret_cast<AdamScalars*>(step_dev + 1)[k] = adam_scalars_dev(tab.hyper[k], lr, step);
+        // torch's per-parameter counts may differ by a constant (a group whose tensor was replaced,
+        // scene/gaussian_model.py:326-339, skips the step of that iteration): offset per tensor
+        reinterpret_cast<AdamScalars*>(step_dev + 1)[k] = adam_scalars_dev(tab.hyper[k], lr, step + tab.hyper[k].step_offset);
     }
     if (k == 0) *step_dev = step;
 }

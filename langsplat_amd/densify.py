@@ -71,12 +71,14 @@ class Densifier:
         _native.densification_stats(radii, viewspace_grad, self.max_radii2D, self.xyz_gradient_accum, self.denom)
 
     # ---- optimizer surgery ------------------------------------------------------------------------
-    def _replace(self, make_param, make_moment):
-        """Every group's parameter p -> make_param(p) and its moments m -> make_moment(m) (the state
-        keeps its step count); the model attributes follow."""
+    def _replace(self, make_param, make_moment, names=None):
+        """Every group's (or the groups in `names`) parameter p -> make_param(p) and its moments
+        m -> make_moment(m) (the state keeps its step count); the model attributes follow."""
         for group in self.optimizer.param_groups:
             if len(group["params"]) != 1 or group.get("name") not in GROUP_ATTR:
                 raise ValueError("Densifier: one parameter per group, named as scene/gaussian_model.py:219-226")
+            if names is not None and group["name"] not in names:
+                continue
             old = group["params"][0]
             state = self.optimizer.state.pop(old, None)
             new = torch.nn.Parameter(make_param(group["name"], old.detach()).requires_grad_(True))
@@ -101,6 +103,19 @@ class Densifier:
         self.xyz_gradient_accum = self.xyz_gradient_accum[keep]
         self.denom = self.denom[keep]
         self.max_radii2D = self.max_radii2D[keep]
+
+    def reset_opacity(self):
+        """scene/gaussian_model.py:277-281 (train.py:132-133, every opacity_reset_interval): every
+        opacity clamped to at most 0.01, as the raw parameter inverse_sigmoid(min(sigmoid(o), 0.01))
+        (utils/general_utils.py:18-19), through replace_tensor_to_optimizer (:326-339): a new
+        Parameter, both Adam moments zeros, the step count kept.  The new tensor has no .grad, so the
+        optimizer step of the same iteration (train.py:135-137) leaves the opacity alone, as in the
+        reference.  A captured step holds the old tensor's address: capture it again afterwards."""
+        def make(name, p):
+            op = torch.sigmoid(p)  # get_opacity (scene/gaussian_model.py:153-155)
+            x = torch.min(op, torch.ones_like(op) * 0.01)
+            return torch.log(x / (1 - x))
+        self._replace(make, torch.zeros_like, names=("opacity",))
 
     # ---- the three operations ------------------------------------------------------------------------
     def _scales(self):

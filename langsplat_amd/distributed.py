@@ -29,6 +29,15 @@ def init_from_env(backend: str = None):
     return dist.get_rank(), dist.get_world_size()
 
 
+def collective_capturable(group=None) -> bool:
+    """True when the gradient collective can be captured into a HIP graph with the step: backend
+    "nccl" (RCCL's kernels run on a stream; torch's ProcessGroupNCCL supports stream capture).  gloo
+    reduces on the host and stays an eager call between two graphs.  LSR_GRAPH_COLLECTIVE=0 keeps
+    the RCCL collective eager too."""
+    return (dist.is_available() and dist.is_initialized() and dist.get_backend(group) == "nccl"
+            and os.environ.get("LSR_GRAPH_COLLECTIVE", "1") != "0")
+
+
 class GradBucket:
     """The trainable parameters' gradients as ONE all-reduce buffer.
 
@@ -150,22 +159,39 @@ class GradBucket:
             xyz_gradient_accum.view(-1).add_(self.stats_norm * n)
             denom.view(-1).add_(torch.round(self.stats_count * n))
 
-    def all_reduce(self, average: bool = True, group=None):
+    def all_reduce(self, average: bool = True, group=None, flag: torch.Tensor = None):
         """SUM over ranks (then / world_size when average) -- the one collective of a step (and, with
-        staged densification statistics, the MAX of max_radii2D)."""
+        staged densification statistics, the MAX of max_radii2D).
+
+        flag: a () int32 device tensor holding 0 or the bits of a positive float -- the rasterizer's
+        capacity overflow flag (include/lsr.h lsr_forward_args.overflow: 1.0f when set) -- reduced in
+        the SAME collective (coalesced with the gradients), so afterwards it is non-zero on every rank
+        as soon as it was on one: every rank then skips the optimizer step on it (optim.Adam
+        step(skip=flag)) and the ranks stay identical, as if that iteration's views had been left out.
+        Inside a HIP graph capture (RCCL) the collective is captured with the step."""
         if not (dist.is_available() and dist.is_initialized()):
             self._divided_by = 1
             return
         self._attach()
         buf = self.buffer()
         world = dist.get_world_size(group)
-        if average and dist.get_backend(group) == "nccl":
-            # RCCL's ncclAvg: the division is part of the collective (no separate scaling kernel)
-            dist.all_reduce(buf, op=dist.ReduceOp.AVG, group=group)
+        nccl = dist.get_backend(group) == "nccl"
+        # RCCL's ncclAvg: the division is part of the collective (no separate scaling kernel)
+        op = dist.ReduceOp.AVG if average and nccl else dist.ReduceOp.SUM
+        if flag is None:
+            dist.all_reduce(buf, op=op, group=group)
         else:
-            dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
-            if average:
-                buf.mul_(1.0 / world)
+            if flag.dtype != torch.int32 or flag.numel() != 1 or flag.device != buf.device:
+                raise ValueError("GradBucket.all_reduce: flag must be a one-element int32 tensor on the bucket's device")
+            if nccl:  # one ncclGroup: one collective launch for both
+                with dist._coalescing_manager(group=group):
+                    dist.all_reduce(buf, op=op, group=group)
+                    dist.all_reduce(flag.view(torch.float32), op=op, group=group)
+            else:  # gloo's coalesced all-reduce takes CPU tensors only; it reduces on the host anyway
+                dist.all_reduce(buf, op=op, group=group)
+                dist.all_reduce(flag.view(torch.float32), op=op, group=group)
+        if average and not nccl:
+            buf.mul_(1.0 / world)
         self._divided_by = world if average else 1
         if self._max_radii is not None:
             dist.all_reduce(self._max_radii, op=dist.ReduceOp.MAX, group=group)

@@ -21,10 +21,15 @@ that view had been left out of the sequence.  Without an optimizer
 after each replay on the gradients the graph wrote into the parameters' .grad tensors.  Either way
 the graph owns those .grad tensors: do not set them to None.
 
-Before capture(), drop the outputs of any eager step (loss, render package): an autograd graph still
-alive binds the parameters' AccumulateGrad nodes to the stream it ran on, the captured backward then
-waits on that non-capturing stream, and this HIP runtime crashes at the end of the capture
-(DESIGN.md §5a).
+Stale autograd state.  LangSplat's train loop keeps the previous iteration's render package and loss
+alive (train.py:92-108).  Such a graph holds the parameters' AccumulateGrad nodes, each bound to the
+stream it was created on; a capture that reused them would make the captured backward wait on that
+non-capturing stream (torch warns "AccumulateGrad node's stream does not match"; this HIP runtime
+then crashes at the end of the capture).  capture() therefore first releases every
+parameter's cached node (release_stale_accumulators, csrc/lsr_autograd.cpp): the warm-up and the
+capture create their own, on their own streams, and the caller's old graph keeps its node.  `params`
+must list every leaf the step differentiates.  The captured graph's own autograd state is not kept
+(the static loss is detached), so eager steps after a capture start clean as well.
 
 A sequence of views (train.py:85-87 picks a random camera every iteration): pass view=ViewSlot(...)
 and have step_fn render from the slot (it is Camera-like, and carries the language target), then
@@ -107,6 +112,31 @@ def _fused_tail_enabled() -> bool:
     return os.environ.get("LSR_FUSED_TAIL", "1") != "0"
 
 
+def release_stale_accumulators(params) -> int:
+    """Make every parameter forget its cached AccumulateGrad node (a node a still-alive autograd graph
+    holds, bound to the stream that graph ran on), so the next graph creates a fresh one on its own
+    stream.  Returns how many parameters had one.  Call before a capture."""
+    helper = _native.autograd_helper()
+    n = 0
+    for p in params:
+        if p.requires_grad and p.is_leaf and helper.release_accumulator(p):
+            n += 1
+        if helper.accumulator_stream(p) is not None:
+            raise RuntimeError("release_stale_accumulators: a parameter's AccumulateGrad node is still cached")
+    return n
+
+
+def capture_key(model, optimizer, params):
+    """What a captured step bakes in that the reference's train loop changes between iterations:
+    the active SH degree (train.py:81-82 oneupSHdegree, scene/gaussian_model.py:166-168: a kernel
+    argument of the captured preprocess) and the parameter tensors themselves (densify_and_prune and
+    reset_opacity, train.py:128-133, replace them: the graph holds the old addresses).  A replay whose
+    key differs from its capture's re-captures first."""
+    deg = getattr(model, "active_sh_degree", None) if model is not None else None
+    ps = [p for g in optimizer.param_groups for p in g["params"]] if optimizer is not None else list(params)
+    return (deg, tuple((id(p), p.data_ptr(), tuple(p.shape)) for p in ps))
+
+
 def _as_view(view):
     """(camera, gt, mask), (camera,) or a camera -> (camera, gt, mask)."""
     if isinstance(view, (tuple, list)):
@@ -119,11 +149,22 @@ def _as_view(view):
 
 class GraphedStep:
     def __init__(self, step_fn: Callable[[], torch.Tensor], params: Iterable[torch.Tensor], headroom: float = 1.125,
-                 warmup: int = 2, optimizer=None, view: Optional[ViewSlot] = None):
+                 warmup: int = 2, optimizer=None, view: Optional[ViewSlot] = None, model=None, bucket=None):
         """step_fn: runs render + loss + loss.backward() and returns the loss; params: the tensors
         whose .grad the step produces (the trainable parameters); optimizer: stepped inside the graph;
-        view: the ViewSlot step_fn renders from (replay(view=...) then changes the view)."""
+        view: the ViewSlot step_fn renders from (replay(view=...) then changes the view); model: the
+        GaussianModel step_fn renders (its active_sh_degree is part of the capture key, capture_key).
+        With an optimizer, a replay after its parameters were replaced (densification, reset_opacity)
+        re-captures over the optimizer's current parameters.  bucket (N > 1, with an optimizer): a
+        langsplat_amd.distributed.GradBucket whose all-reduce -- carrying the overflow flag, so every
+        rank skips when one view overflowed -- runs between the backward and Adam: inside the graph
+        with RCCL, between two graphs with gloo."""
+        if bucket is not None and optimizer is None:
+            raise ValueError("GraphedStep: a bucket is reduced before the captured optimizer step")
+        self.bucket = bucket
+        self.graph_adam = None
         self.step_fn = step_fn
+        self.model = model
         self.optimizer = optimizer
         self.params = [p for p in params]
         self.headroom = float(headroom)
@@ -159,16 +200,40 @@ class GraphedStep:
         self.entries = max(int(e * self.headroom) + 1024, int(min_entries))
 
     def capture(self, min_rendered=0, min_entries=0):
+        if self.optimizer is not None:  # the optimizer's current tensors (densification replaces them)
+            self.params = [p for g in self.optimizer.param_groups for p in g["params"] if p.requires_grad]
+        self.key = capture_key(self.model, self.optimizer, self.params)
+        self.stale_released = release_stale_accumulators(self.params)  # the caller's held graphs (module doc)
         self._measure(min_rendered, min_entries)
         for p in self.params:
             p.grad = None  # the captured backward assigns fresh .grad tensors (no accumulate)
         if self.optimizer is not None:
             self.optimizer.prepare_capture()
             self._skipped_base = self.optimizer.skipped_steps()
-        self.graph = torch.cuda.CUDAGraph()
+        self.graph = self.graph_adam = None  # an earlier graph's pool goes before the new capture allocates
+        self.static_loss = None
+        from .distributed import collective_capturable
+        self._coll_in_graph = self.bucket is not None and collective_capturable()
+        if self._coll_in_graph:  # the communicator exists before the capture (its creation is not capturable)
+            self.bucket.all_reduce(average=True, flag=torch.zeros_like(self.overflow))
+            for p in self.params:
+                p.grad = None
+        graph = torch.cuda.CUDAGraph()
         with _native.capacity(self.rendered, self.entries, self.overflow):
-            with torch.cuda.graph(self.graph):
-                self.static_loss = self._body()
+            with torch.cuda.graph(graph):
+                # detached: the captured step's autograd graph (and its AccumulateGrad nodes, bound
+                # to the capture stream) is not kept alive past the capture
+                self.static_loss = self._body().detach()
+        if self.bucket is not None and not self._coll_in_graph:  # gloo: Adam in a graph of its own
+            # the graph's gradient tensors; Adam reads what the all-reduce leaves in .grad (the bucket's
+            # slices in flat mode, these tensors in direct mode)
+            self._graph_grads = [p.grad for p in self.params]
+            self.bucket._attach()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self.optimizer.step(skip=self.overflow)
+            self.graph_adam = g
+        self.graph = graph
         self.captures += 1
         return self
 
@@ -177,9 +242,13 @@ class GraphedStep:
             return self.step_fn()
         # N = 1, one trainable parameter (the language step): its Adam step runs inside the backward's
         # epilogue pass (_native.fused_update); optimizer.step() then has nothing left to launch
-        fuse = _fused_tail_enabled() and len(self.params) == 1
+        fuse = _fused_tail_enabled() and len(self.params) == 1 and self.bucket is None
         with _native.fused_update(self.optimizer, self.params[0], skip=self.overflow) if fuse else _nullctx():
             loss = self.step_fn()
+            if self.bucket is not None:
+                if not self._coll_in_graph:
+                    return loss  # gloo: the all-reduce and Adam follow the graph (replay)
+                self.bucket.all_reduce(average=True, flag=self.overflow)
             self.optimizer.step(skip=self.overflow)
         return loss
 
@@ -197,9 +266,18 @@ class GraphedStep:
             self.view.load(*_as_view(view))
         if self.graph is None:
             self.capture()
+        elif capture_key(self.model, self.optimizer, self.params) != self.key:
+            # an SH-degree step or replaced parameters since the capture: capture the step as it is now
+            self.sync()
+            self.capture(self.rendered, self.entries)
         if self.optimizer is not None:
             self.optimizer.sync_lr()
         self.graph.replay()
+        if self.graph_adam is not None:
+            for p, g in zip(self.params, self._graph_grads):
+                p.grad = g
+            self.bucket.all_reduce(average=True, flag=self.overflow)
+            self.graph_adam.replay()
         return self.static_loss
 
     def check(self) -> bool:

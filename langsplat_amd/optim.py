@@ -40,6 +40,7 @@ class Adam(torch.optim.Optimizer):
         self._dev_ahead = False  # replays may have advanced the device count past state["step"]
         self._lr_order = None    # group index of each table entry of the captured launch
         self._lr_dev = None      # the learning rates last written to the device block
+        self._step_offset = {}   # parameter -> its count minus the device count (include/lsr.h, ABI 14)
 
     def _params_with_grad(self):
         return [p for g in self.param_groups for p in g["params"] if p.grad is not None]
@@ -51,20 +52,29 @@ class Adam(torch.optim.Optimizer):
         captured launch reads (and advances) them."""
         self.sync_steps()
         ps = [p for g in self.param_groups for p in g["params"]]
-        steps = {int(self.state[p]["step"].item()) for p in ps if len(self.state[p])}
-        if len(steps) > 1:
-            raise RuntimeError("langsplat_amd.optim.Adam: a captured step needs equal step counts")
-        start = steps.pop() if steps else 0
         for p in ps:  # the state torch's first step creates lazily (no allocation may happen in a capture)
             if len(self.state[p]) == 0:
-                self.state[p]["step"] = torch.tensor(float(start))
+                self.state[p]["step"] = torch.tensor(0.0)
                 self.state[p]["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                 self.state[p]["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
         dev = ps[0].device
         if self._step_dev is None or self._step_dev.device != dev:
             self._step_dev = torch.zeros((_native.ADAM_STEP_WORDS,), dtype=torch.int64, device=dev)
-        self._step_dev[0].fill_(start)  # in place: older graphs keep their pointer
+        self._seed_device_count()
         self._dev_ahead = False
+
+    def _seed_device_count(self):
+        """The device count := the largest per-parameter count; every parameter's offset := its count
+        minus that (torch's counts differ once a replaced tensor skipped a step, e.g. reset_opacity,
+        scene/gaussian_model.py:277-281 + 326-339).  In place: older graphs keep their pointer."""
+        counts = {p: int(self.state[p]["step"].item()) for g in self.param_groups for p in g["params"]
+                  if len(self.state[p])}
+        base = max(counts.values()) if counts else 0
+        self._step_offset = {p: c - base for p, c in counts.items()}
+        self._step_dev[0].fill_(base)
+
+    def step_offset(self, p) -> int:
+        return self._step_offset.get(p, 0)
         self._lr_dev = None  # rewritten before the next replay (the table order stays until a capture sets it)
 
     @torch.no_grad()
@@ -72,11 +82,11 @@ class Adam(torch.optim.Optimizer):
         """state["step"] of every parameter from the device count (a device-to-host copy)."""
         if self._step_dev is None or not self._dev_ahead:
             return
-        n = float(self._step_dev[0].item())
+        n = int(self._step_dev[0].item())
         for g in self.param_groups:
             for p in g["params"]:
-                if len(self.state[p]):
-                    self.state[p]["step"] = torch.tensor(n)
+                if len(self.state[p]) and p in self._step_offset:
+                    self.state[p]["step"] = torch.tensor(float(n + self._step_offset[p]))
         self._dev_ahead = False
 
     def skipped_steps(self) -> int:
@@ -154,7 +164,7 @@ class Adam(torch.optim.Optimizer):
                 entries.append(_native.LsrAdamTensor(
                     p.numel(), p.data_ptr(), grad.data_ptr(), state["exp_avg"].data_ptr(),
                     state["exp_avg_sq"].data_ptr(), float(group["lr"]), float(beta1), float(beta2),
-                    float(group["eps"]), 0 if capturing else int(state["step"].item())))
+                    float(group["eps"]), self.step_offset(p) if capturing else int(state["step"].item())))
                 order.append(gi)
                 keep.append(grad)  # a contiguous copy lives until the launch is enqueued (stream order)
         if entries and fused is not None:
@@ -173,6 +183,7 @@ class Adam(torch.optim.Optimizer):
                 _native._check(_native.load().lsr_adam_multi(len(entries), table, float(grad_scale), sd, sk,
                                                              _native._stream(device)), "lsr_adam_multi")
             if not capturing and self._step_dev is not None:
-                # keep the device count equal to the host's (a later replay continues from it)
-                self._step_dev[0].fill_(int(max(float(self.state[p]["step"].item()) for p in self._params_with_grad())))
+                # keep the device count (and the offsets) equal to the host's counts: a later replay
+                # continues from them
+                self._seed_device_count()
         return loss

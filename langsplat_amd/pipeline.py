@@ -37,7 +37,8 @@ import os
 import torch
 
 from . import _native
-from .graph import _as_view, _fused_tail_enabled, _nullctx
+from .distributed import collective_capturable
+from .graph import _as_view, _fused_tail_enabled, _nullctx, capture_key, release_stale_accumulators
 
 
 class ViewPipeline:
@@ -85,22 +86,6 @@ class ViewPipeline:
         ev.record()
         self.ready = ev
 
-    def last_grads(self):
-        """The gradient tensors the last replay wrote (graph-owned; the first replay after a fused
-        capture has its own)."""
-        if self.k == 0:
-            raise RuntimeError("PipelinedGraphStep.last_grads: no replay yet")
-        if self.R > 1 and self.k <= self.R and self.g_rot0 is not None:
-            return self.g_rot0[1][self.k - 1]
-        if self.k == 1 and self.merged and self.g_comp0 is not None:
-            return self.grads0
-        return self.grads[(self.k - 1) % self.S]
-
-    def follow_caller(self):
-        """The next replays wait for everything the caller's stream holds now (e.g. parameters the
-        caller changed between replays)."""
-        self._since_capture = 0
-
     def synchronize(self):
         """The caller's current stream waits for every step enqueued so far."""
         cur = torch.cuda.current_stream()
@@ -121,7 +106,8 @@ class PipelinedGraphStep:
         G_geo[p]:  the geometry half of the view, into set p                  (stream B)
         G_comp[p]: the composite half of set p and the loss, then loss.backward() and
                    optimizer.step(skip=overflow[p])                             (stream A)
-                   (N > 1: the backward only; the bucket's all-reduce launched after it, G_adam[p])
+                   (N > 1: the bucket's all-reduce between the backward and Adam -- inside the
+                   graph with RCCL; with gloo launched between G_comp[p] and G_adam[p])
 
     are captured, and replay k runs (p = k % S; set r = (k + S - 1) % S receives view k + S - 1,
     S - 1 views ahead; its last reader was step k - 1):
@@ -147,10 +133,13 @@ class PipelinedGraphStep:
     forward_fn() renders one fixed view.
 
     The rasterizer runs in capacity mode (capacities from eager warm-up views, with headroom).  A
-    view over capacity is flagged per set; N = 1: the captured Adam skips on that flag (no parameter,
-    moment or step count changes: the view is left out, include/lsr.h lsr_adam_multi), check()
-    counts the skipped steps and re-captures.  N > 1: an over-capacity view contributes a zero
-    gradient to the all-reduce and every rank steps (the ranks stay identical).
+    view over capacity is flagged per set and the captured Adam skips on that flag (no parameter,
+    moment or step count changes: the view is left out, include/lsr.h lsr_adam_multi); check()
+    counts the skipped steps and re-captures.  N > 1: the flag is all-reduced in the same collective
+    as the gradients (GradBucket.all_reduce(flag=)), so when one rank's view overflowed EVERY rank
+    skips that step and re-captures: the ranks stay identical and no zero gradient is averaged in.
+    With RCCL the collective is captured inside the step graph (one stream-A graph per step, as at
+    N = 1); with gloo it runs between the backward and Adam graphs.
 
         g = PipelinedGraphStep(lambda: render(...)["language_l1"], [gaussians._language_feature], optimizer)
         for it in range(iterations):
@@ -171,8 +160,9 @@ class PipelinedGraphStep:
     only after this view's compositing), LSR_PG_PRIO=geo|step (stream priorities), LSR_PG_ROT."""
 
     def __init__(self, forward_fn, params, optimizer, headroom: float = 1.125, warmup: int = 2, bucket=None,
-                 slots=None, sets: int = None, rotation: int = None):
+                 slots=None, sets: int = None, rotation: int = None, model=None):
         self.forward_fn = forward_fn
+        self.model = model  # its active_sh_degree is part of the capture key (graph.capture_key)
         self.params = [p for p in params]
         self.optimizer = optimizer
         self.bucket = bucket
@@ -261,6 +251,10 @@ class PipelinedGraphStep:
             for j in range(S - 1):
                 self.slots[j].load(*_as_view(views[j]))
                 self._loaded[j] = self._assigned[j] = views[j]
+        # the caller's still-alive autograd graphs keep the parameters' AccumulateGrad nodes bound to
+        # their streams: released, so the warm-up and the captures create their own (graph.py)
+        self.key = capture_key(self.model, self.optimizer, self.params)
+        self.stale_released = release_stale_accumulators(self.params)
         self._measure(min_rendered, min_entries)
         self._reset_graphs()
         self.optimizer.prepare_capture()
@@ -276,11 +270,21 @@ class PipelinedGraphStep:
             with torch.cuda.stream(sa), caps[p], self.sets[p]:
                 self._fwd(p)
         sb.wait_stream(sa)
-        skip = None if self.bucket is not None else self.overflow  # N > 1: every rank steps
+        # N > 1: the all-reduce of the gradients (and, in the same collective, of the set's overflow
+        # flag: every rank then skips when one view overflowed) inside the step graph when the backend
+        # can be captured (RCCL), else launched between the backward and Adam graphs (gloo)
+        dev = self.params[0].device
+        coll_in_graph = self.bucket is not None and collective_capturable()
+        self.coll_in_graph = coll_in_graph
+        if coll_in_graph:  # the communicator exists before the capture (its creation is not capturable)
+            with torch.cuda.stream(sa):
+                self.bucket.all_reduce(average=True, flag=torch.zeros((), dtype=torch.int32, device=dev))
+            for q in self.params:
+                q.grad = None
         # N = 1 language step: Adam inside the backward's epilogue pass, which also writes the updated
         # feature into the NEXT set's records (the next composite needs no fill; the geometry call never
         # writes those slots, so it may run before, during or after)
-        fused = skip is not None and len(self.params) == 1 and _fused_tail_enabled()
+        fused = self.bucket is None and len(self.params) == 1 and _fused_tail_enabled()
         self.fused = fused
         comp_phase = _native.forward_phase.COMPOSITE_FILLED if fused else _native.forward_phase.COMPOSITE
         # fused: the first composite after a capture fills set 0's feature records itself (G_comp0, run
@@ -301,8 +305,10 @@ class PipelinedGraphStep:
         def step_body(p, loss):
             with update_ctx(p):  # the backward runs on its forward's stream (sa)
                 loss.backward(self._one)  # dL/dloss = 1 from a static tensor: no seed-fill kernel
-                if skip is not None:
-                    self.optimizer.step(skip=skip[p])
+                if coll_in_graph:
+                    self.bucket.all_reduce(average=True, flag=self.overflow[p])
+                if self.bucket is None or coll_in_graph:
+                    self.optimizer.step(skip=self.overflow[p])
 
         for p in range(S):
             if self.R > 1:
@@ -342,10 +348,10 @@ class PipelinedGraphStep:
                     step_body(p, loss)
                 self.g_step[p] = g
             self.grads[p] = [q.grad for q in self.params]  # this set's graph-owned gradients
-            if skip is None:  # the all-reduce sits between the backward and Adam graphs
+            if self.bucket is not None and not coll_in_graph:  # the all-reduce sits between two graphs
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, stream=sa):
-                    self.optimizer.step()
+                    self.optimizer.step(skip=self.overflow[p])
                 self.g_adam[p] = g
             self.static_loss[p] = loss.detach()  # the set's static loss tensor
             del loss
@@ -360,6 +366,7 @@ class PipelinedGraphStep:
         self.ev_cur = [torch.cuda.Event() for _ in range(S)]
         self._since_capture = 0
         self._fast = False
+        self._refill = False
         self.captures += 1
         return self
 
@@ -426,6 +433,9 @@ class PipelinedGraphStep:
             sa.wait_event(self.ev_geo[j * R])  # the group's geometry graph
             with torch.cuda.stream(sa):
                 self.optimizer.sync_lr()
+                if self._refill and self.fused and not (k == 0 and self.g_rot0 is not None):
+                    self._refill_records(j * R)  # the caller changed the parameter (follow_caller)
+                self._refill = False
                 g, _ = self.g_rot0 if (k == 0 and self.g_rot0 is not None) else self.g_rot[j]
                 g.replay()
             self.ev_rot[j].record(sa)
@@ -491,6 +501,8 @@ class PipelinedGraphStep:
         synchronize() inside the timed region."""
         if self.g_comp[0] is None and getattr(self, "g_rot", None) is None:
             self.capture()
+        elif (self.R == 1 or self.k % self.R == 0) and capture_key(self.model, self.optimizer, self.params) != self.key:
+            self._recapture(self.rendered, self.entries)  # an SH-degree step since the capture
         if self.R > 1:
             return self._replay_rotation(next_view, wait)
         S = self.S
@@ -542,6 +554,9 @@ class PipelinedGraphStep:
         with torch.cuda.stream(sa):
             self.optimizer.sync_lr()  # a changed learning rate: a host-to-device copy on stream A
             first = self.k == 0 and self.g_comp0 is not None
+            if self._refill and self.fused and not first:
+                self._refill_records(p)  # the caller changed the parameter (follow_caller)
+            self._refill = False
             (self.g_comp0 if first else self.g_comp[p]).replay()
             if not self.merged:
                 self.ev_comp[p].record(sa)
@@ -549,7 +564,7 @@ class PipelinedGraphStep:
             if self.g_adam[p] is not None:
                 for q, g in zip(self.params, self.grads[p]):
                     q.grad = g
-                self.bucket.all_reduce(average=True)
+                self.bucket.all_reduce(average=True, flag=self.overflow[p])
                 self.g_adam[p].replay()
         self.ev_step[p].record(sa)
         # view k + S - 1's geometry into set r
@@ -576,8 +591,17 @@ class PipelinedGraphStep:
 
     def follow_caller(self):
         """The next replays wait for everything the caller's stream holds now (e.g. parameters the
-        caller changed between replays)."""
+        caller changed between replays).  With the fused tail the previous step already wrote the
+        updated feature into the next set's records (COMPOSITE_FILLED never re-reads the parameter):
+        the next replay refills them from the parameter first."""
         self._since_capture = 0
+        self._refill = True
+
+    def _refill_records(self, p):
+        """Set p's records' language slots from the parameter as it is now (on the current stream),
+        for a composite that would otherwise blend what the previous step's fused tail wrote."""
+        radii = self.sets[p].tensors[("out", "radii")]
+        _native.fill_language(self.params[0], _native.RAW_LANGUAGE, radii, self._record_ptr(p))
 
     def synchronize(self):
         """The caller's current stream waits for every replay enqueued so far (both streams)."""
@@ -600,11 +624,15 @@ class PipelinedGraphStep:
         skipped = self.optimizer.skipped_steps() - self._skipped_base
         if skipped == 0 and all(int(o.item()) == 0 for o in self.overflow):
             return True
-        self.sync()
         for o in self.overflow:
             o.zero_()
-        # the replays continue with the views already loaded for the next S - 1 steps
+        self._recapture(2 * self.rendered, 2 * self.entries)
+        return False
+
+    def _recapture(self, min_rendered, min_entries):
+        """Capture again, continuing with the views already loaded for the next S - 1 steps."""
+        self.synchronize()
+        self.sync()
         src = self._assigned if self.R > 1 else self._loaded
         views = [src[(self.k + j) % self.S] for j in range(self.S - 1)] if self.slots else None
-        self.capture(2 * self.rendered, 2 * self.entries, views=views)
-        return False
+        self.capture(min_rendered, min_entries, views=views)

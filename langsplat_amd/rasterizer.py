@@ -52,14 +52,23 @@ def _cpu_deep_copy(args):
 
 def rasterize_gaussians(means3D, means2D, sh, colors_precomp, language_feature_precomp, opacities, scales,
                         rotations, cov3Ds_precomp, raster_settings):
+    # grad mode is read HERE: inside Function.forward it is always off, and ctx.needs_input_grad
+    # reflects requires_grad only (True under torch.no_grad() for a parameter that requires grad)
     return _RasterizeGaussians.apply(means3D, means2D, sh, colors_precomp, language_feature_precomp, opacities,
-                                     scales, rotations, cov3Ds_precomp, raster_settings)
+                                     scales, rotations, cov3Ds_precomp, raster_settings, torch.is_grad_enabled())
+
+
+def _forward_flags(ctx, grad_enabled: bool) -> int:
+    """A backward will follow (grad mode on and an input needs a gradient): the compositing kernel
+    clears its gradient records.  None will (inference, render.py:24-55 under torch.no_grad()):
+    LSR_FWD_NO_BACKWARD, the kernel writes no backward state."""
+    return _native.FWD_ZERO_GRAD_RECORDS if grad_enabled and any(ctx.needs_input_grad) else _native.FWD_NO_BACKWARD
 
 
 class _RasterizeGaussians(torch.autograd.Function):
     @staticmethod
     def forward(ctx, means3D, means2D, sh, colors_precomp, language_feature_precomp, opacities, scales, rotations,
-                cov3Ds_precomp, raster_settings):
+                cov3Ds_precomp, raster_settings, grad_enabled=True):
         if means3D.device.type != "cuda":
             raise RuntimeError("langsplat_amd rasterizer: inputs must be on a ROCm GPU device "
                                f"(got {means3D.device}); there is no CPU implementation")
@@ -69,9 +78,7 @@ class _RasterizeGaussians(torch.autograd.Function):
         lang_in = _f32(lang) if use_lang else None
         args = (_f32(means3D), _f32(sh), _f32(colors_precomp), lang_in, _f32(opacities), _f32(scales),
                 _f32(rotations), _f32(cov3Ds_precomp))
-        # a backward will follow: let the compositing kernel clear its gradient records; none will
-        # (inference, render.py:24-55 under torch.no_grad()): it writes no state for one
-        flags = _native.FWD_ZERO_GRAD_RECORDS if any(ctx.needs_input_grad) else _native.FWD_NO_BACKWARD
+        flags = _forward_flags(ctx, grad_enabled)
         ctx.records_zeroed = flags == _native.FWD_ZERO_GRAD_RECORDS
         if raster_settings.debug:
             cpu_args = _cpu_deep_copy(args)
@@ -121,7 +128,7 @@ class _RasterizeGaussians(torch.autograd.Function):
 
         return (want(0, g["means3D"]), want(1, g["means2D"]), want(2, g["shs"]), want(3, g["colors_precomp"]),
                 want(4, g["language_feature_precomp"] if ctx.use_lang else None), want(5, g["opacities"]),
-                want(6, g["scales"]), want(7, g["rotations"]), want(8, g["cov3D_precomp"]), None)
+                want(6, g["scales"]), want(7, g["rotations"]), want(8, g["cov3D_precomp"]), None, None)
 
 
 def rasterize_gaussians_fused(means3D, means2D, features_dc, features_rest, opacity_raw, scaling_raw, rotation_raw,
@@ -152,7 +159,7 @@ def rasterize_gaussians_fused(means3D, means2D, features_dc, features_rest, opac
         mask = mask.contiguous()
     color, lang, radii, visible, loss = _RasterizeGaussiansFused.apply(
         means3D, means2D, features_dc, features_rest, opacity_raw, scaling_raw, rotation_raw, language_feature_raw,
-        raster_settings, gt, mask)
+        raster_settings, gt, mask, torch.is_grad_enabled())
     out = (color, lang, radii, visible) if with_visibility else (color, lang, radii)
     return out + (loss,) if language_target is not None else out
 
@@ -173,7 +180,7 @@ def _guarded(rs, dump, msg, fn, args):
 class _RasterizeGaussiansFused(torch.autograd.Function):
     @staticmethod
     def forward(ctx, means3D, means2D, features_dc, features_rest, opacity_raw, scaling_raw, rotation_raw,
-                language_feature_raw, raster_settings, loss_target=None, loss_mask=None):
+                language_feature_raw, raster_settings, loss_target=None, loss_mask=None, grad_enabled=True):
         if means3D.device.type != "cuda":
             raise RuntimeError("langsplat_amd rasterizer: inputs must be on a ROCm GPU device "
                                f"(got {means3D.device}); there is no CPU implementation")
@@ -191,9 +198,7 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
             raise ValueError("the fused language loss needs include_feature=True")
         # without the fused loss this output is never handed to the caller (no fill kernel)
         loss = _native.output_tensor("loss", (), torch.float32, m3.device)
-        # a backward will follow: let the compositing kernel clear its gradient records; none will
-        # (inference, render.py:24-55 under torch.no_grad()): it writes no state for one
-        flags = _native.FWD_ZERO_GRAD_RECORDS if any(ctx.needs_input_grad) else _native.FWD_NO_BACKWARD
+        flags = _forward_flags(ctx, grad_enabled)
         ctx.records_zeroed = flags == _native.FWD_ZERO_GRAD_RECORDS
         # the language step (train.py:96-104): the loss is the fused language loss, so the colour
         # image is expected off the loss path and the split-replay states skip the colour sums; a
@@ -272,7 +277,7 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
             d_rest = torch.zeros(ctx.rest_shape, dtype=torch.float32, device=m3.device)
         return (want(0, g["means3D"]), want(1, g["means2D"]), want(2, g["shs"]), want(3, d_rest),
                 want(4, g["opacities"]), want(5, g["scales"]), want(6, g["rotations"]),
-                want(7, g["language_feature_precomp"] if ctx.use_lang else None), None, None, None)
+                want(7, g["language_feature_precomp"] if ctx.use_lang else None), None, None, None, None)
 
 
 class GaussianRasterizer(nn.Module):

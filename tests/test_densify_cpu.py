@@ -83,3 +83,54 @@ def test_clone_split_prune_bookkeeping():
     st = opt.state[m._xyz]
     assert not st["exp_avg"][n_keep:].any() and st["exp_avg"][:n_keep].abs().sum() > 0
     assert d.xyz_gradient_accum.shape == (P1, 1) and not d.xyz_gradient_accum.any() and not d.denom.any()
+
+
+def _reference_reset_opacity(model, optimizer):
+    """scene/gaussian_model.py:277-281 and replace_tensor_to_optimizer :326-339, restated with the
+    reference's torch operations (the module itself imports CUDA-only extensions)."""
+    op = torch.sigmoid(model._opacity)
+    x = torch.min(op, torch.ones_like(op) * 0.01)
+    opacities_new = torch.log(x / (1 - x))  # utils/general_utils.py:18-19 inverse_sigmoid
+    for group in optimizer.param_groups:
+        if group["name"] == "opacity":
+            stored_state = optimizer.state.get(group["params"][0], None)
+            stored_state["exp_avg"] = torch.zeros_like(opacities_new)
+            stored_state["exp_avg_sq"] = torch.zeros_like(opacities_new)
+            del optimizer.state[group["params"][0]]
+            group["params"][0] = torch.nn.Parameter(opacities_new.requires_grad_(True))
+            optimizer.state[group["params"][0]] = stored_state
+            model._opacity = group["params"][0]
+
+
+def test_reset_opacity_matches_the_reference_ops():
+    """Densifier.reset_opacity (train.py:132-133): the same raw opacities bit for bit as the
+    reference's ops, zero moments, the step count kept, the other groups untouched, and the next
+    optimizer step (same iteration, train.py:135-137) leaves the opacity alone (no .grad)."""
+    torch.manual_seed(1)
+    m, opt, names = _setup(P=300)
+    with torch.no_grad():
+        m._opacity[:5] = torch.tensor([-8.0, -4.6, -4.5951, 0.0, 3.0]).view(5, 1)  # below, at, above 0.01
+    ref_m, ref_opt, _ = _setup(P=300)
+    with torch.no_grad():
+        for a in names.values():
+            getattr(ref_m, a).copy_(getattr(m, a))
+    for (pa, pb) in zip([g["params"][0] for g in opt.param_groups], [g["params"][0] for g in ref_opt.param_groups]):
+        for k in ("exp_avg", "exp_avg_sq"):
+            ref_opt.state[pb][k].copy_(opt.state[pa][k])
+    others = {n: getattr(m, a) for n, a in names.items() if n != "opacity"}
+    old = m._opacity
+    Densifier(m, opt).reset_opacity()
+    _reference_reset_opacity(ref_m, ref_opt)
+    assert m._opacity is not old and m._opacity.grad is None and m._opacity.requires_grad
+    assert torch.equal(m._opacity.detach(), ref_m._opacity.detach())
+    assert float(torch.sigmoid(m._opacity).max()) <= 0.01 + 1e-7
+    st = opt.state[m._opacity]
+    assert old not in opt.state and not st["exp_avg"].any() and not st["exp_avg_sq"].any()
+    assert int(st["step"].item()) == int(ref_opt.state[ref_m._opacity]["step"].item()) == 1
+    grp = next(g for g in opt.param_groups if g["name"] == "opacity")
+    assert grp["params"][0] is m._opacity
+    for n, p in others.items():
+        assert getattr(m, names[n]) is p
+    before = m._opacity.detach().clone()
+    opt.step()  # the same iteration's step: the old tensor's .grad is gone with it
+    assert torch.equal(m._opacity.detach(), before)

@@ -161,3 +161,47 @@ def test_densification_statistics_sum_over_views(tmp_path, world, average):
         np.testing.assert_array_equal(np.load(tmp_path / f"denom_{r}.npy"), denom.numpy().astype(np.float32))
         np.testing.assert_array_equal(np.load(tmp_path / f"maxr_{r}.npy"), max_radii.numpy().astype(np.float32))
     assert denom.max() > 2.0 + world  # the views overlap: some Gaussians counted by several ranks
+
+
+def _flag_worker(rank, world, port, out_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        lang = torch.nn.Parameter(torch.zeros((150, 3)))
+        opac = torch.nn.Parameter(torch.zeros((150, 1)))
+        out = {}
+        for mode, params in (("direct", [lang]), ("flat", [lang, opac])):
+            bucket = GradBucket(params)
+            assert bucket.direct == (mode == "direct")
+            for step, over in enumerate((None, world - 1)):  # no rank overflows, then only the last one
+                bucket.zero()
+                lang.grad = torch.full((150, 3), float(rank + 1)) if bucket.direct else lang.grad.add_(rank + 1)
+                # the rasterizer's overflow flag: 0, or the bits of 1.0f (include/lsr.h)
+                flag = torch.tensor(0x3F800000 if rank == over else 0, dtype=torch.int32)
+                bucket.all_reduce(average=True, flag=flag)
+                out[f"{mode}{step}_grad"] = lang.grad.clone()
+                out[f"{mode}{step}_flag"] = int(flag.item())
+        torch.save(out, os.path.join(out_dir, f"flag_{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_overflow_flag_rides_the_gradient_collective(tmp_path, world):
+    """a view over capacity on ONE rank sets the flag on EVERY rank (the flag is
+    all-reduced in the same collective as the gradients), so every rank skips the optimizer step and
+    the ranks stay identical; the gradients are averaged as without the flag (direct and flat)."""
+    port = _free_port()
+    mp.spawn(_flag_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True)
+    outs = [torch.load(tmp_path / f"flag_{r}.pt", weights_only=True) for r in range(world)]
+    mean = sum(range(1, world + 1)) / world
+    for o in outs:
+        for mode in ("direct", "flat"):
+            assert o[f"{mode}0_flag"] == 0
+            assert o[f"{mode}1_flag"] != 0  # non-zero as an int: Adam's skip test
+            for step in (0, 1):
+                torch.testing.assert_close(o[f"{mode}{step}_grad"], torch.full((150, 3), mean))
+    for r in range(1, world):
+        for k, v in outs[r].items():
+            assert (torch.equal(v, outs[0][k]) if torch.is_tensor(v) else v == outs[0][k]), k

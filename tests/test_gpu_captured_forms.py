@@ -412,7 +412,7 @@ def test_overflowed_view_is_a_noop_for_the_optimizer(form, monkeypatch):
             losses.append(gs.replay(view=v).clone())
             torch.cuda.synchronize()
             if i == bad:
-                assert int(gs.overflow.item()) == 1
+                assert gs.overflow.view(torch.float32).item() == 1.0  # the bits of 1.0f (include/lsr.h)
                 assert not m._language_feature.grad.any()  # nothing rasterized: a zero gradient
         snaps.append(_snap(m, opt))
         assert opt.skipped_steps() == 1
@@ -430,7 +430,7 @@ def test_overflowed_view_is_a_noop_for_the_optimizer(form, monkeypatch):
             pg.synchronize()
             torch.cuda.synchronize()
             if k == bad:
-                assert int(pg.overflow[k % S].item()) == 1
+                assert pg.overflow[k % S].view(torch.float32).item() == 1.0
                 assert not pg.last_grads()[0].any()
         snaps.append(_snap(m, opt))
         assert opt.skipped_steps() == 1
@@ -582,3 +582,60 @@ def test_fused_tail_matches_separate_launches(form, monkeypatch):
     for k, (a, b) in enumerate(zip(gf, gs_)):
         assert_grad_close(f"{form} step {k} language gradient", a.cpu().numpy(), b.cpu().numpy())
     assert_states_close(sf, ss, f"{form} fused vs separate tail")
+
+
+# ---- a parameter changed by the caller between fused replays ----------------------------------------
+
+@pytest.mark.parametrize("sets,rot", [(2, 1), (3, 1), (4, 2)])
+def test_parameter_change_between_fused_replays(sets, rot, monkeypatch):
+    """with the fused tail, step k writes the updated feature into the next set's
+    records, whose composite (LSR_PHASE_COMPOSITE_FILLED) never re-reads the parameter.  The caller
+    edits the language feature between replays and calls follow_caller(): the next replay refills
+    those records from the parameter, so every loss and the final state equal the eager loop with the
+    same edit at the same point (without the refill the next composite blends the stale feature)."""
+    monkeypatch.setenv("LANGSPLAT_AMD_FUSED", "1")
+    monkeypatch.setenv("LSR_FUSED_TAIL", "1")
+    P, W, H = 60000, 640, 360
+    g = make_gaussians(P, seed=9, scale_range=(0.004, 0.03))
+    cams = make_cameras(8, W, H, device=DEV)
+    views = []
+    for v in (0, 3, 6, 1, 5, 2, 7, 4):
+        gt, mask = bench_target(H, W, v)
+        views.append((cams[v], gt.to(DEV), mask.to(DEV)))
+    edit_after = 3  # a multiple of the rotation: edits land between rotation groups
+
+    def edit(m):
+        with torch.no_grad():
+            m._language_feature.mul_(-0.5).add_(0.25)
+
+    me = _frozen_model(g)
+    oe = _adam(me, lr=0.01)
+    losses_e = []
+    for k, (cam, gt, mask) in enumerate(views):
+        losses_e.append(_eager_step(me, oe, cam, gt, mask))
+        if k + 1 == edit_after + (edit_after % rot):
+            edit(me)
+    se = _state(me, oe)
+    m = _frozen_model(g)
+    opt = _adam(m, lr=0.01)
+    slots = [ViewSlot(*views[0]) for _ in range(sets)]
+    pg = PipelinedGraphStep(_slot_forward(m), [m._language_feature], opt, slots=slots, rotation=rot)
+    pg.capture(1 << 22, 1 << 20, views=views[:sets - 1])
+    assert pg.fused
+    losses = []
+    for k in range(len(views)):
+        nxt = views[k + sets - 1] if k + sets - 1 < len(views) else None
+        losses.append(pg.replay(next_view=nxt).clone())
+        if k + 1 == edit_after + (edit_after % rot):
+            pg.synchronize()
+            edit(m)
+            pg.follow_caller()
+    pg.synchronize()
+    torch.cuda.synchronize()
+    assert pg.check() and pg.captures == 1
+    pg.sync()
+    if rot == 1:
+        torch.testing.assert_close(torch.stack(losses), torch.stack(losses_e), rtol=1e-5, atol=0)
+    else:  # rotation: only the last R losses are still theirs
+        torch.testing.assert_close(torch.stack(losses[-rot:]), torch.stack(losses_e[-rot:]), rtol=1e-5, atol=0)
+    assert_states_close(_state(m, opt), se, f"edited between replays, {sets} sets, rotation {rot}")

@@ -17,8 +17,22 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
+def _spy_flags(monkeypatch):
+    """Record the forward flags every native forward call receives (the NO_BACKWARD path
+    must really be taken under torch.no_grad(), not only produce the same images)."""
+    seen = []
+    real = _native.rasterize_gaussians
+
+    def spy(*a, **kw):
+        seen.append(int(kw.get("flags", 0)))
+        return real(*a, **kw)
+    monkeypatch.setattr(_native, "rasterize_gaussians", spy)
+    return seen
+
+
 @pytest.mark.parametrize("with_loss", [False, True])
-def test_inference_forward_matches_training_forward_c3(with_loss):
+def test_inference_forward_matches_training_forward_c3(with_loss, monkeypatch):
+    seen = _spy_flags(monkeypatch)
     c = CONFIGS["C3"]
     P, W, H = c["P"], c["width"], c["height"]
     model = bench.Model(make_gaussians(P, seed=0).to(DEV), include_feature=True)
@@ -37,10 +51,38 @@ def test_inference_forward_matches_training_forward_c3(with_loss):
     with torch.no_grad():
         infer = bench.render(cam, model, bench.Pipe, bg, bench.Opt, **kw)
     torch.cuda.synchronize()
+    # the training forward cleared its gradient records; the inference forward wrote no backward state
+    assert len(seen) == 2 and seen[0] & _native.FWD_ZERO_GRAD_RECORDS and not seen[0] & _native.FWD_NO_BACKWARD
+    assert seen[1] == _native.FWD_NO_BACKWARD
     keys = ["render", "language_feature_image", "radii"] + (["language_l1"] if with_loss else [])
     for k in keys:
         assert torch.equal(infer[k], out_t[k]), k
     assert int((out_t["radii"] > 0).sum()) > 0.3 * P
+
+
+def test_unfused_rasterizer_under_no_grad_takes_the_inference_flag(monkeypatch):
+    """GaussianRasterizer (the unfused autograd Function) with inputs that require grad: under
+    torch.no_grad() the forward passes LSR_FWD_NO_BACKWARD, with grad on FWD_ZERO_GRAD_RECORDS, and
+    both give the same images."""
+    from langsplat_amd.rasterizer import GaussianRasterizer
+    seen = _spy_flags(monkeypatch)
+    st, inp = scene(P=3000, W=96, H=64, seed=4, scale_range=(0.03, 0.2))
+    std, ind = to_device(st, inp, DEV)
+    leaves = {k: v.clone().requires_grad_(True) for k, v in ind.items()}
+    outs = []
+    for grad in (True, False):
+        with torch.set_grad_enabled(grad):
+            m2 = torch.zeros_like(leaves["means3D"], requires_grad=True)
+            c, lg, r = GaussianRasterizer(std)(
+                means3D=leaves["means3D"], means2D=m2, opacities=leaves["opacities"], shs=leaves["shs"],
+                language_feature_precomp=leaves["language_feature_precomp"], scales=leaves["scales"],
+                rotations=leaves["rotations"])
+            assert c.requires_grad == grad
+            outs.append((c.detach().clone(), lg.detach().clone(), r.clone()))
+    torch.cuda.synchronize()
+    assert seen == [_native.FWD_ZERO_GRAD_RECORDS, _native.FWD_NO_BACKWARD]
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
 
 
 def test_backward_after_inference_forward_is_refused_under_debug():
