@@ -39,7 +39,6 @@ sys.path.insert(0, ROOT)
 
 from langsplat_amd import _native  # noqa: E402
 from langsplat_amd.distributed import GradBucket, init_from_env  # noqa: E402
-from langsplat_amd.graph import GraphedStep  # noqa: E402
 from langsplat_amd.optim import Adam as AmdAdam  # noqa: E402
 from langsplat_amd.pipeline import PipelinedGraphStep, ViewPipeline  # noqa: E402
 from langsplat_amd.render import render  # noqa: E402
@@ -495,55 +494,18 @@ def main():
         elapsed_pipe = time.perf_counter() - tp
         del pipe
 
-    # the timed step: render + loss + backward captured once into a HIP graph (langsplat_amd.graph;
-    # the rasterizer in capacity mode, no host wait), replayed, then [N > 1: the all-reduce] and Adam
-    run = step
+    # The serial HIP-graph form (langsplat_amd.graph.GraphedStep: the whole step as one graph per
+    # replay) is not timed here: its kernels sum to the eager step's (502.6 vs 498.8 us under the
+    # kernel tracer, profiles/r05_graph_vs_eager.txt), and each replay adds a graph boundary (idle
+    # queue between consecutive graph launches) that the eager launches do not pay
+    # (driver, round 4: 0.521 vs 0.497 ms).  The pipelined graph below is the captured form.
     graphed = fused and os.environ.get("LSR_GRAPH", "1") != "0"
-    if graphed:
-        def fwd_bwd():
-            loss = render(cam, model, Pipe, bg, Opt, language_target=(gt, mask))["language_l1"]
-            loss.backward()
-            return loss
-        # Adam inside the graph too (its step count advanced on the device); N > 1: the all-reduce
-        # (with the overflow flag) before it, inside the graph with RCCL
-        gstep = GraphedStep(fwd_bwd, model.trainable(), optimizer=optim, bucket=bucket, model=model)
-        gstep.capture()
-
-        def run():
-            return gstep.replay()
-        for _ in range(3):
-            run()
-        torch.cuda.synchronize()
-        if not gstep.check():
-            run()
-            torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        run()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if graphed and not gstep.check():
-        raise RuntimeError("a captured view exceeded its capacities during the timed steps")
-    # the same steps with train.py:108's loss.item() after each (a device-to-host sync per step: the
-    # host cannot run ahead into the next step), reported beside `value` as ms_per_step_with_sync
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    ts = time.perf_counter()
-    for _ in range(args.steps):
-        run().item()
-    torch.cuda.synchronize()
-    elapsed_sync = time.perf_counter() - ts
     # (6) the pipelined order as HIP graphs on two streams (langsplat_amd.pipeline.PipelinedGraphStep):
     # each replay is one full step -- this view's compositing, loss, backward and Adam on one stream, the
     # next view's geometry stages (the forward's first half) on the other -- with no host work inside
-    elapsed_pg = float("inf")
+    elapsed_pg = elapsed_sync = float("inf")
     pg_rot = None
+    pg_reps = []
     if graphed and os.environ.get("LSR_PIPELINE", "1") != "0":
         # N > 1: the bucket's all-reduce (RCCL) is launched between each set's backward and Adam graphs
         # rotation (N = 1): R steps per stream-A graph (pipeline.py), R dividing the timed steps
@@ -578,6 +540,29 @@ def main():
         elapsed_pg = time.perf_counter() - tq
         if not pg.check():
             raise RuntimeError("a pipelined view exceeded its capacities during the timed steps")
+        # the spread of this form over further reps of the same K steps (not `value`: the run-to-run
+        # levels of DESIGN.md §5b), and train.py:108's loss.item() after every step
+        # (ms_per_step_with_sync: a device-to-host sync per step, no run-ahead)
+        for _ in range(int(os.environ.get("LSR_BENCH_REPS", "4"))):
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize()
+            tr = time.perf_counter()
+            for _ in range(args.steps):
+                pg.replay()
+            pg.synchronize()
+            torch.cuda.synchronize()
+            pg_reps.append(1000.0 * (time.perf_counter() - tr) / args.steps)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        ts = time.perf_counter()
+        for _ in range(args.steps):
+            pg.replay().item()
+        torch.cuda.synchronize()
+        elapsed_sync = time.perf_counter() - ts
+        if not pg.check():
+            raise RuntimeError("a pipelined view exceeded its capacities during the timed steps")
         del pg
     gc.enable()
     # the RGB stage's step on the same scene and view (all six groups trainable, L1 + SSIM, densification
@@ -601,8 +586,7 @@ def main():
 
     # `value`: the fastest of the full-step forms timed above (each does the whole step's work; the
     # others are reported beside it)
-    forms = {"graph" if graphed else "eager": elapsed, "eager": elapsed_eager, "pipelined": elapsed_pipe,
-             "pipelined_graph": elapsed_pg}
+    forms = {"eager": elapsed_eager, "pipelined": elapsed_pipe, "pipelined_graph": elapsed_pg}
     names = sorted(forms)
     t = torch.tensor([min(forms[n], 1e30) for n in names] + [float(blends)], dtype=torch.float64, device=dev)
     if world > 1:
@@ -689,11 +673,13 @@ def main():
                    "gradients": "all geometry" if _native.FORCE_GEOMETRY_GRADS else
                                 "as needed: means2D + language feature (geometry frozen, "
                                 "scene/gaussian_model.py:203-217)"},
-        "ms_per_step_with_sync": round(1000.0 * elapsed_sync / args.steps, 4),
+        "ms_per_step_with_sync": round(1000.0 * elapsed_sync / args.steps, 4) if elapsed_sync < 1e29 else None,
+        "pipelined_graph_reps_ms": {"reps": [round(x, 4) for x in pg_reps],
+                                    "median": round(float(np.median(pg_reps)), 4) if pg_reps else None,
+                                    "min": round(min(pg_reps), 4) if pg_reps else None,
+                                    "max": round(max(pg_reps), 4) if pg_reps else None},
         "ms_per_step_eager": round(1000.0 * elapsed_eager / args.steps, 4),
-        "step_form": {"graph": ("HIP graph replay (render + loss + backward + Adam)" if world == 1 else
-                                "HIP graph replay (render + loss + backward + RCCL all-reduce + Adam)"),
-                      "eager": "eager launches, one stream",
+        "step_form": {"eager": "eager launches, one stream",
                       "pipelined": "eager launches, consecutive views on two streams (the next view's geometry "
                                    "beside this view's backward" + (", RCCL all-reduce" if world > 1 else "")
                                    + " and Adam)",

@@ -360,6 +360,11 @@ uint32_t lsr_debug_set_spin_limit(uint32_t limit);
  * the bucket's key count, the end times of the first pass, of all passes and of the output gathers,
  * and the time the bucket's keys had arrived (synchronous). */
 int32_t lsr_debug_bucket_timeline(uint32_t* out, int32_t n);
+/* Measurement aid (ABI 14): a one-wave kernel on `stream` reads the shader-clock counter (s_memtime)
+ * and the constant 100 MHz counter (s_memrealtime) before and after a ~20 us spin and stores the four
+ * values into out_device[0..3] (a device array of 4 u64): the engine clock the chip ran at meanwhile
+ * is 100 (out[3] - out[1]) / (out[2] - out[0]) MHz (tools/clock_probe.py). */
+int32_t lsr_debug_clock_probe(uint64_t* out_device, void* stream);
 
 /* ---- the language-feature loss around the rasterizer ----------------
  *

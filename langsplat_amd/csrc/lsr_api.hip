@@ -860,6 +860,15 @@ int32_t lsr_debug_bucket_timeline(uint32_t* out, int32_t n)
     return LSR_OK;
 }
 
+int32_t lsr_debug_clock_probe(uint64_t* out_device, void* stream_ptr)
+{
+    if (!out_device) return fail(LSR_ERR_INVALID, "lsr_debug_clock_probe: invalid argument");
+    hipStream_t stream = reinterpret_cast<hipStream_t>(stream_ptr);
+    const bool debug = false;
+    LSR_TRY(launch_clock_probe(out_device, stream), "clock probe");
+    return LSR_OK;
+}
+
 int32_t lsr_mark_visible(int32_t P, const float* means3D, const float* viewmatrix, const float* projmatrix,
                          uint8_t* visible, void* stream_ptr)
 {

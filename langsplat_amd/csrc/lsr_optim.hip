@@ -320,4 +320,28 @@ hipError_t launch_adam(int64_t n, float* param, const float* grad, float* exp_av
     return hipGetLastError();
 }
 
+// ---- measurement aid: the engine clock over a ~20 us window (lsr_debug_clock_probe) ----
+__global__ void k_clock_probe(uint64_t* out)
+{
+    const uint64_t r0 = wall_clock64(), c0 = clock64();
+    uint64_t r1 = r0, c1 = c0;
+    while (r1 - r0 < 2000) {  // 2000 ticks of the 100 MHz counter
+        __builtin_amdgcn_s_sleep(1);
+        r1 = wall_clock64();
+        c1 = clock64();
+    }
+    if (threadIdx.x == 0) {
+        out[0] = r0;
+        out[1] = c0;
+        out[2] = r1;
+        out[3] = c1;
+    }
+}
+
+hipError_t launch_clock_probe(uint64_t* out, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_clock_probe, dim3(1), dim3(64), 0, s, out);
+    return hipGetLastError();
+}
+
 }  // namespace lsr
