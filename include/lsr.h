@@ -98,7 +98,12 @@ enum lsr_raw_flags {
  * buffer's final transmittance and contributor counts.  With settings.debug a backward of such a
  * forward fails with LSR_ERR_INVALID. */
 enum lsr_forward_flags { LSR_FWD_ZERO_GRAD_RECORDS = 1, LSR_FWD_NO_COLOR_GRAD = 2, LSR_FWD_NO_BACKWARD = 4 };
-enum lsr_backward_flags { LSR_BWD_RECORDS_ZEROED = 1 };
+/* LSR_BWD_SHARED_CU (ABI 14): another stream's kernels run beside this backward (the pipelined step,
+ * langsplat_amd/pipeline.py: the next view's preprocess, sort and binning).  The render backward
+ * then runs at most 6 workgroups per CU instead of 8 (extra dynamic LDS), leaving wave slots and LDS
+ * to the other stream's workgroups: measured at C3, 0.417-0.421 -> 0.400-0.401 ms per pipelined step
+ * (DESIGN.md §5b).  Results are unchanged. */
+enum lsr_backward_flags { LSR_BWD_RECORDS_ZEROED = 1, LSR_BWD_SHARED_CU = 2 };
 
 /* GaussianRasterizationSettings (gaussian_renderer/__init__.py:37-51), device-pointer form. */
 typedef struct lsr_settings {

@@ -28,7 +28,7 @@ ADAM_WORD_SKIPPED, ADAM_WORD_LR = 49, 50  # LSR_ADAM_WORD_SKIPPED / LSR_ADAM_WOR
 # lsr_raw_flags (include/lsr.h): inputs are GaussianModel's raw parameters
 RAW_OPACITY, RAW_SCALES, RAW_ROTATIONS, RAW_LANGUAGE = 1, 2, 4, 8
 FWD_ZERO_GRAD_RECORDS, FWD_NO_COLOR_GRAD, FWD_NO_BACKWARD = 1, 2, 4  # lsr_forward_flags
-BWD_RECORDS_ZEROED = 1     # lsr_backward_flags
+BWD_RECORDS_ZEROED, BWD_SHARED_CU = 1, 2  # lsr_backward_flags
 _vp = ctypes.c_void_p
 
 

@@ -615,7 +615,7 @@ int32_t lsr_backward(const lsr_settings* s, const lsr_backward_args* a, lsr_allo
     }
     if (a->raw & ~(LSR_RAW_OPACITY | LSR_RAW_SCALES | LSR_RAW_ROTATIONS | LSR_RAW_LANGUAGE))
         return fail(LSR_ERR_INVALID, "lsr_backward: unknown raw flag");
-    if (a->flags & ~LSR_BWD_RECORDS_ZEROED) return fail(LSR_ERR_INVALID, "lsr_backward: unknown flag");
+    if (a->flags & ~(LSR_BWD_RECORDS_ZEROED | LSR_BWD_SHARED_CU)) return fail(LSR_ERR_INVALID, "lsr_backward: unknown flag");
     if (geometry && a->shs_rest && (!a->shs || a->M < 2 || !a->dL_dsh_rest))
         return fail(LSR_ERR_INVALID, "lsr_backward: shs_rest needs shs, M >= 2 and dL_dsh_rest");
     if ((a->raw & LSR_RAW_OPACITY) && P > 0 && !a->opacities)
@@ -695,6 +695,7 @@ int32_t lsr_backward(const lsr_settings* s, const lsr_backward_args* a, lsr_allo
     rp.grad = grad;
     rp.fwd_flags = reinterpret_cast<uint32_t*>(image + L.counters) + kCntFwdFlags;
     rp.geo = geometry ? 1 : 0;
+    rp.shared_cu = (a->flags & LSR_BWD_SHARED_CU) ? 1 : 0;
     if (a->num_rendered > 0) LSR_TRY(launch_render_backward(rp, L.tiles, stream), "render backward");
     if (a->update) {
         // the language step's tail in one pass: epilogue + Adam (+ the next forward's feature slots)

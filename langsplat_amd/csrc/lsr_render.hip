@@ -1453,6 +1453,43 @@ hipError_t render_timeline_read(uint32_t* out, int kernel, int n)
     return hipSuccess;
 }
 
+// LSR_BWD_SHARED_CU: the dynamic LDS that caps a backward workgroup's CU at kSharedWgs workgroups
+// (kSharedWgs x (static + pad) fits the CU's 160 KiB, one more does not), so that the pipelined
+// step's other stream finds wave slots beside it.  Measured at C3 for the language-step variant
+// (18704 B static; tools/pg_host.py with LSR_BWD_PAD, profiles/r05_occupancy_sweep.txt): 8 workgroups
+// per CU (no pad) 0.417-0.421 ms per step; 7 with 18.6 KB of LDS left over (pad 2048) 0.406; 7 with
+// 4.2 KB left (pad 4096) 0.400-0.401; 6 (pad 5120) 0.478; 5 (pad 8192) 0.416.  So the pad is the
+// largest that still fits 7.  LSR_BWD_SHARE=0 disables it (LSR_BWD_PAD then applies).
+constexpr int kSharedWgs = 7;
+constexpr size_t kCuLds = 160 * 1024;
+template <int V>
+static size_t shared_pad_of()
+{
+    hipFuncAttributes at{};
+    size_t stat = 20 * 1024;
+    if (hipFuncGetAttributes(&at, (const void*)k_render_backward<false, (V & 1) != 0, (V & 2) != 0, (V & 4) != 0>) ==
+        hipSuccess)
+        stat = at.sharedSizeBytes;
+    // rounded down to 1 KiB: the LDS allocation granularity must not push the 7th workgroup out
+    const size_t per = (kCuLds / kSharedWgs) & ~(size_t)1023;  // kSharedWgs of them fit, one more does not
+    const size_t pad = per > stat && per * (kSharedWgs + 1) > kCuLds ? per - stat : 0;
+    if (getenv("LSR_BWD_SHARE_PRINT")) fprintf(stderr, "lsr: backward variant %d static LDS %zu pad %zu\n", V, stat, pad);
+    return pad;
+}
+
+static size_t shared_cu_pad(int variant)
+{
+    static const bool on = [] {
+        const char* e = getenv("LSR_BWD_SHARE");
+        return !(e && e[0] == '0');
+    }();
+    if (!on) return backward_pad();
+    // variant bits (launch_render_backward): 1 feature, 2 colour, 4 geometry
+    static const size_t pad[8] = {shared_pad_of<0>(), shared_pad_of<1>(), shared_pad_of<2>(), shared_pad_of<3>(),
+                                  shared_pad_of<4>(), shared_pad_of<5>(), shared_pad_of<6>(), shared_pad_of<7>()};
+    return pad[variant & 7];
+}
+
 hipError_t launch_render_backward(const RenderParams& pin, int tiles, hipStream_t s)
 {
     if (tiles == 0) return hipSuccess;
@@ -1465,9 +1502,10 @@ hipError_t launch_render_backward(const RenderParams& pin, int tiles, hipStream_
     if (!p.sched_counts || !split_replay()) p.split_pool = nullptr;
     if (p.split_pool) tiles *= kSplitItems;  // the items: up to kSplitItems chunks per tile
     if (render_stats_on()) tiles = debug_grid(tiles);
+    const size_t pad = p.shared_cu && !render_stats_on() ? shared_cu_pad(variant) : backward_pad();
 #define LSR_BWD(S, V)                                                                                         \
     hipLaunchKernelGGL((k_render_backward<S, (V & 1) != 0, (V & 2) != 0, (V & 4) != 0>), dim3(tiles), \
-                       dim3(kTilePixels), backward_pad(), s, p)
+                       dim3(kTilePixels), pad, s, p)
 #define LSR_BWD_ALL(S)            \
     switch (variant) {            \
     case 0: LSR_BWD(S, 0); break; \

@@ -206,6 +206,11 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
         ctx.no_color = fuse_loss and ctx.records_zeroed
         if ctx.no_color:
             flags |= _native.FWD_NO_COLOR_GRAD
+        # a pipelined step (the composite half of a split forward, or a forward deferring the feature
+        # to another stream's update): another stream's kernels run beside this view's backward
+        ctx.shared_cu = (_native.forward_phase.active() in (_native.forward_phase.COMPOSITE,
+                                                            _native.forward_phase.COMPOSITE_FILLED)
+                         or _native.language_ready.active() is not None)
 
         def run(fwd_flags, vis, out_loss):
             return _guarded(raster_settings, "snapshot_fw.dump",
@@ -253,7 +258,8 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
         rest = rest if rest.numel() > 0 else None  # grad_out_color None: zero colour gradient
         gl = grad_out_language_feature if ctx.use_lang else None
         geometry = _native.geometry_grads_needed(ctx.needs_input_grad, (0, 2, 3, 4, 5, 6))
-        flags = _native.BWD_RECORDS_ZEROED if ctx.records_zeroed else 0
+        flags = (_native.BWD_RECORDS_ZEROED if ctx.records_zeroed else 0) | (
+            _native.BWD_SHARED_CU if ctx.shared_cu else 0)
         ctx.records_zeroed = False  # a second backward (retain_graph) clears its own records
         # a captured N = 1 language step may fuse its Adam step into this backward's epilogue
         fu = _native.fused_update.active()
