@@ -78,7 +78,7 @@ def test_capacity_overflow_is_flagged_and_safe(short):
     ovf = torch.zeros((), dtype=torch.int32, device=DEV)
     cap = _native.capacity(R // 2, E, ovf) if short == "rendered" else _native.capacity(R, E // 2, ovf)
     out = _forward(std, ind, cap)
-    assert int(ovf.item()) == 1
+    assert ovf.view(torch.float32).item() == 1.0  # the bits of 1.0f (include/lsr.h)
     bg = torch.tensor([0.25, 0.5, 0.75], device=DEV).view(3, 1, 1).expand(3, H, W)
     assert torch.equal(out[1], bg) and not out[2].any()
     assert not state(out, P, W, H)["n_contrib"].any()
@@ -213,7 +213,7 @@ def test_capacity_mode_lsd_depth_order(monkeypatch):
     np.testing.assert_array_equal(state(c_wide, P, W, H)["point_list"][:Rw], state(e_wide, P, W, H)["point_list"])
     _forward(*narrow)  # the thread's last eager view now needs fewer passes
     c2 = _forward(*wide, cap=_native.capacity(Rw, Ew, ovf))
-    assert int(ovf.item()) == 1 and not c2[2].any()
+    assert ovf.view(torch.float32).item() == 1.0 and not c2[2].any()
     _forward(*wide)
     c3 = _forward(*wide, cap=_native.capacity(Rw, Ew, ovf))
     assert int(ovf.item()) == 0 and torch.equal(c3[1], e_wide[1])
