@@ -256,7 +256,7 @@ STAGE_KERNEL = {"render backward": "lsr::k_render_backward<false, true, false, f
 # profiles this round's bench reads its PMC figures from: profiles/<ROUND>_<config>_{summary,valu}.json
 # (tools/profile_round.sh + tools/prof_summary.py, tools/pmc_valu.sh + tools/valu_summary.py).  A
 # profile of another round or another config is never used: its field is then null.
-ROUND = "r04"
+ROUND = "r05"
 CUS = 256
 CLOCK_HZ = 2.4e9  # MI355X_MICROARCH.md: max engine clock (what the PMC runs' GRBM_GUI_ACTIVE / time gives)
 # wave64 VALU instructions a CU can issue per cycle: 4 SIMD-32 units, each one wave64 instruction per
@@ -517,7 +517,9 @@ def main():
                                 model.trainable(), optim, bucket=bucket, rotation=rot, model=model)
         pg.capture()
         pg_rot = rot
-        warm = rot * max(1, 4 // rot)
+        # untimed replays until the two streams' steady state (the first ~10 replays after a capture run
+        # ~3 % slower: profiles/r05_bench_first.json's timed steps 0.4115 ms against its reps' 0.399)
+        warm = rot * max(1, max(20, 2 * args.warmup) // rot)
         for _ in range(warm):
             pg.replay()
         torch.cuda.synchronize()
