@@ -1707,11 +1707,14 @@ static hipError_t allow_bucket_lds()
     return e;
 }
 
-// LSR_DEPTH_LSD=1 forces the LSD passes at any P (measurement / test knob, read per call)
+// LSR_DEPTH_LSD=1 forces the LSD passes at any P; LSR_MSD_MAX_KEYS=n moves the MSD path's limit
+// (measurement / test knobs, read per call)
 bool depth_order_uses_pass_count(int P)
 {
     const char* e = getenv("LSR_DEPTH_LSD");
-    return P > kMsdMaxKeys || (e && e[0] == '1');
+    const char* m = getenv("LSR_MSD_MAX_KEYS");
+    const int64_t lim = m ? (int64_t)atoll(m) : kMsdMaxKeys;
+    return P > lim || (e && e[0] == '1');
 }
 
 // ---------------------------------------------------------------- depth order + super-tile counts
