@@ -1,3 +1,11 @@
+"""MSD vs LSD depth order at C5 (measurement aid for DESIGN.md §8; profiles/r05_c5_msd_vs_lsd.txt):
+
+    python3 tools/c5_msd_check.py
+
+Renders the C5 forward twice, once with the LSD depth order (LSR_DEPTH_LSD=1) and once with the MSD
+bucket sort forced on (LSR_MSD_MAX_KEYS=4000000), prints each one's per-kernel times, and compares
+the images, tile ranges, point list, final T and contributor counts for bit equality.
+"""
 import os, sys, time
 sys.path.insert(0, os.getcwd())
 import torch, numpy as np
