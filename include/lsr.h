@@ -341,10 +341,13 @@ int32_t lsr_fill_language(int32_t P, const float* language_feature, int32_t raw,
 int32_t lsr_debug_render_stats(uint64_t* out, int32_t n);
 
 /* Measurement hook, not part of the reference interface: with LSR_RENDER_STATS=1 the render
- * kernels (kernel 0 = forward, 1 = backward) record per workgroup b < n into out[8 b .. 8 b + 7]:
+ * kernels (kernel 0 = forward, 1 = backward) record per workgroup b < n into out[11 b .. 11 b + 10]:
  * {start, end} (100 MHz wall clock, low 32 bits), the tile (-1: a workgroup that only filled empty
  * tiles), the hardware slot (XCC_ID << 16 | CU/SH/SE bits of HW_ID), and (forward) the ticks spent
- * loading, compacting and walking its batches and the batch count (synchronous). */
+ * loading, compacting and walking its batches, the batch count | the first batch's load ticks << 16,
+ * and six milestones of the first batch in ticks after the start, two 16-bit fields per word
+ * (begin, tile range loaded, first barrier, point-list ids loaded, records gathered, load phase
+ * done; synchronous). */
 int32_t lsr_debug_render_timeline(int32_t kernel, uint32_t* out, int32_t n);
 
 /* Look-back stalls, not part of the reference interface.  The single-pass scans of the forward

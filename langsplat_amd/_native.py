@@ -769,8 +769,9 @@ def debug_render_stats():
 def debug_render_timeline(kernel, n):
     """Per-workgroup timeline of the LSR_RENDER_STATS=1 render kernels (kernel 0 forward, 1 backward;
     include/lsr.h lsr_debug_render_timeline): for workgroups < n, dicts with start, end, tile,
-    slot and (forward) the load / compact / walk ticks and the batch count."""
-    W = 8
+    slot and (forward) the load / compact / walk ticks, the batch count, the first batch's load ticks and its milestones (ticks after the start: begin,
+    ranges loaded, first barrier, ids loaded, records gathered, load phase done)."""
+    W = 11
     arr = (ctypes.c_uint32 * (W * n))()
     _check(load().lsr_debug_render_timeline(kernel, arr, n), "lsr_debug_render_timeline")
     v = list(arr)
@@ -778,6 +779,8 @@ def debug_render_timeline(kernel, n):
     for i in range(n):
         r = v[W * i:W * i + W]
         out.append({"start": r[0], "end": r[1], "tile": r[2] if r[2] < 2 ** 31 else r[2] - 2 ** 32, "slot": r[3],
-                    "load": r[4], "compact": r[5], "walk": r[6], "batches": r[7]})
+                    "load": r[4], "compact": r[5], "walk": r[6], "batches": r[7] & 0xFFFF,
+                    "first_load": r[7] >> 16,
+                    "first_marks": [r[8] & 0xFFFF, r[8] >> 16, r[9] & 0xFFFF, r[9] >> 16, r[10] & 0xFFFF, r[10] >> 16]})
     return out
 

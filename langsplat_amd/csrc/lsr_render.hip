@@ -161,7 +161,9 @@ __device__ __forceinline__ int scheduled_tile(int b, const uint32_t* counts, con
 // kernels {start, end} (s_memrealtime, 100 MHz), the tile and the hardware slot (XCC_ID << 16 |
 // HW_ID bits 8..15: cu, sh, se).  Off by default.
 constexpr int kTimelineMax = 1 << 15;
-constexpr int kTimelineWords = 8;  // start, end, tile, slot, load, compact, walk (ticks), batches
+// start, end, tile, slot, load, compact, walk (ticks), batches | first load << 16, and the first
+// batch's six milestones (PhaseTicks::st) in ticks after the start, two 16-bit fields per word
+constexpr int kTimelineWords = 11;
 __device__ uint32_t g_render_timeline[2][kTimelineMax * kTimelineWords];
 
 __device__ __forceinline__ uint32_t hw_slot()
@@ -175,7 +177,10 @@ __device__ __forceinline__ uint32_t hw_slot()
 // barrier), compact / cover (up to the next barrier), walk (up to the next batch's start, so it
 // includes the wait for the workgroup's slowest wave).
 struct PhaseTicks {
-    uint64_t load = 0, compact = 0, walk = 0, mark = 0;
+    uint64_t load = 0, compact = 0, walk = 0, mark = 0, first_load = 0;
+    // the first batch's milestones (absolute ticks): begin, ranges loaded, first barrier passed, ids
+    // loaded, records gathered, load phase done (the stats variant waits for each load explicitly)
+    uint64_t st[6] = {0, 0, 0, 0, 0, 0};
     uint32_t batches = 0;
     bool stopped = false;  // left the batch loop at a batch start (its walk time already counted)
     __device__ void begin() { mark = wall_clock64(); }
@@ -199,7 +204,12 @@ __device__ __forceinline__ void timeline_put(int kernel, uint64_t t0, int tile, 
     o[4] = (uint32_t)ph.load;
     o[5] = (uint32_t)ph.compact;
     o[6] = (uint32_t)ph.walk;
-    o[7] = ph.batches;
+    o[7] = (ph.batches & 0xFFFFu) | ((uint32_t)min(ph.first_load, (uint64_t)0xFFFF) << 16);
+    uint32_t rel[6];
+    for (int k = 0; k < 6; k++) rel[k] = ph.st[k] > t0 ? (uint32_t)min(ph.st[k] - t0, (uint64_t)0xFFFF) : 0u;
+    o[8] = rel[0] | (rel[1] << 16);
+    o[9] = rel[2] | (rel[3] << 16);
+    o[10] = rel[4] | (rel[5] << 16);
 }
 
 // Wave priority by launch position (LSR_PRIO=0: off).  A tile's compositing is one serial chain
@@ -524,15 +534,22 @@ __global__ __launch_bounds__(kTilePixels, LSR_FWD_WAVES) void k_render_forward(R
     const float pfx = (float)px, pfy = (float)py;
     const lsr_f2 pxy = make_f2(pfx, pfy);
     const float tx0 = (float)(tx * kTile), ty0 = (float)(ty * kTile);
+    PhaseTicks ph;
+    if (kStats) {
+        ph.begin();
+        ph.st[0] = ph.mark;
+    }
     const uint2 range = p.ranges[tile];
+    if (kStats) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        ph.st[1] = wall_clock64();
+    }
     const uint32_t start = range.x, end = range.y;
     const bool inside = px < p.W && py < p.H;
     if (t == 0) s_last = 0;
     uint32_t nrec = 0;  // split replay: boundaries recorded (256, 512, ... up to kSplitMax; uniform)
 
     FwdPixel q{inside ? 1.0f : -1.0f, make_f2(0.f, 0.f), make_f2(0.f, 0.f), make_f2(0.f, 0.f), 0u, 0u};
-    PhaseTicks ph;
-    if (kStats) ph.begin();
     // Software pipeline over the batches: a batch's records are gathered during the previous batch's
     // walk (into registers the walk leaves free), and the point_list ids one batch earlier still, so
     // a batch's load phase waits for no memory round trip (the timeline showed ~9 us of load phase per
@@ -558,6 +575,11 @@ __global__ __launch_bounds__(kTilePixels, LSR_FWD_WAVES) void k_render_forward(R
         }
         if (kStats) ph.batches++;
         const uint32_t idx = base + t;
+        if (kStats && base == start) {
+            ph.st[2] = wall_clock64();
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            ph.st[3] = wall_clock64();
+        }
 #if !LSR_FWD_PREFETCH
         a = b = c = make_float4(0.f, 0.f, 0.f, 0.f);
         if (idx < end) {
@@ -567,6 +589,10 @@ __global__ __launch_bounds__(kTilePixels, LSR_FWD_WAVES) void k_render_forward(R
             c = p.record[3 * (size_t)g + 2];
         }
 #endif
+        if (kStats && base == start) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            ph.st[4] = wall_clock64();
+        }
         if (p.split_pool && base != start && base - start <= (uint32_t)(kSplitMax * kThreads)) {
             // split replay: every pixel's state before list entry 256 j while some pixel composites,
             // two float4 per pixel in the tile's own slot j - 1 (a grid-wide slot counter cost ~40 us
@@ -589,7 +615,13 @@ __global__ __launch_bounds__(kTilePixels, LSR_FWD_WAVES) void k_render_forward(R
             if (!p.no_bwd) p.cover[idx] = m;  // for the backward (coalesced: one byte per thread)
         }
         __syncthreads();
-        if (kStats) ph.lap(ph.load);
+        if (kStats) {
+            ph.lap(ph.load);
+            if (base == start) {
+                ph.first_load = ph.load;
+                ph.st[5] = ph.mark;
+            }
+        }
         const int cnt = (int)min((uint32_t)kThreads, end - base);
         const int n = __builtin_amdgcn_readfirstlane(
             wave_compact(sM, cnt, 1u << wave, lane, sL[wave]));

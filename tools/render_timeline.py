@@ -3,7 +3,9 @@
     python tools/render_timeline.py [C3] [--full]
 
 The backward runs the bench's language-step variant (no colour gradient, no geometry gradients);
---full runs the variant with every gradient.
+--full runs the variant with every gradient; --zero has the forward clear the language step's
+gradient records (LSR_FWD_ZERO_GRAD_RECORDS, as the benched step does); --fwd-only skips the
+backward (required with a measurement build whose forward leaves tiles unrendered).
 
 Runs one forward + backward with LSR_RENDER_STATS=1 and reads the {start, end, tile, CU} record
 every workgroup wrote (include/lsr.h lsr_debug_render_timeline).  Prints, per kernel, the span,
@@ -29,8 +31,17 @@ from langsplat_amd.synthetic import CONFIGS, activated_inputs, make_cameras, mak
 TICK_US = 0.01  # s_memrealtime: 100 MHz
 
 
+MARKS = ("begin", "range", "barrier", "ids", "gather", "loaded")
+
+
+def marks(ph):
+    """The first batch's milestones, in us after the workgroup's start."""
+    return " ".join(f"{n} {v * TICK_US:.1f}" for n, v in zip(MARKS, ph["first_marks"]))
+
+
 def analyse(name, recs, info=None):
-    recs = [(r["start"], r["end"], r["tile"], r["slot"], r) for r in recs if r["end"] != 0 or r["start"] != 0]
+    recs = [(r["start"], r["end"], r["tile"], r["slot"], dict(r, b=b)) for b, r in enumerate(recs)
+            if r["end"] != 0 or r["start"] != 0]
     if not recs:
         print(f"{name}: no records")
         return
@@ -41,12 +52,14 @@ def analyse(name, recs, info=None):
     phases = {}
     for r in recs:
         phases[r[2]] = r[4]
-    for s, e, tile, slot, _ in recs:
+    blk = {}
+    for s, e, tile, slot, r in recs:
         s, e = (s - t0) & 0xFFFFFFFF, (e - t0) & 0xFFFFFFFF
         ev.append((s, 1))
         ev.append((e, -1))
         per_cu[slot] += e - s
         dur.append((e - s, s, tile))
+        blk[tile] = r["b"]
     span = max(e for e, _ in ev if _ == -1)
     ev.sort()
     cur = peak = 0
@@ -68,6 +81,13 @@ def analyse(name, recs, info=None):
     if sum(tot.values()):
         print("  phases summed over workgroups: " + ", ".join(f"{k} {100.0 * v / busy:.1f}%" for k, v in tot.items())
               + " of workgroup time")
+    first = [(s, phases.get(tile)) for _, s, tile in dur if phases.get(tile) and phases[tile]["batches"]]
+    if first:
+        for lab, sel in (("starting < 2 us", [p for s, p in first if s * TICK_US < 2.0]),
+                         ("starting later", [p for s, p in first if s * TICK_US >= 2.0])):
+            if sel:
+                m = [sum(p["first_marks"][k] for p in sel) / len(sel) for k in range(6)]
+                print(f"  first batch, {len(sel)} workgroups {lab}: milestones " + marks({"first_marks": m}))
     dur.sort(reverse=True)
     mean = busy / len(dur)
     print(f"  workgroup time: mean {mean * TICK_US:.1f} us, max {dur[0][0] * TICK_US:.1f} us")
@@ -75,14 +95,17 @@ def analyse(name, recs, info=None):
         extra = info(tile) if info and tile >= 0 else ""
         ph = phases.get(tile)
         if ph and ph["batches"]:
-            extra += (f"\n        {ph['batches']} batches: load {ph['load'] * TICK_US:.1f} us, compact "
+            extra += (f"\n        {ph['batches']} batches: load {ph['load'] * TICK_US:.1f} us (first "
+                      f"{ph['first_load'] * TICK_US:.1f}; milestones " + marks(ph) + "), compact "
                       f"{ph['compact'] * TICK_US:.1f} us, walk {ph['walk'] * TICK_US:.1f} us")
-        print(f"    tile {tile:6d}: {d * TICK_US:7.1f} us, starts at {s * TICK_US:6.1f} us {extra}")
+        print(f"    tile {tile:6d} (workgroup {blk.get(tile, -1)}): {d * TICK_US:7.1f} us, starts at {s * TICK_US:6.1f} us "
+              f"{extra}")
 
 
 def main():
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
     full = "--full" in sys.argv
+    flags = _native.FWD_ZERO_GRAD_RECORDS if "--zero" in sys.argv else 0
     cfg = args[0] if args else "C3"
     c = CONFIGS[cfg]
     dev = torch.device("cuda")
@@ -100,9 +123,11 @@ def main():
     for it in range(3):  # the last iteration's records are read (warm caches)
         nr, color, lang, radii, geom, binning, image = _native.rasterize_gaussians(
             st, inp["means3D"], inp["shs"], None, inp["language_feature_precomp"], inp["opacities"],
-            inp["scales"], inp["rotations"], None)
+            inp["scales"], inp["rotations"], None, flags=flags)
         torch.cuda.synchronize()
         fwd = _native.debug_render_timeline(0, tiles)
+        if "--fwd-only" in sys.argv:
+            continue
         _native.rasterize_gaussians_backward(st, inp["means3D"], inp["shs"], None, inp["language_feature_precomp"],
                                              inp["scales"], inp["rotations"], None, radii, gc if full else None, gl,
                                              nr, geom, binning, image, geometry=full)
@@ -121,9 +146,10 @@ def main():
         t = fT[ty * 16:(ty + 1) * 16, tx * 16:(tx + 1) * 16]
         return (f"list {int(rng[tile, 1] - rng[tile, 0])}, max n_contrib {int(blk.max())}, "
                 f"saturated px {float((t < 1e-4).mean()):.2f}, mean final T {float(t.mean()):.2e}")
-    nb = sum(1 for r in bwd if r["tile"] >= 0 and r["end"] != 0)
     analyse(f"{cfg} render forward", fwd, info)
-    analyse(f"{cfg} render backward", [r for r in bwd[:nb]], info)
+    if "--fwd-only" not in sys.argv:
+        nb = sum(1 for r in bwd if r["tile"] >= 0 and r["end"] != 0)
+        analyse(f"{cfg} render backward", [r for r in bwd[:nb]], info)
 
 
 if __name__ == "__main__":
