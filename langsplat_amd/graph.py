@@ -112,6 +112,15 @@ def _fused_tail_enabled() -> bool:
     return os.environ.get("LSR_FUSED_TAIL", "1") != "0"
 
 
+def graph_capture(graph, stream=None):
+    """torch.cuda.graph in thread-local capture mode.  In the default (global) mode an unsafe HIP call
+    from ANY thread invalidates the capture, and at N > 1 the process group's watchdog thread polls
+    the events of the eager warm-up collective while the step is captured (seen as
+    hipErrorStreamCaptureInvalidated at capture_end of a re-capture, then an abort from the
+    watchdog); the captures here make no unsafe call themselves."""
+    return torch.cuda.graph(graph, stream=stream, capture_error_mode="thread_local")
+
+
 def release_stale_accumulators(params) -> int:
     """Make every parameter forget its cached AccumulateGrad node (a node a still-alive autograd graph
     holds, bound to the stream that graph ran on), so the next graph creates a fresh one on its own
@@ -220,7 +229,7 @@ class GraphedStep:
                 p.grad = None
         graph = torch.cuda.CUDAGraph()
         with _native.capacity(self.rendered, self.entries, self.overflow):
-            with torch.cuda.graph(graph):
+            with graph_capture(graph):
                 # detached: the captured step's autograd graph (and its AccumulateGrad nodes, bound
                 # to the capture stream) is not kept alive past the capture
                 self.static_loss = self._body().detach()
@@ -230,7 +239,7 @@ class GraphedStep:
             self._graph_grads = [p.grad for p in self.params]
             self.bucket._attach()
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with graph_capture(g):
                 self.optimizer.step(skip=self.overflow)
             self.graph_adam = g
         self.graph = graph

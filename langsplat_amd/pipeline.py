@@ -38,7 +38,7 @@ import torch
 
 from . import _native
 from .distributed import collective_capturable
-from .graph import _as_view, _fused_tail_enabled, _nullctx, capture_key, release_stale_accumulators
+from .graph import _as_view, _fused_tail_enabled, _nullctx, capture_key, graph_capture, release_stale_accumulators
 
 
 class ViewPipeline:
@@ -314,7 +314,7 @@ class PipelinedGraphStep:
             if self.R > 1:
                 continue  # geometry and steps are captured per rotation group below
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, stream=sb), caps[p], self.sets[p], \
+            with graph_capture(g, stream=sb), caps[p], self.sets[p], \
                     _native.forward_phase(_native.forward_phase.GEOMETRY):
                 self._fwd(p)  # its outputs are written by the composite half
             self.g_geo[p] = g
@@ -322,7 +322,7 @@ class PipelinedGraphStep:
                 q.grad = None  # the captured backward assigns its own .grad (no accumulate)
             if fused and p == 0:
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, stream=sa):
+                with graph_capture(g, stream=sa):
                     with caps[p], self.sets[p], _native.forward_phase(_native.forward_phase.COMPOSITE):
                         loss = self._fwd(p)
                     if merged:
@@ -336,7 +336,7 @@ class PipelinedGraphStep:
                     del loss
                 self.g_comp0 = g
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, stream=sa):
+            with graph_capture(g, stream=sa):
                 with caps[p], self.sets[p], _native.forward_phase(comp_phase):
                     loss = self._fwd(p)
                 if merged:
@@ -344,13 +344,13 @@ class PipelinedGraphStep:
             self.g_comp[p] = g
             if not merged:
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, stream=sa):
+                with graph_capture(g, stream=sa):
                     step_body(p, loss)
                 self.g_step[p] = g
             self.grads[p] = [q.grad for q in self.params]  # this set's graph-owned gradients
             if self.bucket is not None and not coll_in_graph:  # the all-reduce sits between two graphs
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, stream=sa):
+                with graph_capture(g, stream=sa):
                     self.optimizer.step(skip=self.overflow[p])
                 self.g_adam[p] = g
             self.static_loss[p] = loss.detach()  # the set's static loss tensor
@@ -379,7 +379,7 @@ class PipelinedGraphStep:
         def rot(j, first):
             g = torch.cuda.CUDAGraph()
             grads = []
-            with torch.cuda.graph(g, stream=sa):
+            with graph_capture(g, stream=sa):
                 for p in range(j * R, (j + 1) * R):
                     for q in self.params:
                         q.grad = None  # each step's backward assigns its own .grad
@@ -399,7 +399,7 @@ class PipelinedGraphStep:
         self.g_geo_rot = []
         for j in range(2):
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, stream=sb):
+            with graph_capture(g, stream=sb):
                 for p in range(j * R, (j + 1) * R):
                     with caps[p], self.sets[p], _native.forward_phase(_native.forward_phase.GEOMETRY):
                         self._fwd(p)

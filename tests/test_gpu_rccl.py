@@ -118,7 +118,7 @@ fout = torch.zeros((), device=dev)
 g = torch.cuda.CUDAGraph()
 side = torch.cuda.Stream()
 side.wait_stream(torch.cuda.current_stream())
-with torch.cuda.stream(side), torch.cuda.graph(g):
+with torch.cuda.stream(side), torch.cuda.graph(g, capture_error_mode="thread_local"):
     lang.grad.copy_(src)
     b.all_reduce(average=True, flag=flag)
     out.copy_(lang.grad)
