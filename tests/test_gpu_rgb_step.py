@@ -67,4 +67,4 @@ def test_rgb_step_matches_reference_ops(monkeypatch):
     torch.testing.assert_close(step.max_radii2D, max_r, rtol=0, atol=0)
     torch.testing.assert_close(step.denom, denom, rtol=0, atol=0)
     assert_grad_close("xyz_gradient_accum", step.xyz_gradient_accum.cpu().numpy(), accum.cpu().numpy())
-    assert int(vis.sum()) > 0 and np.isfinite(float(loss))
+    assert int(vis.sum()) > 0 and np.isfinite(float(loss.detach()))
