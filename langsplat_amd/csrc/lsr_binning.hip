@@ -443,6 +443,16 @@ __device__ __forceinline__ void zero_words_strided(const ZeroList& z)
         for (int w = r; w < z.n[k]; w += stride) z.p[k][w] = 0u;
 }
 
+// LSD depth passes in capacity mode run the most passes any view can need (the host cannot read the
+// key range there): a pass whose shift is at or above the bits of this view's visible key range
+// (krange = {min, max} visible depth key, published by the forward's counter reduction; key_xf maps
+// every key into [0, max - min]) sees digit 0 for every key, so its stable scatter is the identity
+// and its histogram is not needed.
+__device__ __forceinline__ bool uniform_pass(const uint32_t* krange, int shift)
+{
+    return krange && shift < 32 && ((krange[1] - krange[0]) >> shift) == 0u;
+}
+
 // srect (MSD pass with placed emission): the keys' tile rectangles by index; the block's super-tile
 // entry counts then also go to rows 256 + s (s < supers) of hist, so the scan that yields the
 // bucket starts also yields every super-tile's base in the super-tile-major entry list (+ n).
@@ -452,13 +462,15 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_hist(const uint32_t* __
                                                               const uint32_t* __restrict__ kxf, int remap, int msd,
                                                               ZeroList zero, DevCount dc,
                                                               const uint2* __restrict__ srect = nullptr,
-                                                              int supers = 0, int sgx = 0)
+                                                              int supers = 0, int sgx = 0,
+                                                              const uint32_t* __restrict__ krange = nullptr)
 {
     constexpr int kWaves = kRadixThreads / 64;
     __shared__ uint32_t wcnt[kWaves][256];
     __shared__ uint32_t scnt[256];
     zero_words_strided(zero);
     if (dc.abort && *dc.abort) return;
+    if (uniform_pass(krange, shift)) return;  // the scatter copies; its histogram is not read
     if (dc.n) n = min(n, (int)*dc.n);
     MsdMap mm{};
     if (msd) {
@@ -524,12 +536,31 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_scatter(
     const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in, int n, int shift, int nbits,
     const uint32_t* __restrict__ hist, int nblk, uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
     const uint32_t* __restrict__ kxf, ScatterTail tail, int remap, int msd, DevCount dc, int hstride = 0,
-    int hrows = 256, ZeroList zero = ZeroList{})
+    int hrows = 256, ZeroList zero = ZeroList{}, const uint32_t* __restrict__ krange = nullptr)
 {
     zero_words_strided(zero);
     if (dc.abort && *dc.abort) return;
     if (hstride == 0) hstride = nblk;  // histogram rows of nblk blocks (the hist kernel's layout)
     if (dc.n) n = min(n, (int)*dc.n);
+    if (!msd && uniform_pass(krange, shift)) {  // every key's digit is 0: the stable pass is the identity
+        const int blk = xcd_tile(nblk, remap);
+        for (int i = blk * kRadixThreads * kItems + threadIdx.x; i < min(n, (blk + 1) * kRadixThreads * kItems);
+             i += kRadixThreads) {
+            const uint32_t k = kxf ? key_xf(keys_in[i], kxf) : keys_in[i];
+            const uint32_t v = vals_in ? vals_in[i] : (uint32_t)i;
+            if (kCarry || !tail.rect) {
+                keys_out[i] = k;
+                vals_out[i] = v;
+                if (kCarry) tail.rect_ranked[i] = tail.rect[i];
+            } else {  // the last depth pass's tail, as below
+                const uint2 rc = tail.rect[v];
+                vals_out[i] = v;
+                tail.rect_ranked[i] = rc;
+                tail.ns[i] = super_count(rc);
+            }
+        }
+        return;
+    }
     MsdMap mm{};
     if (msd) {
         mm = msd_map(kxf);
@@ -667,7 +698,8 @@ static hipError_t radix_sort(const uint32_t* k0, const uint32_t* v0, int n, int 
                              uint32_t* scan_regions, size_t region_words, uint32_t* stall, hipStream_t s, bool debug,
                              int* passes_out,
                              const uint32_t* kxf = nullptr, ScatterTail last = ScatterTail{nullptr, nullptr, nullptr},
-                             ZeroList zero = ZeroList{}, DevCount dc = DevCount{nullptr, nullptr})
+                             ZeroList zero = ZeroList{}, DevCount dc = DevCount{nullptr, nullptr},
+                             const uint32_t* krange = nullptr)
 {
     const bool small = radix_small(n);
     const int tile = kRadixThreads * (small ? 4 : 16);
@@ -689,10 +721,10 @@ static hipError_t radix_sort(const uint32_t* k0, const uint32_t* v0, int n, int 
         const ZeroList z = pass == 0 ? zero : ZeroList{};
         if (small)
             hipLaunchKernelGGL(k_radix_hist<4>, dim3(nblk), dim3(kRadixThreads), 0, s, kin, n, shift, nbits, hist, nblk,
-                               pass == 0 ? kxf : nullptr, remap, 0, z, dc);
+                               pass == 0 ? kxf : nullptr, remap, 0, z, dc, (const uint2*)nullptr, 0, 0, krange);
         else
             hipLaunchKernelGGL(k_radix_hist<16>, dim3(nblk), dim3(kRadixThreads), 0, s, kin, n, shift, nbits, hist,
-                               nblk, pass == 0 ? kxf : nullptr, remap, 0, z, dc);
+                               nblk, pass == 0 ? kxf : nullptr, remap, 0, z, dc, (const uint2*)nullptr, 0, 0, krange);
         if ((e = post(debug, s)) != hipSuccess) return e;
         if ((e = scan_exclusive(hist, hist_scan, (1 << nbits) * nblk, scan_regions + pass * region_words, nullptr,
                                 stall, s, debug)) != hipSuccess)
@@ -700,10 +732,12 @@ static hipError_t radix_sort(const uint32_t* k0, const uint32_t* v0, int n, int 
         const ScatterTail tail = pass == passes - 1 ? last : ScatterTail{nullptr, nullptr, nullptr};
         if (small)
             hipLaunchKernelGGL(k_radix_scatter<4>, dim3(nblk), dim3(kRadixThreads), 0, s, kin, vin, n, shift, nbits,
-                               hist_scan, nblk, kout, vout, pass == 0 ? kxf : nullptr, tail, remap, 0, dc);
+                               hist_scan, nblk, kout, vout, pass == 0 ? kxf : nullptr, tail, remap, 0, dc, 0, 256,
+                               ZeroList{}, krange);
         else
             hipLaunchKernelGGL(k_radix_scatter<16>, dim3(nblk), dim3(kRadixThreads), 0, s, kin, vin, n, shift, nbits,
-                               hist_scan, nblk, kout, vout, pass == 0 ? kxf : nullptr, tail, remap, 0, dc);
+                               hist_scan, nblk, kout, vout, pass == 0 ? kxf : nullptr, tail, remap, 0, dc, 0, 256,
+                               ZeroList{}, krange);
         if ((e = post(debug, s)) != hipSuccess) return e;
         kin = kout;
         vin = vout;
@@ -1836,9 +1870,9 @@ hipError_t launch_depth_order(int P, int passes, const Layout& L, char* geom, ui
     }
     hipError_t e = (passes & 1)
         ? radix_sort(keys, nullptr, P, 8 * passes, kb, vb, ka, va, hist, hist_scan, regions, L.scan_region_geom, stall,
-                     s, debug, &done, counters + kCntKeyMin, tail)
+                     s, debug, &done, counters + kCntKeyMin, tail, ZeroList{}, DevCount{nullptr, nullptr}, kxf)
         : radix_sort(keys, nullptr, P, 8 * passes, ka, va, kb, vb, hist, hist_scan, regions, L.scan_region_geom, stall,
-                     s, debug, &done, counters + kCntKeyMin, tail);
+                     s, debug, &done, counters + kCntKeyMin, tail, ZeroList{}, DevCount{nullptr, nullptr}, kxf);
     if (e != hipSuccess) return e;
     return scan_exclusive(ka, off, P, regions + passes * L.scan_region_geom, counters + kCntSuper, stall, s, debug);
 }

@@ -199,8 +199,9 @@ def _depth_scene(P, W, H, wide, seed):
 
 def test_capacity_mode_lsd_depth_order(monkeypatch):
     """The LSD depth order (P > 2M, forced here by LSR_DEPTH_LSD=1) in capacity mode uses the pass
-    count of the thread's last eager forward: exact when it suffices, flagged when the view's key range
-    needs more passes, exact again after an eager forward of that view."""
+    count of the thread's last eager forward: exact when it suffices (also when it exceeds the view's
+    need), flagged when the view's key range needs more passes, exact again after an eager forward of
+    that view."""
     monkeypatch.setenv("LSR_DEPTH_LSD", "1")
     P, W, H = 3000, 96, 64
     narrow = _depth_scene(P, W, H, False, 41)
@@ -211,7 +212,14 @@ def test_capacity_mode_lsd_depth_order(monkeypatch):
     c_wide = _forward(*wide, cap=_native.capacity(Rw, Ew, ovf))
     assert int(ovf.item()) == 0 and torch.equal(c_wide[1], e_wide[1])
     np.testing.assert_array_equal(state(c_wide, P, W, H)["point_list"][:Rw], state(e_wide, P, W, H)["point_list"])
-    _forward(*narrow)  # the thread's last eager view now needs fewer passes
+    # more passes than the view needs (the wide view's 4 for the narrow one's 2): the passes above its
+    # key range see one digit and take the scatter's identity path -- the same order
+    c_narrow = _forward(*narrow, cap=_native.capacity(400000, 400000, ovf))
+    assert int(ovf.item()) == 0
+    e_narrow = _forward(*narrow)  # the thread's last eager view now needs fewer passes
+    Rn = _native.LAST_COUNTS[(P, W, H)][0]
+    assert torch.equal(c_narrow[1], e_narrow[1]) and torch.equal(c_narrow[2], e_narrow[2])
+    np.testing.assert_array_equal(state(c_narrow, P, W, H)["point_list"][:Rn], state(e_narrow, P, W, H)["point_list"])
     c2 = _forward(*wide, cap=_native.capacity(Rw, Ew, ovf))
     assert ovf.view(torch.float32).item() == 1.0 and not c2[2].any()
     _forward(*wide)
