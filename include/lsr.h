@@ -186,7 +186,9 @@ typedef struct lsr_forward_args {
      * enqueues the rest: the language feature into the records and the compositing (+ fused loss).
      * Whatever the caller orders between the two calls on the stream (e.g. a wait for the feature's
      * update) runs between them, so the two halves can be captured into two HIP graphs replayed on
-     * different streams.  LSR_PHASE_ALL (0): one call does everything. */
+     * different streams.  The compositing of a composite phase runs at fewer workgroups per CU (6,
+     * leaving wave slots and registers to the other stream; LSR_FWD_SHARE=0: all that fit), which
+     * changes no result.  LSR_PHASE_ALL (0): one call does everything. */
     int32_t phase;
 } lsr_forward_args;
 /* LSR_PHASE_COMPOSITE_FILLED (ABI 12): as LSR_PHASE_COMPOSITE, but the records' language slots already

@@ -282,6 +282,8 @@ static int32_t render_forward_and_finish(const lsr_settings* s, const lsr_forwar
     rp.out_color = a->out_color;
     rp.out_lang = a->out_language_feature;
     rp.split_color = (a->flags & LSR_FWD_NO_COLOR_GRAD) ? 0 : 1;
+    // a composite phase runs beside another stream's geometry phase: fewer workgroups per CU
+    rp.shared_cu = (a->phase == LSR_PHASE_COMPOSITE || a->phase == LSR_PHASE_COMPOSITE_FILLED) ? 1 : 0;
     if (a->flags & LSR_FWD_NO_BACKWARD) {  // inference: no split states, no backward work lists
         rp.no_bwd = 1;
         rp.split_pool = nullptr;

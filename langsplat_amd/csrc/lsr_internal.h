@@ -268,7 +268,8 @@ struct RenderParams {
     int split_color;  // forward: store the colour sums' half of every state (off: LSR_FWD_NO_COLOR_GRAD)
     int no_bwd;       // forward: write no state for a backward (LSR_FWD_NO_BACKWARD)
     int prio;  // wave priority by launch position (longest tiles highest), 0: off
-    int shared_cu;  // backward: another stream runs beside it (LSR_BWD_SHARED_CU): <= 6 workgroups per CU
+    int shared_cu;  // another stream runs beside it (backward: LSR_BWD_SHARED_CU; forward: a composite
+                    // phase): fewer workgroups per CU (lsr_render.hip kSharedWgsBwd / kSharedWgsFwd)
     int geo;   // backward: the conic / opacity partials are needed (geometry gradients)
     float4* zero_records;  // forward: clear these zero_records_n4 float4s (grid-stride), or null
     int64_t zero_records_n4;

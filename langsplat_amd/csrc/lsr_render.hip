@@ -909,6 +909,45 @@ static bool split_color_forced()
     return v;
 }
 
+// Workgroups per CU of the render kernels while another stream's kernels run beside them (the
+// pipelined step, §5b): the backward at 7 of 8 and the forward at 6 of 7, so the geometry stream
+// finds wave slots and VGPRs free on every CU instead of waiting for a render kernel's tail.
+// Measured at C3 (profiles/r05_occupancy_sweep.txt, r05_fwd_share.txt): the backward 8 -> 7
+// 0.418 -> 0.400 ms per step; the forward 7 -> 6 0.400-0.47 (bimodal, by box) -> 0.404-0.405 ms.
+constexpr int kSharedWgsBwd = 7;
+constexpr int kSharedWgsFwd = 6;
+constexpr size_t kCuLds = 160 * 1024;
+// Dynamic LDS that leaves room for exactly `wgs` workgroups of kernel fn per CU (0 if its static
+// LDS already allows no more), rounded to 1 KiB: the allocation granularity must not push the
+// last workgroup out.
+static size_t occupancy_pad(const void* fn, int wgs, const char* what)
+{
+    hipFuncAttributes at{};
+    size_t stat = 20 * 1024;
+    if (hipFuncGetAttributes(&at, fn) == hipSuccess) stat = at.sharedSizeBytes;
+    const size_t per = (kCuLds / wgs) & ~(size_t)1023;  // wgs of them fit, one more does not
+    const size_t pad = per > stat && per * (wgs + 1) > kCuLds ? per - stat : 0;
+    if (getenv("LSR_SHARE_PRINT")) fprintf(stderr, "lsr: %s static LDS %zu pad %zu\n", what, stat, pad);
+    return pad;
+}
+// The forward's LDS pad (variants: 0 feature + fused loss, 1 feature, 2 colour only): LSR_FWD_PAD
+// when set, else in a composite phase (another stream beside it) the kSharedWgsFwd cap unless
+// LSR_FWD_SHARE=0, else none.
+static size_t forward_launch_pad(const RenderParams& p, int variant)
+{
+    static const bool explicit_pad = getenv("LSR_FWD_PAD") != nullptr;
+    static const bool on = [] {
+        const char* e = getenv("LSR_FWD_SHARE");
+        return !(e && e[0] == '0');
+    }();
+    if (explicit_pad || !on || !p.shared_cu) return forward_pad();
+    static const size_t pad[3] = {
+        occupancy_pad((const void*)k_render_forward<false, true, true>, kSharedWgsFwd, "forward (loss)"),
+        occupancy_pad((const void*)k_render_forward<false, true, false>, kSharedWgsFwd, "forward (feature)"),
+        occupancy_pad((const void*)k_render_forward<false, false, false>, kSharedWgsFwd, "forward (colour)")};
+    return pad[variant];
+}
+
 hipError_t launch_render_forward(const RenderParams& pin, int tiles, hipStream_t s)
 {
     if (tiles == 0) return hipSuccess;
@@ -928,11 +967,14 @@ hipError_t launch_render_forward(const RenderParams& pin, int tiles, hipStream_t
             hipLaunchKernelGGL((k_render_forward<true, false, false>), dim3(tiles), dim3(kTilePixels), forward_pad(), s,
                                p);
     } else if (loss) {
-        hipLaunchKernelGGL((k_render_forward<false, true, true>), dim3(tiles), dim3(kTilePixels), forward_pad(), s, p);
+        hipLaunchKernelGGL((k_render_forward<false, true, true>), dim3(tiles), dim3(kTilePixels),
+                           forward_launch_pad(p, 0), s, p);
     } else if (feat) {
-        hipLaunchKernelGGL((k_render_forward<false, true, false>), dim3(tiles), dim3(kTilePixels), forward_pad(), s, p);
+        hipLaunchKernelGGL((k_render_forward<false, true, false>), dim3(tiles), dim3(kTilePixels),
+                           forward_launch_pad(p, 1), s, p);
     } else {
-        hipLaunchKernelGGL((k_render_forward<false, false, false>), dim3(tiles), dim3(kTilePixels), forward_pad(), s, p);
+        hipLaunchKernelGGL((k_render_forward<false, false, false>), dim3(tiles), dim3(kTilePixels),
+                           forward_launch_pad(p, 2), s, p);
     }
     return hipGetLastError();
 }
@@ -1492,21 +1534,11 @@ hipError_t render_timeline_read(uint32_t* out, int kernel, int n)
 // per CU (no pad) 0.417-0.421 ms per step; 7 with 18.6 KB of LDS left over (pad 2048) 0.406; 7 with
 // 4.2 KB left (pad 4096) 0.400-0.401; 6 (pad 5120) 0.478; 5 (pad 8192) 0.416.  So the pad is the
 // largest that still fits 7.  LSR_BWD_SHARE=0 disables it (LSR_BWD_PAD then applies).
-constexpr int kSharedWgs = 7;
-constexpr size_t kCuLds = 160 * 1024;
 template <int V>
 static size_t shared_pad_of()
 {
-    hipFuncAttributes at{};
-    size_t stat = 20 * 1024;
-    if (hipFuncGetAttributes(&at, (const void*)k_render_backward<false, (V & 1) != 0, (V & 2) != 0, (V & 4) != 0>) ==
-        hipSuccess)
-        stat = at.sharedSizeBytes;
-    // rounded down to 1 KiB: the LDS allocation granularity must not push the 7th workgroup out
-    const size_t per = (kCuLds / kSharedWgs) & ~(size_t)1023;  // kSharedWgs of them fit, one more does not
-    const size_t pad = per > stat && per * (kSharedWgs + 1) > kCuLds ? per - stat : 0;
-    if (getenv("LSR_BWD_SHARE_PRINT")) fprintf(stderr, "lsr: backward variant %d static LDS %zu pad %zu\n", V, stat, pad);
-    return pad;
+    return occupancy_pad((const void*)k_render_backward<false, (V & 1) != 0, (V & 2) != 0, (V & 4) != 0>, kSharedWgsBwd,
+                         "backward");
 }
 
 static size_t shared_cu_pad(int variant)
