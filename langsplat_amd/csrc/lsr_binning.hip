@@ -2161,7 +2161,10 @@ __global__ __launch_bounds__(256) void k_bin_count_fused(int S, int sgx, int sgy
     zero_words_strided(zero);
     if (dc.abort && *dc.abort) return;
     if (dc.n) E = min(E, (int64_t)*dc.n);
-    __shared__ uint2 sr[kFusedSupers];
+    // super-tile s's entries are [sstart[s], sstart[s + 1]) (ndig >= S at both call sites, so a
+    // range's end is the next one's start): one word per super-tile keeps the launch under 6 KB of
+    // LDS, i.e. beside the 7 pipelined backward workgroups a CU holds (lsr_render.hip kSharedWgsBwd)
+    __shared__ uint32_t sstart[kFusedSupers + 1];
     __shared__ uint32_t sbase[kFusedSupers + 1];
     __shared__ uint32_t scol[kFusedSupers];
     __shared__ uint32_t srow_tot[kFusedSupers];      // per super-row: segment-weighted count of one tile row
@@ -2174,9 +2177,11 @@ __global__ __launch_bounds__(256) void k_bin_count_fused(int S, int sgx, int sgy
     if (t < S) {
         const uint32_t a = hist[(size_t)t * nblk] - bias;
         const uint32_t b = t + 1 < ndig ? hist[(size_t)(t + 1) * nblk] - bias : (uint32_t)E;
-        sr[t] = make_uint2(a, b);
+        sstart[t] = a;
+        if (t == S - 1) sstart[S] = b;
         nseg = super_segments(make_uint2(a, b));
     }
+    auto sr = [&](int i) { return make_uint2(sstart[i], sstart[i + 1]); };
     uint32_t tot;
     const uint32_t ex = block_exclusive_scan(nseg, wsum, &tot);
     if (t < S) sbase[t] = ex;
@@ -2223,7 +2228,7 @@ __global__ __launch_bounds__(256) void k_bin_count_fused(int S, int sgx, int sgy
     auto row_prefix = [&](int y) { return srow_pre[y / kSuper] + (uint32_t)(y % kSuper) * srow_tot[y / kSuper]; };
     if (blockIdx.x == 0) {  // the map for k_bin_emit
         for (int i = t; i < S; i += blockDim.x) {
-            g_sranges[i] = sr[i];
+            g_sranges[i] = sr(i);
             g_seg_base[i] = sbase[i];
             g_colpre[i] = scol[i];
         }
@@ -2237,9 +2242,9 @@ __global__ __launch_bounds__(256) void k_bin_count_fused(int S, int sgx, int sgy
     c.seg = seg;
     c.ox = (s % sgx) * kSuper;
     c.oy = (s / sgx) * kSuper;
-    c.e0 = sr[s].x + (uint32_t)seg * kSegEntries;
-    c.e1 = min(sr[s].y, c.e0 + (uint32_t)kSegEntries);
-    c.nseg = super_segments(sr[s]);
+    c.e0 = sr(s).x + (uint32_t)seg * kSegEntries;
+    c.e1 = min(sr(s).y, c.e0 + (uint32_t)kSegEntries);
+    c.nseg = super_segments(sr(s));
     c.colpre = scol[s];
     // the segment's (at most 2 x 256) keys loaded together: one memory round trip
     constexpr int kBatches = kSegEntries / 256;
