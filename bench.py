@@ -646,6 +646,11 @@ def main():
         s_ach = sb / (raster_stage_ms * 1e-3) / 1e9
         roofline["fwd_bwd_model"] = {"bytes": int(sb), "ms": round(raster_stage_ms, 4), "achieved": round(s_ach, 2),
                                      "frac": round(s_ach / HBM_PEAK_GBS, 4), "source": "SURVEY.md §8d"}
+        # the same model bytes over the benched step itself: the stages overlap across two streams
+        # there, and the step also holds the optimizer, so this is the rate the whole job sustains
+        st_ach = sb / (ms_per_step * 1e-3) / 1e9
+        roofline["fwd_bwd_model"]["step"] = {"ms": round(ms_per_step, 4), "achieved": round(st_ach, 2),
+                                             "frac": round(st_ach / HBM_PEAK_GBS, 4)}
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(cfg)
