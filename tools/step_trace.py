@@ -1,6 +1,7 @@
 """Kernel timeline of the bench's language step, eager or as a captured graph (measurement aid):
 
     rocprofv3 --kernel-trace --output-format csv -d gpurun_out/st_graph -o t -- python3 tools/step_trace.py graph
+    (ST_CONFIG=C5 for another BASELINE config; modes: eager, graph, pgraph)
     python3 tools/step_trace.py --summary gpurun_out/st_graph/t_kernel_trace.csv
 
 The summary prints, per step (one preprocess launch to the next), the span, the summed kernel time
@@ -19,7 +20,7 @@ def run(mode, steps=30):
     import bench
     from langsplat_amd.graph import GraphedStep
     from langsplat_amd.synthetic import CONFIGS, make_cameras, make_gaussians
-    c = CONFIGS["C3"]
+    c = CONFIGS[os.environ.get("ST_CONFIG", "C3")]
     P, W, H = c["P"], c["width"], c["height"]
     dev = torch.device("cuda", 0)
     params = make_gaussians(P, seed=0).to(dev)
