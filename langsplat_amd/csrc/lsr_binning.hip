@@ -682,13 +682,16 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_scatter(
 // Sorts (keys, vals) by key bits [0, total_bits) in passes of <= 8 bits.  The input is read
 // from (k0, v0) (v0 == null: values are the input indices) and the result lands in
 // (kA, vA) after an even number of passes, or in (kB, vB) after an odd number; returns which.
-// Radix tile size: 4 keys per thread (>= ~1000 workgroups) up to kRadixSmallMax keys, else 16.
+// Radix tile size: 4 keys per thread (>= ~1000 workgroups) up to 16M keys, else 16.  The 4-key
+// tiles (14-22 KB of LDS, 40-50 VGPRs) fit beside the render kernels of the pipelined step where the
+// 16-key ones (39-72 KB, 100-132 VGPRs) wait for them: at C5 (3M depth keys) the pipelined graph
+// step 0.985 -> 0.948 ms with the same eager depth order (profiles/r05_c5_radix_tiles.txt).
 // LSR_RADIX_SMALL_MAX=n moves the threshold (measurement aid).
 static bool radix_small(int64_t n)
 {
     static const int64_t lim = [] {
         const char* e = getenv("LSR_RADIX_SMALL_MAX");
-        return e ? (int64_t)atoll(e) : (int64_t)(1 << 21);
+        return e ? (int64_t)atoll(e) : (int64_t)(1 << 24);
     }();
     return n <= lim;
 }

@@ -138,3 +138,29 @@ def test_placed_emission_dense_bucket_oracle():
     st, inp = dense_bucket_scene()
     run, std, ind, out = check_forward_exact(st, inp)
     check_backward(st, inp, run, out)
+
+
+_RADIX16_CHILD = """
+from tests.scenes import scene
+from tests.test_gpu_parity import check_backward, check_forward_exact
+st, inp = scene(P=20000, W=640, H=360, seed=7, scale_range=(0.02, 0.15))
+run, std, ind, out = check_forward_exact(st, inp)
+assert out[0] > 0
+check_backward(st, inp, run, out)
+print("RADIX16_OK")
+"""
+
+
+def test_sixteen_key_radix_tiles_match_the_oracle():
+    """Sorts above 16M keys use 16-key radix tiles (lsr_binning.hip radix_small), which no test
+    scene reaches: a child process with LSR_RADIX_SMALL_MAX=0 (every sort on 16-key tiles) and
+    LSR_DEPTH_LSD=1 (the depth order as LSD passes) renders a scene bit-exactly against the oracle."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, LSR_RADIX_SMALL_MAX="0", LSR_DEPTH_LSD="1",
+               PYTHONPATH=root + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    r = subprocess.run([sys.executable, "-c", _RADIX16_CHILD], cwd=root, env=env, capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0 and "RADIX16_OK" in r.stdout, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
