@@ -1,6 +1,6 @@
 """Host enqueue time vs device time of the pipelined graph step at C3 (measurement aid):
 
-    python3 tools/pg_host.py [--steps 300] [--nowait]
+    python3 tools/pg_host.py [--steps 300] [--nowait | --sync]
 
 Prints the host time per replay() call (enqueue only) and the wall time per step to the final
 synchronize: when they are close the host, not the GPU, sets the step rate.
@@ -34,6 +34,7 @@ def main():
                                                  language_target=(gt, mask))["language_l1"],
                             [model._language_feature], optim).capture()
     wait = "--nowait" not in sys.argv
+    sync = "--sync" in sys.argv
     for _ in range(20):
         pg.replay(wait=wait)
     pg.synchronize()
@@ -42,7 +43,10 @@ def main():
     for rep in range(int(os.environ.get("PG_HOST_REPS", "3"))):
         t0 = time.perf_counter()
         for _ in range(steps):
-            pg.replay(wait=wait)
+            if sync:  # train.py:108: loss.item() after every step
+                pg.replay().item()
+            else:
+                pg.replay(wait=wait)
         t1 = time.perf_counter()
         pg.synchronize()
         torch.cuda.synchronize()

@@ -81,7 +81,8 @@ def analyse(name, recs, info=None):
     if sum(tot.values()):
         print("  phases summed over workgroups: " + ", ".join(f"{k} {100.0 * v / busy:.1f}%" for k, v in tot.items())
               + " of workgroup time")
-    first = [(s, phases.get(tile)) for _, s, tile in dur if phases.get(tile) and phases[tile]["batches"]]
+    first = [(s, phases.get(tile)) for _, s, tile in dur
+             if phases.get(tile) and phases[tile].get("batches") and "first_marks" in phases[tile]]
     if first:
         for lab, sel in (("starting < 2 us", [p for s, p in first if s * TICK_US < 2.0]),
                          ("starting later", [p for s, p in first if s * TICK_US >= 2.0])):
@@ -94,7 +95,7 @@ def analyse(name, recs, info=None):
     for d, s, tile in dur[:5]:
         extra = info(tile) if info and tile >= 0 else ""
         ph = phases.get(tile)
-        if ph and ph["batches"]:
+        if ph and ph.get("batches") and "first_marks" in ph:
             extra += (f"\n        {ph['batches']} batches: load {ph['load'] * TICK_US:.1f} us (first "
                       f"{ph['first_load'] * TICK_US:.1f}; milestones " + marks(ph) + "), compact "
                       f"{ph['compact'] * TICK_US:.1f} us, walk {ph['walk'] * TICK_US:.1f} us")
