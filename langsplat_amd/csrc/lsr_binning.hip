@@ -2140,9 +2140,6 @@ __global__ __launch_bounds__(256) void k_bin_count(int S, int sgx, int gx, int g
 #define LSR_BIN_STAGE 4096
 #endif
 constexpr int kStage = LSR_BIN_STAGE;
-#ifndef LSR_FWD_CLASS_CAP  // measurement knob: list lengths above it share the forward's top work class
-#define LSR_FWD_CLASS_CAP 0xFFFFFFFFu
-#endif
 
 // k_bin_count with the segment setup folded in, for a super-tile sort of ONE radix pass (S <= 256
 // super-tiles): the super-tile ranges are then the digit starts of the scanned [digit][block]
@@ -2314,8 +2311,8 @@ __global__ __launch_bounds__(256) void k_bin_emit(int S, int sgx, int gx, int gy
         if (seg == 0 && slot >= 0) {
             const uint2 r = make_uint2(table[slot], table[slot + c.nseg]);
             ranges[gt] = r;
-            // the forward's longest-first schedule: work = list length (capped: LSR_FWD_CLASS_CAP)
-            if (r.y > r.x) schedule_tile(sched_counts, sched_lists, gx * gy, gt, min(r.y - r.x, (uint32_t)LSR_FWD_CLASS_CAP));
+            // the forward's longest-first schedule: work = list length
+            if (r.y > r.x) schedule_tile(sched_counts, sched_lists, gx * gy, gt, r.y - r.x);
         }
     }
 #pragma unroll
