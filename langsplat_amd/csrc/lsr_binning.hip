@@ -223,9 +223,9 @@ static hipError_t scan_exclusive(const uint32_t* in, uint32_t* out, int n, uint3
 // (scan fault, the tile schedule's class counts) -- so the counters need no memset before the
 // forward -- then publishes counters[0..7] to pinned host memory (system scope) followed by the
 // sequence number the host spins on (one {value, seq} 64-bit slot per counter).
-#ifndef LSR_PUBLISH_THREADS  // measurement knob: the counter reduction's workgroup size
-#define LSR_PUBLISH_THREADS 1024
-#endif
+#ifndef LSR_PUBLISH_THREADS  // the counter reduction's workgroup size (measurement knob): 256 threads find
+#define LSR_PUBLISH_THREADS 256  // a CU beside the pipelined step's render workgroups sooner than 1024
+#endif                           // (C3 step 0.3999-0.4007 vs 0.4008-0.4015 ms, profiles/r05_publish_threads.txt)
 constexpr int kPublishThreads = LSR_PUBLISH_THREADS;
 
 __global__ __launch_bounds__(kPublishThreads) void k_publish_counters(int nb, const uint4* __restrict__ partial,
