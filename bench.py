@@ -517,9 +517,11 @@ def main():
                                 model.trainable(), optim, bucket=bucket, rotation=rot, model=model)
         pg.capture()
         pg_rot = rot
-        # untimed replays until the two streams' steady state (the first ~10 replays after a capture run
-        # ~3 % slower: profiles/r05_bench_first.json's timed steps 0.4115 ms against its reps' 0.399)
-        warm = rot * max(1, max(20, 2 * args.warmup) // rot)
+        # untimed replays until the two streams' steady state: the first replays after a capture run
+        # slower (profiles/r05_bench_first.json: timed steps 0.4115 ms after 20 warm replays, its reps
+        # 0.399), and a timed pass that starts before the streams have settled can stay at the slow
+        # level (a run with 20: 0.4467 timed, reps 0.4032-0.4039): 200 replays (~80 ms at C3)
+        warm = rot * max(1, max(200, 2 * args.warmup) // rot)
         for _ in range(warm):
             pg.replay()
         torch.cuda.synchronize()
