@@ -465,7 +465,7 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
     pp.zero = reinterpret_cast<uint32_t*>(geom + L.scan_regions);
     pp.zero_words = (int)L.zero_words;  // depth-sort scan status and the fused loss's words
     // placed emission (the MSD depth order's fused emission at super-tile-major positions)
-    const bool placed = !depth_order_uses_pass_count(P) && placed_emit(L, a->phase == LSR_PHASE_GEOMETRY);
+    const bool placed = msd_digits(P) == 256 && placed_emit(L, a->phase == LSR_PHASE_GEOMETRY);
     if (placed) {  // the bucket sort's count table
         pp.zero2 = reinterpret_cast<uint32_t*>(geom + L.sup_status);
         pp.zero2_words = (int)kSupWords;
@@ -965,7 +965,7 @@ int32_t lsr_adam_multi(int32_t count, const lsr_adam_tensor* tensors, float grad
         for (int32_t k = k0; k < count && k < k0 + kAdamMaxTensors; k++) {
             const lsr_adam_tensor& t = tensors[k];
             if (t.n < 0 || (t.n > 0 && (!t.param || !t.grad || !t.exp_avg || !t.exp_avg_sq)) ||
-                (t.step < 1 && !step_dev) || (step_dev && (t.step < -(int64_t)1 << 40 || t.step > (int64_t)1 << 40)))
+                (t.step < 1 && !step_dev) || (step_dev && (t.step < -((int64_t)1 << 40) || t.step > ((int64_t)1 << 40))))
                 return fail(LSR_ERR_INVALID, "lsr_adam_multi: invalid tensor entry");
             if (t.n == 0) continue;
             tab.hyper[tab.count] = AdamHyper{t.lr, t.beta1, t.beta2, t.eps, step_dev ? t.step : 0};

@@ -380,7 +380,7 @@ __device__ __forceinline__ int xcd_tile(int nblk, int remap)
     return x * q + min(x, r) + (i >> 3);
 }
 
-// MSD depth sort (launch_depth_order, P <= kMsdMaxKeys): one radix pass splits the keys into 256
+// MSD depth sort (launch_depth_order, P <= kMsd512MaxKeys): one radix pass splits the keys into 256 (512)
 // buckets by a monotone function of the key, read on the device from kxf (min / max visible key),
 // so no host value is needed; each bucket then sorts its keys on their own range.  The key is the
 // depth's float bits, and two bucket maps are used:
@@ -395,15 +395,19 @@ __device__ __forceinline__ int xcd_tile(int nblk, int remap)
 // widths: 3.7k..4.1k per bucket).  Over a wide range depth counts fall off with distance, where
 // logarithmic buckets stay even.  Culled keys (key_xf: max - min) land in the last bucket.
 constexpr float kMsdLinearRatio = 2.5f;
+// Above kMsdMaxKeys (below) the pass makes 512 buckets (9-bit digits: the same two
+// maps with twice the resolution), so the average bucket stays within one workgroup's LDS sort up
+// to kMsd512MaxKeys; `bits` = 8 or 9 is the digit width.
 
 struct MsdMap {
     uint32_t kmin;
     float dmin, scale;
     int shift;
+    int top;  // 2^bits - 1
     bool linear;
 };
 
-__device__ __forceinline__ MsdMap msd_map(const uint32_t* kxf)
+__device__ __forceinline__ MsdMap msd_map(const uint32_t* kxf, int dbits = 8)
 {
     MsdMap m;
     m.kmin = kxf[0];
@@ -411,19 +415,20 @@ __device__ __forceinline__ MsdMap msd_map(const uint32_t* kxf)
     const float dmax = __uint_as_float(kxf[1]);
     const float w = dmax - m.dmin;
     m.linear = m.dmin > 0.0f && dmax <= kMsdLinearRatio * m.dmin;  // false when none is visible
-    m.scale = w > 1e-30f ? 256.0f / w : 0.0f;
+    m.scale = w > 1e-30f ? (float)(1 << dbits) / w : 0.0f;
     const uint32_t span = kxf[1] - kxf[0];
     const int bits = span ? 32 - __clz(span) : 0;
-    m.shift = bits > 8 ? bits - 8 : 0;
+    m.shift = bits > dbits ? bits - dbits : 0;
+    m.top = (1 << dbits) - 1;
     return m;
 }
 
 // bucket of a transformed key kx = key_xf(key)
 __device__ __forceinline__ uint32_t msd_bucket(uint32_t kx, const MsdMap& m)
 {
-    if (!m.linear) return (kx >> m.shift) & 0xFFu;
+    if (!m.linear) return (kx >> m.shift) & (uint32_t)m.top;
     const float v = (__uint_as_float(kx + m.kmin) - m.dmin) * m.scale;
-    return (uint32_t)min(255, max(0, (int)v));
+    return (uint32_t)min(m.top, max(0, (int)v));
 }
 
 // Word ranges a kernel clears with grid-stride stores besides its own work (n = 0: none).  The
@@ -456,7 +461,8 @@ __device__ __forceinline__ bool uniform_pass(const uint32_t* krange, int shift)
 // srect (MSD pass with placed emission): the keys' tile rectangles by index; the block's super-tile
 // entry counts then also go to rows 256 + s (s < supers) of hist, so the scan that yields the
 // bucket starts also yields every super-tile's base in the super-tile-major entry list (+ n).
-template <int kItems>
+// msd: 0, or the MSD pass's digit bits (8, or 9 with kDig = 512 digit rows)
+template <int kItems, int kDig = 256>
 __global__ __launch_bounds__(kRadixThreads) void k_radix_hist(const uint32_t* __restrict__ keys, int n, int shift,
                                                               int nbits, uint32_t* __restrict__ hist, int nblk,
                                                               const uint32_t* __restrict__ kxf, int remap, int msd,
@@ -466,7 +472,8 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_hist(const uint32_t* __
                                                               const uint32_t* __restrict__ krange = nullptr)
 {
     constexpr int kWaves = kRadixThreads / 64;
-    __shared__ uint32_t wcnt[kWaves][256];
+    static_assert(kDig % kRadixThreads == 0, "digit rows per thread");
+    __shared__ uint32_t wcnt[kWaves][kDig];
     __shared__ uint32_t scnt[256];
     zero_words_strided(zero);
     if (dc.abort && *dc.abort) return;
@@ -474,15 +481,17 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_hist(const uint32_t* __
     if (dc.n) n = min(n, (int)*dc.n);
     MsdMap mm{};
     if (msd) {
-        mm = msd_map(kxf);
+        mm = msd_map(kxf, msd);
         shift = 0;
-        nbits = 8;
+        nbits = msd;
     }
     const int blk = xcd_tile(nblk, remap);
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
     const uint32_t mask = (1u << nbits) - 1u;
 #pragma unroll
-    for (int w = 0; w < kWaves; w++) wcnt[w][t] = 0;
+    for (int w = 0; w < kWaves; w++)
+#pragma unroll
+        for (int j = 0; j < kDig; j += kRadixThreads) wcnt[w][j + t] = 0;
     scnt[t] = 0;
     __syncthreads();
     const int base = blk * kRadixThreads * kItems + wave * 64 * kItems;
@@ -514,13 +523,17 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_hist(const uint32_t* __
         }
     }
     __syncthreads();
-    if (t <= (int)mask) {
-        uint32_t c = 0;
 #pragma unroll
-        for (int w = 0; w < kWaves; w++) c += wcnt[w][t];
-        hist[t * nblk + blk] = c;
+    for (int j = 0; j < kDig; j += kRadixThreads) {
+        const int dg = j + t;
+        if (dg <= (int)mask) {
+            uint32_t c = 0;
+#pragma unroll
+            for (int w = 0; w < kWaves; w++) c += wcnt[w][dg];
+            hist[(size_t)dg * nblk + blk] = c;
+        }
     }
-    if (srect && t < supers) hist[(size_t)(256 + t) * nblk + blk] = scnt[t];
+    if (srect && t < supers) hist[(size_t)(kDig + t) * nblk + blk] = scnt[t];
 }
 
 // Stable scatter of one block's tile.  Ranks: per wave, round by round (ballot match + the wave's
@@ -531,7 +544,8 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_hist(const uint32_t* __
 // kCarry (MSD depth pass, vals_in == null): the Gaussian's rectangle tail.rect[idx] rides along
 // with its key into tail.rect_ranked, so the bucket sort permutes rectangles inside its bucket
 // instead of gathering them across all of rect (tail.ns is not used).
-template <int kItems, bool kCarry = false>
+// kDig = 512: the 9-bit MSD pass (msd = 9), thread t ranking digits 2t and 2t + 1.
+template <int kItems, bool kCarry = false, int kDig = 256>
 __global__ __launch_bounds__(kRadixThreads) void k_radix_scatter(
     const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in, int n, int shift, int nbits,
     const uint32_t* __restrict__ hist, int nblk, uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
@@ -563,26 +577,32 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_scatter(
     }
     MsdMap mm{};
     if (msd) {
-        mm = msd_map(kxf);
+        mm = msd_map(kxf, msd);
         shift = 0;
-        nbits = 8;
+        nbits = msd;
     }
     auto digit_of = [&](uint32_t k) { return msd ? msd_bucket(k, mm) : (k >> shift) & ((1u << nbits) - 1u); };
     const int blk = xcd_tile(nblk, remap);
     constexpr int kTile = kRadixThreads * kItems;
     constexpr int kWaves = kRadixThreads / 64;
+    constexpr int kPerT = kDig / kRadixThreads;  // digits per thread in the digit loops
+    static_assert(kDig % kRadixThreads == 0, "digit rows per thread");
     __shared__ uint32_t sk[kTile];
     __shared__ uint32_t sv[kTile];
-    __shared__ uint32_t wcnt[kWaves][256];  // running counts, then each wave's offset within the digit
-    __shared__ uint32_t gbase[256];         // global output position of this block's first key per digit
-    __shared__ uint32_t dstart[256];        // block-local start of each digit in the reordered tile
+    __shared__ uint32_t wcnt[kWaves][kDig];  // running counts, then each wave's offset within the digit
+    __shared__ uint32_t gbase[kDig];         // global output position of this block's first key per digit
+    __shared__ uint32_t dstart[kDig];        // block-local start of each digit in the reordered tile
     __shared__ uint32_t wsum[kWaves];
     __shared__ uint2 sr[kCarry ? kTile : 1];
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
     const uint32_t mask = (1u << nbits) - 1u;
 #pragma unroll
-    for (int w = 0; w < kWaves; w++) wcnt[w][t] = 0;
-    gbase[t] = t <= (int)mask && t < hrows ? hist[t * hstride + blk] : 0u;
+    for (int j = 0; j < kPerT; j++) {
+        const int dg = kPerT * t + j;
+#pragma unroll
+        for (int w = 0; w < kWaves; w++) wcnt[w][dg] = 0;
+        gbase[dg] = dg <= (int)mask && dg < hrows ? hist[(size_t)dg * hstride + blk] : 0u;
+    }
     const int tile0 = blk * kTile;
     const int base = tile0 + wave * 64 * kItems;
     uint32_t key[kItems], val[kItems], rank[kItems];
@@ -608,14 +628,22 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_scatter(
         if (valid && r == 0) wcnt[wave][d] = c + (uint32_t)__popcll(peers);
     }
     __syncthreads();
-    // per digit: waves' exclusive offsets and the block-local digit start
+    // per digit: waves' exclusive offsets and the block-local digit start (thread t: digits
+    // kPerT t .. kPerT t + kPerT - 1, consecutive, so one scan of their sums orders them all)
     {
-        uint32_t tot = 0;
+        uint32_t dt[kPerT], tot = 0;
 #pragma unroll
-        for (int w = 0; w < kWaves; w++) {
-            const uint32_t c = wcnt[w][t];
-            wcnt[w][t] = tot;
-            tot += c;
+        for (int j = 0; j < kPerT; j++) {
+            const int dg = kPerT * t + j;
+            uint32_t run = 0;
+#pragma unroll
+            for (int w = 0; w < kWaves; w++) {
+                const uint32_t c = wcnt[w][dg];
+                wcnt[w][dg] = run;
+                run += c;
+            }
+            dt[j] = run;
+            tot += run;
         }
         uint32_t x = tot;
 #pragma unroll
@@ -627,7 +655,12 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_scatter(
         __syncthreads();
         uint32_t before = 0;
         for (int w = 0; w < wave; w++) before += wsum[w];
-        dstart[t] = before + x - tot;
+        uint32_t ex = before + x - tot;
+#pragma unroll
+        for (int j = 0; j < kPerT; j++) {
+            dstart[kPerT * t + j] = ex;
+            ex += dt[j];
+        }
     }
     __syncthreads();
 #pragma unroll
@@ -794,8 +827,9 @@ __device__ __forceinline__ uint64_t transpose64(uint64_t x)
 
 // ---------------------------------------------------------------- MSD depth sort: bucket pass
 //
-// Depth order for P <= kMsdMaxKeys: ONE stable radix pass on the top <= 8 bits of the key range
-// (k_radix_hist / scan / k_radix_scatter with msd = 1) puts every key in its bucket in id order;
+// Depth order for P <= kMsd512MaxKeys: ONE stable radix pass on the top <= 8 bits of the key range
+// (9 bits, 512 buckets, above kMsdMaxKeys; k_radix_hist / scan / k_radix_scatter with msd = the digit
+// bits) puts every key in its bucket in id order;
 // then one workgroup per bucket sorts the bucket on the remaining low bits in LDS (stable LSD
 // passes of 8 bits, wave64 ballot ranking) and writes the depth-order outputs (sorted ids, the
 // rectangle in depth order, super-tile entry counts).  Same (key, id) order as the LSD sort: four
@@ -809,7 +843,7 @@ constexpr int kBucketWaves = kBucketThreads / 64;
 constexpr int kBucketCap = LSR_BUCKET_CAP;
 static_assert(kBucketCap % 1024 == 0 && kBucketCap <= 8192, "bucket capacity");
 constexpr int kBucketRounds = kBucketCap / kBucketThreads;  // rounds of 64 keys per wave
-constexpr int64_t kMsdMaxKeys = 2000000;                    // above: expected buckets exceed LDS
+constexpr int64_t kMsdMaxKeys = 2000000;                    // above: 512 buckets (msd_digits)
 
 // A bucket in LDS is kBucketCap packed words {key bits not yet ranked, local index (13 bits)}:
 // pass 0 ranks on the low 8 key bits held in registers and packs the rest (<= 16 bits) above the
@@ -997,7 +1031,8 @@ struct BucketEmit {
     uint32_t* keys;  // null: no emission
     uint32_t* vals;
     uint32_t cap;
-    uint64_t* status;  // 256 words + the ticket (status[256]), zero at launch
+    uint64_t* status;  // one word per bucket + the ticket (status[buckets]), zero at launch
+    int msd_bits;      // the bucket map's digit bits (stall fallbacks)
     int sgx;
     uint32_t* stall;
     uint32_t spin_limit;
@@ -1055,6 +1090,7 @@ __device__ __forceinline__ void publish_bucket_total(const BucketEmit& em, int d
 }
 
 // The entry base of bucket d: the sum of the totals of buckets 0..d-1 (every thread calls it).
+template <int kDig>
 __device__ __forceinline__ uint32_t bucket_entry_base(const BucketEmit& em, int d, const uint32_t* kxf, uint32_t* wsum)
 {
     __shared__ uint32_t s_base;
@@ -1063,9 +1099,9 @@ __device__ __forceinline__ uint32_t bucket_entry_base(const BucketEmit& em, int 
     if (t < 64) {
         uint32_t part = 0, spins = 0;
         bool ok = true;
-        // every predecessor's word requested at once (up to 4 per lane: one memory round trip when
-        // they are all published, instead of one per 64 predecessors), then the missing ones polled
-        constexpr int kPer = 256 / 64;
+        // every predecessor's word requested at once (up to kDig / 64 per lane: one memory round trip
+        // when they are all published, instead of one per 64 predecessors), then the missing ones polled
+        constexpr int kPer = kDig / 64;
         uint64_t w[kPer];
 #pragma unroll
         for (int k = 0; k < kPer; k++) {
@@ -1096,7 +1132,7 @@ __device__ __forceinline__ uint32_t bucket_entry_base(const BucketEmit& em, int 
     __syncthreads();
     if (s_ok) return s_base;
     // stalled: the entries of every Gaussian whose bucket is below d, from the inputs
-    const MsdMap mm = msd_map(kxf);
+    const MsdMap mm = msd_map(kxf, em.msd_bits);
     uint32_t part = 0;
     for (int g = t; g < em.P; g += kBucketThreads)
         if (msd_bucket(key_xf(em.depth_key[g], kxf), mm) < (uint32_t)d) part += super_count(em.rect[g]);
@@ -1214,7 +1250,7 @@ __device__ __forceinline__ void super_cursors(BucketLds& L, const BucketEmit& em
     if (!s_ok) {  // stalled: per super-tile, the entries of every Gaussian whose bucket is below d
         if (t < 256) L.run[t] = 0u;
         __syncthreads();
-        const MsdMap mm = msd_map(em.kxf);
+        const MsdMap mm = msd_map(em.kxf, em.msd_bits);
         for (int gg = t; gg < em.P; gg += kBucketThreads) {
             const uint2 rc = em.rect[gg];
             if (rc.x == rc.y || msd_bucket(key_xf(em.depth_key[gg], em.kxf), mm) >= (uint32_t)d) continue;
@@ -1346,7 +1382,7 @@ __device__ __forceinline__ void place_runs(BucketLds& L, const BucketEmit& em, c
 // Measurement hook (LSR_BUCKET_TIMELINE=1): per bucket workgroup {start, end} (s_memrealtime,
 // 100 MHz), its hardware slot (XCC_ID << 16 | HW_ID bits 8..15), its key count and the times at
 // which the first pass, all passes and the output gathers ended.
-__device__ uint32_t g_bucket_timeline[256 * 8];
+__device__ uint32_t g_bucket_timeline[512 * 8];
 
 #ifndef LSR_BUCKET_MARK_BASE  // measurement knob: the timeline's 4th mark when the entry base is known
                               // (placed emission: when the entries are listed and ranked)
@@ -1355,6 +1391,8 @@ __device__ uint32_t g_bucket_timeline[256 * 8];
 #ifndef LSR_BUCKET_WAVES  // one bucket workgroup per CU: no need to squeeze registers for two
 #define LSR_BUCKET_WAVES 4
 #endif
+// kDig buckets (256, or 512 above kMsdMaxKeys); placed emission only with 256.
+template <int kDig>
 __global__ __launch_bounds__(kBucketThreads) __attribute__((amdgpu_waves_per_eu(LSR_BUCKET_WAVES, 8)))
 void k_depth_bucket_sort(
     int n, uint32_t* __restrict__ keys, uint32_t* __restrict__ ids, const uint32_t* __restrict__ hist_scan, int nblk,
@@ -1394,16 +1432,17 @@ void k_depth_bucket_sort(
     int d = (int)blockIdx.x;
     // every bucket's start from the scanned [bucket][block] histogram, loaded while the ticket is
     // taken (the range no longer waits behind the ticket's round trip)
-    __shared__ uint32_t s_start[257];
-    if (t < 256) s_start[t] = hist_scan[(size_t)t * nblk];
-    if (t == 256) s_start[256] = (uint32_t)n;
+    static_assert(kDig <= kBucketThreads, "one bucket start per thread");
+    __shared__ uint32_t s_start[kDig + 1];
+    if (t < kDig) s_start[t] = hist_scan[(size_t)t * nblk];
+    if (t == kDig) s_start[kDig] = (uint32_t)n;
     // placed emission: on when the view's entries fit (block-uniform); base(s) loaded early
-    const bool placed = em.sup_status && *em.etotal <= em.cap;
+    const bool placed = kDig == 256 && em.sup_status && *em.etotal <= em.cap;
     const uint32_t base_s = placed && t < em.supers ? em.sup_base[(size_t)t * em.sup_stride] - (uint32_t)em.P : 0u;
     if (t < 256) L.scnt[t] = 0u;
     if (em.keys) {  // fused emission: buckets by ticket (a waiting workgroup's predecessors run)
         __shared__ int s_d;
-        if (t == 0) s_d = (int)atomicAdd(reinterpret_cast<uint32_t*>(em.status + 256), 1u);
+        if (t == 0) s_d = (int)atomicAdd(reinterpret_cast<uint32_t*>(em.status + kDig), 1u);
         __syncthreads();
         d = s_d;
     } else {
@@ -1642,7 +1681,7 @@ void k_depth_bucket_sort(
         // its own does (publishing before the sort put a rectangle load and a scan on every
         // workgroup's critical path instead)
         publish_bucket_total(em, d, tot);
-        const uint32_t ebase = bucket_entry_base(em, d, kxf, L.wsum);
+        const uint32_t ebase = bucket_entry_base<kDig>(em, d, kxf, L.wsum);
         if (LSR_BUCKET_MARK_BASE) guard.mark(3);  // measurement only: the entry base known
         if ((uint64_t)ebase + tot > (uint64_t)em.cap) return;  // over capacity: the host re-runs unfused
         // the bucket's entries [ebase, ebase + tot) meet nbl blocks of the super-tile pass: their
@@ -1688,7 +1727,7 @@ void k_depth_bucket_sort(
         place_etot = etot;
         goto placed_tail;
     }
-    const uint32_t ebase = em.keys ? bucket_entry_base(em, d, kxf, L.wsum) : 0u;
+    const uint32_t ebase = em.keys ? bucket_entry_base<kDig>(em, d, kxf, L.wsum) : 0u;
     const bool emit = em.keys && (uint64_t)ebase + etot <= (uint64_t)em.cap;
     uint32_t carry = 0;
     for (int c0 = 0; c0 < nb; c0 += kBucketThreads) {  // in order, 1024 positions at a time
@@ -1732,27 +1771,39 @@ static int bucket_timeline_on()
 
 hipError_t bucket_timeline_read(uint32_t* out, int n)
 {
-    if (n > 256) n = 256;
+    if (n > 512) n = 512;
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bucket_timeline), sizeof(uint32_t) * 8 * n, 0,
                                hipMemcpyDeviceToHost);
 }
 
+template <int kDig>
 static hipError_t allow_bucket_lds()
 {
-    static const hipError_t e = hipFuncSetAttribute((const void*)k_depth_bucket_sort,
+    static const hipError_t e = hipFuncSetAttribute((const void*)k_depth_bucket_sort<kDig>,
                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)kBucketLdsBytes);
     return e;
 }
 
-// LSR_DEPTH_LSD=1 forces the LSD passes at any P; LSR_MSD_MAX_KEYS=n moves the MSD path's limit
-// (measurement / test knobs, read per call)
-bool depth_order_uses_pass_count(int P)
+// The depth order of P keys: 0 = LSD passes, else the MSD pass's bucket count -- 256 up to
+// kMsdMaxKeys, 512 up to kMsd512MaxKeys (about 8k keys per bucket on average: the LDS sort's
+// capacity), LSD above.  Knobs (measurement / tests, read per call): LSR_DEPTH_LSD=1 forces the LSD
+// passes; LSR_MSD_MAX_KEYS=n and LSR_MSD512_MAX_KEYS=n move the two limits; LSR_MSD_BUCKETS=512
+// takes 512 buckets wherever the MSD pass runs.
+constexpr int64_t kMsd512MaxKeys = 4200000;
+int msd_digits(int P)
 {
     const char* e = getenv("LSR_DEPTH_LSD");
+    if (e && e[0] == '1') return 0;
     const char* m = getenv("LSR_MSD_MAX_KEYS");
+    const char* m2 = getenv("LSR_MSD512_MAX_KEYS");
+    const char* b = getenv("LSR_MSD_BUCKETS");
     const int64_t lim = m ? (int64_t)atoll(m) : kMsdMaxKeys;
-    return P > lim || (e && e[0] == '1');
+    const int64_t lim2 = m2 ? (int64_t)atoll(m2) : kMsd512MaxKeys;
+    if (P <= lim) return b && atoi(b) == 512 ? 512 : 256;
+    return P <= lim2 ? 512 : 0;
 }
+
+bool depth_order_uses_pass_count(int P) { return msd_digits(P) == 0; }
 
 // ---------------------------------------------------------------- depth order + super-tile counts
 
@@ -1800,8 +1851,9 @@ hipError_t launch_depth_order(int P, int passes, const Layout& L, char* geom, ui
     const ScatterTail tail{reinterpret_cast<const uint2*>(geom + L.rect), reinterpret_cast<uint2*>(geom + L.rect_ranked),
                            ka};
     const uint32_t* kxf = counters + kCntKeyMin;
-    if (!depth_order_uses_pass_count(P)) {  // MSD pass + per-bucket LDS sort; `passes` is not used
-        hipError_t e = allow_bucket_lds();
+    const int nd = msd_digits(P);
+    if (nd) {  // MSD pass + per-bucket LDS sort; `passes` is not used
+        hipError_t e = nd == 512 ? allow_bucket_lds<512>() : allow_bucket_lds<256>();
         if (e != hipSuccess) return e;
         static const int remap = [] {
             const char* v = getenv("LSR_XCD_REMAP");
@@ -1809,9 +1861,11 @@ hipError_t launch_depth_order(int P, int passes, const Layout& L, char* geom, ui
         }();
         const bool small = radix_small(P);
         const int nblk = (P + kRadixThreads * (small ? 4 : 16) - 1) / (kRadixThreads * (small ? 4 : 16));
-        // placed emission: the MSD histogram also counts each block's super-tile entries (rows 256 +
-        // s); else the super-tile histogram the bucket sort counts into, and its scan's status words
-        const bool placed = fused_emit && placed_req && L.supers <= 256;
+        const int dbits = nd == 512 ? 9 : 8;
+        // placed emission (256 buckets): the MSD histogram also counts each block's super-tile entries
+        // (rows 256 + s); else the super-tile histogram the bucket sort counts into, and its scan's
+        // status words
+        const bool placed = fused_emit && placed_req && L.supers <= 256 && nd == 256;
         const bool shist_on = fused_emit && !placed && L.super_hist_words > 0;
         const ZeroList zmsd = shist_on
             ? ZeroList{{reinterpret_cast<uint32_t*>(geom + L.super_hist), reinterpret_cast<uint32_t*>(geom + L.super_hist_status),
@@ -1819,30 +1873,48 @@ hipError_t launch_depth_order(int P, int passes, const Layout& L, char* geom, ui
                        {(int)L.super_hist_words, (int)L.super_hist_status_words, 0, 0}}
             : ZeroList{};
         const uint2* srect = placed ? tail.rect : nullptr;
-        if (small)
+        const DevCount nodc{nullptr, nullptr};
+        if (nd == 512) {
+            if (small)
+                hipLaunchKernelGGL((k_radix_hist<4, 512>), dim3(nblk), dim3(kRadixThreads), 0, s, keys, P, 0, 9, hist,
+                                   nblk, kxf, remap, 9, zmsd, nodc, (const uint2*)nullptr, 0, 0, (const uint32_t*)nullptr);
+            else
+                hipLaunchKernelGGL((k_radix_hist<16, 512>), dim3(nblk), dim3(kRadixThreads), 0, s, keys, P, 0, 9, hist,
+                                   nblk, kxf, remap, 9, zmsd, nodc, (const uint2*)nullptr, 0, 0, (const uint32_t*)nullptr);
+        } else if (small) {
             hipLaunchKernelGGL(k_radix_hist<4>, dim3(nblk), dim3(kRadixThreads), 0, s, keys, P, 0, 8, hist, nblk, kxf,
-                               remap, 1, zmsd, DevCount{nullptr, nullptr}, srect, L.supers, L.sgx);
-        else
+                               remap, 8, zmsd, nodc, srect, L.supers, L.sgx);
+        } else {
             hipLaunchKernelGGL(k_radix_hist<16>, dim3(nblk), dim3(kRadixThreads), 0, s, keys, P, 0, 8, hist, nblk, kxf,
-                               remap, 1, zmsd, DevCount{nullptr, nullptr}, srect, L.supers, L.sgx);
+                               remap, 8, zmsd, nodc, srect, L.supers, L.sgx);
+        }
         if ((e = post(debug, s)) != hipSuccess) return e;
-        if ((e = scan_exclusive(hist, hist_scan, (256 + (placed ? L.supers : 0)) * nblk, regions, nullptr, stall, s,
+        if ((e = scan_exclusive(hist, hist_scan, (nd + (placed ? L.supers : 0)) * nblk, regions, nullptr, stall, s,
                                 debug)) != hipSuccess)
             return e;
         // the rectangles ride along into rect_ranked (bucket layout); the bucket sort permutes them
         const ScatterTail carry{tail.rect, tail.rect_ranked, nullptr};
-        if (small)
+        if (nd == 512) {
+            if (small)
+                hipLaunchKernelGGL((k_radix_scatter<4, true, 512>), dim3(nblk), dim3(kRadixThreads), 0, s, keys,
+                                   (const uint32_t*)nullptr, P, 0, 9, hist_scan, nblk, kb, vb, kxf, carry, remap, 9, nodc,
+                                   0, 512, ZeroList{}, (const uint32_t*)nullptr);
+            else
+                hipLaunchKernelGGL((k_radix_scatter<16, true, 512>), dim3(nblk), dim3(kRadixThreads), 0, s, keys,
+                                   (const uint32_t*)nullptr, P, 0, 9, hist_scan, nblk, kb, vb, kxf, carry, remap, 9, nodc,
+                                   0, 512, ZeroList{}, (const uint32_t*)nullptr);
+        } else if (small) {
             hipLaunchKernelGGL((k_radix_scatter<4, true>), dim3(nblk), dim3(kRadixThreads), 0, s, keys,
-                               (const uint32_t*)nullptr, P, 0, 8, hist_scan, nblk, kb, vb, kxf, carry, remap, 1,
-                               DevCount{nullptr, nullptr});
-        else
+                               (const uint32_t*)nullptr, P, 0, 8, hist_scan, nblk, kb, vb, kxf, carry, remap, 8, nodc);
+        } else {
             hipLaunchKernelGGL((k_radix_scatter<16, true>), dim3(nblk), dim3(kRadixThreads), 0, s, keys,
-                               (const uint32_t*)nullptr, P, 0, 8, hist_scan, nblk, kb, vb, kxf, carry, remap, 1,
-                               DevCount{nullptr, nullptr});
+                               (const uint32_t*)nullptr, P, 0, 8, hist_scan, nblk, kb, vb, kxf, carry, remap, 8, nodc);
+        }
         if ((e = post(debug, s)) != hipSuccess) return e;
         // bucket-local offsets into super_offset, bucket totals for k_emit_super (no P-long scan);
         // with fused emission also the super-tile entries themselves
         BucketEmit em{};
+        em.msd_bits = dbits;
         if (fused_emit) {
             em.keys = reinterpret_cast<uint32_t*>(geom + L.fused_keys);
             em.vals = reinterpret_cast<uint32_t*>(geom + L.fused_vals);
@@ -1866,9 +1938,14 @@ hipError_t launch_depth_order(int P, int passes, const Layout& L, char* geom, ui
                 em.kxf = kxf;
             }
         }
-        hipLaunchKernelGGL(k_depth_bucket_sort, dim3(256), dim3(kBucketThreads), kBucketLdsBytes, s, P, kb, vb,
-                           (const uint32_t*)hist_scan, nblk, kxf, tail.rect, va, tail.rect_ranked, off,
-                           reinterpret_cast<uint32_t*>(geom + L.bucket_totals), ka, bucket_timeline_on(), em);
+        if (nd == 512)
+            hipLaunchKernelGGL(k_depth_bucket_sort<512>, dim3(512), dim3(kBucketThreads), kBucketLdsBytes, s, P, kb, vb,
+                               (const uint32_t*)hist_scan, nblk, kxf, tail.rect, va, tail.rect_ranked, off,
+                               reinterpret_cast<uint32_t*>(geom + L.bucket_totals), ka, bucket_timeline_on(), em);
+        else
+            hipLaunchKernelGGL(k_depth_bucket_sort<256>, dim3(256), dim3(kBucketThreads), kBucketLdsBytes, s, P, kb, vb,
+                               (const uint32_t*)hist_scan, nblk, kxf, tail.rect, va, tail.rect_ranked, off,
+                               reinterpret_cast<uint32_t*>(geom + L.bucket_totals), ka, bucket_timeline_on(), em);
         return post(debug, s);
     }
     hipError_t e = (passes & 1)
@@ -1891,6 +1968,7 @@ struct MsdOffsets {
     const uint32_t* hist_scan;  // the MSD pass's scanned [digit][block] histogram: bucket starts
     int nblk;
     const uint32_t* kxf;        // visible depth-key min / max: the number of buckets
+    int ndig;                   // buckets: 256 or 512
 };
 
 __global__ __launch_bounds__(256) void k_emit_super(int P, int sgx, const uint32_t* __restrict__ sorted_ids,
@@ -1901,7 +1979,7 @@ __global__ __launch_bounds__(256) void k_emit_super(int P, int sgx, const uint32
                                                     int n1, uint32_t* __restrict__ z2, int n2,
                                                     uint32_t* __restrict__ z3, int n3, MsdOffsets msd, DevCount dc)
 {
-    __shared__ uint32_t s_start[256], s_base[256], s_wsum[4];
+    __shared__ uint32_t s_start[512], s_base[512], s_wsum[4];
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
     const int stride = gridDim.x * blockDim.x;
     // this rank's inputs first: their round trip overlaps the bucket bases' below
@@ -1912,10 +1990,17 @@ __global__ __launch_bounds__(256) void k_emit_super(int P, int sgx, const uint32
         g = sorted_ids[r];
         o = offset[r];
     }
-    if (msd.totals) {  // bucket starts and bases (every workgroup, 256 threads = 256 buckets)
-        const int t = threadIdx.x, ndig = 256;
-        s_start[t] = t < ndig ? msd.hist_scan[(size_t)t * msd.nblk] : (uint32_t)P;
-        uint32_t x = msd.totals[t], v = x;
+    const int per = msd.ndig / 256;  // buckets per thread (1 or 2, consecutive)
+    if (msd.totals) {  // bucket starts and bases (every workgroup, 256 threads)
+        const int t = threadIdx.x;
+        uint32_t v[2] = {0u, 0u}, x = 0;
+        for (int j = 0; j < per; j++) {
+            const int b = per * t + j;
+            s_start[b] = msd.hist_scan[(size_t)b * msd.nblk];
+            v[j] = msd.totals[b];
+            x += v[j];
+        }
+        const uint32_t sum = x;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
             const uint32_t y = __shfl_up(x, o, 64);
@@ -1925,7 +2010,11 @@ __global__ __launch_bounds__(256) void k_emit_super(int P, int sgx, const uint32
         __syncthreads();
         uint32_t before = 0;
         for (int i = 0; i < (t >> 6); i++) before += s_wsum[i];
-        s_base[t] = before + x - v;
+        uint32_t ex = before + x - sum;
+        for (int j = 0; j < per; j++) {
+            s_base[per * t + j] = ex;
+            ex += v[j];
+        }
         __syncthreads();
     }
     for (int w = r; w < n0; w += stride) z0[w] = 0u;
@@ -1937,7 +2026,7 @@ __global__ __launch_bounds__(256) void k_emit_super(int P, int sgx, const uint32
     int sx0, sy0, sx1, sy1;
     super_rect(rc, sx0, sy0, sx1, sy1);
     if (msd.totals) {  // + the base of the bucket holding rank r: the last bucket starting at or before r
-        int lo = 0, hi = 255;
+        int lo = 0, hi = msd.ndig - 1;
         while (lo < hi) {
             const int mid = (lo + hi + 1) >> 1;
             if (s_start[mid] <= (uint32_t)r) lo = mid;
@@ -2378,8 +2467,9 @@ __global__ __launch_bounds__(256) void k_bin_emit(int S, int sgx, int gx, int gy
 // the MSD depth order's offset parts for k_emit_super (null totals: LSD order, global offsets)
 static MsdOffsets msd_offsets(int P, const Layout& L, char* geom, char* image)
 {
-    MsdOffsets m{nullptr, nullptr, 0, nullptr};
-    if (depth_order_uses_pass_count(P)) return m;
+    MsdOffsets m{nullptr, nullptr, 0, nullptr, 256};
+    m.ndig = msd_digits(P);
+    if (m.ndig == 0) return m;
     const int tile = kRadixThreads * (radix_small(P) ? 4 : 16);
     m.totals = reinterpret_cast<const uint32_t*>(geom + L.bucket_totals);
     m.hist_scan = reinterpret_cast<const uint32_t*>(geom + L.radix_hist_scan);

@@ -74,8 +74,8 @@ struct Layout {
     size_t scan_region_geom;  // u32 words per depth-order scan region
     size_t loss_words;        // fused loss: per-workgroup / per-group words and tickets, after the scan regions
     size_t zero_words;        // u32 words preprocess clears from scan_regions (scan status + loss words)
-    size_t bucket_totals;     // MSD depth order: super-tile entries per top-digit bucket (256 u32)
-    size_t bucket_status;     // MSD depth order with fused emission: 256 {flag, bucket total} u64 words
+    size_t bucket_totals;     // MSD depth order: super-tile entries per top-digit bucket (<= 512 u32)
+    size_t bucket_status;     // MSD depth order with fused emission: <= 512 {flag, bucket total} u64 words
                               // + the bucket ticket, inside the range preprocess clears
     size_t fused_keys, fused_vals;  // the super-tile entries the bucket sort emits (fused_cap each)
     int64_t fused_cap;
@@ -134,12 +134,12 @@ inline Layout make_layout(int P, int W, int H, int64_t R, int64_t E)
         const size_t gx = (size_t)(W + kTile - 1) / kTile, gy = (size_t)(H + kTile - 1) / kTile;
         const size_t loss_bytes = 8 * gx * gy;  // one word per render forward workgroup
         L.loss_words = take(loss_bytes);
-        L.bucket_status = take(8 * 257);
-        L.zero_words = (L.bucket_status + 8 * 257 - L.scan_regions + 3) / 4;
+        L.bucket_status = take(8 * 513);
+        L.zero_words = (L.bucket_status + 8 * 513 - L.scan_regions + 3) / 4;
     }
     L.rect_ranked = take(8 * p);
     L.grad_records = take(4 * kGradStrideLang * p + 16);  // + padding: cleared as whole float4s
-    L.bucket_totals = take(4 * 256);
+    L.bucket_totals = take(4 * 512);
     {
         const int gx = (W + kTile - 1) / kTile, gy = (H + kTile - 1) / kTile;
         const int supers = ((gx + kSuper - 1) / kSuper) * ((gy + kSuper - 1) / kSuper);
@@ -312,6 +312,7 @@ hipError_t launch_depth_order(int P, int passes, const Layout& L, char* geom, ui
 // false: the depth order reads its pass count on the device (MSD pass + per-bucket LDS sort) and
 // ignores `passes`; true (large P): LSD passes, `passes` must cover the visible key range
 bool depth_order_uses_pass_count(int P);
+int msd_digits(int P);  // the depth order's MSD buckets (256 / 512), 0: LSD passes
 // LSR_FUSED_EMIT=0 turns the fused super-tile emission off (measurement knob, read once)
 bool fused_emit_enabled();
 // placed emission: the fused emission writes every entry at its super-tile-major position, so the

@@ -164,3 +164,51 @@ def test_sixteen_key_radix_tiles_match_the_oracle():
     r = subprocess.run([sys.executable, "-c", _RADIX16_CHILD], cwd=root, env=env, capture_output=True, text=True,
                        timeout=240)
     assert r.returncode == 0 and "RADIX16_OK" in r.stdout, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
+
+
+@pytest.mark.parametrize("kind", ["dense_bucket", "c3"])
+def test_512_msd_buckets_equal_256(kind, monkeypatch):
+    """Above 2M Gaussians the depth order's MSD pass makes 512 buckets (9-bit digits, lsr_binning.hip
+    msd_digits) so the buckets stay within one LDS sort.  Forced at smaller P (LSR_MSD_BUCKETS=512):
+    the same depth order, hence the same per-tile lists, ranges and images as the 256-bucket pass, bit
+    for bit.  Placed emission (a 256-bucket path) is off in both runs.  dense_bucket also puts one
+    bucket beyond LDS (the global-memory sort) beside the LDS buckets."""
+    from tests.test_gpu_parity import native_forward, state
+    st, inp = dense_bucket_scene() if kind == "dense_bucket" else c3_scene()
+    P = inp["means3D"].shape[0]
+    W, H = st.image_width, st.image_height
+    monkeypatch.setenv("LSR_PLACED", "0")
+    res = {}
+    for nb in ("512", "256"):
+        monkeypatch.setenv("LSR_MSD_BUCKETS", nb)
+        _, _, out = native_forward(st, inp)
+        s = state(out, P, W, H)
+        s.update(nr=out[0], color=out[1].cpu().numpy(), lang=out[2].cpu().numpy(), radii=out[3].cpu().numpy())
+        res[nb] = s
+    a, b = res["512"], res["256"]
+    assert a["nr"] == b["nr"] > 0
+    for k in ("ranges", "point_list", "final_T", "n_contrib", "color", "lang", "radii", "counters"):
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+
+
+def test_512_msd_buckets_oracle_and_stall_fallback(monkeypatch):
+    """The 512-bucket depth order against the oracle (forward bit-exact, backward within the parity
+    tolerance), then with every look-back on its stall path (spin limit 0: the bucket entry bases
+    from the inputs, through the 9-bit bucket map): the same forward, and the stall reported."""
+    from langsplat_amd import _native
+    from tests.scenes import scene
+    monkeypatch.setenv("LSR_MSD_BUCKETS", "512")
+    st, inp = scene(P=40000, W=320, H=240, seed=9, sh_degree=1, scale_range=(0.01, 0.06))
+    run, std, ind, out = check_forward_exact(st, inp)
+    assert out[0] > 0
+    check_backward(st, inp, run, out)
+    lib = _native.load()
+    torch.cuda.synchronize()
+    lib.lsr_debug_scan_stalls()  # clear
+    old = lib.lsr_debug_set_spin_limit(0)
+    try:
+        check_forward_exact(st, inp, run)
+        torch.cuda.synchronize()
+        assert lib.lsr_debug_scan_stalls() == 1
+    finally:
+        lib.lsr_debug_set_spin_limit(old)

@@ -3,7 +3,8 @@
 
 bench.py's `value` comes from langsplat_amd.pipeline.PipelinedGraphStep (capacity mode, the forward
 split in its geometry and composite halves, graphs on two streams).  Here, at full C3 (BASELINE.json
-configs[2]) and C5 (configs[4], the LSD depth order):
+configs[2]) and C5 (configs[4], the 512-bucket MSD depth order; the LSD passes where a test sets
+LSR_DEPTH_LSD=1):
   - the capacity-mode forward is bit-identical to the eager one and its backward matches it;
   - the benched pipelined form's first replay matches the oracle's language step (images bit for
     bit, loss, d(loss)/d(_language_feature)), and its later replays equal eager serial steps.
@@ -90,7 +91,7 @@ def test_capacity_mode_matches_eager_full_size(cfg, monkeypatch):
     """The benched language step's forward (fused activations + fused loss, raw parameters) in
     capacity mode against the eager forward at full size: images, radii, loss, per-tile ranges and
     order, final T and contributor counts bit-identical; the language-step backward's gradients
-    within the parity tolerance.  C5 (3M Gaussians) takes the LSD depth order."""
+    within the parity tolerance.  C5 (3M Gaussians) takes the 512-bucket MSD depth order."""
     monkeypatch.setenv("LANGSPLAT_AMD_FUSED", "1")
     c = CONFIGS[cfg]
     P, W, H = c["P"], c["width"], c["height"]
@@ -177,9 +178,11 @@ def test_pipelined_graph_full_c3_matches_oracle_and_eager(monkeypatch):
 
 
 def test_graphed_step_full_c5_matches_eager(monkeypatch):
-    """GraphedStep (one graph: render + loss + backward + Adam) at C5, where the depth order is the
-    LSD passes with the pass count of the last eager forward: 3 replays equal 3 eager steps."""
+    """GraphedStep (one graph: render + loss + backward + Adam) at C5 with the depth order as LSD
+    passes (LSR_DEPTH_LSD=1, the order above 4.2M Gaussians) and the pass count of the last eager
+    forward: 3 replays equal 3 eager steps."""
     monkeypatch.setenv("LANGSPLAT_AMD_FUSED", "1")
+    monkeypatch.setenv("LSR_DEPTH_LSD", "1")
     c = CONFIGS["C5"]
     P, W, H = c["P"], c["width"], c["height"]
     g = make_gaussians(P, seed=0)

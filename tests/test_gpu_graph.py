@@ -198,7 +198,7 @@ def _depth_scene(P, W, H, wide, seed):
 
 
 def test_capacity_mode_lsd_depth_order(monkeypatch):
-    """The LSD depth order (P > 2M, forced here by LSR_DEPTH_LSD=1) in capacity mode uses the pass
+    """The LSD depth order (P > 4.2M, forced here by LSR_DEPTH_LSD=1) in capacity mode uses the pass
     count of the thread's last eager forward: exact when it suffices (also when it exceeds the view's
     need), flagged when the view's key range needs more passes, exact again after an eager forward of
     that view."""

@@ -280,11 +280,12 @@ def test_full_size_oracle_parity(cfg):
     check_backward(st, inp, run, out, seed=3, outliers=1e-5)
 
 
-def test_full_size_oracle_parity_C5():
+def test_full_size_oracle_parity_C5(monkeypatch):
     """BASELINE.json configs[4]'s scene (3M Gaussians, 1920x1080, camera 0): above 2M Gaussians the
-    depth order takes the LSD passes, checked here at full size against the oracle -- forward
+    depth order's MSD pass makes 512 buckets, checked here at full size against the oracle -- forward
     bit-exact (images, radii, tile ranges, per-tile order, final T, contributor counts) and every
-    gradient within the tolerance of test_full_size_oracle_parity."""
+    gradient within the tolerance of test_full_size_oracle_parity -- and the LSD passes (the order
+    above 4.2M Gaussians, LSR_DEPTH_LSD=1) give the same bit-exact forward."""
     c = CONFIGS["C5"]
     g = make_gaussians(c["P"], seed=0)
     cam = make_cameras(1, c["width"], c["height"])[0]
@@ -295,6 +296,9 @@ def test_full_size_oracle_parity_C5():
     assert run.blends > 0
     run, std, ind, out = check_forward_exact(st, inp, run)
     check_backward(st, inp, run, out, seed=3, outliers=1e-5)
+    del std, ind, out
+    monkeypatch.setenv("LSR_DEPTH_LSD", "1")
+    check_forward_exact(st, inp, run)
 
 
 @pytest.mark.parametrize("cfg", ["C2", "C3", "C5"])
@@ -348,17 +352,20 @@ def test_full_size_properties(cfg):
         assert (lhs - rhs).abs().max().item() <= 1e-3 * scale, k
 
 
-@pytest.mark.parametrize("lsd", [False, True])
+@pytest.mark.parametrize("order", ["msd", "msd512", "lsd"])
 @pytest.mark.parametrize("kind", ["wide", "narrow", "ties", "cluster"])
-def test_depth_sort_pass_counts(kind, lsd, monkeypatch):
+def test_depth_sort_pass_counts(kind, order, monkeypatch):
     """The depth sort orders only the bits the visible keys span (key - min): a depth range of
     0.3..80 spans 27 bits, a sliver 12, exact ties none (id order).  cluster: 20k of 30k Gaussians
     within 1e-3 of one depth, the rest over 0.5..50 -- one top-digit bucket far larger than the
     MSD sort's LDS capacity (its global fallback).  The per-tile order (and everything downstream)
-    must stay bit-identical to the oracle's.  lsd: the LSD passes large P uses (LSR_DEPTH_LSD=1),
-    with the host's pass count: 4 passes, 2, none."""
-    if lsd:
+    must stay bit-identical to the oracle's.  msd512: the 512-bucket MSD pass of 2M..4.2M Gaussians
+    (LSR_MSD_BUCKETS=512); lsd: the LSD passes larger P uses (LSR_DEPTH_LSD=1), with the host's pass
+    count: 4 passes, 2, none."""
+    if order == "lsd":
         monkeypatch.setenv("LSR_DEPTH_LSD", "1")
+    if order == "msd512":
+        monkeypatch.setenv("LSR_MSD_BUCKETS", "512")
     g = torch.Generator().manual_seed({"wide": 31, "narrow": 32, "ties": 33, "cluster": 34}[kind])
     P, W, H = (30000, 160, 120) if kind == "cluster" else (3000, 96, 64)
     cam = make_cameras(1, W, H)[0]  # at (0, 0, -4) looking along +z: view depth = z + 4
