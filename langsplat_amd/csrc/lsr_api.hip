@@ -465,10 +465,10 @@ int32_t lsr_forward(const lsr_settings* s, const lsr_forward_args* a, lsr_alloc_
     pp.zero = reinterpret_cast<uint32_t*>(geom + L.scan_regions);
     pp.zero_words = (int)L.zero_words;  // depth-sort scan status and the fused loss's words
     // placed emission (the MSD depth order's fused emission at super-tile-major positions)
-    const bool placed = msd_digits(P) == 256 && placed_emit(L, a->phase == LSR_PHASE_GEOMETRY);
+    const bool placed = !depth_order_uses_pass_count(P) && placed_emit(L, a->phase == LSR_PHASE_GEOMETRY, msd_digits(P));
     if (placed) {  // the bucket sort's count table
         pp.zero2 = reinterpret_cast<uint32_t*>(geom + L.sup_status);
-        pp.zero2_words = (int)kSupWords;
+        pp.zero2_words = (int)sup_words(msd_digits(P));
     }
     pp.raw = a->raw;
     pp.shs_rest = a->shs_rest;

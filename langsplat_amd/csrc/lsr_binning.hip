@@ -1143,23 +1143,29 @@ __device__ __forceinline__ uint32_t bucket_entry_base(const BucketEmit& em, int 
 }
 
 // Placed emission's counts, in em.sup_status (cleared by preprocess): [super-tile][bucket] words
-// {kSupAgg | count} (row stride 256), then per group of 16 buckets [group][super-tile] words
-// {kSupAgg | the group's count}, then 16 group arrival counters.  Every bucket publishes its
+// {kSupAgg | count} (row stride kDig buckets), then per group of 16 buckets [group][super-tile] words
+// {kSupAgg | the group's count}, then kDig / 16 group arrival counters.  Every bucket publishes its
 // counts as soon as its rectangles are loaded; the last of a group to arrive also publishes the
-// group's sums.  A bucket's prefix for super-tile s is then <= 15 group sums + <= 15 counts of
-// its own group (30 words, not d), read once the bucket is sorted, when they are long published.
-constexpr size_t kSupGroupOff = 256 * 256;                       // words: the group sums
-constexpr size_t kSupArriveOff = kSupGroupOff + 256 * (256 / kSupGroup);  // words: the counters
-static_assert(kSupArriveOff + 256 / kSupGroup == kSupWords, "placed emission's count words");
+// group's sums.  A bucket's prefix for super-tile s is then < kDig / 16 group sums + <= 15 counts
+// of its own group (30 words with 256 buckets, 46 with 512; not d), read once the bucket is sorted,
+// when they are long published.
+template <int kDig>
+constexpr size_t sup_group_off() { return 256 * (size_t)kDig; }  // words: the group sums
+template <int kDig>
+constexpr size_t sup_arrive_off() { return sup_group_off<kDig>() + 256 * (size_t)(kDig / kSupGroup); }  // the counters
+static_assert(sup_arrive_off<256>() + 256 / kSupGroup == sup_words(256), "placed emission's count words");
+static_assert(sup_arrive_off<512>() + 512 / kSupGroup == kSupWords, "placed emission's count words");
 
+template <int kDig>
 __device__ __forceinline__ void publish_super_counts(const BucketLds& L, const BucketEmit& em, int d)
 {
+    constexpr size_t kSupGroupOff = sup_group_off<kDig>(), kSupArriveOff = sup_arrive_off<kDig>();
     const int t = threadIdx.x, g = d / kSupGroup;
     __shared__ int s_last;
     // relaxed atomics throughout (release / acquire at agent scope would write back / invalidate the
     // L2 per operation): every word carries its own flag, and readers poll for it
     if (t < em.supers)
-        __hip_atomic_store(&em.sup_status[(size_t)t * 256 + d], kSupAgg | L.scnt[t], __ATOMIC_RELAXED,
+        __hip_atomic_store(&em.sup_status[(size_t)t * kDig + d], kSupAgg | L.scnt[t], __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     if (t == 0)
@@ -1171,7 +1177,7 @@ __device__ __forceinline__ void publish_super_counts(const BucketLds& L, const B
     uint32_t v[kSupGroup];
 #pragma unroll
     for (int j = 0; j < kSupGroup; j++)
-        v[j] = __hip_atomic_load(&em.sup_status[(size_t)t * 256 + g * kSupGroup + j], __ATOMIC_RELAXED,
+        v[j] = __hip_atomic_load(&em.sup_status[(size_t)t * kDig + g * kSupGroup + j], __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_AGENT);
     uint32_t sum = 0, spins = 0;
 #pragma unroll
@@ -1181,7 +1187,7 @@ __device__ __forceinline__ void publish_super_counts(const BucketLds& L, const B
             // takes its own bounded wait and then its fallback (the prefixes from the inputs)
             if (++spins > em.spin_limit) return;
             __builtin_amdgcn_s_sleep(1);
-            v[j] = __hip_atomic_load(&em.sup_status[(size_t)t * 256 + g * kSupGroup + j], __ATOMIC_RELAXED,
+            v[j] = __hip_atomic_load(&em.sup_status[(size_t)t * kDig + g * kSupGroup + j], __ATOMIC_RELAXED,
                                      __HIP_MEMORY_SCOPE_AGENT);
         }
         sum += v[j] & kSupVal;
@@ -1192,26 +1198,30 @@ __device__ __forceinline__ void publish_super_counts(const BucketLds& L, const B
 
 // Adds to L.run[s] the entries of super-tile s in buckets 0..d-1 (s < S; every thread calls it):
 // the group sums below d's group and the counts of d's group members below d, one word per
-// thread and pair (s, j < 30) in flight at once; false when a wait passed the spin bound.
+// thread and pair (s, j < kSlots) in flight at once; false when a wait passed the spin bound.
+template <int kDig>
 __device__ __forceinline__ bool super_sum(BucketLds& L, const BucketEmit& em, int d)
 {
     if (em.spin_limit == 0u) return false;  // never wait: the fallback (tests)
+    constexpr size_t kSupGroupOff = sup_group_off<kDig>();
+    constexpr int kGroups = kDig / kSupGroup;
+    constexpr int kSlots = kGroups + kSupGroup;  // per super-tile: group sums, then group members
     const int t = threadIdx.x;
     const int g = d / kSupGroup, r = d - g * kSupGroup;
-    constexpr int kPer = 256 * 32 / kBucketThreads;  // (s, j) pairs per thread, j < 32
-    const int total = em.supers * 32;
+    constexpr int kPer = 256 * kSlots / kBucketThreads;  // (s, j) pairs per thread, j < kSlots
+    const int total = em.supers * kSlots;
     uint32_t v[kPer];
     int at[kPer];  // word index, -1: none
 #pragma unroll
     for (int k = 0; k < kPer; k++) {
-        const int f = k * kBucketThreads + t, sj = f >> 5, j = f & 31;
+        const int f = k * kBucketThreads + t, sj = f / kSlots, j = f % kSlots;
         at[k] = -1;
         v[k] = kSupAgg;
         if (f < total) {
             if (j < g)
                 at[k] = (int)(kSupGroupOff + (size_t)j * 256 + sj);
-            else if (j >= 16 && j - 16 < r)
-                at[k] = sj * 256 + g * kSupGroup + (j - 16);
+            else if (j >= kGroups && j - kGroups < r)
+                at[k] = sj * kDig + g * kSupGroup + (j - kGroups);
             if (at[k] >= 0)
                 v[k] = __hip_atomic_load(&em.sup_status[at[k]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
@@ -1231,20 +1241,21 @@ __device__ __forceinline__ bool super_sum(BucketLds& L, const BucketEmit& em, in
     }
 #pragma unroll
     for (int k = 0; k < kPer; k++)
-        if (at[k] >= 0 && (v[k] & kSupVal)) atomicAdd(&L.run[(k * kBucketThreads + t) >> 5], v[k] & kSupVal);
+        if (at[k] >= 0 && (v[k] & kSupVal)) atomicAdd(&L.run[(k * kBucketThreads + t) / kSlots], v[k] & kSupVal);
     return true;
 }
 
 // Placed emission: the write cursors L.run[s] = base(s) (thread s holds it) + the entries of
 // super-tile s in buckets 0..d-1 (every thread calls it).  A sum that waited past the spin bound
 // is computed from the inputs instead (same values).
+template <int kDig>
 __device__ __forceinline__ void super_cursors(BucketLds& L, const BucketEmit& em, int d, uint32_t base_s)
 {
     const int t = threadIdx.x;
     __shared__ int s_ok;
     if (t < 256) L.run[t] = 0u;
     __syncthreads();
-    const bool ok = super_sum(L, em, d);
+    const bool ok = super_sum<kDig>(L, em, d);
     if (t == 0) s_ok = ok ? 1 : 0;
     __syncthreads();
     if (!s_ok) {  // stalled: per super-tile, the entries of every Gaussian whose bucket is below d
@@ -1391,9 +1402,13 @@ __device__ uint32_t g_bucket_timeline[512 * 8];
 #ifndef LSR_BUCKET_WAVES  // one bucket workgroup per CU: no need to squeeze registers for two
 #define LSR_BUCKET_WAVES 4
 #endif
-// kDig buckets (256, or 512 above kMsdMaxKeys); placed emission only with 256.
+#ifndef LSR_BUCKET_WAVES_512  // the 512-bucket sort (measurement knob): 8 = two workgroups per CU, all 512
+#define LSR_BUCKET_WAVES_512 4  // at once, at 64 VGPRs + 56 B of scratch without placed emission: C5 depth
+#endif                          // order 150.9-151.7 against 148.6-148.9 us at 4 (profiles/r05_c5_msd512.txt)
+// kDig buckets (256, or 512 above kMsdMaxKeys).
 template <int kDig>
-__global__ __launch_bounds__(kBucketThreads) __attribute__((amdgpu_waves_per_eu(LSR_BUCKET_WAVES, 8)))
+__global__ __launch_bounds__(kBucketThreads)
+__attribute__((amdgpu_waves_per_eu(kDig == 512 ? LSR_BUCKET_WAVES_512 : LSR_BUCKET_WAVES, 8)))
 void k_depth_bucket_sort(
     int n, uint32_t* __restrict__ keys, uint32_t* __restrict__ ids, const uint32_t* __restrict__ hist_scan, int nblk,
     const uint32_t* __restrict__ kxf, const uint2* __restrict__ rect, uint32_t* __restrict__ sorted_ids,
@@ -1437,7 +1452,7 @@ void k_depth_bucket_sort(
     if (t < kDig) s_start[t] = hist_scan[(size_t)t * nblk];
     if (t == kDig) s_start[kDig] = (uint32_t)n;
     // placed emission: on when the view's entries fit (block-uniform); base(s) loaded early
-    const bool placed = kDig == 256 && em.sup_status && *em.etotal <= em.cap;
+    const bool placed = em.sup_status && *em.etotal <= em.cap;
     const uint32_t base_s = placed && t < em.supers ? em.sup_base[(size_t)t * em.sup_stride] - (uint32_t)em.P : 0u;
     if (t < 256) L.scnt[t] = 0u;
     if (em.keys) {  // fused emission: buckets by ticket (a waiting workgroup's predecessors run)
@@ -1454,7 +1469,7 @@ void k_depth_bucket_sort(
     guard.nb = nb;
     if (nb <= 0) {  // no key in this depth interval
         if (t == 0) totals[d] = 0u;
-        if (placed) publish_super_counts(L, em, d);  // zeros (L.scnt cleared before the ticket's barrier)
+        if (placed) publish_super_counts<kDig>(L, em, d);  // zeros (L.scnt cleared before the ticket's barrier)
         if (!placed) publish_bucket_total(em, d, 0u);
         return;
     }
@@ -1512,7 +1527,7 @@ void k_depth_bucket_sort(
     }
     const uint32_t span = khi - klo;
     const int lowbits = span ? 32 - __clz(span) : 0;
-    if (placed) publish_super_counts(L, em, d);  // counts completed by the barrier above
+    if (placed) publish_super_counts<kDig>(L, em, d);  // counts completed by the barrier above
     const uint32_t* place_rid = nullptr;  // placed tail: ids in depth order, and the entry total
     uint32_t place_etot = 0;
     // the LDS sort packs {key bits 8.., local index} in one word: at most 27 key bits
@@ -1651,7 +1666,7 @@ void k_depth_bucket_sort(
                 __syncthreads();
                 rank_entries(L, em, (int)tot);
                 if (LSR_BUCKET_MARK_BASE) guard.mark(3);  // measurement only: listed and ranked
-                super_cursors(L, em, d, base_s);
+                super_cursors<kDig>(L, em, d, base_s);
                 write_entries(L, em, tot);
                 return;
             }
@@ -1755,7 +1770,7 @@ void k_depth_bucket_sort(
     return;
     }
 placed_tail:  // placed emission from global memory: the Gaussians' ids in depth order at place_rid
-    super_cursors(L, em, d, base_s);  // its barriers also order the id stores before the reads
+    super_cursors<kDig>(L, em, d, base_s);  // its barriers also order the id stores before the reads
     place_runs(L, em, place_rid, nb);
     if (t == 0) totals[d] = place_etot;
 }
@@ -1822,12 +1837,12 @@ int msd_blocks(int P)
     return (P + tile - 1) / tile;
 }
 
-bool placed_emit(const Layout& L, bool geometry_phase)
+bool placed_emit(const Layout& L, bool geometry_phase, int buckets)
 {
     if (L.supers > 256) return false;
     const char* e = getenv("LSR_PLACED");
     if (e && (e[0] == '0' || e[0] == '1')) return e[0] == '1';
-    return !geometry_phase;
+    return !geometry_phase && buckets == 256;
 }
 
 hipError_t launch_depth_order(int P, int passes, const Layout& L, char* geom, uint32_t* counters, uint32_t* stall,
@@ -1862,10 +1877,9 @@ hipError_t launch_depth_order(int P, int passes, const Layout& L, char* geom, ui
         const bool small = radix_small(P);
         const int nblk = (P + kRadixThreads * (small ? 4 : 16) - 1) / (kRadixThreads * (small ? 4 : 16));
         const int dbits = nd == 512 ? 9 : 8;
-        // placed emission (256 buckets): the MSD histogram also counts each block's super-tile entries
-        // (rows 256 + s); else the super-tile histogram the bucket sort counts into, and its scan's
-        // status words
-        const bool placed = fused_emit && placed_req && L.supers <= 256 && nd == 256;
+        // placed emission: the MSD histogram also counts each block's super-tile entries (rows nd + s);
+        // else the super-tile histogram the bucket sort counts into, and its scan's status words
+        const bool placed = fused_emit && placed_req && L.supers <= 256;
         const bool shist_on = fused_emit && !placed && L.super_hist_words > 0;
         const ZeroList zmsd = shist_on
             ? ZeroList{{reinterpret_cast<uint32_t*>(geom + L.super_hist), reinterpret_cast<uint32_t*>(geom + L.super_hist_status),
@@ -1877,10 +1891,10 @@ hipError_t launch_depth_order(int P, int passes, const Layout& L, char* geom, ui
         if (nd == 512) {
             if (small)
                 hipLaunchKernelGGL((k_radix_hist<4, 512>), dim3(nblk), dim3(kRadixThreads), 0, s, keys, P, 0, 9, hist,
-                                   nblk, kxf, remap, 9, zmsd, nodc, (const uint2*)nullptr, 0, 0, (const uint32_t*)nullptr);
+                                   nblk, kxf, remap, 9, zmsd, nodc, srect, L.supers, L.sgx, (const uint32_t*)nullptr);
             else
                 hipLaunchKernelGGL((k_radix_hist<16, 512>), dim3(nblk), dim3(kRadixThreads), 0, s, keys, P, 0, 9, hist,
-                                   nblk, kxf, remap, 9, zmsd, nodc, (const uint2*)nullptr, 0, 0, (const uint32_t*)nullptr);
+                                   nblk, kxf, remap, 9, zmsd, nodc, srect, L.supers, L.sgx, (const uint32_t*)nullptr);
         } else if (small) {
             hipLaunchKernelGGL(k_radix_hist<4>, dim3(nblk), dim3(kRadixThreads), 0, s, keys, P, 0, 8, hist, nblk, kxf,
                                remap, 8, zmsd, nodc, srect, L.supers, L.sgx);
@@ -1931,7 +1945,7 @@ hipError_t launch_depth_order(int P, int passes, const Layout& L, char* geom, ui
             em.supers = L.supers;
             if (placed) {
                 em.sup_status = reinterpret_cast<uint32_t*>(geom + L.sup_status);
-                em.sup_base = hist_scan + 256 * (size_t)nblk;
+                em.sup_base = hist_scan + (size_t)nd * nblk;
                 em.sup_stride = nblk;
                 em.etotal = counters + kCntSuper;
                 em.sbits = L.super_bits;
@@ -2528,7 +2542,8 @@ hipError_t launch_binning(int P, int64_t R, const Layout& L, char* geom, char* i
                                {2 * L.tiles, (int)L.scan_region_bin, 0, 0}};
         hipLaunchKernelGGL(k_bin_count_fused, dim3((unsigned)L.seg_blocks), dim3(256), 0, s, L.supers, L.sgx, L.sgy,
                            L.gx, L.gy, nblk, L.supers, E,
-                           (const uint32_t*)(reinterpret_cast<uint32_t*>(geom + L.radix_hist_scan) + 256 * (size_t)nblk),
+                           (const uint32_t*)(reinterpret_cast<uint32_t*>(geom + L.radix_hist_scan) +
+                                             (size_t)msd_digits(P) * nblk),
                            sranges, seg_base, colpre, rowpre, k0, table, dc, (uint32_t)P, zplaced,
                            (int64_t)L.seg_table_words);
         if ((e = post(debug, s)) != hipSuccess) return e;

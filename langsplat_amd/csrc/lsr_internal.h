@@ -63,7 +63,11 @@ int msd_blocks(int P);                 // blocks of the MSD depth pass's histogr
 // placed emission's count words (lsr_binning.hip): [super-tile][bucket] counts, per group of
 // kSupGroup buckets the group sums, the group arrival counters
 constexpr int kSupGroup = 16;
-constexpr size_t kSupWords = 256 * 256 + 256 * (256 / kSupGroup) + 256 / kSupGroup;
+constexpr size_t sup_words(int buckets)  // with 256 or 512 depth-order buckets
+{
+    return 256 * (size_t)buckets + 256 * (size_t)(buckets / kSupGroup) + (size_t)(buckets / kSupGroup);
+}
+constexpr size_t kSupWords = sup_words(512);  // the allocation (either bucket count)
 size_t scan_region_words(int64_t n);  // look-back status + ticket of one scan of n words
 constexpr int kDepthScans = 5;         // 4 depth-sort passes + the instance-offset scan
 
@@ -124,8 +128,8 @@ inline Layout make_layout(int P, int W, int H, int64_t R, int64_t E)
     L.keys_a = take(4 * p);
     L.keys_b = take(4 * p);
     L.vals_b = take(4 * p);
-    // 256 digit rows, then (placed emission) <= 256 super-tile rows
-    const size_t hw_p = 2 * radix_hist_words((int64_t)p);
+    // 256 or 512 digit rows, then (placed emission) <= 256 super-tile rows
+    const size_t hw_p = 3 * radix_hist_words((int64_t)p);
     L.radix_hist = take(4 * hw_p);
     L.radix_hist_scan = take(4 * hw_p);  // scans are out-of-place (k_scan's stall fallback)
     L.scan_region_geom = scan_region_words((int64_t)(hw_p > p ? hw_p : p));
@@ -319,8 +323,11 @@ bool fused_emit_enabled();
 // binning's super-tile pass (scan + scatter) is not launched.  Needs <= 256 super-tiles.  Default:
 // on for a whole forward, off for the split geometry phase (whose kernels run beside the previous
 // view's render kernels, where the narrow scan + scatter launches fill gaps better than the longer
-// bucket kernel: measured); LSR_PLACED=1 / 0 forces it (read per call)
-bool placed_emit(const Layout& L, bool geometry_phase);
+// bucket kernel: measured) and for the 512-bucket depth order (2M..4.2M
+// Gaussians: a bucket's ~6k Gaussians have more entries than one LDS list, and the bucket kernel's
+// global-memory tail took C5's depth order from 149 to 242 us for 31 us less binning: measured);
+// LSR_PLACED=1 / 0 forces it (read per call)
+bool placed_emit(const Layout& L, bool geometry_phase, int buckets);
 // super-tile lists, per-(tile, segment) counts, scanned bases -> point_list and tile ranges.
 // emitted: the depth order's bucket sort already wrote the E entries into L.fused_keys / fused_vals
 // (super-tile-major when `placed`, the depth order's choice, else in depth order).

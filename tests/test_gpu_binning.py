@@ -166,18 +166,20 @@ def test_sixteen_key_radix_tiles_match_the_oracle():
     assert r.returncode == 0 and "RADIX16_OK" in r.stdout, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
 
 
+@pytest.mark.parametrize("placed", ["1", "0"])
 @pytest.mark.parametrize("kind", ["dense_bucket", "c3"])
-def test_512_msd_buckets_equal_256(kind, monkeypatch):
+def test_512_msd_buckets_equal_256(kind, placed, monkeypatch):
     """Above 2M Gaussians the depth order's MSD pass makes 512 buckets (9-bit digits, lsr_binning.hip
     msd_digits) so the buckets stay within one LDS sort.  Forced at smaller P (LSR_MSD_BUCKETS=512):
     the same depth order, hence the same per-tile lists, ranges and images as the 256-bucket pass, bit
-    for bit.  Placed emission (a 256-bucket path) is off in both runs.  dense_bucket also puts one
-    bucket beyond LDS (the global-memory sort) beside the LDS buckets."""
+    for bit, with placed emission (its [super-tile][bucket] counts over 32 groups of 16 buckets) and
+    with depth-order emission.  dense_bucket also puts one bucket beyond LDS (the global-memory sort,
+    and placed emission's multi-list tail) beside the LDS buckets."""
     from tests.test_gpu_parity import native_forward, state
     st, inp = dense_bucket_scene() if kind == "dense_bucket" else c3_scene()
     P = inp["means3D"].shape[0]
     W, H = st.image_width, st.image_height
-    monkeypatch.setenv("LSR_PLACED", "0")
+    monkeypatch.setenv("LSR_PLACED", placed)
     res = {}
     for nb in ("512", "256"):
         monkeypatch.setenv("LSR_MSD_BUCKETS", nb)
