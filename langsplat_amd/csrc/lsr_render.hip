@@ -920,12 +920,17 @@ constexpr size_t kCuLds = 160 * 1024;
 // Dynamic LDS that leaves room for exactly `wgs` workgroups of kernel fn per CU (0 if its static
 // LDS already allows no more), rounded to 1 KiB: the allocation granularity must not push the
 // last workgroup out.
+#ifndef LSR_PAD_MIN
+#define LSR_PAD_MIN 0
+#endif
 static size_t occupancy_pad(const void* fn, int wgs, const char* what)
 {
     hipFuncAttributes at{};
     size_t stat = 20 * 1024;
     if (hipFuncGetAttributes(&at, fn) == hipSuccess) stat = at.sharedSizeBytes;
-    const size_t per = (kCuLds / wgs) & ~(size_t)1023;  // wgs of them fit, one more does not
+    // wgs of them fit, one more does not: the largest such 1 KiB multiple, or (LSR_PAD_MIN=1) the
+    // smallest, which leaves the most LDS to the other stream's workgroups
+    const size_t per = LSR_PAD_MIN ? ((kCuLds / (wgs + 1) + 1024) & ~(size_t)1023) : (kCuLds / wgs) & ~(size_t)1023;
     const size_t pad = per > stat && per * (wgs + 1) > kCuLds ? per - stat : 0;
     if (getenv("LSR_SHARE_PRINT")) fprintf(stderr, "lsr: %s static LDS %zu pad %zu\n", what, stat, pad);
     return pad;
