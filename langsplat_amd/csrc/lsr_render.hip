@@ -1178,14 +1178,17 @@ __device__ __forceinline__ void bwd_pixel_blend(BwdPixel& q, float G, float og, 
 // v[9..11] (language).  Reduce-scatter: lane bit 5 picks v0 / f0, v1 / f1, f2 / - (permlane32),
 // bit 4 r0 / r1 (permlane16; r2 summed on both sides), bit 3 s0 / s1 (row_mirror), then bits 2..0.
 // Lane l then holds the wave total of value scatter_index5(l); scatter_writer5 picks one lane each.
+#ifndef LSR_BWD_DPP_DROP  // measurement knob: the last n (0..2) quad DPP steps left to the LDS atomics
+#define LSR_BWD_DPP_DROP 0  // (2^n writer lanes per value, each adding a partial sum): backward 141 ->
+#endif                      // 145 (n = 1) and 224 us (n = 2), same-address ds_add_f32 serialise
 __device__ __forceinline__ float wave_reduce_scatter5(const float (&v)[12], int lane)
 {
     const float r0 = swap32_add(v[0], v[9]), r1 = swap32_add(v[1], v[10]), r2 = swap32_add(v[11], 0.0f);
     const float s0 = swap16_add(r0, r1), s1 = swap16_add(r2, r2);
     float w = mirror_add<0x140>(s0, s1, (lane & 8) != 0);  // row_mirror
     w += dpp<0x141>(w);                                   // row_half_mirror
-    w += dpp<0x4E>(w);                                    // quad_perm [2,3,0,1]
-    w += dpp<0xB1>(w);                                    // quad_perm [1,0,3,2]
+    if (LSR_BWD_DPP_DROP < 2) w += dpp<0x4E>(w);          // quad_perm [2,3,0,1]
+    if (LSR_BWD_DPP_DROP < 1) w += dpp<0xB1>(w);          // quad_perm [1,0,3,2]
     // keep the last add next to its DPP move (one v_add_f32_dpp) instead of letting it sink into
     // the writers' branch as a separate v_mov_dpp + v_add
     asm volatile("" : "+v"(w));
@@ -1200,7 +1203,8 @@ __device__ __forceinline__ int scatter_index5(int lane)
 
 __device__ __forceinline__ bool scatter_writer5(int lane)
 {
-    return (lane & 7) == 0 && (!(lane & 8) || (lane & 48) == 0);
+    constexpr int kPart = (1 << LSR_BWD_DPP_DROP) - 1;  // lanes of a quad holding partial sums
+    return (lane & 7 & ~kPart) == 0 && (!(lane & 8) || (lane & 48) == 0);
 }
 
 // LDS slot of gradient value c: without the colour gradient values 6..8 are not stored; in the
