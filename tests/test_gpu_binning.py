@@ -47,12 +47,15 @@ def test_super_tile_counts(W, H, supers):
     check_backward(st, inp, run, out)
 
 
-def test_fused_emission_over_capacity():
+@pytest.mark.parametrize("buckets", ["256", "512"])
+def test_fused_emission_over_capacity(buckets, monkeypatch):
     """The depth sort's bucket workgroups write the super-tile entries themselves, into arrays of
     kFusedEntries (3) entries per Gaussian (lsr_internal.h).  A view whose Gaussians meet more
-    super-tiles than that (E > 3 P) emits nothing there and takes k_emit_super after the host wait.
-    Large Gaussians on a 1280x720 image: both the forward and the backward stay exact."""
+    super-tiles than that (E > 3 P) emits nothing there and takes k_emit_super after the host wait
+    (its bucket bases from the 256 or 512 bucket totals).  Large Gaussians on a 1280x720 image: both
+    the forward and the backward stay exact."""
     from tests.test_gpu_parity import state
+    monkeypatch.setenv("LSR_MSD_BUCKETS", buckets)
     P, W, H = 300, 1280, 720
     g = torch.Generator().manual_seed(41)
     cam = make_cameras(1, W, H)[0]
