@@ -1831,9 +1831,21 @@ bool fused_emit_enabled()
     return v;
 }
 
+// Keys per thread of the MSD pass's radix tiles: 16 above radix_small's limit, else 8 with 512
+// buckets (C5 depth order 152 -> 139 us against 4, profiles/r05_c5_msd512.txt) and 4 with 256 (the
+// tiles that fit beside the pipelined step's render kernels, radix_small); LSR_MSD_ITEMS=4 / 8
+// (measurement knob, read per call) sets it for either bucket count.
+static int msd_items(int P)
+{
+    if (!radix_small(P)) return 16;
+    const char* e = getenv("LSR_MSD_ITEMS");
+    if (e && (atoi(e) == 4 || atoi(e) == 8)) return atoi(e);
+    return msd_digits(P) == 512 ? 8 : 4;
+}
+
 int msd_blocks(int P)
 {
-    const int tile = kRadixThreads * (radix_small(P) ? 4 : 16);
+    const int tile = kRadixThreads * msd_items(P);
     return (P + tile - 1) / tile;
 }
 
@@ -1874,8 +1886,9 @@ hipError_t launch_depth_order(int P, int passes, const Layout& L, char* geom, ui
             const char* v = getenv("LSR_XCD_REMAP");
             return v && v[0] == '0' ? 0 : 1;
         }();
-        const bool small = radix_small(P);
-        const int nblk = (P + kRadixThreads * (small ? 4 : 16) - 1) / (kRadixThreads * (small ? 4 : 16));
+        const int items = msd_items(P);
+        const bool small = items == 4;
+        const int nblk = (P + kRadixThreads * items - 1) / (kRadixThreads * items);
         const int dbits = nd == 512 ? 9 : 8;
         // placed emission: the MSD histogram also counts each block's super-tile entries (rows nd + s);
         // else the super-tile histogram the bucket sort counts into, and its scan's status words
@@ -1892,11 +1905,17 @@ hipError_t launch_depth_order(int P, int passes, const Layout& L, char* geom, ui
             if (small)
                 hipLaunchKernelGGL((k_radix_hist<4, 512>), dim3(nblk), dim3(kRadixThreads), 0, s, keys, P, 0, 9, hist,
                                    nblk, kxf, remap, 9, zmsd, nodc, srect, L.supers, L.sgx, (const uint32_t*)nullptr);
+            else if (items == 8)
+                hipLaunchKernelGGL((k_radix_hist<8, 512>), dim3(nblk), dim3(kRadixThreads), 0, s, keys, P, 0, 9, hist,
+                                   nblk, kxf, remap, 9, zmsd, nodc, srect, L.supers, L.sgx, (const uint32_t*)nullptr);
             else
                 hipLaunchKernelGGL((k_radix_hist<16, 512>), dim3(nblk), dim3(kRadixThreads), 0, s, keys, P, 0, 9, hist,
                                    nblk, kxf, remap, 9, zmsd, nodc, srect, L.supers, L.sgx, (const uint32_t*)nullptr);
         } else if (small) {
             hipLaunchKernelGGL(k_radix_hist<4>, dim3(nblk), dim3(kRadixThreads), 0, s, keys, P, 0, 8, hist, nblk, kxf,
+                               remap, 8, zmsd, nodc, srect, L.supers, L.sgx);
+        } else if (items == 8) {
+            hipLaunchKernelGGL(k_radix_hist<8>, dim3(nblk), dim3(kRadixThreads), 0, s, keys, P, 0, 8, hist, nblk, kxf,
                                remap, 8, zmsd, nodc, srect, L.supers, L.sgx);
         } else {
             hipLaunchKernelGGL(k_radix_hist<16>, dim3(nblk), dim3(kRadixThreads), 0, s, keys, P, 0, 8, hist, nblk, kxf,
@@ -1913,12 +1932,19 @@ hipError_t launch_depth_order(int P, int passes, const Layout& L, char* geom, ui
                 hipLaunchKernelGGL((k_radix_scatter<4, true, 512>), dim3(nblk), dim3(kRadixThreads), 0, s, keys,
                                    (const uint32_t*)nullptr, P, 0, 9, hist_scan, nblk, kb, vb, kxf, carry, remap, 9, nodc,
                                    0, 512, ZeroList{}, (const uint32_t*)nullptr);
+            else if (items == 8)
+                hipLaunchKernelGGL((k_radix_scatter<8, true, 512>), dim3(nblk), dim3(kRadixThreads), 0, s, keys,
+                                   (const uint32_t*)nullptr, P, 0, 9, hist_scan, nblk, kb, vb, kxf, carry, remap, 9, nodc,
+                                   0, 512, ZeroList{}, (const uint32_t*)nullptr);
             else
                 hipLaunchKernelGGL((k_radix_scatter<16, true, 512>), dim3(nblk), dim3(kRadixThreads), 0, s, keys,
                                    (const uint32_t*)nullptr, P, 0, 9, hist_scan, nblk, kb, vb, kxf, carry, remap, 9, nodc,
                                    0, 512, ZeroList{}, (const uint32_t*)nullptr);
         } else if (small) {
             hipLaunchKernelGGL((k_radix_scatter<4, true>), dim3(nblk), dim3(kRadixThreads), 0, s, keys,
+                               (const uint32_t*)nullptr, P, 0, 8, hist_scan, nblk, kb, vb, kxf, carry, remap, 8, nodc);
+        } else if (items == 8) {
+            hipLaunchKernelGGL((k_radix_scatter<8, true>), dim3(nblk), dim3(kRadixThreads), 0, s, keys,
                                (const uint32_t*)nullptr, P, 0, 8, hist_scan, nblk, kb, vb, kxf, carry, remap, 8, nodc);
         } else {
             hipLaunchKernelGGL((k_radix_scatter<16, true>), dim3(nblk), dim3(kRadixThreads), 0, s, keys,
@@ -2484,7 +2510,7 @@ static MsdOffsets msd_offsets(int P, const Layout& L, char* geom, char* image)
     MsdOffsets m{nullptr, nullptr, 0, nullptr, 256};
     m.ndig = msd_digits(P);
     if (m.ndig == 0) return m;
-    const int tile = kRadixThreads * (radix_small(P) ? 4 : 16);
+    const int tile = kRadixThreads * msd_items(P);
     m.totals = reinterpret_cast<const uint32_t*>(geom + L.bucket_totals);
     m.hist_scan = reinterpret_cast<const uint32_t*>(geom + L.radix_hist_scan);
     m.nblk = (P + tile - 1) / tile;
@@ -2535,8 +2561,7 @@ hipError_t launch_binning(int P, int64_t R, const Layout& L, char* geom, char* i
     if (emitted && placed && L.supers <= 256) {
         // the bucket sort wrote the entries super-tile-major; the super-tile starts are the MSD
         // histogram's scanned super-tile rows (minus its P keys)
-        const bool small = radix_small(P);
-        const int nblk = (P + kRadixThreads * (small ? 4 : 16) - 1) / (kRadixThreads * (small ? 4 : 16));
+        const int nblk = msd_blocks(P);
         const ZeroList zplaced{{reinterpret_cast<uint32_t*>(ranges), regions + L.super_passes * L.scan_region_bin,
                                 nullptr, nullptr},
                                {2 * L.tiles, (int)L.scan_region_bin, 0, 0}};
