@@ -1310,6 +1310,31 @@ __device__ __forceinline__ void list_entries(BucketLds& L, const BucketEmit& em,
     }
 }
 
+// list_entries for the nb Gaussians of a bucket parked in global memory in depth order (ids, tile
+// rectangles, first entry offsets), one thread per Gaussian.
+__device__ __forceinline__ void list_entries_parked(BucketLds& L, const BucketEmit& em, const uint32_t* gid,
+                                                    const uint2* grc, const uint32_t* goff, int nb, uint32_t e0,
+                                                    uint32_t n)
+{
+    for (int i = threadIdx.x; i < nb; i += kBucketThreads) {
+        const uint32_t o = goff[i];
+        if (o >= e0 + n) continue;
+        const uint2 rc = grc[i];
+        if (rc.x == rc.y) continue;  // culled
+        int sx0, sy0, sx1, sy1;
+        super_rect(rc, sx0, sy0, sx1, sy1);
+        if (o + (uint32_t)((sx1 - sx0) * (sy1 - sy0)) <= e0) continue;  // all before this list
+        const uint32_t g = gid[i];
+        uint32_t e = o;
+        for (int y = sy0; y < sy1; y++)
+            for (int x = sx0; x < sx1; x++, e++)
+                if (e >= e0 && e < e0 + n) {
+                    L.w[0][e - e0] = entry_key(rc, x, y, em.sgx);
+                    L.w[1][e - e0] = g;
+                }
+    }
+}
+
 // Reorders the n listed entries stably by super-tile id (the key's low 8 bits), in place, with the
 // sort's ballot ranking; leaves the chunk-local super-tile starts in L.dstart.
 __device__ __forceinline__ void rank_entries(BucketLds& L, const BucketEmit& em, int n)
@@ -1668,6 +1693,35 @@ void k_depth_bucket_sort(
                 if (LSR_BUCKET_MARK_BASE) guard.mark(3);  // measurement only: listed and ranked
                 super_cursors<kDig>(L, em, d, base_s);
                 write_entries(L, em, tot);
+                return;
+            }
+            if constexpr (kDig == 512) {
+                // more entries than one list (the 512 buckets' ~6k Gaussians): lists of kBucketCap
+                // entries in the bucket's entry order, each listed from the sorted Gaussians parked
+                // in the depth-order arrays this fused emission leaves unused (write_entries advances
+                // the super-tile cursors, so a later list's entries follow an earlier one's in every
+                // super-tile); the arrays' barrier-ordered stores and loads stay in this workgroup.
+                // (256 buckets keep the global tail below: this path's registers, 127 instead of
+                // 104, would keep the bucket workgroup from sharing a CU in the pipelined step)
+#pragma unroll
+                for (int r = 0; r < kBucketRounds; r++) {
+                    if (r >= R) break;
+                    const int i = t + r * kBucketThreads;
+                    if (i < nb) {
+                        sorted_ids[start + i] = id[r];
+                        rect_ranked[start + i] = rc[r];
+                        local_off[start + i] = off[r];
+                    }
+                }
+                super_cursors<kDig>(L, em, d, base_s);  // its barriers order the stores before the loads
+                for (uint32_t e0 = 0; e0 < tot; e0 += (uint32_t)kBucketCap) {
+                    const uint32_t n = min((uint32_t)kBucketCap, tot - e0);
+                    list_entries_parked(L, em, sorted_ids + start, rect_ranked + start, local_off + start, nb, e0,
+                                        n);
+                    __syncthreads();
+                    rank_entries(L, em, (int)n);
+                    write_entries(L, em, n);
+                }
                 return;
             }
             // more entries than one list: the Gaussians' ids in depth order through global memory

@@ -324,8 +324,8 @@ bool fused_emit_enabled();
 // on for a whole forward, off for the split geometry phase (whose kernels run beside the previous
 // view's render kernels, where the narrow scan + scatter launches fill gaps better than the longer
 // bucket kernel: measured) and for the 512-bucket depth order (2M..4.2M
-// Gaussians: a bucket's ~6k Gaussians have more entries than one LDS list, and the bucket kernel's
-// global-memory tail took C5's depth order from 149 to 242 us for 31 us less binning: measured);
+// Gaussians: a bucket's ~6k Gaussians have more entries than one LDS list; listed from parked
+// arrays they take C5's depth order from 140 to 189 us for 32 us less binning: measured);
 // LSR_PLACED=1 / 0 forces it (read per call)
 bool placed_emit(const Layout& L, bool geometry_phase, int buckets);
 // super-tile lists, per-(tile, segment) counts, scanned bases -> point_list and tile ranges.
