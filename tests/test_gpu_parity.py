@@ -352,7 +352,7 @@ def test_full_size_properties(cfg):
         assert (lhs - rhs).abs().max().item() <= 1e-3 * scale, k
 
 
-@pytest.mark.parametrize("order", ["msd", "msd512", "lsd"])
+@pytest.mark.parametrize("order", ["msd", "msd512", "msd_items8", "msd512_items4", "lsd"])
 @pytest.mark.parametrize("kind", ["wide", "narrow", "ties", "cluster"])
 def test_depth_sort_pass_counts(kind, order, monkeypatch):
     """The depth sort orders only the bits the visible keys span (key - min): a depth range of
@@ -360,12 +360,15 @@ def test_depth_sort_pass_counts(kind, order, monkeypatch):
     within 1e-3 of one depth, the rest over 0.5..50 -- one top-digit bucket far larger than the
     MSD sort's LDS capacity (its global fallback).  The per-tile order (and everything downstream)
     must stay bit-identical to the oracle's.  msd512: the 512-bucket MSD pass of 2M..4.2M Gaussians
-    (LSR_MSD_BUCKETS=512); lsd: the LSD passes larger P uses (LSR_DEPTH_LSD=1), with the host's pass
-    count: 4 passes, 2, none."""
+    (LSR_MSD_BUCKETS=512, 8-key radix tiles); the _items variants swap the MSD pass's tile sizes
+    (LSR_MSD_ITEMS); lsd: the LSD passes larger P uses (LSR_DEPTH_LSD=1), with the host's pass count:
+    4 passes, 2, none."""
     if order == "lsd":
         monkeypatch.setenv("LSR_DEPTH_LSD", "1")
-    if order == "msd512":
+    if order.startswith("msd512"):
         monkeypatch.setenv("LSR_MSD_BUCKETS", "512")
+    if "_items" in order:
+        monkeypatch.setenv("LSR_MSD_ITEMS", order[-1])
     g = torch.Generator().manual_seed({"wide": 31, "narrow": 32, "ties": 33, "cluster": 34}[kind])
     P, W, H = (30000, 160, 120) if kind == "cluster" else (3000, 96, 64)
     cam = make_cameras(1, W, H)[0]  # at (0, 0, -4) looking along +z: view depth = z + 4
