@@ -37,7 +37,7 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from langsplat_amd import _native  # noqa: E402
+from langsplat_amd import _native, launch  # noqa: E402
 from langsplat_amd.distributed import GradBucket, init_from_env  # noqa: E402
 from langsplat_amd.optim import Adam as AmdAdam  # noqa: E402
 from langsplat_amd.pipeline import PipelinedGraphStep, ViewPipeline  # noqa: E402
@@ -344,8 +344,17 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--json-out", default=None)
     args = ap.parse_args()
+    if launch.should_launch(args.gpus):
+        # a plain `python bench.py --gpus N`: start the N ranks here (before anything touches the GPU)
+        sys.exit(launch.launch([os.path.abspath(__file__)] + sys.argv[1:], args.gpus))
 
     rank, world = init_from_env()
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the process group has {world} rank(s)")
+    backend = dist.get_backend() if world > 1 else None
+    if backend == "nccl" and world > torch.cuda.device_count():
+        raise SystemExit(f"bench.py: {world} RCCL ranks need {world} GPUs ({torch.cuda.device_count()} visible); "
+                         "LSR_DIST_BACKEND=gloo rehearses several ranks on one GPU")
     # one GPU per rank; the modulo only matters for a gloo rehearsal of N ranks on fewer GPUs
     local_rank = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local_rank)
@@ -677,6 +686,7 @@ def main():
         "config": {"workload": f"{cfg}: {P} Gaussians, {W}x{H}, SH deg 3 + 3-ch language feature, "
                                f"include_feature train step, 1 view per GPU",
                    "gaussians": P, "width": W, "height": H, "views": world, "parallelism": f"dp{world} (views)",
+                   "ranks": world, "backend": backend or "none (1 rank)",
                    "blends_per_step": blends_all, "num_rendered_rank0": nr, "visible_rank0": visible,
                    "activation_and_loss": "fused" if fused else "torch",
                    "gradients": "all geometry" if _native.FORCE_GEOMETRY_GRADS else

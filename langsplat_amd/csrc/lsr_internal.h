@@ -445,7 +445,7 @@ hipError_t launch_render_backward(const RenderParams& p, int tiles, hipStream_t 
 hipError_t launch_loss_background(const RenderParams& p, hipStream_t s);
 hipError_t render_stats_read(unsigned long long* out, int n);  // reads and clears
 hipError_t render_timeline_read(uint32_t* out, int kernel, int n);
-hipError_t bucket_timeline_read(uint32_t* out, int n);
-hipError_t launch_clock_probe(uint64_t* out, hipStream_t s);  // lsr_debug_clock_probe  // LSR_BUCKET_TIMELINE=1 records (k_depth_bucket_sort)
+hipError_t bucket_timeline_read(uint32_t* out, int n);  // LSR_BUCKET_TIMELINE=1 records (k_depth_bucket_sort)
+hipError_t launch_clock_probe(uint64_t* out, hipStream_t s);  // lsr_debug_clock_probe
 
 }  // namespace lsr

@@ -91,6 +91,17 @@ class GradBucket:
             self.stats_norm = self.flat[off:off + P]
             self.stats_count = self.flat[off + P:off + 2 * P]
 
+    def matches(self, params: Iterable[torch.Tensor]) -> bool:
+        """True when the bucket was built over exactly these (trainable) tensors, with their current
+        sizes.  densify_and_prune and reset_opacity (scene/gaussian_model.py:277-281,326-482) replace
+        the parameters: a bucket built before reduces the old tensors' slices."""
+        ps = [p for p in params if p.requires_grad]
+        if [id(p) for p in ps] != [id(p) for p in self.params]:
+            return False
+        if not self.direct and any(v.shape != p.shape for p, v in zip(ps, self.views)):
+            return False
+        return not self.densify_points or self.densify_points == int(ps[0].shape[0])
+
     @property
     def nbytes(self) -> int:
         return sum(p.numel() for p in self.params) * 4

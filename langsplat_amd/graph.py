@@ -146,6 +146,29 @@ def capture_key(model, optimizer, params):
     return (deg, tuple((id(p), p.data_ptr(), tuple(p.shape)) for p in ps))
 
 
+def current_params(optimizer, params):
+    """The tensors a captured step differentiates: the optimizer's current trainable parameters
+    (densification and reset_opacity replace them in its groups), else the given list."""
+    if optimizer is None:
+        return list(params)
+    return [p for g in optimizer.param_groups for p in g["params"] if p.requires_grad]
+
+
+def resolve_bucket(bucket, factory, params):
+    """The gradient bucket a (re-)capture reduces: `bucket` while it was built over `params`;
+    otherwise a fresh one from factory(params) -- or an error, since a stale bucket would reduce the
+    replaced tensors' slices and leave the new gradients un-averaged (ranks drifting apart)."""
+    if bucket is None or bucket.matches(params):
+        return bucket
+    if factory is None:
+        raise RuntimeError("the parameters were replaced since the GradBucket was built (densification, "
+                           "reset_opacity): pass bucket_factory= to rebuild it at the re-capture")
+    nb = factory(params)
+    if not nb.matches(params):
+        raise RuntimeError("bucket_factory(params) returned a bucket over other tensors")
+    return nb
+
+
 def _as_view(view):
     """(camera, gt, mask), (camera,) or a camera -> (camera, gt, mask)."""
     if isinstance(view, (tuple, list)):
@@ -158,7 +181,8 @@ def _as_view(view):
 
 class GraphedStep:
     def __init__(self, step_fn: Callable[[], torch.Tensor], params: Iterable[torch.Tensor], headroom: float = 1.125,
-                 warmup: int = 2, optimizer=None, view: Optional[ViewSlot] = None, model=None, bucket=None):
+                 warmup: int = 2, optimizer=None, view: Optional[ViewSlot] = None, model=None, bucket=None,
+                 bucket_factory=None):
         """step_fn: runs render + loss + loss.backward() and returns the loss; params: the tensors
         whose .grad the step produces (the trainable parameters); optimizer: stepped inside the graph;
         view: the ViewSlot step_fn renders from (replay(view=...) then changes the view); model: the
@@ -167,10 +191,13 @@ class GraphedStep:
         re-captures over the optimizer's current parameters.  bucket (N > 1, with an optimizer): a
         langsplat_amd.distributed.GradBucket whose all-reduce -- carrying the overflow flag, so every
         rank skips when one view overflowed -- runs between the backward and Adam: inside the graph
-        with RCCL, between two graphs with gloo."""
+        with RCCL, between two graphs with gloo.  A re-capture after the parameters were replaced
+        rebuilds the bucket with bucket_factory(params) (`self.bucket` is then the new one; a step_fn
+        that stages densification statistics reads it from there) and raises without a factory."""
         if bucket is not None and optimizer is None:
             raise ValueError("GraphedStep: a bucket is reduced before the captured optimizer step")
         self.bucket = bucket
+        self.bucket_factory = bucket_factory
         self.graph_adam = None
         self.step_fn = step_fn
         self.model = model
@@ -209,8 +236,9 @@ class GraphedStep:
         self.entries = max(int(e * self.headroom) + 1024, int(min_entries))
 
     def capture(self, min_rendered=0, min_entries=0):
-        if self.optimizer is not None:  # the optimizer's current tensors (densification replaces them)
-            self.params = [p for g in self.optimizer.param_groups for p in g["params"] if p.requires_grad]
+        # the optimizer's current tensors (densification replaces them), and a bucket over those
+        self.params = current_params(self.optimizer, self.params)
+        self.bucket = resolve_bucket(self.bucket, self.bucket_factory, self.params)
         self.key = capture_key(self.model, self.optimizer, self.params)
         self.stale_released = release_stale_accumulators(self.params)  # the caller's held graphs (module doc)
         self._measure(min_rendered, min_entries)

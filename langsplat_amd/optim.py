@@ -61,6 +61,7 @@ class Adam(torch.optim.Optimizer):
         if self._step_dev is None or self._step_dev.device != dev:
             self._step_dev = torch.zeros((_native.ADAM_STEP_WORDS,), dtype=torch.int64, device=dev)
         self._seed_device_count()
+        self._lr_dev = None  # rewritten before the next replay (the table order stays until a capture sets it)
         self._dev_ahead = False
 
     def _seed_device_count(self):
@@ -75,7 +76,6 @@ class Adam(torch.optim.Optimizer):
 
     def step_offset(self, p) -> int:
         return self._step_offset.get(p, 0)
-        self._lr_dev = None  # rewritten before the next replay (the table order stays until a capture sets it)
 
     @torch.no_grad()
     def sync_steps(self):

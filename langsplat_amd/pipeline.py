@@ -38,7 +38,8 @@ import torch
 
 from . import _native
 from .distributed import collective_capturable
-from .graph import _as_view, _fused_tail_enabled, _nullctx, capture_key, graph_capture, release_stale_accumulators
+from .graph import (_as_view, _fused_tail_enabled, _nullctx, capture_key, current_params, graph_capture,
+                    release_stale_accumulators, resolve_bucket)
 
 
 class ViewPipeline:
@@ -160,12 +161,13 @@ class PipelinedGraphStep:
     only after this view's compositing), LSR_PG_PRIO=geo|step (stream priorities), LSR_PG_ROT."""
 
     def __init__(self, forward_fn, params, optimizer, headroom: float = 1.125, warmup: int = 2, bucket=None,
-                 slots=None, sets: int = None, rotation: int = None, model=None):
+                 slots=None, sets: int = None, rotation: int = None, model=None, bucket_factory=None):
         self.forward_fn = forward_fn
         self.model = model  # its active_sh_degree is part of the capture key (graph.capture_key)
         self.params = [p for p in params]
         self.optimizer = optimizer
         self.bucket = bucket
+        self.bucket_factory = bucket_factory  # rebuilds the bucket at a re-capture over replaced parameters
         self.headroom = float(headroom)
         self.warmup = int(warmup)
         dev = self.params[0].device
@@ -251,6 +253,10 @@ class PipelinedGraphStep:
             for j in range(S - 1):
                 self.slots[j].load(*_as_view(views[j]))
                 self._loaded[j] = self._assigned[j] = views[j]
+        # the optimizer's current tensors (a parameter replaced since the last capture: the capture key
+        # changed, replay() re-captures here) and a gradient bucket built over them
+        self.params = current_params(self.optimizer, self.params)
+        self.bucket = resolve_bucket(self.bucket, self.bucket_factory, self.params)
         # the caller's still-alive autograd graphs keep the parameters' AccumulateGrad nodes bound to
         # their streams: released, so the warm-up and the captures create their own (graph.py)
         self.key = capture_key(self.model, self.optimizer, self.params)
@@ -502,7 +508,8 @@ class PipelinedGraphStep:
         if self.g_comp[0] is None and getattr(self, "g_rot", None) is None:
             self.capture()
         elif (self.R == 1 or self.k % self.R == 0) and capture_key(self.model, self.optimizer, self.params) != self.key:
-            self._recapture(self.rendered, self.entries)  # an SH-degree step since the capture
+            # an SH-degree step or replaced parameters since the capture
+            self._recapture(self.rendered, self.entries)
         if self.R > 1:
             return self._replay_rotation(next_view, wait)
         S = self.S

@@ -1,5 +1,6 @@
-"""View-sharded data parallelism on CPU (gloo, world_size 2 and 3): the all-reduced gradient
-bucket equals the sum of the per-view single-process gradients (SURVEY.md §8e parity)."""
+"""View-sharded data parallelism on CPU (gloo, world_size 2, 3 and 8 -- north_star's 8-view
+partitioning): the all-reduced gradient bucket equals the sum of the per-view
+single-process gradients (SURVEY.md §8e parity)."""
 import os
 import socket
 
@@ -78,7 +79,7 @@ def _worker(rank, world, port, out_dir):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_allreduced_bucket_equals_sum_of_view_gradients(tmp_path, world):
     port = _free_port()
     mp.spawn(_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True)
@@ -140,7 +141,7 @@ def _densify_worker(rank, world, port, out_dir, average):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,average", [(2, True), (3, True), (3, False)])
+@pytest.mark.parametrize("world,average", [(2, True), (3, True), (3, False), (8, True)])
 def test_densification_statistics_sum_over_views(tmp_path, world, average):
     """RGB-mode densification statistics (train.py:125-126, scene/gaussian_model.py:480-482) over
     view-sharded ranks equal the reference's accumulation over the same views done one after
@@ -187,7 +188,7 @@ def _flag_worker(rank, world, port, out_dir):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_overflow_flag_rides_the_gradient_collective(tmp_path, world):
     """a view over capacity on ONE rank sets the flag on EVERY rank (the flag is
     all-reduced in the same collective as the gradients), so every rank skips the optimizer step and
@@ -205,3 +206,27 @@ def test_overflow_flag_rides_the_gradient_collective(tmp_path, world):
     for r in range(1, world):
         for k, v in outs[r].items():
             assert (torch.equal(v, outs[0][k]) if torch.is_tensor(v) else v == outs[0][k]), k
+
+
+def test_bucket_matches_and_is_rebuilt_after_parameter_replacement():
+    """a capture over replaced parameters (reset_opacity, densify_and_prune) must not keep
+    a bucket built over the old tensors: resolve_bucket keeps a matching bucket, rebuilds with the
+    factory, and raises without one."""
+    from langsplat_amd.graph import resolve_bucket
+    xyz = torch.nn.Parameter(torch.zeros((10, 3)))
+    opac = torch.nn.Parameter(torch.zeros((10, 1)))
+    b = GradBucket([xyz, opac], densify_points=10)
+    assert b.matches([xyz, opac]) and resolve_bucket(b, None, [xyz, opac]) is b
+    new_opac = torch.nn.Parameter(torch.zeros((10, 1)))  # reset_opacity: same shape, a new tensor
+    assert not b.matches([xyz, new_opac])
+    with pytest.raises(RuntimeError, match="bucket_factory"):
+        resolve_bucket(b, None, [xyz, new_opac])
+    nb = resolve_bucket(b, lambda ps: GradBucket(ps, densify_points=ps[0].shape[0]), [xyz, new_opac])
+    assert nb is not b and nb.matches([xyz, new_opac]) and new_opac.grad.data_ptr() == nb.views[1].data_ptr()
+    grown = [torch.nn.Parameter(torch.zeros((12, 3))), torch.nn.Parameter(torch.zeros((12, 1)))]
+    assert not nb.matches(grown)  # densification: other tensors, other P
+    with pytest.raises(RuntimeError, match="other tensors"):
+        resolve_bucket(nb, lambda ps: GradBucket(ps, densify_points=10), grown)
+    d = GradBucket([xyz])
+    assert d.direct and d.matches([xyz, torch.nn.Parameter(torch.zeros(2), requires_grad=False)])
+    assert resolve_bucket(None, None, [xyz]) is None

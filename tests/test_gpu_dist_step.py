@@ -63,3 +63,27 @@ def test_two_rank_language_step_averages_the_views_gradients(tmp_path):
     a, b = outs[0]["pipelined_graph"]["param"].double(), outs[0]["eager"]["param"].double()
     off = int(((a - b).abs() > 1e-6 + 1e-5 * b.abs()).sum())
     assert off <= 1e-5 * a.numel(), off
+
+
+def test_two_rank_graphed_rgb_step_rebuilds_its_bucket_after_reset_opacity(tmp_path):
+    """GraphedStep(bucket=) re-captured after reset_opacity replaced the opacity tensor
+    reduces the new tensor's gradient through a bucket rebuilt by bucket_factory (both ranks end
+    identical and equal to the eager loop with its own rebuilt bucket), and refuses without one."""
+    env = dict(os.environ, LSR_DIST_BACKEND="gloo", OMP_NUM_THREADS="4")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "tests", "dist_worker_graph.py"), str(tmp_path)]
+    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    outs = [torch.load(tmp_path / f"graph{k}.pt", weights_only=True) for k in (0, 1)]
+    from tests.test_gpu_captured_forms import assert_close_mostly
+    for o in outs:
+        assert o["refused"]
+        (pe, se, _), (pg, sg, caps) = o["eager"], o["graph"]
+        assert se == sg and se["opacity"] == se["xyz"] - 1  # the reset iteration left opacity out
+        assert caps == 2  # the first capture and the one after the reset
+        for n in pe:
+            assert_close_mostly(n, pg[n], pe[n], rtol=1e-5, atol=1e-6, outliers=1e-4)
+    for form in ("eager", "graph"):
+        for n, v in outs[0][form][0].items():
+            assert torch.equal(v, outs[1][form][0][n]), (form, n)  # the ranks stay identical
