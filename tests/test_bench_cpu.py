@@ -67,3 +67,21 @@ def test_closing_line_is_consistent():
         assert abs(m["step"]["frac"] - m["bytes"] / (d["ms_per_step"] * 1e-3) / 1e9 / bench.HBM_PEAK_GBS) < 1e-3
     cpu = d["cpu_baseline"]
     assert cpu["kind"] in ("port", "reference") and cpu["cores"] >= 1 and cpu["value"] > 0
+
+
+def test_compulsory_model_and_refused_fractions():
+    """the compulsory-bytes model counts a render kernel's record once per visible
+    Gaussian and 4 B per instance, never more than the literal §8d bytes once instances outnumber the
+    visible Gaussians; a fraction above 1 is refused, naming the model."""
+    P, V, R, HW, M = 3_000_000, 2_900_000, 40_000_000, 1920 * 1080, 16
+    for stage in ("render forward", "render backward"):
+        lit = bench.algorithmic_bytes(stage, P, V, R, HW, M, color_grad=False, geometry=False, fused_loss=True)
+        comp = bench.compulsory_bytes(stage, P, V, R, HW, M, color_grad=False, geometry=False, fused_loss=True)
+        assert lit - comp == R * 48 - V * 48
+    assert bench.compulsory_bytes("preprocess", P, V, R, HW, M) == bench.algorithmic_bytes("preprocess", P, V, R, HW, M)
+    assert bench.compulsory_step_bytes(P, V, R, HW, M, False) == \
+        bench.survey_step_bytes(P, R, HW, M, False) - 136 * R + 96 * V
+    ok = bench.hbm_view(4e9, 1e-3, "m")  # 4 TB/s
+    assert ok["frac"] == 0.5 and "frac_refused" not in ok
+    bad = bench.hbm_view(9e9, 1e-3, "literal model")
+    assert bad["frac"] is None and bad["frac_refused"].startswith("literal model: 1.125")
