@@ -547,7 +547,10 @@ def main():
     elapsed_pg = elapsed_sync = float("inf")
     pg_rot = None
     pg_reps = []
-    if graphed and os.environ.get("LSR_PIPELINE", "1") != "0":
+
+    def run_pipelined_graph():
+        """The pipelined graph form's timed steps, reps and with-sync steps."""
+        reps = []
         # N > 1: the bucket's all-reduce (RCCL) is launched between each set's backward and Adam graphs
         # rotation (N = 1): R steps per stream-A graph (pipeline.py), R dividing the timed steps
         rot = 1
@@ -557,7 +560,6 @@ def main():
         pg = PipelinedGraphStep(lambda: render(cam, model, Pipe, bg, Opt, language_target=(gt, mask))["language_l1"],
                                 model.trainable(), optim, bucket=bucket, rotation=rot, model=model)
         pg.capture()
-        pg_rot = rot
         # untimed replays until the two streams' steady state: the first replays after a capture run
         # slower (profiles/r05_bench_first.json: timed steps 0.4115 ms after 20 warm replays, its reps
         # 0.399), and a timed pass that starts before the streams have settled can stay at the slow
@@ -597,7 +599,7 @@ def main():
                 pg.replay()
             pg.synchronize()
             torch.cuda.synchronize()
-            pg_reps.append(1000.0 * (time.perf_counter() - tr) / args.steps)
+            reps.append(1000.0 * (time.perf_counter() - tr) / args.steps)
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
@@ -609,6 +611,23 @@ def main():
         if not pg.check():
             raise RuntimeError("a pipelined view exceeded its capacities during the timed steps")
         del pg
+        return elapsed_pg, elapsed_sync, rot, reps
+
+    pg_error = None
+    if graphed and os.environ.get("LSR_PIPELINE", "1") != "0":
+        if world == 1:
+            elapsed_pg, elapsed_sync, pg_rot, pg_reps = run_pipelined_graph()
+        else:
+            # N > 1 with RCCL the collective is captured inside the step graphs, a path a one-GPU box
+            # cannot run with two ranks (RCCL refuses two ranks on one GPU, profiles/r06_rccl_two_ranks_one_gpu.txt):
+            # a failure there (every rank fails alike: the same capture) leaves the eager forms as `value`
+            try:
+                elapsed_pg, elapsed_sync, pg_rot, pg_reps = run_pipelined_graph()
+            except RuntimeError as e:
+                pg_error = f"{type(e).__name__}: {e}"[:400]
+                print(f"rank {rank}: pipelined graph form failed: {pg_error}", file=sys.stderr, flush=True)
+                torch.cuda.synchronize()
+                dist.barrier()
     gc.enable()
     # the RGB stage's step on the same scene and view (all six groups trainable, L1 + SSIM, densification
     # statistics): reported beside, never as `value`
@@ -747,6 +766,7 @@ def main():
                                          "Adam on one, the next view's geometry (forward split in two calls) on "
                                          "the other"}[best],
         "pipelined_graph_rotation": pg_rot,
+        "pipelined_graph_error": pg_error,
         "ms_per_step_forms": {n: (round(1000.0 * v / args.steps, 4) if v < 1e29 else None) for n, v in times.items()},
         "ms_per_step_all_gradients": round(1000.0 * elapsed_all / args.steps, 4),
         "ms_forward_only": round(1000.0 * elapsed_fwd / args.steps, 4),
