@@ -491,6 +491,9 @@ __device__ float render_empty_tiles(const RenderParams& p, int j, int M)
 #ifndef LSR_FWD_PREFETCH  // 1: the next batch's records are gathered during the walk
 #define LSR_FWD_PREFETCH 0
 #endif
+#ifndef LSR_FWD_STATE_SKIP  // 1: split-replay states stored only for the pixels the backward starts from them
+#define LSR_FWD_STATE_SKIP 1
+#endif
 template <bool kStats, bool kFeat, bool kLoss>
 __global__ __launch_bounds__(kTilePixels, LSR_FWD_WAVES) void k_render_forward(RenderParams p)
 {
@@ -599,9 +602,13 @@ __global__ __launch_bounds__(kTilePixels, LSR_FWD_WAVES) void k_render_forward(R
             // of contended cross-XCD atomics); a pixel already done is never started from here
             // {T, feature sums}, then {colour sums} unless no colour gradient can follow (the language
             // step: half the state traffic)
+            // A pixel already done (or outside the image: T < 0) has its last contributor before the
+            // boundary, so the backward never starts it from here: no store (LSR_FWD_STATE_SKIP=0 stores)
             float4* st = reinterpret_cast<float4*>(p.split_pool) + ((size_t)tile * kSplitSlots + nrec) * (2 * kThreads);
-            st[2 * t] = make_float4(q.T, q.C2F0.y, q.F12.x, q.F12.y);
-            if (p.split_color) st[2 * t + 1] = make_float4(q.C01.x, q.C01.y, q.C2F0.x, 0.0f);
+            if (!LSR_FWD_STATE_SKIP || q.T > 0.0f) {
+                st[2 * t] = make_float4(q.T, q.C2F0.y, q.F12.x, q.F12.y);
+                if (p.split_color) st[2 * t + 1] = make_float4(q.C01.x, q.C01.y, q.C2F0.x, 0.0f);
+            }
             nrec++;
         }
         if (idx < end) {
@@ -745,7 +752,8 @@ __global__ __launch_bounds__(kTilePixels, LSR_FWD_WAVES) void k_render_forward(R
     // the final sums, for the backward's running `acc` at each boundary, (C_final - C_front) / T_b: a
     // store here (the tile's extra slot), the arithmetic in the backward -- normalising the slots in
     // place needed a load round trip at the end of every long tile, i.e. on the kernel's critical path
-    if (nsplit > 0) {
+    // (read only for pixels that composite past the first boundary, 256: q.last > hi >= 256)
+    if (nsplit > 0 && (!LSR_FWD_STATE_SKIP || qlast > (uint32_t)kThreads)) {
         float4* fin = reinterpret_cast<float4*>(p.split_pool) + ((size_t)tile * kSplitSlots + kSplitMax) * (2 * kThreads);
         fin[2 * t] = make_float4(q.C2F0.y, q.F12.x, q.F12.y, 0.0f);
         if (p.split_color) fin[2 * t + 1] = make_float4(q.C01.x, q.C01.y, q.C2F0.x, 0.0f);
