@@ -1,6 +1,9 @@
 """Where a synced step's extra time goes (measurement aid):
 
-    python3 tools/sync_gap.py [--steps 200] [--loss-wait]
+    python3 tools/sync_gap.py [--steps 200] [--spin]
+
+(--spin: hipSetDeviceFlags(hipDeviceScheduleSpin) before the HIP runtime starts, i.e. the waiting
+host thread spins instead of yielding)
 
 train.py:108 reads loss.item() after every iteration.  With the pipelined graph (bench.py's
 `pipelined_graph` form) that is `pg.replay().item()`: the host waits for the step, then enqueues
@@ -39,6 +42,10 @@ class _Timed:
 
 
 def main():
+    if "--spin" in sys.argv:  # before anything initialises the HIP runtime
+        import ctypes
+        hip = ctypes.CDLL("libamdhip64.so")
+        print("sync_gap: hipSetDeviceFlags(spin) ->", hip.hipSetDeviceFlags(1), flush=True)
     import torch
     import bench
     from langsplat_amd.pipeline import PipelinedGraphStep
