@@ -35,11 +35,19 @@ constexpr int kCntBwdClass = kCntSlots + kWorkClasses;
 constexpr int kCntWords = kCntSlots + 2 * kWorkClasses;
 
 // Split replay (lsr_render.hip): the render forward records each pixel's state (T and the colour /
-// feature sums) before list entries 256, 512, 768 of a tile it is still compositing (in the tile's
-// own kSplitMax slots), so the backward
-// can replay a long tile as up to kSplitItems independent work items of <= 256 entries each
-// (the last one: the rest) instead of one long serial chain.
-constexpr int kSplitMax = 3;                // recorded boundaries per tile
+// feature sums) before list entries kSplitChunk, 2 kSplitChunk, ... (up to entry 1024 - kSplitChunk)
+// of a tile it is still compositing (in the tile's own kSplitMax slots), so the backward can replay
+// a long tile as up to kSplitItems independent work items of <= kSplitChunk entries each (the last
+// one: the rest) instead of one long serial chain.  LSR_SPLIT_CHUNK=128 (round 6, measured and not
+// the default: each wave records the boundary inside a 256-entry batch mid-walk) halved the items
+// but cost more than it saved -- C3 render backward 141 -> 152 us, forward 125 -> 132 us, pipelined
+// step 0.400 -> 0.465 ms (profiles/r06_split128_ab.txt).
+#ifndef LSR_SPLIT_CHUNK
+#define LSR_SPLIT_CHUNK 256
+#endif
+constexpr int kSplitChunk = LSR_SPLIT_CHUNK;
+static_assert(kSplitChunk == 128 || kSplitChunk == 256, "split chunks of 128 or 256 list entries");
+constexpr int kSplitMax = 1024 / kSplitChunk - 1;  // recorded boundaries per tile
 constexpr int kSplitItems = kSplitMax + 1;  // backward work items per tile
 constexpr int kSplitVals = 8;               // per pixel {T, feature (3)}, {colour (3), -}
 constexpr int kSplitSlots = kSplitMax + 1;  // per tile: the boundaries' states, then the final sums

@@ -108,16 +108,22 @@ __device__ __forceinline__ uint32_t entry_cover(float x, float y, float a, float
 
 // Compacts the batch slots [0, cnt) whose cover mask meets `bits` (the wave's blocks) into
 // list[0, n) as LDS byte offsets 16 e of their 16-B records; returns n.
-__device__ __forceinline__ int wave_compact(const uint8_t* sM, int cnt, uint32_t bits, int lane, uint16_t* list)
+// n_mid: how many of them lie in slots [0, kSplitChunk) (the walk's split-replay boundary inside the
+// batch when kSplitChunk < 256).
+__device__ __forceinline__ int wave_compact(const uint8_t* sM, int cnt, uint32_t bits, int lane, uint16_t* list,
+                                            int& n_mid)
 {
     int n = 0;
+    n_mid = 0;
     for (int r = 0; r < cnt; r += 64) {
         const int e = r + lane;
         const bool ov = e < cnt && (sM[e] & bits) != 0u;
         const uint64_t m = __ballot(ov);
         if (ov) list[n + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)(16 * e);
         n += __popcll(m);
+        if (r + 64 == kSplitChunk) n_mid = n;
     }
+    if (cnt <= kSplitChunk) n_mid = n;
     return n;
 }
 
@@ -488,6 +494,9 @@ __device__ float render_empty_tiles(const RenderParams& p, int j, int M)
 #ifndef LSR_FWD_QUAD  // 1: four list entries per walk step (two packed exp chains), 0: two
 #define LSR_FWD_QUAD 0
 #endif
+#if LSR_FWD_QUAD && LSR_SPLIT_CHUNK != 256
+#error "the four-entry walk records split-replay states at batch starts only: LSR_SPLIT_CHUNK=256"
+#endif
 #ifndef LSR_FWD_PREFETCH  // 1: the next batch's records are gathered during the walk
 #define LSR_FWD_PREFETCH 0
 #endif
@@ -550,7 +559,7 @@ __global__ __launch_bounds__(kTilePixels, LSR_FWD_WAVES) void k_render_forward(R
     const uint32_t start = range.x, end = range.y;
     const bool inside = px < p.W && py < p.H;
     if (t == 0) s_last = 0;
-    uint32_t nrec = 0;  // split replay: boundaries recorded (256, 512, ... up to kSplitMax; uniform)
+    uint32_t nrec = 0;  // split replay: boundaries recorded (kSplitChunk, 2 kSplitChunk, ... up to kSplitMax; uniform)
 
     FwdPixel q{inside ? 1.0f : -1.0f, make_f2(0.f, 0.f), make_f2(0.f, 0.f), make_f2(0.f, 0.f), 0u, 0u};
     // Software pipeline over the batches: a batch's records are gathered during the previous batch's
@@ -596,19 +605,24 @@ __global__ __launch_bounds__(kTilePixels, LSR_FWD_WAVES) void k_render_forward(R
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             ph.st[4] = wall_clock64();
         }
-        if (p.split_pool && base != start && base - start <= (uint32_t)(kSplitMax * kThreads)) {
+        // split-replay state of each pixel at list entry e (e = base - start here, or the middle of the
+        // batch, below): slot e / kSplitChunk - 1, two float4 per pixel
+        auto record_state = [&](uint32_t slot) {
+            float4* st = reinterpret_cast<float4*>(p.split_pool) + ((size_t)tile * kSplitSlots + slot) * (2 * kThreads);
+            // A pixel already done (or outside the image: T < 0) has its last contributor before the
+            // boundary, so the backward never starts it from here: no store (LSR_FWD_STATE_SKIP=0 stores)
+            if (!LSR_FWD_STATE_SKIP || q.T > 0.0f) {
+                st[2 * t] = make_float4(q.T, q.C2F0.y, q.F12.x, q.F12.y);
+                if (p.split_color) st[2 * t + 1] = make_float4(q.C01.x, q.C01.y, q.C2F0.x, 0.0f);
+            }
+        };
+        if (p.split_pool && base != start && base - start <= (uint32_t)(kSplitMax * kSplitChunk)) {
             // split replay: every pixel's state before list entry 256 j while some pixel composites,
             // two float4 per pixel in the tile's own slot j - 1 (a grid-wide slot counter cost ~40 us
             // of contended cross-XCD atomics); a pixel already done is never started from here
             // {T, feature sums}, then {colour sums} unless no colour gradient can follow (the language
             // step: half the state traffic)
-            // A pixel already done (or outside the image: T < 0) has its last contributor before the
-            // boundary, so the backward never starts it from here: no store (LSR_FWD_STATE_SKIP=0 stores)
-            float4* st = reinterpret_cast<float4*>(p.split_pool) + ((size_t)tile * kSplitSlots + nrec) * (2 * kThreads);
-            if (!LSR_FWD_STATE_SKIP || q.T > 0.0f) {
-                st[2 * t] = make_float4(q.T, q.C2F0.y, q.F12.x, q.F12.y);
-                if (p.split_color) st[2 * t + 1] = make_float4(q.C01.x, q.C01.y, q.C2F0.x, 0.0f);
-            }
+            record_state(nrec);
             nrec++;
         }
         if (idx < end) {
@@ -630,8 +644,14 @@ __global__ __launch_bounds__(kTilePixels, LSR_FWD_WAVES) void k_render_forward(R
             }
         }
         const int cnt = (int)min((uint32_t)kThreads, end - base);
+        int n_mid_raw;
         const int n = __builtin_amdgcn_readfirstlane(
-            wave_compact(sM, cnt, 1u << wave, lane, sL[wave]));
+            wave_compact(sM, cnt, 1u << wave, lane, sL[wave], n_mid_raw));
+        const int n_mid = __builtin_amdgcn_readfirstlane(n_mid_raw);
+        // the boundary in the middle of the batch (kSplitChunk < 256), recorded by each wave when its
+        // walk reaches it: uniform over the workgroup
+        const bool mid = kSplitChunk < kThreads && p.split_pool && cnt > kSplitChunk &&
+                         base - start + kSplitChunk <= (uint32_t)(kSplitMax * kSplitChunk);
         if (lane < 4) sL[wave][n + lane] = 0;
         __syncthreads();  // list visible to the wave's other lanes
         if (kStats) ph.lap(ph.compact);
@@ -706,18 +726,39 @@ __global__ __launch_bounds__(kTilePixels, LSR_FWD_WAVES) void k_render_forward(R
         } while (i < n && __ballot(q.T > 0.0f) != 0ull);
 #else
         const uint32_t* const sL2 = reinterpret_cast<const uint32_t*>(sL[wave]);
-        uint32_t oo = sL2[0];
-        if (n > 0 && __ballot(q.T > 0.0f) != 0ull) do {
-            const uint32_t o0 = oo & 0xFFFFu, o1 = oo >> 16;
-            oo = sL2[(i >> 1) + 1];  // slots i + 2, i + 3 (<= n + 1)
-            float al0, al1;
-            bool ok0, ok1;
-            pair_alpha(o0, o1, i + 1 < n, al0, al1, ok0, ok1);
-            blend_at(al0, ok0, o0);
-            blend_at(al1, ok1, o1);
-            asm volatile("" : "+v"(oo));
-            i += 2;
-        } while (i < n && __ballot(q.T > 0.0f) != 0ull);
+        // the pairs of list slots [i, lim), i even (a last odd slot alone)
+        auto walk = [&](int lim) {
+            uint32_t oo = sL2[i >> 1];
+            if (i < lim && __ballot(q.T > 0.0f) != 0ull) do {
+                const uint32_t o0 = oo & 0xFFFFu, o1 = oo >> 16;
+                oo = sL2[(i >> 1) + 1];  // slots i + 2, i + 3 (<= n + 1)
+                float al0, al1;
+                bool ok0, ok1;
+                pair_alpha(o0, o1, i + 1 < lim, al0, al1, ok0, ok1);
+                blend_at(al0, ok0, o0);
+                blend_at(al1, ok1, o1);
+                asm volatile("" : "+v"(oo));
+                i += 2;
+            } while (i < lim && __ballot(q.T > 0.0f) != 0ull);
+        };
+        if (!mid) {
+            walk(n);
+        } else {
+            // the wave's entries before the batch's middle, its pixels' state there, the rest
+            walk(n_mid);
+            record_state(nrec);
+            i = n_mid;
+            if ((n_mid & 1) && n_mid < n && __ballot(q.T > 0.0f) != 0ull) {  // slot n_mid alone
+                const uint32_t o0 = sL[wave][n_mid];
+                float al0, al1;
+                bool ok0, ok1;
+                pair_alpha(o0, o0, false, al0, al1, ok0, ok1);
+                blend_at(al0, ok0, o0);
+            }
+            i = (n_mid + 1) & ~1;
+            walk(n);
+        }
+        if (mid) nrec++;
 #endif
         if (lo != 0xFFFFFFFFu) q.last16 = lb16 + lo;
     }
@@ -732,7 +773,7 @@ __global__ __launch_bounds__(kTilePixels, LSR_FWD_WAVES) void k_render_forward(R
     // the backward's work items: the tile's replay [0, s_last) cut at the recorded boundaries below
     // s_last (split replay), each appended to the class of its length
     const uint32_t maxl = s_last;
-    const uint32_t nsplit = p.split_pool && maxl > 0 ? min(nrec, (maxl - 1u) / (uint32_t)kThreads) : 0u;
+    const uint32_t nsplit = p.split_pool && maxl > 0 ? min(nrec, (maxl - 1u) / (uint32_t)kSplitChunk) : 0u;
     // the backward's items into the longest-first class lists: the tile's full 256-entry chunks with
     // ONE returning atomic on their class (+nsplit), its last chunk with another, in parallel (thread
     // 1): an atomic per chunk put every heavy tile's chunks on one hot counter across the XCDs
@@ -742,18 +783,18 @@ __global__ __launch_bounds__(kTilePixels, LSR_FWD_WAVES) void k_render_forward(R
         const size_t stride = (size_t)kSplitItems * T;
         if (t == 0 && p.split_pool) p.split_desc[tile] = make_uint4(nsplit, maxl, 0u, 0u);
         if (t == 0 && nsplit > 0) {
-            const int c = work_class((uint32_t)kThreads);
+            const int c = work_class((uint32_t)kSplitChunk);
             const uint32_t base = atomicAdd(&counts[c], nsplit);
             for (uint32_t k = 0; k < nsplit; k++) lists[(size_t)c * stride + base + k] = kSplitItems * tile + k;
         }
         if (t == (nsplit > 0 ? 1 : 0))
-            schedule_tile(counts, lists, (int)stride, kSplitItems * tile + (int)nsplit, maxl - nsplit * kThreads);
+            schedule_tile(counts, lists, (int)stride, kSplitItems * tile + (int)nsplit, maxl - nsplit * kSplitChunk);
     }
     // the final sums, for the backward's running `acc` at each boundary, (C_final - C_front) / T_b: a
     // store here (the tile's extra slot), the arithmetic in the backward -- normalising the slots in
     // place needed a load round trip at the end of every long tile, i.e. on the kernel's critical path
-    // (read only for pixels that composite past the first boundary, 256: q.last > hi >= 256)
-    if (nsplit > 0 && (!LSR_FWD_STATE_SKIP || qlast > (uint32_t)kThreads)) {
+    // (read only for pixels that composite past the first boundary: q.last > hi >= kSplitChunk)
+    if (nsplit > 0 && (!LSR_FWD_STATE_SKIP || qlast > (uint32_t)kSplitChunk)) {
         float4* fin = reinterpret_cast<float4*>(p.split_pool) + ((size_t)tile * kSplitSlots + kSplitMax) * (2 * kThreads);
         fin[2 * t] = make_float4(q.C2F0.y, q.F12.x, q.F12.y, 0.0f);
         if (p.split_color) fin[2 * t + 1] = make_float4(q.C01.x, q.C01.y, q.C2F0.x, 0.0f);
@@ -1372,7 +1413,7 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
     // reader in this launch
     if (p.fwd_flags && blockIdx.x == 0 && threadIdx.x == 0) *p.fwd_flags &= ~kFwdZeroedRecords;
     int tile = (int)blockIdx.x;
-    uint32_t chunk = 0;  // split replay: this workgroup replays list entries [256 chunk, ...) of the tile
+    uint32_t chunk = 0;  // split replay: this workgroup replays list entries [kSplitChunk chunk, ...) of the tile
     if (p.sched_counts) {  // tiles without contributors are not scheduled: nothing to do
         const int T = p.gx * p.gy;
         const int item = scheduled_tile((int)blockIdx.x, p.sched_counts + kCntBwdClass,
@@ -1393,14 +1434,14 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
 
     BwdPixel q;
     bwd_pixel_init<kFeat, kColor>(q, p, px < p.W && py < p.H, (size_t)py * p.W + px, HW);
-    // split replay: a chunk that ends at a recorded boundary hi = 256 (chunk + 1) starts the pixels
+    // split replay: a chunk that ends at a recorded boundary hi = kSplitChunk (chunk + 1) starts the pixels
     // that composite past hi from the forward's state there (T and the normalised sums behind it);
     // pixels whose last contributor lies inside the chunk start from T_final as usual, and pixels
     // that end before it have nothing here (every entry >= their count is skipped)
-    const uint32_t lo = chunk * (uint32_t)kThreads;
+    const uint32_t lo = chunk * (uint32_t)kSplitChunk;
     if (p.split_pool && p.sched_counts) {
         const uint4 desc = p.split_desc[tile];
-        const uint32_t hi = lo + (uint32_t)kThreads;
+        const uint32_t hi = lo + (uint32_t)kSplitChunk;
         if (chunk < desc.x && q.last > hi) {
             // the boundary's {T, feature sums}, {colour sums} and the tile's final sums (extra slot);
             // the colour halves exist unless the forward was told no colour gradient follows (a
