@@ -288,7 +288,7 @@ STAGE_KERNEL = {"render backward": "lsr::k_render_backward<false, true, false, f
 # profiles this round's bench reads its PMC figures from: profiles/<ROUND>_<config>_{summary,valu}.json
 # (tools/profile_round.sh + tools/prof_summary.py, tools/pmc_valu.sh + tools/valu_summary.py).  A
 # profile of another round or another config is never used: its field is then null.
-ROUND = "r05"
+ROUND = "r06"
 CUS = 256
 CLOCK_HZ = 2.4e9  # MI355X_MICROARCH.md: max engine clock (what the PMC runs' GRBM_GUI_ACTIVE / time gives)
 # wave64 VALU instructions a CU can issue per cycle: 4 SIMD-32 units, each one wave64 instruction per
