@@ -705,7 +705,7 @@ def main():
                         "hbm_compulsory": hbm_c}
         else:  # no VALU profile of this round and config: the compulsory HBM view is the headline
             roofline = dict(hbm_c, kernel=dom_name, avg_ms=round(dom["avg_ms"], 4), traffic=hbm["traffic"],
-                            valu_source=None, hbm=hbm)
+                            valu_source=None, hbm=hbm, hbm_compulsory=hbm_c)
         # north_star's "% of HBM roofline" (DESIGN.md §4): the whole rasterizer fwd+bwd (every profiled
         # stage except the optimizer) against SURVEY.md §8d's step model as written, and against its
         # compulsory form; each also over the benched step (the stages overlap across two streams

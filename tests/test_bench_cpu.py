@@ -85,3 +85,26 @@ def test_compulsory_model_and_refused_fractions():
     assert ok["frac"] == 0.5 and "frac_refused" not in ok
     bad = bench.hbm_view(9e9, 1e-3, "literal model")
     assert bad["frac"] is None and bad["frac_refused"].startswith("literal model: 1.125")
+
+
+def _fracs(node, path=""):
+    if isinstance(node, dict):
+        for k, v in node.items():
+            if k == "frac" or k.endswith("_frac"):
+                yield f"{path}.{k}", v
+            yield from _fracs(v, f"{path}.{k}")
+
+
+@pytest.mark.parametrize("cfg", ["", "_C5", "_C2"])
+def test_committed_lines_have_no_fraction_above_one(cfg):
+    """no roofline fraction in this round's committed bench lines exceeds 1 (a
+    model whose bytes cannot move in the measured time is refused, and names itself)."""
+    path = os.path.join(ROOT, "profiles", f"{bench.ROUND}_bench{cfg}.json")
+    if not os.path.exists(path):
+        pytest.skip("line not committed")
+    d = json.load(open(path))
+    for where, f in _fracs(d["roofline"], "roofline"):
+        assert f is None or 0.0 < f <= 1.0, (where, f)
+    refused = [v for k, v in d["roofline"].items() if isinstance(v, dict) and v.get("frac_refused")]
+    for v in refused:
+        assert v["frac"] is None and v["model"] in v["frac_refused"]
