@@ -38,7 +38,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from langsplat_amd import _native, launch  # noqa: E402
-from langsplat_amd.distributed import GradBucket, init_from_env  # noqa: E402
+from langsplat_amd.distributed import GradBucket, collective_capturable, init_from_env  # noqa: E402
 from langsplat_amd.optim import Adam as AmdAdam  # noqa: E402
 from langsplat_amd.pipeline import PipelinedGraphStep, ViewPipeline  # noqa: E402
 from langsplat_amd.render import render  # noqa: E402
@@ -762,7 +762,9 @@ def main():
                                    "beside this view's backward" + (", RCCL all-reduce" if world > 1 else "")
                                    + " and Adam)",
                       "pipelined_graph": "HIP graphs on two streams: this view's compositing + loss, backward, "
-                                         + ("RCCL all-reduce (in the graph), " if world > 1 else "") +
+                                         + ((f"{backend} all-reduce ("
+                                             + ("in the graph" if collective_capturable() else "between two graphs")
+                                             + "), ") if world > 1 else "") +
                                          "Adam on one, the next view's geometry (forward split in two calls) on "
                                          "the other"}[best],
         "pipelined_graph_rotation": pg_rot,

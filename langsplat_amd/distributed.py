@@ -30,12 +30,19 @@ def init_from_env(backend: str = None):
 
 
 def collective_capturable(group=None) -> bool:
-    """True when the gradient collective can be captured into a HIP graph with the step: backend
-    "nccl" (RCCL's kernels run on a stream; torch's ProcessGroupNCCL supports stream capture).  gloo
-    reduces on the host and stays an eager call between two graphs.  LSR_GRAPH_COLLECTIVE=0 keeps
-    the RCCL collective eager too."""
-    return (dist.is_available() and dist.is_initialized() and dist.get_backend(group) == "nccl"
-            and os.environ.get("LSR_GRAPH_COLLECTIVE", "1") != "0")
+    """True when the gradient collective is captured into a HIP graph with the step: backend "nccl"
+    (RCCL's kernels run on a stream; torch's ProcessGroupNCCL supports stream capture) and
+    LSR_GRAPH_COLLECTIVE=1.  gloo reduces on the host and stays an eager call between two graphs.
+
+    The default follows what has run on hardware: with one rank the captured RCCL
+    collective is tested (tests/test_gpu_rccl.py) and on; with several ranks it has never run -- a
+    one-GPU box cannot host two RCCL ranks (profiles/r06_rccl_two_ranks_one_gpu.txt) -- so there the
+    RCCL all-reduce stays an eager launch between the backward and Adam graphs, the form the
+    multi-rank gloo runs exercise, unless LSR_GRAPH_COLLECTIVE=1 asks for the captured one."""
+    if not (dist.is_available() and dist.is_initialized() and dist.get_backend(group) == "nccl"):
+        return False
+    default = "1" if dist.get_world_size(group) == 1 else "0"
+    return os.environ.get("LSR_GRAPH_COLLECTIVE", default) == "1"
 
 
 class GradBucket:
