@@ -413,7 +413,9 @@ def main():
         optim = torch.optim.Adam(groups, lr=0.0, eps=1e-15, fused=True)
     # N > 1: .grad tensors are views of one flat bucket (one all-reduce); N = 1: train.py:138's
     # zero_grad(set_to_none=True), so autograd hands the rasterizer's gradient over without a copy
-    bucket = GradBucket(model.trainable()) if world > 1 else None
+    # (LSR_BENCH_BUCKET=1 at N = 1: the N > 1 step structure without its collective -- the all-reduce
+    # is a no-op on one process -- a measurement aid for the cost of the N > 1 form itself)
+    bucket = GradBucket(model.trainable()) if world > 1 or os.environ.get("LSR_BENCH_BUCKET") == "1" else None
 
     def step():
         if fused:  # the loss inside the compositing kernel, its backward in the replay
