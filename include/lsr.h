@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define LSR_ABI_VERSION 14
+#define LSR_ABI_VERSION 15
 
 enum lsr_status {
     LSR_OK = 0,
@@ -444,6 +444,18 @@ typedef struct lsr_adam_tensor {
 } lsr_adam_tensor;
 int32_t lsr_adam_multi(int32_t count, const lsr_adam_tensor* tensors, float grad_scale, int64_t* step_dev,
                        const int32_t* skip, void* stream);
+
+/* The language step's update at N > 1 (ABI 15): lsr_adam_multi of ONE tensor -- the raw language
+ * feature, P x 3 (tensor->n = 3 P), its gradient the all-reduced one (times grad_scale) -- in the
+ * device form (step_dev and its learning-rate word 0 as lsr_adam_multi's; skip as there), which
+ * also writes the updated feature (activated when raw has LSR_RAW_LANGUAGE) into the language
+ * slots of fill_record, another forward's render records (lsr_state_layout.record; the same slots
+ * lsr_backward_args.fill_record receives at N = 1), so that forward's composite phase runs as
+ * LSR_PHASE_COMPOSITE_FILLED.  A skipped step still fills (with the unchanged feature).  Replaces
+ * lsr_adam_multi + the fill of LSR_PHASE_COMPOSITE when the gradient all-reduce sits between the
+ * backward and the update (langsplat_amd.pipeline.PipelinedGraphStep with a bucket). */
+int32_t lsr_adam_fill_language(const lsr_adam_tensor* tensor, float grad_scale, int64_t* step_dev, const int32_t* skip,
+                               void* fill_record, int32_t raw, void* stream);
 
 /* Densification statistics of one rendered view, one pass (train.py:125-126 with
  * GaussianModel.add_densification_stats, scene/gaussian_model.py:480-482), for Gaussians with

@@ -22,7 +22,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LSR_LIB") or os.path.join(_HERE, "liblsr.so")
 
 LSR_BUF_GEOM, LSR_BUF_BINNING, LSR_BUF_IMAGE, LSR_BUF_BACKWARD = 0, 1, 2, 3
-ABI_VERSION = 14
+ABI_VERSION = 15
 ADAM_STEP_WORDS = 66  # include/lsr.h LSR_ADAM_STEP_WORDS
 ADAM_WORD_SKIPPED, ADAM_WORD_LR = 49, 50  # LSR_ADAM_WORD_SKIPPED / LSR_ADAM_WORD_LR
 # lsr_raw_flags (include/lsr.h): inputs are GaussianModel's raw parameters
@@ -111,6 +111,8 @@ SIGNATURES = {
                                        ctypes.c_double, ctypes.c_double, ctypes.c_int64, _vp]),
     "lsr_adam_multi": (ctypes.c_int32, [ctypes.c_int32, ctypes.POINTER(LsrAdamTensor), ctypes.c_float, _vp, _vp,
                                         _vp]),
+    "lsr_adam_fill_language": (ctypes.c_int32, [ctypes.POINTER(LsrAdamTensor), ctypes.c_float, _vp, _vp, _vp,
+                                                ctypes.c_int32, _vp]),
     "lsr_densification_stats": (ctypes.c_int32, [ctypes.c_int32, _vp, _vp, _vp, _vp, _vp, _vp]),
     "lsr_dist_cuda2": (ctypes.c_int32, [ctypes.c_int64, _vp, _vp, ALLOC_FN, _vp, _vp]),
     "lsr_masked_l1_scratch_bytes": (ctypes.c_size_t, [ctypes.c_int32, ctypes.c_int64]),

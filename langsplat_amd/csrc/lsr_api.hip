@@ -984,6 +984,24 @@ int32_t lsr_adam_multi(int32_t count, const lsr_adam_tensor* tensors, float grad
     return LSR_OK;
 }
 
+int32_t lsr_adam_fill_language(const lsr_adam_tensor* t, float grad_scale, int64_t* step_dev, const int32_t* skip,
+                               void* fill_record, int32_t raw, void* stream_ptr)
+{
+    if (!t || !step_dev || !fill_record || t->n < 0 || t->n % 3 != 0 || t->n / 3 > INT32_MAX ||
+        (t->n > 0 && (!t->param || !t->grad || !t->exp_avg || !t->exp_avg_sq)) ||
+        t->step < -((int64_t)1 << 40) || t->step > ((int64_t)1 << 40))
+        return fail(LSR_ERR_INVALID, "lsr_adam_fill_language: invalid argument");
+    if (reinterpret_cast<uintptr_t>(fill_record) & 15)
+        return fail(LSR_ERR_INVALID, "lsr_adam_fill_language: fill_record must be 16-byte aligned");
+    hipStream_t stream = reinterpret_cast<hipStream_t>(stream_ptr);
+    const bool debug = false;
+    const AdamHyper h{t->lr, t->beta1, t->beta2, t->eps, t->step};
+    LSR_TRY(launch_adam_fill((int)(t->n / 3), t->grad, grad_scale, t->param, t->exp_avg, t->exp_avg_sq, h, step_dev,
+                             skip, reinterpret_cast<float4*>(fill_record), raw, stream),
+            "adam fill");
+    return LSR_OK;
+}
+
 int32_t lsr_densification_stats(int32_t P, const int32_t* radii, const float* dL_dmeans2D, float* max_radii2D,
                                 float* xyz_gradient_accum, float* denom, void* stream_ptr)
 {

@@ -418,6 +418,9 @@ hipError_t launch_adam_multi(AdamTable& tab, float grad_scale, hipStream_t s);
 hipError_t launch_language_tail(int P, const int32_t* radii, const float* grad, float* lang, float* exp_avg,
                                 float* exp_avg_sq, float* dmeans2D, float* dlang, const AdamHyper& h, int64_t* step_dev,
                                 const int32_t* skip, float4* fill, hipStream_t s);
+hipError_t launch_adam_fill(int P, const float* grad, float grad_scale, float* lang, float* exp_avg, float* exp_avg_sq,
+                            const AdamHyper& h, int64_t* step_dev, const int32_t* skip, float4* fill, int raw,
+                            hipStream_t s);
 // zero `bytes` bytes at p with a kernel (no memset node in a captured graph)
 hipError_t zero_fill(void* p, size_t bytes, hipStream_t s);
 hipError_t launch_densification_stats(int P, const int* radii, const float* dmeans2D, float* max_radii, float* accum,

@@ -216,6 +216,57 @@ hipError_t launch_language_tail(int P, const int32_t* radii, const float* grad, 
     return hipGetLastError();
 }
 
+// The language step's update at N > 1 (lsr_adam_fill_language): after the gradient all-reduce, the
+// Adam step of the raw feature from its averaged gradient (one tensor; the scalars k_adam_advance
+// formed) and -- as k_language_tail does at N = 1 -- the activated updated feature into the language
+// slots of another forward's records, so that forward's composite phase needs no fill kernel
+// (LSR_PHASE_COMPOSITE_FILLED).  One Gaussian per thread, its three values as three dwords of
+// consecutive lanes; a skipped step leaves feature and moments alone and still fills.
+__global__ __launch_bounds__(256) void k_adam_fill(int P, const float* __restrict__ grad, float grad_scale,
+                                                   float* __restrict__ lang, float* __restrict__ m,
+                                                   float* __restrict__ v, const int64_t* __restrict__ step_dev,
+                                                   const int32_t* __restrict__ skip, float4* __restrict__ fill, int raw)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    const size_t i3 = 3 * (size_t)i;
+    float g[3] = {grad[i3], grad[i3 + 1], grad[i3 + 2]};
+    float l[3] = {lang[i3], lang[i3 + 1], lang[i3 + 2]};
+    float mm[3] = {m[i3], m[i3 + 1], m[i3 + 2]};
+    float vv[3] = {v[i3], v[i3 + 1], v[i3 + 2]};
+    if (!(skip && *skip)) {
+        const AdamScalars a = *reinterpret_cast<const AdamScalars*>(step_dev + 1);  // tensor 0
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            adam_one(l[k], grad_scale != 1.0f ? g[k] * grad_scale : g[k], mm[k], vv[k], a);
+            lang[i3 + k] = l[k];
+            m[i3 + k] = mm[k];
+            v[i3 + k] = vv[k];
+        }
+    }
+    float3 f = make_float3(l[0], l[1], l[2]);
+    if (raw & LSR_RAW_LANGUAGE) f = act_lang(l[0], l[1], l[2]);
+    float* slot = reinterpret_cast<float*>(fill + 3 * (size_t)i + 2);  // {b, f0, f1, f2}, b untouched
+    slot[1] = f.x;
+    *reinterpret_cast<float2*>(slot + 2) = make_float2(f.y, f.z);
+}
+
+hipError_t launch_adam_fill(int P, const float* grad, float grad_scale, float* lang, float* exp_avg, float* exp_avg_sq,
+                            const AdamHyper& h, int64_t* step_dev, const int32_t* skip, float4* fill, int raw,
+                            hipStream_t s)
+{
+    AdamTable tab{};
+    tab.count = 1;
+    tab.hyper[0] = h;
+    tab.step_dev = step_dev;
+    tab.skip = skip;
+    hipLaunchKernelGGL(k_adam_advance, dim3(1), dim3(64), 0, s, step_dev, tab);
+    if (P == 0) return hipGetLastError();
+    hipLaunchKernelGGL(k_adam_fill, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, P, grad, grad_scale, lang,
+                       exp_avg, exp_avg_sq, (const int64_t*)step_dev, skip, fill, raw);
+    return hipGetLastError();
+}
+
 // Zero fill by a kernel instead of hipMemsetAsync: inside a stream capture the runtime turns a
 // memset into a graph memset node, and instantiating a graph that held a ~220 MB one (the full
 // backward's gradient records at 3.4M Gaussians) crashed the host runtime (tests/test_gpu_densify.py,

@@ -118,11 +118,15 @@ class Adam(torch.optim.Optimizer):
         self._lr_order, self._lr_dev = [group_index], None
 
     @torch.no_grad()
-    def step(self, closure=None, grad_scale: float = 1.0, skip: torch.Tensor = None):
+    def step(self, closure=None, grad_scale: float = 1.0, skip: torch.Tensor = None, fill=None):
         """One Adam step of every parameter with a gradient; grad_scale multiplies the gradients
         first (1 / N after a SUM all-reduce of N views' gradients; 1.0: as torch.optim.Adam).
         skip (inside a graph capture only): a device int32 flag; a replay that finds it set changes
-        nothing (a view the rasterizer did not render, include/lsr.h lsr_adam_multi)."""
+        nothing (a view the rasterizer did not render, include/lsr.h lsr_adam_multi).
+        fill (inside a graph capture only): (record address, raw flags) -- the optimizer's one
+        parameter is the language feature, and its updated value also goes into the language slots
+        of that forward's render records (include/lsr.h lsr_adam_fill_language: the N > 1 language
+        step, whose next composite then needs no fill)."""
         loss = None
         if closure is not None:
             with torch.enable_grad():
@@ -170,6 +174,17 @@ class Adam(torch.optim.Optimizer):
         if entries and fused is not None:
             raise RuntimeError("langsplat_amd.optim.Adam: a fused update steps the optimizer's only trainable "
                                "parameter (the language feature of the language step)")
+        if fill is not None:
+            if not capturing or len(entries) != 1 or entries[0].n % 3 != 0:
+                raise RuntimeError("langsplat_amd.optim.Adam: step(fill=) is for a captured step of one "
+                                   "P x 3 parameter (the language feature)")
+            self._lr_order, self._lr_dev = order, None
+            with _native._on_device(device):
+                _native._check(_native.load().lsr_adam_fill_language(
+                    ctypes.byref(entries[0]), float(grad_scale), ctypes.c_void_p(self._step_dev.data_ptr()),
+                    None if skip is None else ctypes.c_void_p(skip.data_ptr()), ctypes.c_void_p(int(fill[0])),
+                    int(fill[1]), _native._stream(device)), "lsr_adam_fill_language")
+            return loss
         if entries:
             table = (_native.LsrAdamTensor * len(entries))(*entries)
             sd = sk = None

@@ -204,6 +204,7 @@ class PipelinedGraphStep:
         self.captures = 0
         self.rendered = self.entries = 0
         self._skipped_base = 0
+        self.fused = self.fill_after = False  # the update's record fill (set by capture)
         self._loaded = [None] * S  # the view each set's slot holds (slots only)
         self._assigned = [None] * S  # rotation mode: the view each set's next geometry renders
 
@@ -292,7 +293,13 @@ class PipelinedGraphStep:
         # writes those slots, so it may run before, during or after)
         fused = self.bucket is None and len(self.params) == 1 and _fused_tail_enabled()
         self.fused = fused
-        comp_phase = _native.forward_phase.COMPOSITE_FILLED if fused else _native.forward_phase.COMPOSITE
+        # N > 1 language step: the update after the all-reduce writes the feature into the next set's
+        # records (lsr_adam_fill_language), so every composite but the first after a capture (refilled
+        # from the parameter by replay(), _refill) needs no fill either
+        fill_after = self.bucket is not None and len(self.params) == 1 and _fused_tail_enabled()
+        self.fill_after = fill_after
+        comp_phase = (_native.forward_phase.COMPOSITE_FILLED if fused or fill_after
+                      else _native.forward_phase.COMPOSITE)
         # fused: the first composite after a capture fills set 0's feature records itself (G_comp0, run
         # by replay k = 0 instead of G_comp[0]; it owns its own gradients, grads0); later sets are
         # filled by the step before
@@ -308,13 +315,16 @@ class PipelinedGraphStep:
             return _native.fused_update(self.optimizer, self.params[0], skip=self.overflow[p],
                                         fill=self._record_ptr((p + 1) % S)) if fused else _nullctx()
 
+        def adam_fill(p):  # (N > 1) the set's update fills the next set's records
+            return (self._record_ptr((p + 1) % S), _native.RAW_LANGUAGE) if fill_after else None
+
         def step_body(p, loss):
             with update_ctx(p):  # the backward runs on its forward's stream (sa)
                 loss.backward(self._one)  # dL/dloss = 1 from a static tensor: no seed-fill kernel
                 if coll_in_graph:
                     self.bucket.all_reduce(average=True, flag=self.overflow[p])
                 if self.bucket is None or coll_in_graph:
-                    self.optimizer.step(skip=self.overflow[p])
+                    self.optimizer.step(skip=self.overflow[p], fill=adam_fill(p))
 
         for p in range(S):
             if self.R > 1:
@@ -357,7 +367,7 @@ class PipelinedGraphStep:
             if self.bucket is not None and not coll_in_graph:  # the all-reduce sits between two graphs
                 g = torch.cuda.CUDAGraph()
                 with graph_capture(g, stream=sa):
-                    self.optimizer.step(skip=self.overflow[p])
+                    self.optimizer.step(skip=self.overflow[p], fill=adam_fill(p))
                 self.g_adam[p] = g
             self.static_loss[p] = loss.detach()  # the set's static loss tensor
             del loss
@@ -372,7 +382,7 @@ class PipelinedGraphStep:
         self.ev_cur = [torch.cuda.Event() for _ in range(S)]
         self._since_capture = 0
         self._fast = False
-        self._refill = False
+        self._refill = fill_after  # the first composite's records: from the parameter (replay)
         self.captures += 1
         return self
 
@@ -561,8 +571,10 @@ class PipelinedGraphStep:
         with torch.cuda.stream(sa):
             self.optimizer.sync_lr()  # a changed learning rate: a host-to-device copy on stream A
             first = self.k == 0 and self.g_comp0 is not None
-            if self._refill and self.fused and not first:
-                self._refill_records(p)  # the caller changed the parameter (follow_caller)
+            if self._refill and (self.fused or self.fill_after) and not first:
+                # the caller changed the parameter (follow_caller), or the first composite after an
+                # N > 1 capture (its records were filled by no earlier update)
+                self._refill_records(p)
             self._refill = False
             (self.g_comp0 if first else self.g_comp[p]).replay()
             if not self.merged:

@@ -25,6 +25,7 @@ import torch
 
 from langsplat_amd import _native
 from langsplat_amd.graph import GraphedStep, ViewSlot
+from langsplat_amd.distributed import GradBucket
 from langsplat_amd.optim import Adam
 from langsplat_amd.pipeline import PipelinedGraphStep
 from langsplat_amd.render import render
@@ -274,13 +275,17 @@ def test_graphed_step_over_a_view_sequence(monkeypatch):
     assert_states_close(_state(m, opt), se, "graph sequence")
 
 
-@pytest.mark.parametrize("sets,wait", [(2, True), (3, True), (3, False)])
-def test_pipelined_graph_over_a_view_sequence(sets, wait, monkeypatch):
+@pytest.mark.parametrize("sets,wait,bucket", [(2, True, False), (3, True, False), (3, False, False),
+                                              (3, True, True), (2, True, True)])
+def test_pipelined_graph_over_a_view_sequence(sets, wait, bucket, monkeypatch):
     """PipelinedGraphStep with one ViewSlot per buffer set: capture(views=the first S - 1 views),
     replay(next_view=the view S - 1 ahead); every replay composites its own view's geometry with its
     own target, and the sequence reproduces the eager loop.  wait=False (bench.py's form): no
     per-replay join with the caller's stream, the views loaded on the geometry stream; the last S
-    losses (valid after synchronize()) and the final state reproduce the eager loop."""
+    losses (valid after synchronize()) and the final state reproduce the eager loop.  bucket (round
+    6): the N > 1 structure on one process (a GradBucket, no process group: its all-reduce is a
+    no-op) -- the backward and the update as two graphs, the update filling the next set's records
+    (lsr_adam_fill_language), the first composite refilled from the parameter."""
     monkeypatch.setenv("LANGSPLAT_AMD_FUSED", "1")
     g = make_gaussians(CONFIGS["C4"]["P"], seed=0)
     views = _c4_views()
@@ -288,8 +293,10 @@ def test_pipelined_graph_over_a_view_sequence(sets, wait, monkeypatch):
     m = _frozen_model(g)
     opt = _adam(m)
     slots = [ViewSlot(*views[0]) for _ in range(sets)]
-    pg = PipelinedGraphStep(_slot_forward(m), [m._language_feature], opt, slots=slots)
+    pg = PipelinedGraphStep(_slot_forward(m), [m._language_feature], opt, slots=slots,
+                            bucket=GradBucket([m._language_feature]) if bucket else None)
     pg.capture(Rc, Ec, views=views[:sets - 1])
+    assert pg.fill_after == bucket and (pg.g_adam[0] is not None) == bucket
     L = sets - 1
     losses = []
     for k in range(len(views)):

@@ -1,7 +1,8 @@
 """Kernel timeline of the bench's language step, eager or as a captured graph (measurement aid):
 
     rocprofv3 --kernel-trace --output-format csv -d gpurun_out/st_graph -o t -- python3 tools/step_trace.py graph
-    (ST_CONFIG=C5 for another BASELINE config; modes: eager, graph, pgraph)
+    (ST_CONFIG=C5 for another BASELINE config; modes: eager, graph, pgraph; ST_BUCKET=1: pgraph with the
+    N > 1 structure)
     python3 tools/step_trace.py --summary gpurun_out/st_graph/t_kernel_trace.csv
 
 The summary prints, per step (one preprocess launch to the next), the span, the summed kernel time
@@ -47,9 +48,12 @@ def run(mode, steps=30):
         fwd_bwd()
         optim.step()
         optim.zero_grad(set_to_none=True)
+        # ST_BUCKET=1: the N > 1 structure (a GradBucket; no process group, so its all-reduce is a no-op)
+        from langsplat_amd.distributed import GradBucket
+        bucket = GradBucket([model._language_feature]) if os.environ.get("ST_BUCKET") == "1" else None
         pg = PipelinedGraphStep(lambda: bench.render(cam, model, bench.Pipe, bg, bench.Opt,
                                                      language_target=(gt, mask))["language_l1"],
-                                [model._language_feature], optim).capture()
+                                [model._language_feature], optim, bucket=bucket).capture()
 
         wait = os.environ.get("LSR_TRACE_NOWAIT", "0") != "1"
 
