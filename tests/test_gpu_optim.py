@@ -163,3 +163,53 @@ def test_densification_stats_kernel_matches_reference_ops():
     torch.testing.assert_close(accum, ref[1], rtol=1e-6, atol=0)
     torch.testing.assert_close(denom, ref[2], rtol=0, atol=0)
     assert vis.any() and (~vis).any()
+
+
+def test_adam_fill_language_matches_torch_and_fills_records():
+    """lsr_adam_fill_language (ABI 15, the N > 1 language update): a captured step(fill=) over the
+    raw P x 3 language feature equals torch.optim.Adam on the same (scaled) gradients, step after
+    step, writes normalize(feature) -- the activation of gaussian_renderer/__init__.py:87-88 -- into
+    the language slots {f0, f1, f2} of every record (3 float4 per Gaussian, slot word b untouched),
+    and with the skip flag set changes no parameter or moment but still fills."""
+    from langsplat_amd import _native
+    from langsplat_amd.graph import graph_capture
+    P = 3001
+    g = torch.Generator().manual_seed(7)
+    p0 = torch.randn((P, 3), generator=g)
+    a = p0.clone().to(DEV).requires_grad_(True)
+    b = p0.clone().to(DEV).requires_grad_(True)
+    mine = Adam([{"params": [a], "lr": 0.0025, "name": "language_feature"}], lr=0.0, eps=1e-15)
+    ref = torch.optim.Adam([{"params": [b], "lr": 0.0025, "name": "language_feature"}], lr=0.0, eps=1e-15,
+                           foreach=False)
+    records = torch.full((P, 12), 7.0, device=DEV)  # {x y cx cy}{cz o r g}{b f0 f1 f2}
+    skip = torch.zeros((), dtype=torch.int32, device=DEV)
+    grad = torch.zeros((P, 3), device=DEV)
+    a.grad = grad
+    mine.prepare_capture()
+    graph = torch.cuda.CUDAGraph()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side), graph_capture(graph):
+        mine.step(grad_scale=0.5, skip=skip, fill=(records.data_ptr(), _native.RAW_LANGUAGE))
+    torch.cuda.current_stream().wait_stream(side)
+    for it in range(4):
+        gr = torch.randn((P, 3), generator=g).to(DEV)
+        grad.copy_(gr)
+        skip.fill_(1 if it == 2 else 0)
+        before = (a.detach().clone(), mine.state[a]["exp_avg"].clone(), mine.state[a]["exp_avg_sq"].clone())
+        mine.sync_lr()
+        graph.replay()
+        torch.cuda.synchronize()
+        if it == 2:  # skipped: nothing changes, the records still receive the (unchanged) feature
+            assert torch.equal(a.detach(), before[0]) and torch.equal(mine.state[a]["exp_avg"], before[1])
+            assert torch.equal(mine.state[a]["exp_avg_sq"], before[2])
+        else:
+            b.grad = 0.5 * gr
+            ref.step()
+        torch.testing.assert_close(a.detach(), b.detach(), rtol=2e-6, atol=1e-6 * float(b.abs().max()))
+        f = a.detach()
+        want = f / (f.norm(dim=-1, keepdim=True) + 1e-9)
+        torch.testing.assert_close(records[:, 9:12], want, rtol=1e-6, atol=1e-7)
+        assert torch.all(records[:, :9] == 7.0)
+    mine.sync_steps()
+    assert float(mine.state[a]["step"]) == 3.0 and mine.skipped_steps() == 1
