@@ -206,7 +206,7 @@ def test_adam_fill_language_matches_torch_and_fills_records():
         else:
             b.grad = 0.5 * gr
             ref.step()
-        torch.testing.assert_close(a.detach(), b.detach(), rtol=2e-6, atol=1e-6 * float(b.abs().max()))
+        torch.testing.assert_close(a.detach(), b.detach(), rtol=2e-6, atol=1e-6 * float(b.detach().abs().max()))
         f = a.detach()
         want = f / (f.norm(dim=-1, keepdim=True) + 1e-9)
         torch.testing.assert_close(records[:, 9:12], want, rtol=1e-6, atol=1e-7)
