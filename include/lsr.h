@@ -375,6 +375,10 @@ int32_t lsr_debug_bucket_timeline(uint32_t* out, int32_t n);
  * values into out_device[0..3] (a device array of 4 u64): the engine clock the chip ran at meanwhile
  * is 100 (out[3] - out[1]) / (out[2] - out[0]) MHz (tools/clock_probe.py). */
 int32_t lsr_debug_clock_probe(uint64_t* out_device, void* stream);
+/* Measurement aid (ABI 15): a one-wave kernel on `stream` that spins for `microseconds` (at most
+ * 1e6) of the constant 100 MHz counter -- a delay between two launches of one stream (the
+ * pipelined step's stream phase, LSR_PG_GEO_DELAY_US). */
+int32_t lsr_debug_delay(uint32_t microseconds, void* stream);
 
 /* ---- the language-feature loss around the rasterizer ----------------
  *

@@ -127,6 +127,7 @@ SIGNATURES = {
     "lsr_debug_set_spin_limit": (ctypes.c_uint32, [ctypes.c_uint32]),
     "lsr_debug_bucket_timeline": (ctypes.c_int32, [ctypes.POINTER(ctypes.c_uint32), ctypes.c_int32]),
     "lsr_debug_clock_probe": (ctypes.c_int32, [_vp, _vp]),
+    "lsr_debug_delay": (ctypes.c_int32, [ctypes.c_uint32, _vp]),
     "lsr_debug_render_stats": (ctypes.c_int32, [ctypes.POINTER(ctypes.c_uint64), ctypes.c_int32]),
     "lsr_debug_render_timeline": (ctypes.c_int32, [ctypes.c_int32, ctypes.POINTER(ctypes.c_uint32), ctypes.c_int32]),
     "lsr_profile_enable": (ctypes.c_int32, [ctypes.c_int32]),

@@ -872,6 +872,15 @@ int32_t lsr_debug_clock_probe(uint64_t* out_device, void* stream_ptr)
     return LSR_OK;
 }
 
+int32_t lsr_debug_delay(uint32_t microseconds, void* stream_ptr)
+{
+    if (microseconds > 1000000u) return fail(LSR_ERR_INVALID, "lsr_debug_delay: at most one second");
+    hipStream_t stream = reinterpret_cast<hipStream_t>(stream_ptr);
+    const bool debug = false;
+    LSR_TRY(launch_delay(100u * microseconds, stream), "delay");
+    return LSR_OK;
+}
+
 int32_t lsr_mark_visible(int32_t P, const float* means3D, const float* viewmatrix, const float* projmatrix,
                          uint8_t* visible, void* stream_ptr)
 {

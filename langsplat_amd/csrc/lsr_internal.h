@@ -458,5 +458,6 @@ hipError_t render_stats_read(unsigned long long* out, int n);  // reads and clea
 hipError_t render_timeline_read(uint32_t* out, int kernel, int n);
 hipError_t bucket_timeline_read(uint32_t* out, int n);  // LSR_BUCKET_TIMELINE=1 records (k_depth_bucket_sort)
 hipError_t launch_clock_probe(uint64_t* out, hipStream_t s);  // lsr_debug_clock_probe
+hipError_t launch_delay(uint32_t ticks, hipStream_t s);        // lsr_debug_delay
 
 }  // namespace lsr

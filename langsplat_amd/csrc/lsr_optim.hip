@@ -209,7 +209,10 @@ hipError_t launch_language_tail(int P, const int32_t* radii, const float* grad, 
     tab.hyper[0] = h;
     tab.step_dev = step_dev;
     tab.skip = skip;
-    hipLaunchKernelGGL(k_adam_advance, dim3(1), dim3(64), 0, s, step_dev, tab);
+#ifndef LSR_TAIL_NO_ADVANCE  // timing-only knob: 1 leaves the step scalars as they are (wrong results)
+#define LSR_TAIL_NO_ADVANCE 0
+#endif
+    if (!LSR_TAIL_NO_ADVANCE) hipLaunchKernelGGL(k_adam_advance, dim3(1), dim3(64), 0, s, step_dev, tab);
     if (P == 0) return hipGetLastError();
     hipLaunchKernelGGL(k_language_tail, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, P, radii, grad, lang,
                        exp_avg, exp_avg_sq, dmeans2D, dlang, (const int64_t*)step_dev, skip, fill);
@@ -392,6 +395,19 @@ __global__ void k_clock_probe(uint64_t* out)
 hipError_t launch_clock_probe(uint64_t* out, hipStream_t s)
 {
     hipLaunchKernelGGL(k_clock_probe, dim3(1), dim3(64), 0, s, out);
+    return hipGetLastError();
+}
+
+// ---- a one-wave delay of `ticks` of the 100 MHz counter on a stream (lsr_debug_delay) ----
+__global__ void k_delay(uint32_t ticks)
+{
+    const uint64_t r0 = wall_clock64();
+    while (wall_clock64() - r0 < ticks) __builtin_amdgcn_s_sleep(1);
+}
+
+hipError_t launch_delay(uint32_t ticks, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_delay, dim3(1), dim3(64), 0, s, ticks);
     return hipGetLastError();
 }
 

@@ -326,12 +326,16 @@ class PipelinedGraphStep:
                 if self.bucket is None or coll_in_graph:
                     self.optimizer.step(skip=self.overflow[p], fill=adam_fill(p))
 
+        geo_delay = int(os.environ.get("LSR_PG_GEO_DELAY_US", "0"))
+        step_delay = int(os.environ.get("LSR_PG_STEP_DELAY_US", "0"))
         for p in range(S):
             if self.R > 1:
                 continue  # geometry and steps are captured per rotation group below
             g = torch.cuda.CUDAGraph()
             with graph_capture(g, stream=sb), caps[p], self.sets[p], \
                     _native.forward_phase(_native.forward_phase.GEOMETRY):
+                if geo_delay:  # measurement knob: the geometry stream starts later in each step
+                    _native._check(_native.load().lsr_debug_delay(geo_delay, _native._stream(dev)), "delay")
                 self._fwd(p)  # its outputs are written by the composite half
             self.g_geo[p] = g
             for q in self.params:
@@ -353,6 +357,8 @@ class PipelinedGraphStep:
                 self.g_comp0 = g
             g = torch.cuda.CUDAGraph()
             with graph_capture(g, stream=sa):
+                if step_delay:  # measurement knob: the step stream starts each step later
+                    _native._check(_native.load().lsr_debug_delay(step_delay, _native._stream(dev)), "delay")
                 with caps[p], self.sets[p], _native.forward_phase(comp_phase):
                     loss = self._fwd(p)
                 if merged:
