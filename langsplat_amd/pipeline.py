@@ -139,8 +139,9 @@ class PipelinedGraphStep:
     counts the skipped steps and re-captures.  N > 1: the flag is all-reduced in the same collective
     as the gradients (GradBucket.all_reduce(flag=)), so when one rank's view overflowed EVERY rank
     skips that step and re-captures: the ranks stay identical and no zero gradient is averaged in.
-    With RCCL the collective is captured inside the step graph (one stream-A graph per step, as at
-    N = 1); with gloo it runs between the backward and Adam graphs.
+    The collective runs between the backward and Adam graphs (gloo; RCCL at N > 1 by default), or
+    inside the step graph when captured (distributed.collective_capturable); the update then also
+    fills the next set's records (lsr_adam_fill_language), as the fused tail does at N = 1.
 
         g = PipelinedGraphStep(lambda: render(...)["language_l1"], [gaussians._language_feature], optimizer)
         for it in range(iterations):
@@ -278,8 +279,9 @@ class PipelinedGraphStep:
                 self._fwd(p)
         sb.wait_stream(sa)
         # N > 1: the all-reduce of the gradients (and, in the same collective, of the set's overflow
-        # flag: every rank then skips when one view overflowed) inside the step graph when the backend
-        # can be captured (RCCL), else launched between the backward and Adam graphs (gloo)
+        # flag: every rank then skips when one view overflowed) inside the step graph when the collective
+        # is captured (distributed.collective_capturable: RCCL with one rank, or LSR_GRAPH_COLLECTIVE=1),
+        # else launched between the backward and Adam graphs (gloo, and RCCL at N > 1 by default)
         dev = self.params[0].device
         coll_in_graph = self.bucket is not None and collective_capturable()
         self.coll_in_graph = coll_in_graph
