@@ -413,9 +413,14 @@ def main():
         optim = torch.optim.Adam(groups, lr=0.0, eps=1e-15, fused=True)
     # N > 1: .grad tensors are views of one flat bucket (one all-reduce); N = 1: train.py:138's
     # zero_grad(set_to_none=True), so autograd hands the rasterizer's gradient over without a copy
-    # (LSR_BENCH_BUCKET=1 at N = 1: the N > 1 step structure without its collective -- the all-reduce
-    # is a no-op on one process -- a measurement aid for the cost of the N > 1 form itself)
-    bucket = GradBucket(model.trainable()) if world > 1 or os.environ.get("LSR_BENCH_BUCKET") == "1" else None
+    # (LSR_BENCH_BUCKET=1 at N = 1: the N > 1 step structure around a one-rank RCCL all-reduce -- a
+    # measurement aid for the cost of the N > 1 form itself, collective eager between two graphs or,
+    # with LSR_GRAPH_COLLECTIVE=1, captured; LSR_BENCH_BUCKET=nodist: no process group, no collective)
+    bench_bucket = os.environ.get("LSR_BENCH_BUCKET", "0")
+    if world == 1 and bench_bucket == "1" and not dist.is_initialized():
+        dist.init_process_group("nccl", rank=0, world_size=1,
+                                init_method=f"tcp://127.0.0.1:{launch.free_port()}")
+    bucket = GradBucket(model.trainable()) if world > 1 or bench_bucket in ("1", "nodist") else None
 
     def step():
         if fused:  # the loss inside the compositing kernel, its backward in the replay
@@ -787,6 +792,7 @@ def main():
             f.write(line + "\n")
     if world > 1:
         dist.barrier()
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 
