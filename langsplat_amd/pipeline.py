@@ -162,8 +162,12 @@ class PipelinedGraphStep:
     only after this view's compositing), LSR_PG_PRIO=geo|step (stream priorities), LSR_PG_ROT."""
 
     def __init__(self, forward_fn, params, optimizer, headroom: float = 1.125, warmup: int = 2, bucket=None,
-                 slots=None, sets: int = None, rotation: int = None, model=None, bucket_factory=None):
+                 slots=None, sets: int = None, rotation: int = None, model=None, bucket_factory=None,
+                 ahead: int = None):
         self.forward_fn = forward_fn
+        # replay() waits on the host until step k - ahead has finished before enqueuing step k
+        # (0: no limit; LSR_PG_AHEAD)
+        self.ahead = int(ahead if ahead is not None else os.environ.get("LSR_PG_AHEAD", "0"))
         self.model = model  # its active_sh_degree is part of the capture key (graph.capture_key)
         self.params = [p for p in params]
         self.optimizer = optimizer
@@ -535,6 +539,10 @@ class PipelinedGraphStep:
         cur = torch.cuda.current_stream()
         p = self.k % S
         r = (self.k + S - 1) % S
+        if 0 < self.ahead < S and self._since_capture >= self.ahead:
+            # host throttle: at most `ahead` steps enqueued beyond the running one (the queues stay
+            # short; a step's stream-A work still follows the previous step without a host gap)
+            self.ev_step[(self.k - self.ahead) % S].synchronize()
         if not self.primed:  # the first S - 1 views' geometry (nothing ran since the capture)
             for j in range(S - 1):
                 self._geometry((self.k + j) % S)
