@@ -37,7 +37,7 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from langsplat_amd import _native, launch  # noqa: E402
+from langsplat_amd import _native, launch, rccl  # noqa: E402
 from langsplat_amd.distributed import GradBucket, collective_capturable, init_from_env  # noqa: E402
 from langsplat_amd.optim import Adam as AmdAdam  # noqa: E402
 from langsplat_amd.pipeline import PipelinedGraphStep, ViewPipeline  # noqa: E402
@@ -673,6 +673,8 @@ def main():
 
     if rank != 0:
         dist.barrier()
+        torch.cuda.synchronize()
+        rccl.destroy_default()
         dist.destroy_process_group()
         return
 
@@ -793,6 +795,8 @@ def main():
     if world > 1:
         dist.barrier()
     if dist.is_initialized():
+        torch.cuda.synchronize()
+        rccl.destroy_default()
         dist.destroy_process_group()
 
 

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define LSR_ABI_VERSION 15
+#define LSR_ABI_VERSION 16
 
 enum lsr_status {
     LSR_OK = 0,
@@ -103,7 +103,21 @@ enum lsr_forward_flags { LSR_FWD_ZERO_GRAD_RECORDS = 1, LSR_FWD_NO_COLOR_GRAD = 
  * then runs at most 6 workgroups per CU instead of 8 (extra dynamic LDS), leaving wave slots and LDS
  * to the other stream's workgroups: measured at C3, 0.417-0.421 -> 0.400-0.401 ms per pipelined step
  * (DESIGN.md §5b).  Results are unchanged. */
-enum lsr_backward_flags { LSR_BWD_RECORDS_ZEROED = 1, LSR_BWD_SHARED_CU = 2 };
+/* LSR_BWD_DEFER_TAIL (ABI 16): the fused update (lsr_backward_args.update) split around a gradient
+ * all-reduce (train.py:104 + 134-137 with the views of N ranks: langsplat_amd.pipeline at N > 1).
+ * lsr_backward then runs the render backward only and leaves the language step's gradient records
+ * in the geometry buffer (lsr_state_layout.grad_records) in planar form: float[3P] language partials
+ * (dL/d of the activated feature, before the activation's chain rule), one word holding
+ * *update_skip (0 when NULL), three padding words, then float[2P] screen-space partials.  The caller
+ * reduces the first 3 P + 1 floats over the ranks -- an AVG: the chain rule and the Adam step are
+ * linear / pointwise in the partials, a Gaussian another rank saw has partials here too, and the
+ * skip word (0 or the bits of 1.0f) stays non-zero on every rank once one rank's view overflowed --
+ * then calls lsr_language_tail with the same arguments: ONE pass writes dL_dmeans2D (this view's,
+ * from the unreduced screen-space partials), dL_dlanguage_feature (from the reduced partials) and
+ * the Adam step on the reduced skip word (+ the fill): what lsr_backward with update does at N = 1,
+ * with no gradient epilogue before the collective.  The records need no LSR_BWD_RECORDS_ZEROED (they
+ * are cleared here otherwise). */
+enum lsr_backward_flags { LSR_BWD_RECORDS_ZEROED = 1, LSR_BWD_SHARED_CU = 2, LSR_BWD_DEFER_TAIL = 4 };
 
 /* GaussianRasterizationSettings (gaussian_renderer/__init__.py:37-51), device-pointer form. */
 typedef struct lsr_settings {
@@ -276,6 +290,10 @@ typedef struct lsr_state_layout {
     /* binning buffer */
     size_t point_list;     /* uint32[num_rendered] Gaussian ids, tile-major, (depth, id) order;
                               entry k belongs to the tile t with ranges[t].x <= k < ranges[t].y */
+    /* geometry buffer (ABI 16) */
+    size_t grad_records;   /* float[5P] the language step's gradient records; after a backward with
+                              LSR_BWD_DEFER_TAIL: float[3P] language partials, the skip word, 3 words,
+                              then float[2P] dx, dy */
 } lsr_state_layout;
 
 int32_t lsr_abi_version(void);
@@ -460,6 +478,13 @@ int32_t lsr_adam_multi(int32_t count, const lsr_adam_tensor* tensors, float grad
  * backward and the update (langsplat_amd.pipeline.PipelinedGraphStep with a bucket). */
 int32_t lsr_adam_fill_language(const lsr_adam_tensor* tensor, float grad_scale, int64_t* step_dev, const int32_t* skip,
                                void* fill_record, int32_t raw, void* stream);
+
+/* The second half of a backward made with LSR_BWD_DEFER_TAIL (ABI 16): settings and args as passed
+ * to that lsr_backward (same buffers, update, update_step_dev, update_skip, fill_record; flags may
+ * keep LSR_BWD_DEFER_TAIL), after the caller reduced the records' language partials.  Launches the
+ * Adam step advance and one pass per Gaussian: dL_dmeans2D, dL_dlanguage_feature, the Adam step and
+ * the fill, as lsr_backward with update (not deferred) does after its render backward. */
+int32_t lsr_language_tail(const lsr_settings* settings, const lsr_backward_args* args, void* stream);
 
 /* Densification statistics of one rendered view, one pass (train.py:125-126 with
  * GaussianModel.add_densification_stats, scene/gaussian_model.py:480-482), for Gaussians with

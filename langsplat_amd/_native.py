@@ -22,13 +22,13 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LSR_LIB") or os.path.join(_HERE, "liblsr.so")
 
 LSR_BUF_GEOM, LSR_BUF_BINNING, LSR_BUF_IMAGE, LSR_BUF_BACKWARD = 0, 1, 2, 3
-ABI_VERSION = 15
+ABI_VERSION = 16
 ADAM_STEP_WORDS = 66  # include/lsr.h LSR_ADAM_STEP_WORDS
 ADAM_WORD_SKIPPED, ADAM_WORD_LR = 49, 50  # LSR_ADAM_WORD_SKIPPED / LSR_ADAM_WORD_LR
 # lsr_raw_flags (include/lsr.h): inputs are GaussianModel's raw parameters
 RAW_OPACITY, RAW_SCALES, RAW_ROTATIONS, RAW_LANGUAGE = 1, 2, 4, 8
 FWD_ZERO_GRAD_RECORDS, FWD_NO_COLOR_GRAD, FWD_NO_BACKWARD = 1, 2, 4  # lsr_forward_flags
-BWD_RECORDS_ZEROED, BWD_SHARED_CU = 1, 2  # lsr_backward_flags
+BWD_RECORDS_ZEROED, BWD_SHARED_CU, BWD_DEFER_TAIL = 1, 2, 4  # lsr_backward_flags
 _vp = ctypes.c_void_p
 
 
@@ -82,7 +82,7 @@ class LsrBackwardArgs(ctypes.Structure):
 class LsrStateLayout(ctypes.Structure):
     _fields_ = [(n, ctypes.c_size_t) for n in (
         "depth_key", "tiles_touched", "rect", "record", "clamped", "sorted_ids", "super_offset",
-        "counters", "ranges", "final_T", "n_contrib", "point_list")]
+        "counters", "ranges", "final_T", "n_contrib", "point_list", "grad_records")]
 
 
 class LsrKernelStat(ctypes.Structure):
@@ -113,6 +113,7 @@ SIGNATURES = {
                                         _vp]),
     "lsr_adam_fill_language": (ctypes.c_int32, [ctypes.POINTER(LsrAdamTensor), ctypes.c_float, _vp, _vp, _vp,
                                                 ctypes.c_int32, _vp]),
+    "lsr_language_tail": (ctypes.c_int32, [ctypes.POINTER(LsrSettings), ctypes.POINTER(LsrBackwardArgs), _vp]),
     "lsr_densification_stats": (ctypes.c_int32, [ctypes.c_int32, _vp, _vp, _vp, _vp, _vp, _vp]),
     "lsr_dist_cuda2": (ctypes.c_int32, [ctypes.c_int64, _vp, _vp, ALLOC_FN, _vp, _vp]),
     "lsr_masked_l1_scratch_bytes": (ctypes.c_size_t, [ctypes.c_int32, ctypes.c_int64]),
@@ -389,15 +390,41 @@ class fused_update:
     then leaves it alone.  The optimizer must be a langsplat_amd.optim.Adam prepared for a capture
     (its device step block; only inside a graph capture) with `param` its one parameter.  skip: its
     skip flag (the overflow flag); fill: a device pointer to another forward's record array whose
-    language slots receive the updated activated feature (langsplat_amd.pipeline), or None."""
+    language slots receive the updated activated feature (langsplat_amd.pipeline), or None.
+
+    defer=True (N > 1, include/lsr.h LSR_BWD_DEFER_TAIL): the backward runs the render backward only
+    and leaves the per-Gaussian language partials in its geometry buffer; partials() is that (P, 3)
+    tensor, which the caller all-reduces (AVG over the ranks), then run_tail() launches the rest in
+    one pass -- the gradient outputs, the Adam step and the fill (lsr_language_tail).  The backward's
+    returned gradients hold their values only after run_tail()."""
 
     # process-wide, not thread-local: autograd runs a CUDA node's backward on its device thread, not
     # on the thread that called loss.backward()
     _cur = None
 
-    def __init__(self, optimizer, param: torch.Tensor, skip: Optional[torch.Tensor] = None, fill: Optional[int] = None):
+    def __init__(self, optimizer, param: torch.Tensor, skip: Optional[torch.Tensor] = None, fill: Optional[int] = None,
+                 defer: bool = False):
         self.optimizer, self.param, self.skip, self.fill = optimizer, param, skip, fill
+        self.defer = bool(defer)
         self.used = False
+        self.pending = None  # defer: the deferred tail's arguments (and every tensor they point into)
+
+    def partials(self) -> torch.Tensor:
+        """defer: what the caller all-reduces -- the deferred backward's 3 P language partials and the
+        step's skip word after them, (3 P + 1,) fp32, a view of its buffer (include/lsr.h)."""
+        if self.pending is None:
+            raise RuntimeError("fused_update.partials: no deferred backward ran in this block")
+        return self.pending[3]
+
+    def run_tail(self):
+        """defer: lsr_language_tail on the current stream, after the caller reduced partials()."""
+        if self.pending is None:
+            raise RuntimeError("fused_update.run_tail: no deferred backward ran in this block")
+        s, a, _keep, part, device = self.pending
+        if part.numel() == 0:
+            return
+        with _on_device(device):
+            _check(load().lsr_language_tail(ctypes.byref(s), ctypes.byref(a), _stream(device)), "lsr_language_tail")
 
     @staticmethod
     def active():
@@ -630,6 +657,9 @@ def rasterize_gaussians_backward(rs, means3D, shs, colors_precomp, language_feat
         g[name] = flat[off:off + n].view(sh)
         off += na
     if P == 0:
+        if update is not None and update.defer:
+            update.pending = (None, None, [], torch.empty((0,), dtype=torch.float32, device=device), device)
+            update.used = True
         return {k: (v.zero_() if v is not None else None) for k, v in g.items()}
     a = LsrBackwardArgs()
     a.P = P
@@ -679,9 +709,18 @@ def rasterize_gaussians_backward(rs, means3D, shs, colors_precomp, language_feat
         a.update_skip = _ptr(update.skip)
         a.fill_record = None if update.fill is None else ctypes.c_void_p(int(update.fill))
         update.used = True
+        if update.defer:
+            a.flags |= BWD_DEFER_TAIL
     alloc = _Allocator(device)
     with _on_device(device), alloc:
         _check(lib.lsr_backward(ctypes.byref(s), ctypes.byref(a), _ALLOC_CB, None, _stream(device)), "lsr_backward")
+    if update is not None and update.defer:
+        # the records' language partials and the skip word: the first 3 P + 1 floats of grad_records
+        off = state_layout(P, int(rs.image_width), int(rs.image_height), int(num_rendered))["grad_records"]
+        part = geom[off:off + 4 * (3 * P + 1)].view(torch.float32)
+        # every tensor the deferred launch's pointers reach stays alive with it
+        keep += [flat, geom, binning, image, radii, language_feature, update.skip, gl, gls, gc, means3D]
+        update.pending = (s, a, keep, part, device)
     return g
 
 

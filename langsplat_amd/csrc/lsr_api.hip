@@ -290,7 +290,7 @@ static int32_t render_forward_and_finish(const lsr_settings* s, const lsr_forwar
     }
     if (a->flags & LSR_FWD_ZERO_GRAD_RECORDS) {
         rp.zero_records = reinterpret_cast<float4*>(geom + L.grad_records);
-        rp.zero_records_n4 = ((int64_t)P * kGradStrideLang + 3) / 4;
+        rp.zero_records_n4 = ((int64_t)P * kGradStrideLang + kDeferXyOffset + 3) / 4;
     }
     if (a->out_loss && rp.include_feature) {
         rp.loss_gt = a->loss_target;
@@ -340,6 +340,7 @@ int32_t lsr_state_layout_of(int32_t P, int32_t width, int32_t height, int64_t nu
     out->final_T = L.final_T;
     out->n_contrib = L.n_contrib;
     out->point_list = L.point_list;
+    out->grad_records = L.grad_records;
     return LSR_OK;
 }
 
@@ -617,7 +618,10 @@ int32_t lsr_backward(const lsr_settings* s, const lsr_backward_args* a, lsr_allo
     }
     if (a->raw & ~(LSR_RAW_OPACITY | LSR_RAW_SCALES | LSR_RAW_ROTATIONS | LSR_RAW_LANGUAGE))
         return fail(LSR_ERR_INVALID, "lsr_backward: unknown raw flag");
-    if (a->flags & ~(LSR_BWD_RECORDS_ZEROED | LSR_BWD_SHARED_CU)) return fail(LSR_ERR_INVALID, "lsr_backward: unknown flag");
+    if (a->flags & ~(LSR_BWD_RECORDS_ZEROED | LSR_BWD_SHARED_CU | LSR_BWD_DEFER_TAIL))
+        return fail(LSR_ERR_INVALID, "lsr_backward: unknown flag");
+    const bool defer = (a->flags & LSR_BWD_DEFER_TAIL) != 0;
+    if (defer && !a->update) return fail(LSR_ERR_INVALID, "lsr_backward: LSR_BWD_DEFER_TAIL needs update");
     if (geometry && a->shs_rest && (!a->shs || a->M < 2 || !a->dL_dsh_rest))
         return fail(LSR_ERR_INVALID, "lsr_backward: shs_rest needs shs, M >= 2 and dL_dsh_rest");
     if ((a->raw & LSR_RAW_OPACITY) && P > 0 && !a->opacities)
@@ -667,6 +671,10 @@ int32_t lsr_backward(const lsr_settings* s, const lsr_backward_args* a, lsr_allo
     float* grad = nullptr;
     if (compact && (a->flags & LSR_BWD_RECORDS_ZEROED)) {
         grad = reinterpret_cast<float*>(geom + L.grad_records);
+    } else if (defer) {  // (update implies the compact form) the records stay for lsr_language_tail
+        grad = reinterpret_cast<float*>(geom + L.grad_records);
+        LSR_TRY(zero_fill(grad, 4 * ((size_t)kGradStrideLang * (size_t)P + kDeferXyOffset), stream),
+                "memset grad records");
     } else {
         grad = static_cast<float*>(alloc(user, LSR_BUF_BACKWARD, lsr_backward_bytes(P)));
         if (!grad) return fail(LSR_ERR_ALLOC, "lsr_backward: gradient scratch allocation failed");
@@ -695,17 +703,30 @@ int32_t lsr_backward(const lsr_settings* s, const lsr_backward_args* a, lsr_allo
     rp.dL_dloss = a->dL_dloss;
     rp.loss_code = reinterpret_cast<uint8_t*>(image + L.loss_code);
     rp.grad = grad;
+    if (defer) {  // planar records (LSR_BWD_DEFER_TAIL), the skip flag after the language partials
+        rp.grad_xy = grad + 3 * (size_t)P + kDeferXyOffset;
+        rp.flag_src = a->update_skip;
+        rp.flag_dst = reinterpret_cast<int32_t*>(grad + 3 * (size_t)P);
+    }
     rp.fwd_flags = reinterpret_cast<uint32_t*>(image + L.counters) + kCntFwdFlags;
     rp.geo = geometry ? 1 : 0;
     rp.shared_cu = (a->flags & LSR_BWD_SHARED_CU) ? 1 : 0;
-    if (a->num_rendered > 0) LSR_TRY(launch_render_backward(rp, L.tiles, stream), "render backward");
+    if (a->num_rendered > 0) {
+        LSR_TRY(launch_render_backward(rp, L.tiles, stream), "render backward");
+    } else if (defer) {  // no render backward: the flag word by a copy
+        if (a->update_skip)
+            LSR_TRY(hipMemcpyAsync(rp.flag_dst, a->update_skip, 4, hipMemcpyDeviceToDevice, stream), "copy skip flag");
+        else
+            LSR_TRY(zero_fill(rp.flag_dst, 4, stream), "clear skip flag");
+    }
     if (a->update) {
+        if (defer) return LSR_OK;  // lsr_language_tail runs the rest after the caller's all-reduce
         // the language step's tail in one pass: epilogue + Adam (+ the next forward's feature slots)
         const lsr_adam_tensor& u = *a->update;
         AdamHyper h{u.lr, u.beta1, u.beta2, u.eps, u.step};
         LSR_TRY(launch_language_tail(P, a->radii, grad, const_cast<float*>(a->language_feature), u.exp_avg, u.exp_avg_sq,
                                      a->dL_dmeans2D, a->dL_dlanguage_feature, h, a->update_step_dev, a->update_skip,
-                                     reinterpret_cast<float4*>(a->fill_record), stream),
+                                     reinterpret_cast<float4*>(a->fill_record), 0, stream),
                 "language tail");
         return LSR_OK;
     }
@@ -1008,6 +1029,34 @@ int32_t lsr_adam_fill_language(const lsr_adam_tensor* t, float grad_scale, int64
     LSR_TRY(launch_adam_fill((int)(t->n / 3), t->grad, grad_scale, t->param, t->exp_avg, t->exp_avg_sq, h, step_dev,
                              skip, reinterpret_cast<float4*>(fill_record), raw, stream),
             "adam fill");
+    return LSR_OK;
+}
+
+int32_t lsr_language_tail(const lsr_settings* s, const lsr_backward_args* a, void* stream_ptr)
+{
+    if (!s || !a) return fail(LSR_ERR_INVALID, "lsr_language_tail: null argument");
+    const int P = a->P, W = s->image_width, H = s->image_height;
+    if (P < 0 || W <= 0 || H <= 0) return fail(LSR_ERR_INVALID, "lsr_language_tail: invalid P or image size");
+    if (!a->update || !a->update_step_dev || !a->dL_dlanguage_feature || !(a->raw & LSR_RAW_LANGUAGE) ||
+        !a->language_feature || a->update->param != a->language_feature || a->update->n != 3 * (int64_t)P ||
+        !a->update->exp_avg || !a->update->exp_avg_sq)
+        return fail(LSR_ERR_INVALID, "lsr_language_tail: the arguments of a fused update (lsr_backward_args.update) "
+                                     "are needed");
+    if (P > 0 && (!a->geom_buffer || !a->radii)) return fail(LSR_ERR_INVALID, "lsr_language_tail: missing forward state");
+    if (a->fill_record && (reinterpret_cast<uintptr_t>(a->fill_record) & 15))
+        return fail(LSR_ERR_INVALID, "lsr_language_tail: fill_record must be 16-byte aligned");
+    hipStream_t stream = reinterpret_cast<hipStream_t>(stream_ptr);
+    const bool debug = s->debug != 0;
+    const Layout L = make_layout(P, W, H, a->num_rendered, 0);
+    float* grad = P > 0 ? reinterpret_cast<float*>(static_cast<char*>(a->geom_buffer) + L.grad_records) : nullptr;
+    const lsr_adam_tensor& u = *a->update;
+    AdamHyper h{u.lr, u.beta1, u.beta2, u.eps, u.step};
+    // the skip flag the all-reduce carried (the word after the language partials): any rank's overflow
+    const int32_t* skip = P > 0 ? reinterpret_cast<const int32_t*>(grad + 3 * (size_t)P) : a->update_skip;
+    LSR_TRY(launch_language_tail(P, a->radii, grad, const_cast<float*>(a->language_feature), u.exp_avg, u.exp_avg_sq,
+                                 a->dL_dmeans2D, a->dL_dlanguage_feature, h, a->update_step_dev, skip,
+                                 reinterpret_cast<float4*>(a->fill_record), 1, stream),
+            "language tail");
     return LSR_OK;
 }
 

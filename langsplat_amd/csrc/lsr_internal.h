@@ -63,6 +63,9 @@ constexpr int kSuper = 8;          // super-tile = kSuper x kSuper tiles (64-bit
 constexpr int kSegEntries = 512;   // super-tile list entries per binning workgroup
 constexpr int kGradStride = 16;                          // floats per Gaussian grad record
 constexpr int kGradStrideLang = 5;  // without geometry gradients: {dxy, dlang}, packed 20-B records
+// LSR_BWD_DEFER_TAIL's planar records: P x 3 language partials, the step's skip flag (one word: the
+// all-reduce carries it with the partials), padding, then P x 2 screen-space partials at 3 P + 4
+constexpr int kDeferXyOffset = 4;  // floats after the 3 P language partials
 constexpr int kFusedEntries = 3;    // capacity of the fused super-tile emission, entries per Gaussian
 constexpr int kSuperHistBlock = 1024;  // entries per block of the super-tile pass (k_radix_scatter<4>)
 
@@ -150,7 +153,8 @@ inline Layout make_layout(int P, int W, int H, int64_t R, int64_t E)
         L.zero_words = (L.bucket_status + 8 * 513 - L.scan_regions + 3) / 4;
     }
     L.rect_ranked = take(8 * p);
-    L.grad_records = take(4 * kGradStrideLang * p + 16);  // + padding: cleared as whole float4s
+    // + padding: cleared as whole float4s, and the deferred form's flag slot (kDeferFlagSlot)
+    L.grad_records = take(4 * kGradStrideLang * p + 32);
     L.bucket_totals = take(4 * 512);
     {
         const int gx = (W + kTile - 1) / kTile, gy = (H + kTile - 1) / kTile;
@@ -288,6 +292,13 @@ struct RenderParams {
     // backward
     const float *dL_dcolor, *dL_dlang;
     float* grad;
+    // the language step's planar records (LSR_BWD_DEFER_TAIL): grad = P x 3 language partials, grad_xy
+    // = P x 2 screen-space partials; null: the packed 20-B records {dx, dy, l0, l1, l2} at grad
+    float* grad_xy;
+    // LSR_BWD_DEFER_TAIL: the first workgroup copies *flag_src (0 if null) to *flag_dst, the word after
+    // the language partials, so the one all-reduce of the partials carries the skip flag too
+    const int32_t* flag_src;
+    int32_t* flag_dst;
     uint32_t* fwd_flags;  // counters[kCntFwdFlags] of the forward (its records bit is cleared)
     // fused language-feature loss (null: off).  forward: gt (3 x HW), mask (HW bool bytes) -> codes,
     // per-workgroup partials, out_loss; backward: dL_dloss (device scalar) with the forward's codes
@@ -414,10 +425,12 @@ hipError_t launch_adam_multi(AdamTable& tab, float grad_scale, hipStream_t s);
 // lsr_backward_args.update: k_adam_advance (one tensor, the skip flag), then one pass per Gaussian: the
 // gradient epilogue (dmeans2D, dlang from the 20-B records and the raw feature), the Adam step of the
 // raw feature (its device scalars; nothing on *skip) and, with fill, the activated updated feature
-// into fill's language slots of every Gaussian
+// into fill's language slots of every Gaussian.  deferred (lsr_language_tail): the records are planar
+// and their language partials reduced over the ranks (no radius gate on dlang: a Gaussian this view
+// culled may carry another view's partials)
 hipError_t launch_language_tail(int P, const int32_t* radii, const float* grad, float* lang, float* exp_avg,
                                 float* exp_avg_sq, float* dmeans2D, float* dlang, const AdamHyper& h, int64_t* step_dev,
-                                const int32_t* skip, float4* fill, hipStream_t s);
+                                const int32_t* skip, float4* fill, int deferred, hipStream_t s);
 hipError_t launch_adam_fill(int P, const float* grad, float grad_scale, float* lang, float* exp_avg, float* exp_avg_sq,
                             const AdamHyper& h, int64_t* step_dev, const int32_t* skip, float4* fill, int raw,
                             hipStream_t s);

@@ -154,13 +154,29 @@ __global__ __launch_bounds__(256) void k_language_tail(int P, const int32_t* __r
                                                        float* __restrict__ m, float* __restrict__ v,
                                                        float* __restrict__ dmeans2D, float* __restrict__ dlang,
                                                        const int64_t* __restrict__ step_dev,
-                                                       const int32_t* __restrict__ skip, float4* __restrict__ fill)
+                                                       const int32_t* __restrict__ skip, float4* __restrict__ fill,
+                                                       int deferred)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P) return;
     const size_t i3 = 3 * (size_t)i;
-    const float* r = grad + (size_t)i * kGradStrideLang;
-    const float r0 = r[0], r1 = r[1], r2 = r[2], r3 = r[3], r4 = r[4];
+    float r0, r1, r2, r3, r4;
+    if (deferred) {  // planar: P x 3 language partials (all-reduced), the flag word, P x 2 screen-space partials
+        const float* rl = grad + i3;
+        const float* rxy = grad + 3 * (size_t)P + kDeferXyOffset + 2 * (size_t)i;
+        r0 = rxy[0];
+        r1 = rxy[1];
+        r2 = rl[0];
+        r3 = rl[1];
+        r4 = rl[2];
+    } else {
+        const float* r = grad + (size_t)i * kGradStrideLang;
+        r0 = r[0];
+        r1 = r[1];
+        r2 = r[2];
+        r3 = r[3];
+        r4 = r[4];
+    }
     const int rad = radii[i];
     float l[3] = {lang[i3], lang[i3 + 1], lang[i3 + 2]};
     float mm[3] = {m[i3], m[i3 + 1], m[i3 + 2]};
@@ -173,7 +189,7 @@ __global__ __launch_bounds__(256) void k_language_tail(int P, const int32_t* __r
         dmeans2D[i3 + 2] = 0.f;
     }
     float3 d = make_float3(0.f, 0.f, 0.f);
-    if (live) d = act_lang_backward(l[0], l[1], l[2], r2, r3, r4);
+    if (live || deferred) d = act_lang_backward(l[0], l[1], l[2], r2, r3, r4);
     dlang[i3] = d.x;
     dlang[i3 + 1] = d.y;
     dlang[i3 + 2] = d.z;
@@ -202,7 +218,7 @@ __global__ __launch_bounds__(256) void k_language_tail(int P, const int32_t* __r
 
 hipError_t launch_language_tail(int P, const int32_t* radii, const float* grad, float* lang, float* exp_avg,
                                 float* exp_avg_sq, float* dmeans2D, float* dlang, const AdamHyper& h, int64_t* step_dev,
-                                const int32_t* skip, float4* fill, hipStream_t s)
+                                const int32_t* skip, float4* fill, int deferred, hipStream_t s)
 {
     AdamTable tab{};
     tab.count = 1;
@@ -215,7 +231,7 @@ hipError_t launch_language_tail(int P, const int32_t* radii, const float* grad, 
     if (!LSR_TAIL_NO_ADVANCE) hipLaunchKernelGGL(k_adam_advance, dim3(1), dim3(64), 0, s, step_dev, tab);
     if (P == 0) return hipGetLastError();
     hipLaunchKernelGGL(k_language_tail, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, P, radii, grad, lang,
-                       exp_avg, exp_avg_sq, dmeans2D, dlang, (const int64_t*)step_dev, skip, fill);
+                       exp_avg, exp_avg_sq, dmeans2D, dlang, (const int64_t*)step_dev, skip, fill, deferred);
     return hipGetLastError();
 }
 

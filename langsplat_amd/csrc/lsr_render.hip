@@ -1412,6 +1412,7 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
     // the forward's cleared records are used by this backward only (include/lsr.h): one store, no
     // reader in this launch
     if (p.fwd_flags && blockIdx.x == 0 && threadIdx.x == 0) *p.fwd_flags &= ~kFwdZeroedRecords;
+    if (p.flag_dst && blockIdx.x == 0 && threadIdx.x == 0) *p.flag_dst = p.flag_src ? *p.flag_src : 0;
     int tile = (int)blockIdx.x;
     uint32_t chunk = 0;  // split replay: this workgroup replays list entries [kSplitChunk chunk, ...) of the tile
     if (p.sched_counts) {  // tiles without contributors are not scheduled: nothing to do
@@ -1547,7 +1548,11 @@ __global__ __launch_bounds__(kTilePixels) void k_render_backward(RenderParams p)
             if (v == 0.0f || LSR_BWD_NOFLUSH) continue;
             if (k5) {  // packed 20-B record: dxy in slots 0, 1, the language feature in 2..4
                 const float val = v * (cs == 0 ? (float)p.W : cs == 1 ? (float)p.H : 1.0f);
-                atomicAdd(&p.grad[(size_t)s_gid[e] * kGradStrideLang + cs], val);
+                const size_t g = s_gid[e];
+                // (LSR_BWD_DEFER_TAIL: planar records, the language partials one all-reducible block)
+                float* dst = !p.grad_xy ? p.grad + g * kGradStrideLang + cs
+                                        : (cs < 2 ? p.grad_xy + 2 * g + cs : p.grad + 3 * g + (cs - 2));
+                atomicAdd(dst, val);
             } else {
                 const int c = (kColor || cs < 6) ? cs : cs + 3;  // gslot's inverse
                 if (!gvalue<kColor, kGeo>(c)) continue;          // a value this variant does not produce

@@ -16,6 +16,8 @@ from typing import Iterable, List
 import torch
 import torch.distributed as dist
 
+from . import rccl
+
 
 def init_from_env(backend: str = None):
     """Initialise torch.distributed from torchrun's RANK/WORLD_SIZE/MASTER_* (no-op if WORLD_SIZE<=1)."""
@@ -191,16 +193,44 @@ class GradBucket:
             self._divided_by = 1
             return
         self._attach()
-        buf = self.buffer()
+        self._reduce(self.buffer(), average, group, flag)
+        if self._max_radii is not None:
+            dist.all_reduce(self._max_radii, op=dist.ReduceOp.MAX, group=group)
+            self._max_radii = None
+
+    def all_reduce_partials(self, partials: torch.Tensor, average: bool = True, group=None,
+                            flag: torch.Tensor = None):
+        """The step's collective over a deferred language backward's per-Gaussian partials
+        (_native.fused_update(defer=True).partials(), include/lsr.h LSR_BWD_DEFER_TAIL: they end with
+        the step's skip word, so no separate flag) instead of the parameter's .grad: the same SUM / AVG
+        as all_reduce, before the gradient epilogue, which is linear in them (lsr_language_tail then
+        writes the reduced gradient and steps on the reduced skip word).  One parameter (direct mode)
+        only."""
+        if not self.direct:
+            raise RuntimeError("GradBucket.all_reduce_partials: for the one-parameter language step only")
+        if not (dist.is_available() and dist.is_initialized()):
+            self._divided_by = 1
+            return
+        self._reduce(partials, average, group, flag)
+
+    def _reduce(self, buf: torch.Tensor, average: bool, group, flag: torch.Tensor):
         world = dist.get_world_size(group)
         nccl = dist.get_backend(group) == "nccl"
+        if flag is not None and (flag.dtype != torch.int32 or flag.numel() != 1 or flag.device != buf.device):
+            raise ValueError("GradBucket.all_reduce: flag must be a one-element int32 tensor on the bucket's device")
+        if nccl and group is None and rccl.direct_enabled(group) and (
+                rccl._default is not None or not torch.cuda.is_current_stream_capturing()):
+            # RCCL on the caller's stream (langsplat_amd.rccl: no round trip through torch's internal
+            # stream); its communicator is built at the first (eager) reduction
+            rccl.default_communicator().all_reduce([buf] + ([flag.view(torch.float32)] if flag is not None else []),
+                                                   op="avg" if average else "sum")
+            self._divided_by = world if average else 1
+            return
         # RCCL's ncclAvg: the division is part of the collective (no separate scaling kernel)
         op = dist.ReduceOp.AVG if average and nccl else dist.ReduceOp.SUM
         if flag is None:
             dist.all_reduce(buf, op=op, group=group)
         else:
-            if flag.dtype != torch.int32 or flag.numel() != 1 or flag.device != buf.device:
-                raise ValueError("GradBucket.all_reduce: flag must be a one-element int32 tensor on the bucket's device")
             if nccl:  # one ncclGroup: one collective launch for both
                 with dist._coalescing_manager(group=group):
                     dist.all_reduce(buf, op=op, group=group)
@@ -211,9 +241,6 @@ class GradBucket:
         if average and not nccl:
             buf.mul_(1.0 / world)
         self._divided_by = world if average else 1
-        if self._max_radii is not None:
-            dist.all_reduce(self._max_radii, op=dist.ReduceOp.MAX, group=group)
-            self._max_radii = None
 
 
 class UpdateOverlap:

@@ -209,7 +209,8 @@ class PipelinedGraphStep:
         self.captures = 0
         self.rendered = self.entries = 0
         self._skipped_base = 0
-        self.fused = self.fill_after = False  # the update's record fill (set by capture)
+        self.fused = self.fill_after = self.defer = False  # the update's record fill (set by capture)
+        self._tails = [None] * self.S
         self._loaded = [None] * S  # the view each set's slot holds (slots only)
         self._assigned = [None] * S  # rotation mode: the view each set's next geometry renders
 
@@ -304,6 +305,14 @@ class PipelinedGraphStep:
         # from the parameter by replay(), _refill) needs no fill either
         fill_after = self.bucket is not None and len(self.params) == 1 and _fused_tail_enabled()
         self.fill_after = fill_after
+        # ... and the gradient epilogue moves behind the collective: the backward leaves the language
+        # partials (include/lsr.h LSR_BWD_DEFER_TAIL), the all-reduce averages them, and ONE pass
+        # (lsr_language_tail) writes the gradients, steps and fills -- the N = 1 tail with the collective
+        # before it (LSR_PG_DEFER=0: the epilogue in the backward, the collective over .grad, then
+        # lsr_adam_fill_language)
+        defer = fill_after and self.bucket.direct and os.environ.get("LSR_PG_DEFER", "1") != "0"
+        self.defer = defer
+        self._tails = [None] * S
         comp_phase = (_native.forward_phase.COMPOSITE_FILLED if fused or fill_after
                       else _native.forward_phase.COMPOSITE)
         # fused: the first composite after a capture fills set 0's feature records itself (G_comp0, run
@@ -318,6 +327,10 @@ class PipelinedGraphStep:
         self.merged = merged
 
         def update_ctx(p):
+            if defer:  # this set's deferred tail (its arguments stay with the context)
+                self._tails[p] = _native.fused_update(self.optimizer, self.params[0], skip=self.overflow[p],
+                                                      fill=self._record_ptr((p + 1) % S), defer=True)
+                return self._tails[p]
             return _native.fused_update(self.optimizer, self.params[0], skip=self.overflow[p],
                                         fill=self._record_ptr((p + 1) % S)) if fused else _nullctx()
 
@@ -328,8 +341,11 @@ class PipelinedGraphStep:
             with update_ctx(p):  # the backward runs on its forward's stream (sa)
                 loss.backward(self._one)  # dL/dloss = 1 from a static tensor: no seed-fill kernel
                 if coll_in_graph:
-                    self.bucket.all_reduce(average=True, flag=self.overflow[p])
-                if self.bucket is None or coll_in_graph:
+                    self._collective(p)
+                if defer:
+                    if coll_in_graph:
+                        self._tails[p].run_tail()
+                elif self.bucket is None or coll_in_graph:
                     self.optimizer.step(skip=self.overflow[p], fill=adam_fill(p))
 
         geo_delay = int(os.environ.get("LSR_PG_GEO_DELAY_US", "0"))
@@ -379,7 +395,10 @@ class PipelinedGraphStep:
             if self.bucket is not None and not coll_in_graph:  # the all-reduce sits between two graphs
                 g = torch.cuda.CUDAGraph()
                 with graph_capture(g, stream=sa):
-                    self.optimizer.step(skip=self.overflow[p], fill=adam_fill(p))
+                    if defer:
+                        self._tails[p].run_tail()
+                    else:
+                        self.optimizer.step(skip=self.overflow[p], fill=adam_fill(p))
                 self.g_adam[p] = g
             self.static_loss[p] = loss.detach()  # the set's static loss tensor
             del loss
@@ -492,6 +511,14 @@ class PipelinedGraphStep:
         self.k += 1
         return self.static_loss[k % S]
 
+    def _collective(self, p):
+        """Set p's step collective (N > 1): the deferred backward's language partials, or the .grad
+        tensors, with the set's overflow flag."""
+        if self.defer:  # the partials carry the set's overflow flag themselves (include/lsr.h)
+            self.bucket.all_reduce_partials(self._tails[p].partials(), average=True)
+        else:
+            self.bucket.all_reduce(average=True, flag=self.overflow[p])
+
     def _record_ptr(self, p):
         """Device address of set p's per-Gaussian render records (include/lsr.h lsr_state_layout.record)."""
         geom = self.sets[p].tensors[("scratch", _native.LSR_BUF_GEOM)]
@@ -599,7 +626,7 @@ class PipelinedGraphStep:
             if self.g_adam[p] is not None:
                 for q, g in zip(self.params, self.grads[p]):
                     q.grad = g
-                self.bucket.all_reduce(average=True, flag=self.overflow[p])
+                self._collective(p)
                 self.g_adam[p].replay()
         self.ev_step[p].record(sa)
         # view k + S - 1's geometry into set r

@@ -7,7 +7,9 @@ Each rank trains BASELINE.json configs[3] (C4: 1M Gaussians, 1920x1080) on camer
 bench.py's synthetic language target of that view, in two step forms bench.py times at N > 1:
   eager            render + fused loss, backward, GradBucket.all_reduce (average), Adam;
   pipelined_graph  langsplat_amd.pipeline.PipelinedGraphStep(..., bucket=): the backward and Adam
-                   graphs of the view's buffer set with the all-reduce launched between them.
+                   graphs of the view's buffer set with the all-reduce launched between them (the
+                   deferred tail: the collective over the backward's language partials);
+  pipelined_graph_fill  the same with LSR_PG_DEFER=0 (the collective over .grad).
 After one step each rank writes OUT_DIR/rank<r>.pt with the averaged language gradient, the loss and
 the updated parameter of both forms."""
 import os
@@ -60,20 +62,26 @@ def main():
     torch.cuda.synchronize()
     out["eager"] = dict(grad=grad.cpu(), loss=loss.detach().cpu(), param=m._language_feature.detach().cpu())
     del m, opt, bucket, loss
-    # the pipelined graph form with the all-reduce between its backward and Adam graphs
-    m = frozen_model(g, dev)
-    opt = Adam([{"params": [m._language_feature], "lr": LR, "name": "language_feature"}], lr=0.0, eps=1e-8)
-    bucket = GradBucket([m._language_feature])
-    pg = PipelinedGraphStep(lambda: render(cam, m, _Pipe, bg, _Opt, language_target=(gt, mask))["language_l1"],
-                            [m._language_feature], opt, bucket=bucket).capture()
-    loss = pg.replay().clone()
-    pg.synchronize()
-    torch.cuda.synchronize()
-    assert pg.check()
-    pg.sync()
-    out["pipelined_graph"] = dict(grad=pg.last_grads()[0].detach().cpu(), loss=loss.cpu(),
-                                  param=m._language_feature.detach().cpu(),
-                                  step=int(opt.state[m._language_feature]["step"].item()))
+    # the pipelined graph form with the all-reduce between its backward and Adam graphs: the deferred
+    # tail (the collective over the backward's language partials, then one pass: gradients, Adam,
+    # fill; include/lsr.h LSR_BWD_DEFER_TAIL) and, LSR_PG_DEFER=0, the epilogue before the collective
+    for form, defer in (("pipelined_graph", "1"), ("pipelined_graph_fill", "0")):
+        os.environ["LSR_PG_DEFER"] = defer
+        m = frozen_model(g, dev)
+        opt = Adam([{"params": [m._language_feature], "lr": LR, "name": "language_feature"}], lr=0.0, eps=1e-8)
+        bucket = GradBucket([m._language_feature])
+        pg = PipelinedGraphStep(lambda: render(cam, m, _Pipe, bg, _Opt, language_target=(gt, mask))["language_l1"],
+                                [m._language_feature], opt, bucket=bucket).capture()
+        assert pg.defer == (defer == "1")
+        loss = pg.replay().clone()
+        pg.synchronize()
+        torch.cuda.synchronize()
+        assert pg.check()
+        pg.sync()
+        out[form] = dict(grad=pg.last_grads()[0].detach().cpu(), loss=loss.cpu(),
+                         param=m._language_feature.detach().cpu(),
+                         step=int(opt.state[m._language_feature]["step"].item()))
+        del pg, m, opt, bucket
     torch.save(out, os.path.join(out_dir, f"rank{rank}.pt"))
     torch.distributed.barrier()
     torch.distributed.destroy_process_group()

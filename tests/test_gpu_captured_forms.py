@@ -276,7 +276,7 @@ def test_graphed_step_over_a_view_sequence(monkeypatch):
 
 
 @pytest.mark.parametrize("sets,wait,bucket", [(2, True, False), (3, True, False), (3, False, False),
-                                              (3, True, True), (2, True, True)])
+                                              (3, True, "defer"), (2, True, "defer"), (3, True, "fill")])
 def test_pipelined_graph_over_a_view_sequence(sets, wait, bucket, monkeypatch):
     """PipelinedGraphStep with one ViewSlot per buffer set: capture(views=the first S - 1 views),
     replay(next_view=the view S - 1 ahead); every replay composites its own view's geometry with its
@@ -285,8 +285,12 @@ def test_pipelined_graph_over_a_view_sequence(sets, wait, bucket, monkeypatch):
     losses (valid after synchronize()) and the final state reproduce the eager loop.  bucket (round
     6): the N > 1 structure on one process (a GradBucket, no process group: its all-reduce is a
     no-op) -- the backward and the update as two graphs, the update filling the next set's records
-    (lsr_adam_fill_language), the first composite refilled from the parameter."""
+    (lsr_adam_fill_language), the first composite refilled from the parameter.  "defer" (the default
+    since ABI 16): the backward leaves the language partials, the collective reduces them and ONE
+    tail pass (lsr_language_tail) writes the gradients, steps and fills; "fill" (LSR_PG_DEFER=0): the
+    epilogue in the backward, then lsr_adam_fill_language."""
     monkeypatch.setenv("LANGSPLAT_AMD_FUSED", "1")
+    monkeypatch.setenv("LSR_PG_DEFER", "0" if bucket == "fill" else "1")
     g = make_gaussians(CONFIGS["C4"]["P"], seed=0)
     views = _c4_views()
     losses_e, se, (Rc, Ec) = _eager_sequence(g, views)
@@ -296,7 +300,8 @@ def test_pipelined_graph_over_a_view_sequence(sets, wait, bucket, monkeypatch):
     pg = PipelinedGraphStep(_slot_forward(m), [m._language_feature], opt, slots=slots,
                             bucket=GradBucket([m._language_feature]) if bucket else None)
     pg.capture(Rc, Ec, views=views[:sets - 1])
-    assert pg.fill_after == bucket and (pg.g_adam[0] is not None) == bucket
+    assert pg.fill_after == bool(bucket) and (pg.g_adam[0] is not None) == bool(bucket)
+    assert pg.defer == (bucket == "defer")
     L = sets - 1
     losses = []
     for k in range(len(views)):
@@ -377,13 +382,16 @@ def _assert_bit_equal(a, b):
     assert a[3] == b[3]
 
 
-@pytest.mark.parametrize("form", ["graph", "pipelined2", "pipelined3"])
+@pytest.mark.parametrize("form", ["graph", "pipelined2", "pipelined3", "pipelined3_defer", "pipelined3_fill"])
 def test_overflowed_view_is_a_noop_for_the_optimizer(form, monkeypatch):
     """Capacities from the far views (headroom 1.0); the near view overflows: its replay leaves the
     language feature, both Adam moments and the device step count bit-unchanged, its gradient is zero
     (nothing was rasterized), the optimizer counts one skipped step, check() re-captures -- and the
-    parameters then match the eager loop over the sequence WITHOUT that view."""
+    parameters then match the eager loop over the sequence WITHOUT that view.  _defer / _fill: the
+    N > 1 structure (a GradBucket without a process group) with the deferred tail, whose skip word
+    travels in the reduced partials (include/lsr.h LSR_BWD_DEFER_TAIL), or with LSR_PG_DEFER=0."""
     monkeypatch.setenv("LANGSPLAT_AMD_FUSED", "1")
+    monkeypatch.setenv("LSR_PG_DEFER", "0" if form.endswith("_fill") else "1")
     P = 20000
     g = make_gaussians(P, seed=5, scale_range=(0.005, 0.04))
     views = _overflow_views()
@@ -430,8 +438,10 @@ def test_overflowed_view_is_a_noop_for_the_optimizer(form, monkeypatch):
     else:
         S = 2 if form == "pipelined2" else 3
         slots = [ViewSlot(*views[0]) for _ in range(S)]
-        pg = PipelinedGraphStep(fwd, [m._language_feature], opt, slots=slots, headroom=1.0)
+        bucket = GradBucket([m._language_feature]) if "_" in form else None
+        pg = PipelinedGraphStep(fwd, [m._language_feature], opt, slots=slots, headroom=1.0, bucket=bucket)
         pg.capture(R, E, views=views[:S - 1])
+        assert pg.defer == form.endswith("_defer")
         L = S - 1
         for k in range(len(views)):
             snaps.append(_snap(m, opt))

@@ -31,7 +31,7 @@ def test_library_loads_and_exports_every_declared_symbol():
     for name in _declared_functions():
         assert hasattr(lib, name), name
         assert name in _native.SIGNATURES, f"ctypes binding misses {name}"
-    assert lib.lsr_abi_version() == _native.ABI_VERSION == 15
+    assert lib.lsr_abi_version() == _native.ABI_VERSION == 16
 
 
 def test_header_constants_match_the_python_side():
@@ -60,6 +60,9 @@ def test_sizes_and_layout_are_consistent():
     assert lib.lsr_geom_bytes(2 * P, W, H) > lib.lsr_geom_bytes(P, W, H)
     # the geometry buffer carries one fused-loss word per tile: it grows with the image
     assert lib.lsr_geom_bytes(P, 1920, 1080) > lib.lsr_geom_bytes(P, W, H)
+    # the language step's gradient records (ABI 16: the deferred tail's all-reduce reads their first 3 P
+    # floats as a (P, 3) view): 4-B aligned floats inside the geometry buffer
+    assert lay["grad_records"] % 256 == 0 and lay["grad_records"] + 20 * P <= lib.lsr_geom_bytes(P, W, H)
 
 
 def test_invalid_arguments_report_errors_without_gpu():
@@ -133,6 +136,30 @@ def test_backward_fused_update_validation_without_gpu():
     assert call(dL_dout_color=dummy) != 0 and "fused update" in _native.last_error()
     assert call(update_step_dev=None) != 0 and "fused update" in _native.last_error()
     assert call(with_update=False, fill_record=dummy) != 0 and "need update" in _native.last_error()
+    # LSR_BWD_DEFER_TAIL (ABI 16) is a form of the fused update
+    assert call(with_update=False, flags=_native.BWD_DEFER_TAIL) != 0 and "needs update" in _native.last_error()
+    assert call(geometry=True, flags=_native.BWD_DEFER_TAIL) != 0 and "fused update" in _native.last_error()
+
+    def tail(**kw):
+        a = _native.LsrBackwardArgs()
+        a.P, a.M, a.num_rendered = P, 1, 16
+        a.radii = a.geom_buffer = dummy
+        a.language_feature = ctypes.c_void_p(256)
+        a.dL_dlanguage_feature = dummy
+        a.raw = _native.RAW_LANGUAGE
+        t = _native.LsrAdamTensor(3 * P, 256, None, 512, 768, 0.01, 0.9, 0.999, 1e-15, 0)
+        a.update = ctypes.pointer(t)
+        a.update_step_dev = dummy
+        for k, v in kw.items():
+            setattr(a, k, v)
+        return lib.lsr_language_tail(ctypes.byref(s), ctypes.byref(a), None)
+
+    assert lib.lsr_language_tail(None, None, None) != 0 and "null" in _native.last_error()
+    assert tail(update=None) != 0 and "fused update" in _native.last_error()
+    assert tail(raw=0) != 0 and "fused update" in _native.last_error()
+    assert tail(dL_dlanguage_feature=None) != 0 and "fused update" in _native.last_error()
+    assert tail(geom_buffer=None) != 0 and "forward state" in _native.last_error()
+    assert tail(fill_record=ctypes.c_void_p(264)) != 0 and "16-byte" in _native.last_error()
 
 
 def test_spin_limit_knob_round_trips_without_gpu():

@@ -48,9 +48,16 @@ def run(mode, steps=30):
         fwd_bwd()
         optim.step()
         optim.zero_grad(set_to_none=True)
-        # ST_BUCKET=1: the N > 1 structure (a GradBucket; no process group, so its all-reduce is a no-op)
+        # ST_BUCKET=1: the N > 1 structure (a GradBucket; no process group, so its all-reduce is a no-op);
+        # ST_BUCKET=rccl: the same around a one-rank RCCL group (LSR_GRAPH_COLLECTIVE=0: the collective
+        # launched between the graphs, as at N > 1)
         from langsplat_amd.distributed import GradBucket
-        bucket = GradBucket([model._language_feature]) if os.environ.get("ST_BUCKET") == "1" else None
+        if os.environ.get("ST_BUCKET") == "rccl":
+            import torch.distributed as dist
+            from langsplat_amd import launch
+            dist.init_process_group("nccl", rank=0, world_size=1,
+                                    init_method=f"tcp://127.0.0.1:{launch.free_port()}")
+        bucket = GradBucket([model._language_feature]) if os.environ.get("ST_BUCKET") in ("1", "rccl") else None
         pg = PipelinedGraphStep(lambda: bench.render(cam, model, bench.Pipe, bg, bench.Opt,
                                                      language_target=(gt, mask))["language_l1"],
                                 [model._language_feature], optim, bucket=bucket).capture()
