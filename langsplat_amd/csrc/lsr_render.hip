@@ -500,6 +500,9 @@ __device__ float render_empty_tiles(const RenderParams& p, int j, int M)
 #ifndef LSR_FWD_PREFETCH  // 1: the next batch's records are gathered during the walk
 #define LSR_FWD_PREFETCH 0
 #endif
+#ifndef LSR_BWD_WORK_ORDER  // 1: the backward's items ordered by the forward's walk counts, 0: by entries
+#define LSR_BWD_WORK_ORDER 1
+#endif
 #ifndef LSR_FWD_STATE_SKIP  // 1: split-replay states stored only for the pixels the backward starts from them
 #define LSR_FWD_STATE_SKIP 1
 #endif
@@ -519,6 +522,12 @@ __global__ __launch_bounds__(kTilePixels, LSR_FWD_WAVES) void k_render_forward(R
     // reads the next step's one step ahead (up to slot n + 7)
     __shared__ __attribute__((aligned(8))) uint16_t sL[kThreads / 64][kThreads + 8];
     __shared__ uint32_t s_last;
+    // LSR_BWD_WORK_ORDER: per wave, the list slots its walk visited in batches 0, 1, 2 and from 3 on
+    // (one batch = one split-replay chunk): what the backward's item of that chunk visits in this wave
+    constexpr bool kWorkOrder = LSR_BWD_WORK_ORDER && kSplitChunk == kThreads;
+    __shared__ uint32_t s_walk[kWorkOrder ? kThreads / 64 : 1][kSplitItems];
+    uint32_t wk0 = 0, wk1 = 0, wk2 = 0, wk3 = 0;  // (wave-uniform)
+    uint32_t bi = 0;                              // batch index
 
     const int T = p.gx * p.gy;
     if (p.zero_records) {  // the backward's gradient records: stores beside the VALU-bound walk
@@ -760,7 +769,22 @@ __global__ __launch_bounds__(kTilePixels, LSR_FWD_WAVES) void k_render_forward(R
         }
         if (mid) nrec++;
 #endif
+        if (kWorkOrder) {
+            const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(min(i, n));
+            if (bi == 0) wk0 = wv;
+            else if (bi == 1) wk1 = wv;
+            else if (bi == 2) wk2 = wv;
+            else wk3 += wv;
+            bi++;
+        }
         if (lo != 0xFFFFFFFFu) q.last16 = lb16 + lo;
+    }
+    if (kWorkOrder && lane == 0) {
+        static_assert(kSplitItems == 4, "four walk counters per wave");
+        s_walk[wave][0] = wk0;
+        s_walk[wave][1] = wk1;
+        s_walk[wave][2] = wk2;
+        s_walk[wave][3] = wk3;
     }
     const uint32_t qlast = q.last16 >> 4;
     // the tile's replay length, for the backward's launch order
@@ -777,7 +801,27 @@ __global__ __launch_bounds__(kTilePixels, LSR_FWD_WAVES) void k_render_forward(R
     // the backward's items into the longest-first class lists: the tile's full 256-entry chunks with
     // ONE returning atomic on their class (+nsplit), its last chunk with another, in parallel (thread
     // 1): an atomic per chunk put every heavy tile's chunks on one hot counter across the XCDs
-    if (t < 2 && p.sched_counts && maxl > 0 && !p.no_bwd) {
+    if (kWorkOrder && p.sched_counts && maxl > 0 && !p.no_bwd) {
+        // one item per thread t <= nsplit, classed by its work: the walk's visits in the chunk's batch
+        // (the last item: its batches' visits summed) in the wave that visited most, plus a fixed share
+        // for its record loads and flush.  The class lists stay longest first by what the backward
+        // will do, not by entry counts (a chunk whose pixels are mostly done replays little).
+        if (t == 0 && p.split_pool) p.split_desc[tile] = make_uint4(nsplit, maxl, 0u, 0u);
+        if (t <= (int)nsplit) {
+            uint32_t w = 0;
+            for (int wv = 0; wv < kThreads / 64; wv++) {
+                uint32_t v = 0;
+                if (t < (int)nsplit) {
+                    v = s_walk[wv][t];
+                } else {
+                    for (int k = t; k < kSplitItems; k++) v += s_walk[wv][k];
+                }
+                w = max(w, v);
+            }
+            schedule_tile(p.sched_counts + kCntBwdClass, p.sched_lists + (size_t)kWorkClasses * T,
+                          kSplitItems * T, kSplitItems * tile + t, 32u + w);
+        }
+    } else if (t < 2 && p.sched_counts && maxl > 0 && !p.no_bwd) {
         uint32_t* counts = p.sched_counts + kCntBwdClass;
         uint32_t* lists = p.sched_lists + (size_t)kWorkClasses * T;
         const size_t stride = (size_t)kSplitItems * T;
