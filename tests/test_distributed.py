@@ -183,6 +183,17 @@ def _flag_worker(rank, world, port, out_dir):
                 bucket.all_reduce(average=True, flag=flag)
                 out[f"{mode}{step}_grad"] = lang.grad.clone()
                 out[f"{mode}{step}_flag"] = int(flag.item())
+        # the deferred language tail (include/lsr.h LSR_BWD_DEFER_TAIL): ONE all-reduce over the backward's
+        # 3 P language partials followed by the skip word, which carries the overflow flag itself
+        bucket = GradBucket([lang])
+        from langsplat_amd import rccl
+        assert not rccl.direct_enabled()  # gloo: torch.distributed's all-reduce (the direct one is RCCL's)
+        for step, over in enumerate((None, world - 1)):
+            part = torch.full((3 * 150 + 1,), float(rank + 1))
+            part[-1:].view(torch.int32)[0] = 0x3F800000 if rank == over else 0
+            bucket.all_reduce_partials(part, average=True)
+            out[f"partials{step}_grad"] = part[:-1].clone()
+            out[f"partials{step}_flag"] = int(part[-1:].view(torch.int32).item())
         torch.save(out, os.path.join(out_dir, f"flag_{rank}.pt"))
     finally:
         dist.destroy_process_group()
@@ -192,7 +203,8 @@ def _flag_worker(rank, world, port, out_dir):
 def test_overflow_flag_rides_the_gradient_collective(tmp_path, world):
     """a view over capacity on ONE rank sets the flag on EVERY rank (the flag is
     all-reduced in the same collective as the gradients), so every rank skips the optimizer step and
-    the ranks stay identical; the gradients are averaged as without the flag (direct and flat)."""
+    the ranks stay identical; the gradients are averaged as without the flag (direct and flat).  Also
+    the deferred tail's collective (round 6): the language partials with the skip word after them."""
     port = _free_port()
     mp.spawn(_flag_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True)
     outs = [torch.load(tmp_path / f"flag_{r}.pt", weights_only=True) for r in range(world)]
@@ -203,6 +215,9 @@ def test_overflow_flag_rides_the_gradient_collective(tmp_path, world):
             assert o[f"{mode}1_flag"] != 0  # non-zero as an int: Adam's skip test
             for step in (0, 1):
                 torch.testing.assert_close(o[f"{mode}{step}_grad"], torch.full((150, 3), mean))
+        assert o["partials0_flag"] == 0 and o["partials1_flag"] != 0
+        for step in (0, 1):
+            torch.testing.assert_close(o[f"partials{step}_grad"], torch.full((450,), mean))
     for r in range(1, world):
         for k, v in outs[r].items():
             assert (torch.equal(v, outs[0][k]) if torch.is_tensor(v) else v == outs[0][k]), k
