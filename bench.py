@@ -771,11 +771,15 @@ def main():
                                    "beside this view's backward" + (", RCCL all-reduce" if world > 1 else "")
                                    + " and Adam)",
                       "pipelined_graph": "HIP graphs on two streams: this view's compositing + loss, backward, "
-                                         + ((f"{backend} all-reduce ("
+                                         + ((f"{backend} all-reduce of the language partials and skip flag ("
                                              + ("in the graph" if collective_capturable() else "between two graphs")
-                                             + "), ") if world > 1 else "") +
-                                         "Adam on one, the next view's geometry (forward split in two calls) on "
-                                         "the other"}[best],
+                                             + ("; RCCL on the step's stream" if rccl.direct_enabled() else "")
+                                             + "), ") if world > 1 and os.environ.get("LSR_PG_DEFER", "1") != "0"
+                                            else (f"{backend} all-reduce ("
+                                                  + ("in the graph" if collective_capturable() else "between two graphs")
+                                                  + "), ") if world > 1 else "") +
+                                         "gradient + Adam + next records' fill pass on one, the next view's "
+                                         "geometry (forward split in two calls) on the other"}[best],
         "pipelined_graph_rotation": pg_rot,
         "pipelined_graph_error": pg_error,
         "ms_per_step_forms": {n: (round(1000.0 * v / args.steps, 4) if v < 1e29 else None) for n, v in times.items()},
