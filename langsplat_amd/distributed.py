@@ -218,12 +218,15 @@ class GradBucket:
         nccl = dist.get_backend(group) == "nccl"
         if flag is not None and (flag.dtype != torch.int32 or flag.numel() != 1 or flag.device != buf.device):
             raise ValueError("GradBucket.all_reduce: flag must be a one-element int32 tensor on the bucket's device")
+        comm = None
         if nccl and group is None and rccl.direct_enabled(group) and (
                 rccl._default is not None or not torch.cuda.is_current_stream_capturing()):
             # RCCL on the caller's stream (langsplat_amd.rccl: no round trip through torch's internal
             # stream); its communicator is built at the first (eager) reduction
-            rccl.default_communicator().all_reduce([buf] + ([flag.view(torch.float32)] if flag is not None else []),
-                                                   op="avg" if average else "sum")
+            comm = rccl.default_communicator()
+        if comm is not None:
+            comm.all_reduce([buf] + ([flag.view(torch.float32)] if flag is not None else []),
+                            op="avg" if average else "sum")
             self._divided_by = world if average else 1
             return
         # RCCL's ncclAvg: the division is part of the collective (no separate scaling kernel)

@@ -115,20 +115,26 @@ class Communicator:
 
 
 _default: Optional[Communicator] = None
+_failed: Optional[str] = None  # why the direct communicator could not be built (then torch's path is used)
 
 
 def direct_enabled(group=None) -> bool:
-    """The direct communicator is used for a group whose backend is "nccl" unless LSR_DIRECT_RCCL=0."""
-    return (os.environ.get("LSR_DIRECT_RCCL", "1") != "0" and dist.is_available() and dist.is_initialized()
-            and dist.get_backend(group) == "nccl")
+    """The direct communicator is used for a group whose backend is "nccl" unless LSR_DIRECT_RCCL=0
+    (or it failed to build on this process)."""
+    return (_failed is None and os.environ.get("LSR_DIRECT_RCCL", "1") != "0" and dist.is_available()
+            and dist.is_initialized() and dist.get_backend(group) == "nccl")
 
 
-def default_communicator() -> Communicator:
+def default_communicator() -> Optional[Communicator]:
     """The world's direct communicator, built on first use (a collective: every rank's first
-    GradBucket reduction happens at the same point of the step)."""
-    global _default
-    if _default is None:
-        _default = Communicator()
+    GradBucket reduction happens at the same point of the step).  None if it could not be built
+    (e.g. the library lacks a symbol: every rank fails alike and keeps torch.distributed's path)."""
+    global _default, _failed
+    if _default is None and _failed is None:
+        try:
+            _default = Communicator()
+        except (OSError, AttributeError, RuntimeError) as e:  # noqa: PERF203
+            _failed = f"{type(e).__name__}: {e}"
     return _default
 
 

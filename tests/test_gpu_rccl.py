@@ -65,6 +65,18 @@ lang.grad = None  # a rank whose parameter got no gradient joins with zeros
 direct.all_reduce(average=False)
 torch.cuda.synchronize()
 assert lang.grad is not None and not lang.grad.any()
+# the reductions above went through the direct communicator (langsplat_amd.rccl: RCCL on the caller's
+# stream), unless LSR_DIRECT_RCCL=0; the deferred tail's partials + skip word: one collective
+from langsplat_amd import rccl
+assert (rccl._default is not None) == (os.environ.get("LSR_DIRECT_RCCL", "1") != "0"), rccl._failed
+part = torch.randn((3 * P + 1,), generator=g).to(dev)
+part[-1:].view(torch.int32)[0] = 0x3F800000
+ref = part.clone()
+direct.all_reduce_partials(part, average=True)
+torch.cuda.synchronize()
+assert torch.equal(part, ref)
+torch.cuda.synchronize()
+rccl.destroy_default()
 dist.destroy_process_group()
 print("RCCL_OK")
 """
@@ -86,7 +98,11 @@ def _run_child(script, timeout=110):
     assert r.returncode == 0 and "RCCL_OK" in r.stdout, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
 
 
-def test_rccl_bucket_with_densification_statistics():
+@pytest.mark.parametrize("direct", ["1", "0"])
+def test_rccl_bucket_with_densification_statistics(direct, monkeypatch):
+    """direct: the step's collectives through langsplat_amd.rccl (RCCL on the caller's stream) or,
+    LSR_DIRECT_RCCL=0, through torch.distributed."""
+    monkeypatch.setenv("LSR_DIRECT_RCCL", direct)
     _run_child(CHILD)
 
 
