@@ -123,7 +123,7 @@ def test_reset_opacity_matches_the_reference_ops():
     _reference_reset_opacity(ref_m, ref_opt)
     assert m._opacity is not old and m._opacity.grad is None and m._opacity.requires_grad
     assert torch.equal(m._opacity.detach(), ref_m._opacity.detach())
-    assert float(torch.sigmoid(m._opacity).max()) <= 0.01 + 1e-7
+    assert float(torch.sigmoid(m._opacity.detach()).max()) <= 0.01 + 1e-7
     st = opt.state[m._opacity]
     assert old not in opt.state and not st["exp_avg"].any() and not st["exp_avg_sq"].any()
     assert int(st["step"].item()) == int(ref_opt.state[ref_m._opacity]["step"].item()) == 1
