@@ -9,7 +9,9 @@ bench.py's synthetic language target of that view, in two step forms bench.py ti
   pipelined_graph  langsplat_amd.pipeline.PipelinedGraphStep(..., bucket=): the backward and Adam
                    graphs of the view's buffer set with the all-reduce launched between them (the
                    deferred tail: the collective over the backward's language partials);
-  pipelined_graph_fill  the same with LSR_PG_DEFER=0 (the collective over .grad).
+  pipelined_graph_fill  the same with LSR_PG_DEFER=0 (the collective over .grad);
+  multi_step       four steps of the eager loop and of the deferred-tail pipelined graph at Adam eps
+                   1e-15, with the entries above the float-atomic noise floor.
 After one step each rank writes OUT_DIR/rank<r>.pt with the averaged language gradient, the loss and
 the updated parameter of both forms."""
 import os
@@ -82,6 +84,53 @@ def main():
                          param=m._language_feature.detach().cpu(),
                          step=int(opt.state[m._language_feature]["step"].item()))
         del pg, m, opt, bucket
+    # K steps at the reference's Adam eps 1e-15 (scene/gaussian_model.py:229): the eager loop and the
+    # deferred-tail pipelined graph, with the entries whose averaged gradient stays above the
+    # float-atomic noise floor at every step (tests/test_gpu_captured_forms.py
+    # test_pipelined_graph_multi_step_at_reference_eps explains the floor)
+    os.environ["LSR_PG_DEFER"] = "1"
+    K = 4
+
+    def adam15(m):
+        return Adam([{"params": [m._language_feature], "lr": LR, "name": "language_feature"}], lr=0.0, eps=1e-15)
+
+    def fwd(m):
+        return render(cam, m, _Pipe, bg, _Opt, language_target=(gt, mask))["language_l1"]
+    mn = frozen_model(g, dev)
+    runs = []
+    for _ in range(2):
+        mn._language_feature.grad = None
+        fwd(mn).backward()
+        runs.append(mn._language_feature.grad.detach().clone())
+    floor = 16.0 * max(float((runs[0] - runs[1]).abs().max()), 1e-30)
+    del mn, runs
+    me = frozen_model(g, dev)
+    oe = adam15(me)
+    be = GradBucket([me._language_feature])
+    above = None
+    for _ in range(K):
+        fwd(me).backward()
+        be.all_reduce(average=True)
+        gr = me._language_feature.grad.detach().abs() > floor
+        above = gr if above is None else above & gr
+        oe.step()
+        oe.zero_grad(set_to_none=True)
+    st = oe.state[me._language_feature]
+    ref = (me._language_feature.detach().cpu(), st["exp_avg"].cpu(), st["exp_avg_sq"].cpu())
+    mg = frozen_model(g, dev)
+    og = adam15(mg)
+    pg = PipelinedGraphStep(lambda: fwd(mg), [mg._language_feature], og, bucket=GradBucket([mg._language_feature])).capture()
+    assert pg.defer
+    for _ in range(K):
+        pg.replay()
+    pg.synchronize()
+    torch.cuda.synchronize()
+    assert pg.check()
+    pg.sync()
+    st = og.state[mg._language_feature]
+    out["multi_step"] = dict(eager=ref, graph=(mg._language_feature.detach().cpu(), st["exp_avg"].cpu(),
+                                               st["exp_avg_sq"].cpu()),
+                             above=above.cpu(), step=int(st["step"].item()), floor=floor)
     torch.save(out, os.path.join(out_dir, f"rank{rank}.pt"))
     torch.distributed.barrier()
     torch.distributed.destroy_process_group()
