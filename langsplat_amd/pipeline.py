@@ -603,8 +603,10 @@ class PipelinedGraphStep:
             # ~35 us of idle stream A per step at C3).  It waits instead for the
             # caller's work up to the start of replay k - S + 1, long done: the caller's uses of the
             # loss of replay k - S (whose tensor composite k rewrites) precede that.  The first
-            # S - 1 replays after a capture wait for the caller's stream itself.
-            self.ev_cur[self.k % S].record(cur)
+            # S - 1 replays after a capture wait for the caller's stream itself.  (This replay's own
+            # mark on the caller's stream, ev_cur[k], is recorded after the step's launch below: the
+            # caller's stream gets nothing from replay() before it, and a synced loop's stream A idles
+            # until the launch.)
             if self._since_capture < S - 1:
                 sa.wait_stream(cur)
             else:
@@ -628,6 +630,8 @@ class PipelinedGraphStep:
                     q.grad = g
                 self._collective(p)
                 self.g_adam[p].replay()
+        if not fast:
+            self.ev_cur[self.k % S].record(cur)
         self.ev_step[p].record(sa)
         # view k + S - 1's geometry into set r
         after = self.ev_comp[p] if self.geo_after_fwd and not self.merged else None
