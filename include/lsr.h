@@ -397,6 +397,14 @@ int32_t lsr_debug_clock_probe(uint64_t* out_device, void* stream);
  * 1e6) of the constant 100 MHz counter -- a delay between two launches of one stream (the
  * pipelined step's stream phase, LSR_PG_GEO_DELAY_US). */
 int32_t lsr_debug_delay(uint32_t microseconds, void* stream);
+/* Host runtime helper (round 6): `stream` waits for each of the n_waits events, then the
+ * instantiated graph `graph_exec` (a hipGraphExec_t) is launched on it and, if record_event is not
+ * null, that event recorded after it -- the stream-A half of a pipelined step's replay in one call
+ * (langsplat_amd/pipeline.py PipelinedGraphStep.replay), replacing torch's stream context, event
+ * waits and CUDAGraph.replay() in Python (~8 us of host time before every synced step's launch,
+ * profiles/r06_sync_gap.txt).  No reference counterpart: the reference has no captured step. */
+int32_t lsr_graph_launch(void* graph_exec, void* stream, void* const* wait_events, int32_t n_waits,
+                         void* record_event);
 
 /* ---- the language-feature loss around the rasterizer ----------------
  *

@@ -129,6 +129,7 @@ SIGNATURES = {
     "lsr_debug_bucket_timeline": (ctypes.c_int32, [ctypes.POINTER(ctypes.c_uint32), ctypes.c_int32]),
     "lsr_debug_clock_probe": (ctypes.c_int32, [_vp, _vp]),
     "lsr_debug_delay": (ctypes.c_int32, [ctypes.c_uint32, _vp]),
+    "lsr_graph_launch": (ctypes.c_int32, [_vp, _vp, ctypes.POINTER(_vp), ctypes.c_int32, _vp]),
     "lsr_debug_render_stats": (ctypes.c_int32, [ctypes.POINTER(ctypes.c_uint64), ctypes.c_int32]),
     "lsr_debug_render_timeline": (ctypes.c_int32, [ctypes.c_int32, ctypes.POINTER(ctypes.c_uint32), ctypes.c_int32]),
     "lsr_profile_enable": (ctypes.c_int32, [ctypes.c_int32]),
@@ -182,6 +183,27 @@ def last_error() -> str:
 def _check(status: int, what: str):
     if status != 0:
         raise RuntimeError(f"{what} failed (status {status}): {last_error()}")
+
+
+class GraphLauncher:
+    """One captured graph's launch on one stream after given events, with an event recorded after it
+    (lsr_graph_launch): the raw handles are read once, so a call costs one ctypes round trip instead
+    of torch's stream context, event waits and CUDAGraph.replay() (pipeline.py's synced replays)."""
+
+    def __init__(self, graph: "torch.cuda.CUDAGraph", stream: "torch.cuda.Stream", waits, record):
+        self._lib = load()
+        self._exec = _vp(graph.raw_cuda_graph_exec())
+        if not self._exec.value:
+            raise RuntimeError("GraphLauncher: the graph has no instantiated executable")
+        self._stream = _vp(stream.cuda_stream)
+        self._events = list(waits) + [record]  # kept alive with their handles
+        self._waits = (_vp * max(1, len(waits)))(*[e.cuda_event for e in waits])
+        self._n = len(waits)
+        self._record = _vp(record.cuda_event) if record is not None else None
+
+    def __call__(self):
+        _check(self._lib.lsr_graph_launch(self._exec, self._stream, self._waits, self._n, self._record),
+               "lsr_graph_launch")
 
 
 def _ptr(t: Optional[torch.Tensor]):

@@ -902,6 +902,23 @@ int32_t lsr_debug_delay(uint32_t microseconds, void* stream_ptr)
     return LSR_OK;
 }
 
+int32_t lsr_graph_launch(void* graph_exec, void* stream_ptr, void* const* wait_events, int32_t n_waits,
+                         void* record_event)
+{
+    if (!graph_exec || n_waits < 0 || (n_waits > 0 && !wait_events))
+        return fail(LSR_ERR_INVALID, "lsr_graph_launch: invalid argument");
+    hipStream_t stream = reinterpret_cast<hipStream_t>(stream_ptr);
+    hipError_t e;
+    for (int32_t i = 0; i < n_waits; i++)
+        if ((e = hipStreamWaitEvent(stream, reinterpret_cast<hipEvent_t>(wait_events[i]), 0)) != hipSuccess)
+            return fail(LSR_ERR_HIP, "lsr_graph_launch: stream wait", e);
+    if ((e = hipGraphLaunch(reinterpret_cast<hipGraphExec_t>(graph_exec), stream)) != hipSuccess)
+        return fail(LSR_ERR_HIP, "lsr_graph_launch: graph launch", e);
+    if (record_event && (e = hipEventRecord(reinterpret_cast<hipEvent_t>(record_event), stream)) != hipSuccess)
+        return fail(LSR_ERR_HIP, "lsr_graph_launch: event record", e);
+    return LSR_OK;
+}
+
 int32_t lsr_mark_visible(int32_t P, const float* means3D, const float* viewmatrix, const float* projmatrix,
                          uint8_t* visible, void* stream_ptr)
 {

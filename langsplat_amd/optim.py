@@ -94,9 +94,10 @@ class Adam(torch.optim.Optimizer):
         return 0 if self._step_dev is None else int(self._step_dev[_native.ADAM_WORD_SKIPPED].item())
 
     @torch.no_grad()
-    def sync_lr(self):
+    def sync_lr(self, stream=None):
         """Before a replay of a captured step: the groups' current learning rates into the device
-        block (a small host-to-device copy on the current stream, only when one changed)."""
+        block (a small host-to-device copy on the current stream, or on `stream`, only when one
+        changed)."""
         if self._step_dev is None:
             return
         self._dev_ahead = True
@@ -107,7 +108,11 @@ class Adam(torch.optim.Optimizer):
             return
         src = torch.tensor(lrs, dtype=torch.float64).view(torch.int64).pin_memory()
         w = _native.ADAM_WORD_LR
-        self._step_dev[w:w + len(lrs)].copy_(src, non_blocking=True)
+        if stream is None:
+            self._step_dev[w:w + len(lrs)].copy_(src, non_blocking=True)
+        else:
+            with torch.cuda.stream(stream):
+                self._step_dev[w:w + len(lrs)].copy_(src, non_blocking=True)
         self._lr_dev = lrs
 
     def _register_fused(self, group_index: int):

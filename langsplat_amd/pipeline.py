@@ -42,6 +42,9 @@ from .graph import (_as_view, _fused_tail_enabled, _nullctx, capture_key, curren
                     release_stale_accumulators, resolve_bucket)
 
 
+# LSR_PG_NATIVE_LAUNCH=0: every replay through torch's stream context and CUDAGraph.replay() (A/B)
+_NATIVE_LAUNCH = os.environ.get("LSR_PG_NATIVE_LAUNCH", "1") != "0"
+
 class ViewPipeline:
     def __init__(self, optimizer, bucket=None, device=None):
         """optimizer: steps the trainable parameters; bucket: a langsplat_amd.distributed.GradBucket
@@ -413,6 +416,7 @@ class PipelinedGraphStep:
         self.ev_cur = [torch.cuda.Event() for _ in range(S)]
         self._since_capture = 0
         self._fast = False
+        self._launchers = {}  # (set, fast) -> _native.GraphLauncher (replay's steady state)
         self._refill = fill_after  # the first composite's records: from the parameter (replay)
         self.captures += 1
         return self
@@ -541,6 +545,23 @@ class PipelinedGraphStep:
             self.g_geo[r].replay()
         self.ev_geo[r].record(sb)
 
+    def _launcher(self, p, fast):
+        """Set p's steady-state stream-A launch (replay): after the caller's mark of replay k - S + 1
+        (ev_cur[p + 1], not in the fast form) and set p's geometry, the step graph, then ev_step[p].
+        None until every one of those events exists (torch creates an event at its first record)."""
+        if not _NATIVE_LAUNCH:
+            return None
+        key = (p, fast)
+        fn = self._launchers.get(key)
+        if fn is None:
+            S = self.S
+            waits = ([] if fast else [self.ev_cur[(p + 1) % S]]) + [self.ev_geo[p]]
+            if any(e.cuda_event == 0 for e in waits + [self.ev_step[p]]):
+                return None
+            fn = _native.GraphLauncher(self.g_comp[p], self.streams[0], waits, self.ev_step[p])
+            self._launchers[key] = fn
+        return fn
+
     def replay(self, next_view=None, wait: bool = True) -> torch.Tensor:
         """One language step of the view loaded S - 1 replays ago (or at capture); next_view
         (camera, gt, mask) is the view of the replay S - 1 ahead (ViewSlots only; None: the view of
@@ -563,20 +584,22 @@ class PipelinedGraphStep:
             return self._replay_rotation(next_view, wait)
         S = self.S
         sa, sb = self.streams
-        cur = torch.cuda.current_stream()
         p = self.k % S
         r = (self.k + S - 1) % S
         if 0 < self.ahead < S and self._since_capture >= self.ahead:
             # host throttle: at most `ahead` steps enqueued beyond the running one (the queues stay
             # short; a step's stream-A work still follows the previous step without a host gap)
             self.ev_step[(self.k - self.ahead) % S].synchronize()
+        fast = not wait and self._since_capture >= S - 1
+        if wait and self._fast:  # back from fast replays: the lagged events were not recorded
+            self._since_capture = 0
+        # the caller's stream object (~2.4 us of host time) only where it is used before the launch
+        cur = torch.cuda.current_stream() if (next_view is not None or not self.primed
+                                               or self._since_capture < S - 1) else None
         if not self.primed:  # the first S - 1 views' geometry (nothing ran since the capture)
             for j in range(S - 1):
                 self._geometry((self.k + j) % S)
             self.primed = True
-        fast = not wait and self._since_capture >= S - 1
-        if wait and self._fast:  # back from fast replays: the lagged events were not recorded
-            self._since_capture = 0
         self._fast = fast
         # set r's last reader was step k - 1 (the view S - 1 ahead goes there)
         released = self.ev_step[(self.k - 1) % S] if self.k > 0 else None
@@ -597,42 +620,56 @@ class PipelinedGraphStep:
                 # the caller's stream waited for step k - 1 at the end of the previous replay
                 self.slots[r].load(*_as_view(next_view))
             self._loaded[r] = next_view
-        if not fast:
-            # Stream A does not wait for the caller's stream as it is now: that stream waits for the
-            # previous step (below), so the wait would be a round trip between two queues (measured
-            # ~35 us of idle stream A per step at C3).  It waits instead for the
-            # caller's work up to the start of replay k - S + 1, long done: the caller's uses of the
-            # loss of replay k - S (whose tensor composite k rewrites) precede that.  The first
-            # S - 1 replays after a capture wait for the caller's stream itself.  (This replay's own
-            # mark on the caller's stream, ev_cur[k], is recorded after the step's launch below: the
-            # caller's stream gets nothing from replay() before it, and a synced loop's stream A idles
-            # until the launch.)
-            if self._since_capture < S - 1:
-                sa.wait_stream(cur)
-            else:
-                sa.wait_event(self.ev_cur[(self.k + 1) % S])  # recorded at replay k - S + 1
-        self._since_capture += 1
-        sa.wait_event(self.ev_geo[p])
-        with torch.cuda.stream(sa):
-            self.optimizer.sync_lr()  # a changed learning rate: a host-to-device copy on stream A
-            first = self.k == 0 and self.g_comp0 is not None
-            if self._refill and (self.fused or self.fill_after) and not first:
-                # the caller changed the parameter (follow_caller), or the first composite after an
-                # N > 1 capture (its records were filled by no earlier update)
-                self._refill_records(p)
+        first = self.k == 0 and self.g_comp0 is not None
+        refill = self._refill and (self.fused or self.fill_after) and not first
+        # Steady state (the merged step graph, no update graph, no refill): the stream-A waits, the
+        # launch and the step's event in ONE native call (lsr_graph_launch); the Python path below
+        # costs ~8 us more host time before the launch, which a loss.item() loop pays every step
+        launcher = (self._launcher(p, fast) if self.merged and self.g_adam[p] is None and not first and not refill
+                    and self._since_capture >= S - 1 else None)
+        if launcher is not None:
+            self._since_capture += 1
+            self.optimizer.sync_lr(stream=sa)
             self._refill = False
-            (self.g_comp0 if first else self.g_comp[p]).replay()
-            if not self.merged:
-                self.ev_comp[p].record(sa)
-                self.g_step[p].replay()
-            if self.g_adam[p] is not None:
-                for q, g in zip(self.params, self.grads[p]):
-                    q.grad = g
-                self._collective(p)
-                self.g_adam[p].replay()
+            launcher()
+        else:
+            if not fast:
+                # Stream A does not wait for the caller's stream as it is now: that stream waits for the
+                # previous step (below), so the wait would be a round trip between two queues (measured
+                # ~35 us of idle stream A per step at C3).  It waits instead for the
+                # caller's work up to the start of replay k - S + 1, long done: the caller's uses of the
+                # loss of replay k - S (whose tensor composite k rewrites) precede that.  The first
+                # S - 1 replays after a capture wait for the caller's stream itself.  (This replay's own
+                # mark on the caller's stream, ev_cur[k], is recorded after the step's launch below: the
+                # caller's stream gets nothing from replay() before it, and a synced loop's stream A
+                # idles until the launch.)
+                if self._since_capture < S - 1:
+                    sa.wait_stream(cur)
+                else:
+                    sa.wait_event(self.ev_cur[(self.k + 1) % S])  # recorded at replay k - S + 1
+            self._since_capture += 1
+            sa.wait_event(self.ev_geo[p])
+            with torch.cuda.stream(sa):
+                self.optimizer.sync_lr()  # a changed learning rate: a host-to-device copy on stream A
+                if refill:
+                    # the caller changed the parameter (follow_caller), or the first composite after an
+                    # N > 1 capture (its records were filled by no earlier update)
+                    self._refill_records(p)
+                self._refill = False
+                (self.g_comp0 if first else self.g_comp[p]).replay()
+                if not self.merged:
+                    self.ev_comp[p].record(sa)
+                    self.g_step[p].replay()
+                if self.g_adam[p] is not None:
+                    for q, g in zip(self.params, self.grads[p]):
+                        q.grad = g
+                    self._collective(p)
+                    self.g_adam[p].replay()
+            self.ev_step[p].record(sa)
+        if cur is None:
+            cur = torch.cuda.current_stream()
         if not fast:
             self.ev_cur[self.k % S].record(cur)
-        self.ev_step[p].record(sa)
         # view k + S - 1's geometry into set r
         after = self.ev_comp[p] if self.geo_after_fwd and not self.merged else None
         if fast:

@@ -276,7 +276,8 @@ def test_graphed_step_over_a_view_sequence(monkeypatch):
 
 
 @pytest.mark.parametrize("sets,wait,bucket", [(2, True, False), (3, True, False), (3, False, False),
-                                              (3, True, "defer"), (2, True, "defer"), (3, True, "fill")])
+                                              (3, True, "defer"), (2, True, "defer"), (3, True, "fill"),
+                                              (3, True, "python"), (3, False, "python")])
 def test_pipelined_graph_over_a_view_sequence(sets, wait, bucket, monkeypatch):
     """PipelinedGraphStep with one ViewSlot per buffer set: capture(views=the first S - 1 views),
     replay(next_view=the view S - 1 ahead); every replay composites its own view's geometry with its
@@ -288,8 +289,14 @@ def test_pipelined_graph_over_a_view_sequence(sets, wait, bucket, monkeypatch):
     (lsr_adam_fill_language), the first composite refilled from the parameter.  "defer" (the default
     since ABI 16): the backward leaves the language partials, the collective reduces them and ONE
     tail pass (lsr_language_tail) writes the gradients, steps and fills; "fill" (LSR_PG_DEFER=0): the
-    epilogue in the backward, then lsr_adam_fill_language."""
+    epilogue in the backward, then lsr_adam_fill_language.  "python": no bucket, and every replay
+    through torch's stream context and CUDAGraph.replay() instead of the native steady-state launch
+    (lsr_graph_launch, LSR_PG_NATIVE_LAUNCH=0)."""
+    import langsplat_amd.pipeline as pipeline_mod
     monkeypatch.setenv("LANGSPLAT_AMD_FUSED", "1")
+    native = bucket != "python"
+    monkeypatch.setattr(pipeline_mod, "_NATIVE_LAUNCH", native)
+    bucket = False if bucket == "python" else bucket
     monkeypatch.setenv("LSR_PG_DEFER", "0" if bucket == "fill" else "1")
     g = make_gaussians(CONFIGS["C4"]["P"], seed=0)
     views = _c4_views()
@@ -316,6 +323,8 @@ def test_pipelined_graph_over_a_view_sequence(sets, wait, bucket, monkeypatch):
         losses = [t.clone() for t in losses[-sets:]]
         losses_e = losses_e[-sets:]
     assert pg.check() and pg.captures == 1
+    # the steady-state replays of the N = 1 form went through the native launch (lsr_graph_launch)
+    assert bool(pg._launchers) == (native and not bucket)
     pg.sync()
     assert int(opt.state[m._language_feature]["step"].item()) == len(views)
     if wait:

@@ -102,6 +102,9 @@ def main():
     med = statistics.median
     print(f"sync_gap: steps {steps}  run-ahead {ahead:.4f} ms/step  synced {synced:.4f} ms/step  "
           f"(+{1e3 * (synced - ahead):.1f} us)", flush=True)
+    if not gap:  # the steady-state replays launch natively (lsr_graph_launch), past the timed wrapper
+        print("sync_gap: per-step breakdown needs LSR_PG_NATIVE_LAUNCH=0", flush=True)
+        return
     print(f"sync_gap: step graph on stream A {med(span):.1f} us; gap_gpu {med(gap):.1f} us "
           f"(p10 {sorted(gap)[len(gap) // 10]:.1f}, p90 {sorted(gap)[9 * len(gap) // 10]:.1f}); "
           f"host_item {med(host_item):.1f} us; host_pre {med(pre):.1f} us; "
