@@ -22,7 +22,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LSR_LIB") or os.path.join(_HERE, "liblsr.so")
 
 LSR_BUF_GEOM, LSR_BUF_BINNING, LSR_BUF_IMAGE, LSR_BUF_BACKWARD = 0, 1, 2, 3
-ABI_VERSION = 16
+ABI_VERSION = 17
 ADAM_STEP_WORDS = 66  # include/lsr.h LSR_ADAM_STEP_WORDS
 ADAM_WORD_SKIPPED, ADAM_WORD_LR = 49, 50  # LSR_ADAM_WORD_SKIPPED / LSR_ADAM_WORD_LR
 # lsr_raw_flags (include/lsr.h): inputs are GaussianModel's raw parameters

@@ -31,7 +31,7 @@ def test_library_loads_and_exports_every_declared_symbol():
     for name in _declared_functions():
         assert hasattr(lib, name), name
         assert name in _native.SIGNATURES, f"ctypes binding misses {name}"
-    assert lib.lsr_abi_version() == _native.ABI_VERSION == 16
+    assert lib.lsr_abi_version() == _native.ABI_VERSION == 17
 
 
 def test_header_constants_match_the_python_side():
