@@ -250,3 +250,14 @@ def test_optim_adam_refuses_cpu_parameters():
     opt = Adam([p], lr=0.1)
     with pytest.raises(RuntimeError, match="no CPU path"):
         opt.step()
+
+
+def test_graph_launch_refuses_invalid_arguments_without_a_gpu():
+    """lsr_graph_launch (ABI 17) checks its arguments before any HIP call: no executable, a negative
+    wait count, or waits without an array are LSR_ERR_INVALID with a message."""
+    lib = _native.load()
+    assert lib.lsr_graph_launch(None, None, None, 0, None) == 1
+    assert b"lsr_graph_launch" in lib.lsr_last_error()
+    dummy = ctypes.c_void_p(1)
+    assert lib.lsr_graph_launch(dummy, None, None, -1, None) == 1
+    assert lib.lsr_graph_launch(dummy, None, None, 2, None) == 1
