@@ -607,6 +607,8 @@ def main():
             pg.synchronize()
             torch.cuda.synchronize()
             reps.append(1000.0 * (time.perf_counter() - tr) / args.steps)
+        for _ in range(10):  # untimed: the synced form's own warm-up (its first replays take the Python path)
+            pg.replay().item()
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
